@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Lloyd iterations/sec at N=1e8, D=128, K=1024, bf16 (BASELINE.json).
+
+Driver contract: ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is
+launched by ``torch.distributed.run`` (one rank per GPU, RCCL over xGMI).  The
+dataset is 1e8 synthetic Gaussian-blob points in total (1024 blobs, generated on
+device, each rank its own contiguous row range; identical data for any world
+size), centroids are K random data rows.  One timed step is one full Lloyd
+iteration on every rank: MFMA assign + LDS scatter-add update + slab reduce +
+f64 all-reduce + finalize.  Total work is fixed as N grows ("strong" scaling).
+W untimed warmup iterations, then exactly K timed ones bracketed by a barrier and
+``torch.cuda.synchronize()``; the max over ranks is reported by rank 0 as one
+JSON line.  ``value`` is whole-job iterations/s; point-assignments/s and the
+achieved MFMA TFLOP/s are included as extra fields.
+
+Other BASELINE configs (own measurements, not the driver's): ``--config cfg2``
+(N=1e6, D=128, K=256 fp32, one GPU), ``cfg4`` (N=1e7, D=64, K=4096: k-means++
+seeding time + Lloyd it/s), ``cfg5`` (mini-batch, streamed blobs, D=256, K=512).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+METRIC = "Lloyd iterations/sec (and point-assignments/sec) at N=1e8, D=128, K=1024, 1/2/4/8 MI355X"
+
+CONFIGS = {
+    "cfg3": dict(n=100_000_000, d=128, k=1024, dtype="bfloat16", model="kmeans-lloyd N=1e8 D=128 K=1024"),
+    "cfg2": dict(n=1_000_000, d=128, k=256, dtype="float32", model="kmeans-lloyd N=1e6 D=128 K=256"),
+    "cfg4": dict(n=10_000_000, d=64, k=4096, dtype="bfloat16", model="kmeans-lloyd N=1e7 D=64 K=4096 k-means++"),
+    "cfg5": dict(n=1_000_000_000, d=256, k=512, dtype="bfloat16", model="minibatch-kmeans N=1e9 D=256 K=512"),
+}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--n", type=int, default=None, help="override total points")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=1 << 24, help="cfg5 rows per rank per step")
+    args = ap.parse_args(argv)
+
+    import mikmeans
+    from mikmeans.data.blobs import make_blobs, blob_centers
+    from mikmeans.models.init import init_random, init_kmeanspp
+    from mikmeans.models.lloyd import LloydEngine
+    from mikmeans.parallel import Comm, shard_range
+
+    cfg = dict(CONFIGS[args.config])
+    if args.n:
+        cfg["n"] = args.n
+    comm = Comm.from_env("cuda")
+    world = comm.world
+    if args.gpus != world and comm.rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = comm.device
+    dtype = torch.bfloat16 if cfg["dtype"] == "bfloat16" else torch.float32
+    N, D, K = cfg["n"], cfg["d"], cfg["k"]
+    extra = {}
+
+    if args.config == "cfg5":
+        value, ms, extra = _bench_minibatch(args, cfg, comm, dtype)
+        unit = "points/s"
+    else:
+        s, e = shard_range(N, comm.rank, world)
+        t0 = time.perf_counter()
+        centers = blob_centers(K, D, 10.0, args.seed, device=dev)
+        X = make_blobs(e - s, D, K, seed=args.seed, i0=s, dtype=dtype, device=dev, centers=centers)
+        torch.cuda.synchronize()
+        extra["datagen_s"] = round(time.perf_counter() - t0, 3)
+        t0 = time.perf_counter()
+        if args.config == "cfg4":
+            C0 = init_kmeanspp(X, D, K, N, s, comm, args.seed)
+        else:
+            C0 = init_random(X, D, K, N, s, comm, args.seed)
+        torch.cuda.synchronize()
+        extra["init_s"] = round(time.perf_counter() - t0, 3)
+        eng = LloydEngine(X, K, comm=comm).set_centers(C0)
+        for _ in range(args.warmup):
+            eng.step()
+        comm.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            eng.step()
+        torch.cuda.synchronize()
+        comm.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        comm.allreduce_max_(el)
+        elapsed = float(el.item())
+        ms = elapsed * 1e3 / args.steps
+        value = args.steps / elapsed
+        unit = "iter/s"
+        st = eng.last_stats()
+        extra.update(
+            assignments_per_s=value * N,
+            mfma_tflops=2.0 * N * K * D * value / 1e12,
+            inertia=st.inertia,
+            n_changed=st.n_changed,
+        )
+    if comm.rank == 0:
+        out = {
+            "metric": METRIC if args.config == "cfg3" else f"{cfg['model']} ({unit})",
+            "value": value,
+            "unit": unit,
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,  # the reference publishes no number
+            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "data": "synthetic gaussian blobs (on-device Philox), random-init centroids",
+            "config": {
+                "model": cfg["model"],
+                "global_batch": N,
+                "seq_len": D,
+                "n_points": N,
+                "n_features": D,
+                "n_clusters": K,
+                "parallelism": f"dp{world}",
+            },
+            **extra,
+        }
+        print(json.dumps(out), flush=True)
+    comm.close()
+
+
+def _bench_minibatch(args, cfg, comm, dtype):
+    from mikmeans.data.blobs import BlobStream
+    from mikmeans.models.init import init_random
+    from mikmeans.models.minibatch import MiniBatchEngine
+
+    N, D, K = cfg["n"], cfg["d"], cfg["k"]
+    b = args.batch
+    stream = BlobStream(N, D, K, b, seed=args.seed, dtype=dtype, device=comm.device, rank=comm.rank,
+                        world=comm.world)
+    eng = MiniBatchEngine(K, D, b, dtype=dtype, device=comm.device, comm=comm)
+    first = next(stream)
+    eng.set_centers(init_random(first, D, K, b * comm.world, comm.rank * b, comm, args.seed))
+    for _ in range(args.warmup):
+        eng.partial_fit(next(stream))
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.partial_fit(next(stream))  # includes on-device generation of the batch
+    torch.cuda.synchronize()
+    comm.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=comm.device)
+    comm.allreduce_max_(el)
+    elapsed = float(el.item())
+    pts = args.steps * b * comm.world
+    return pts / elapsed, elapsed * 1e3 / args.steps, {"batch_per_rank": b, "steps_cover_points": pts}
+
+
+if __name__ == "__main__":
+    main()

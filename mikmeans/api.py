@@ -1,0 +1,395 @@
+"""Public estimator API: ``KMeans``, ``MiniBatchKMeans``, functional ``fit`` / ``predict``.
+
+The surface follows scikit-learn's (``fit``, ``predict``, ``fit_predict``,
+``transform``, ``score``, ``cluster_centers_``, ``labels_``, ``inertia_``,
+``n_iter_``) on a PyTorch-ROCm engine: GPU tensors run the gfx950 kernels, CPU
+tensors the PyTorch reference path, and a multi-process job (one rank per GPU,
+RCCL) fits on per-rank shards with :class:`~mikmeans.parallel.Comm`.
+
+Reference parity map: assignment of points to centroids
+(R14/R25-R27 drag/drop + select, app.mjs:358-402) -> ``predict``/E-step;
+centroid management (R13 addCentroid/removeCentroid, app.mjs:125-142) ->
+``n_clusters``/``init``; locked centroids (app.mjs:128, :360) -> ``frozen``;
+iteration counter + metric snapshots (R23/R31, app.mjs:288, :498-508) ->
+``n_iter_`` / ``history_``; export/import (R21/R22) -> ``save``/``load`` and
+:mod:`mikmeans.utils.io_json`.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+import torch
+
+from .config import KMeansConfig, resolve_dtype
+from .models.init import resolve_init
+from .models.lloyd import LloydEngine, tol_to_abs
+from .models.minibatch import MiniBatchEngine
+from .ops import cpu as cpu_ops
+from .ops import pad_columns
+from .parallel.comm import Comm, get_comm
+from .utils import metrics as mmetrics
+
+
+def _default_device(device):
+    if device is not None:
+        return torch.device(device)
+    return torch.device("cuda" if torch.cuda.is_available() else "cpu")
+
+
+def _to_tensor(X, device, dtype):
+    was_numpy = not torch.is_tensor(X)
+    t = torch.as_tensor(np.asarray(X) if was_numpy else X)
+    if t.dim() != 2:
+        raise ValueError(f"X must be 2-D [n_samples, n_features], got shape {tuple(t.shape)}")
+    t = t.to(device=device)
+    if t.dtype != dtype:
+        t = t.to(dtype)
+    return t, was_numpy
+
+
+def _shard_info(n_local: int, comm: Comm, device):
+    sizes = comm.all_gather(torch.tensor([n_local], dtype=torch.int64, device=device)).reshape(-1).cpu()
+    start = int(sizes[: comm.rank].sum())
+    return int(sizes.sum()), start
+
+
+class KMeans:
+    """Lloyd k-means on MI355X (full batch, data-parallel over ranks)."""
+
+    def __init__(self, n_clusters: int = 8, *, init="k-means++", n_init: int = 1, max_iter: int = 300,
+                 tol: float = 1e-4, dtype="float32", device=None, seed: int | None = 0,
+                 random_state: int | None = None, comm: Comm | None = None, frozen=None,
+                 empty_cluster: str = "keep", check_every: int = 1, n_local_trials=None,
+                 verbose: int = 0, mode: str = "learn", run_id: str | None = None,
+                 checkpoint_every: int = 0, checkpoint_dir: str | None = None):
+        self.n_clusters = int(n_clusters)
+        self.init = init
+        self.n_init = int(n_init)
+        self.max_iter = int(max_iter)
+        self.tol = float(tol)
+        self.dtype = resolve_dtype(dtype)
+        self.device = device
+        self.seed = int(random_state if random_state is not None else (seed or 0))
+        self.comm = comm
+        self.frozen = frozen
+        self.empty_cluster = empty_cluster
+        self.check_every = int(check_every)
+        self.n_local_trials = n_local_trials
+        self.verbose = verbose
+        self.mode = mode
+        self.run_id = run_id
+        self.checkpoint_every = int(checkpoint_every)
+        self.checkpoint_dir = checkpoint_dir
+        self.history_: list[dict] = []
+
+    # ---------------------------------------------------------------- config
+    @classmethod
+    def from_config(cls, cfg: KMeansConfig, **kw):
+        return cls(n_clusters=cfg.n_clusters, init=cfg.init, n_init=cfg.n_init, max_iter=cfg.max_iter,
+                   tol=cfg.tol, dtype=cfg.dtype, device=cfg.device, seed=cfg.seed,
+                   empty_cluster=cfg.empty_cluster, check_every=cfg.check_every,
+                   n_local_trials=cfg.n_local_trials, verbose=cfg.verbose, mode=cfg.mode,
+                   run_id=cfg.run_id, checkpoint_every=cfg.checkpoint_every,
+                   checkpoint_dir=cfg.checkpoint_dir, **kw)
+
+    def get_config(self) -> KMeansConfig:
+        return KMeansConfig(n_clusters=self.n_clusters, init=self.init if isinstance(self.init, str) else "array",
+                            n_init=self.n_init, max_iter=self.max_iter, tol=self.tol,
+                            dtype="bfloat16" if self.dtype == torch.bfloat16 else "float32",
+                            device=str(self.device) if self.device else None, seed=self.seed,
+                            empty_cluster=self.empty_cluster, check_every=self.check_every,
+                            n_local_trials=self.n_local_trials, mode=self.mode, run_id=self.run_id,
+                            verbose=self.verbose, checkpoint_every=self.checkpoint_every,
+                            checkpoint_dir=self.checkpoint_dir)
+
+    # ------------------------------------------------------------------- fit
+    def fit(self, X, y=None, sample_weight=None, *, resume_from=None):
+        comm = self.comm or get_comm()
+        device = _default_device(self.device) if self.device is not None or comm.world == 1 else comm.device
+        Xt, was_numpy = _to_tensor(X, device, self.dtype)
+        self._numpy_io = was_numpy
+        D = Xt.shape[1]
+        if Xt.is_cuda:
+            Xt = pad_columns(Xt)
+        n_global, start = _shard_info(Xt.shape[0], comm, device)
+        if n_global < self.n_clusters:
+            raise ValueError(f"n_samples={n_global} should be >= n_clusters={self.n_clusters}")
+        w = None
+        if sample_weight is not None:
+            w = torch.as_tensor(np.asarray(sample_weight) if not torch.is_tensor(sample_weight)
+                                else sample_weight, dtype=torch.float32).to(device)
+        tol_abs = tol_to_abs(self.tol, Xt[:, :D] if Xt.shape[1] != D else Xt, comm, n_global)
+        best = None
+        t0 = time.perf_counter()
+        start_iter = 0
+        for trial in range(max(1, self.n_init)):
+            eng = LloydEngine(Xt, self.n_clusters, comm=comm, sample_weight=w, frozen=self.frozen,
+                              empty_policy=self.empty_cluster, n_features=D)
+            if resume_from is not None and trial == 0:
+                from .utils.checkpoint import load_checkpoint
+
+                ck = load_checkpoint(resume_from, comm=comm)
+                centers = ck["centers"].to(device)
+                start_iter = int(ck["iteration"])
+            else:
+                centers = resolve_init(self.init, Xt, D, self.n_clusters, n_global, start, comm,
+                                       self.seed + trial, self.n_local_trials)
+            eng.set_centers(centers[:, :D])
+            eng.iteration = start_iter
+            hist = []
+
+            def cb(st, _eng=eng, _hist=hist):
+                rec = st.as_dict()
+                rec["counts"] = _eng.counts.tolist() if self.verbose > 1 else None
+                _hist.append(rec)
+                if self.verbose and comm.rank == 0:
+                    print(f"[mikmeans] iter {st.iteration} inertia {st.inertia:.6g} "
+                          f"shift {st.shift:.3g} changed {st.n_changed}", flush=True)
+                if self.checkpoint_every and self.checkpoint_dir and st.iteration % self.checkpoint_every == 0:
+                    from .utils.checkpoint import save_checkpoint
+
+                    save_checkpoint(self.checkpoint_dir, _eng.centers, st.iteration, self.get_config(),
+                                    history=_hist, comm=comm)
+
+            remaining = max(0, self.max_iter - start_iter)
+            n_iter, converged, _ = eng.run(remaining, tol_abs, check_every=self.check_every, callback=cb)
+            labels, mind = eng.assign(True)
+            wt = eng.weights.double() if eng.weights is not None else 1.0
+            inert = (mind.double() * wt).sum().reshape(1) if eng.n else torch.zeros(1, dtype=torch.float64,
+                                                                                    device=device)
+            comm.allreduce_(inert)
+            inertia = float(inert.item())
+            if best is None or inertia < best[0]:
+                best = (inertia, eng, labels, n_iter, converged, hist)
+        inertia, eng, labels, n_iter, converged, hist = best
+        self._engine = eng
+        self.cluster_centers_ = eng.centers.clone()
+        self.labels_ = labels
+        self.inertia_ = inertia
+        self.n_iter_ = n_iter
+        self.converged_ = converged
+        self.history_ = hist
+        self.n_features_in_ = D
+        self.fit_time_s_ = time.perf_counter() - t0
+        cnt = torch.bincount(labels.long(), minlength=self.n_clusters).to(torch.float64)
+        comm.allreduce_(cnt)
+        self.counts_ = cnt.cpu()
+        return self
+
+    def fit_predict(self, X, y=None, sample_weight=None):
+        return self.fit(X, sample_weight=sample_weight)._out(self.labels_)
+
+    # --------------------------------------------------------------- predict
+    def _check_fitted(self):
+        if not hasattr(self, "cluster_centers_"):
+            raise RuntimeError("KMeans instance is not fitted yet; call fit() first")
+
+    def _out(self, t):
+        if getattr(self, "_numpy_io", False):
+            return t.cpu().numpy()
+        return t
+
+    def predict(self, X):
+        self._check_fitted()
+        from . import ops
+
+        device = self.cluster_centers_.device
+        Xt, was_numpy = _to_tensor(X, device, self.dtype)
+        labels, _ = ops.assign(Xt, self.cluster_centers_, with_dist=False)
+        return labels.cpu().numpy() if was_numpy else labels
+
+    def transform(self, X):
+        """Euclidean distances to every centre, ``[n, K]`` (float32)."""
+        self._check_fitted()
+        device = self.cluster_centers_.device
+        Xt, was_numpy = _to_tensor(X, device, self.dtype)
+        c = cpu_ops.quantize_centers(self.cluster_centers_, self.dtype)
+        d = torch.cdist(Xt.to(torch.float32), c)
+        return d.cpu().numpy() if was_numpy else d
+
+    def score(self, X, sample_weight=None):
+        """Negative inertia of ``X`` under the fitted centres."""
+        self._check_fitted()
+        from . import ops
+
+        device = self.cluster_centers_.device
+        Xt, _ = _to_tensor(X, device, self.dtype)
+        _, mind = ops.assign(Xt, self.cluster_centers_, with_dist=True)
+        if sample_weight is not None:
+            mind = mind * torch.as_tensor(np.asarray(sample_weight), dtype=torch.float32, device=device)
+        return -float(mind.double().sum())
+
+    # --------------------------------------------------------------- metrics
+    def metrics(self) -> dict:
+        """Dashboard metrics of the fit (reference snapshotMetrics parity, app.mjs:481-496)."""
+        self._check_fitted()
+        counts = [int(c) for c in self.counts_.tolist()]
+        return {
+            "k": self.n_clusters,
+            "counts": counts,
+            "balance": mmetrics.balance(counts),
+            "inertia": self.inertia_,
+            "n_iter": self.n_iter_,
+        }
+
+    # ------------------------------------------------------------- persist
+    def save(self, path):
+        from .utils.checkpoint import save_checkpoint
+
+        self._check_fitted()
+        return save_checkpoint(path, self.cluster_centers_, self.n_iter_, self.get_config(),
+                               history=self.history_, comm=self.comm or get_comm())
+
+    @classmethod
+    def load(cls, path, device=None):
+        from .utils.checkpoint import load_checkpoint
+
+        ck = load_checkpoint(path)
+        cfg = KMeansConfig.from_dict(ck["config"])
+        km = cls.from_config(cfg)
+        dev = _default_device(device)
+        km.cluster_centers_ = ck["centers"].to(dev)
+        km.n_iter_ = int(ck["iteration"])
+        km.history_ = ck.get("history", [])
+        km.n_features_in_ = km.cluster_centers_.shape[1]
+        return km
+
+
+class MiniBatchKMeans:
+    """Mini-batch k-means (Sculley 2010) over tensors or device-generated streams."""
+
+    def __init__(self, n_clusters: int = 8, *, batch_size: int = 1024, max_iter: int = 100,
+                 max_steps: int | None = None, init="k-means++", init_size: int | None = None,
+                 dtype="float32", device=None, seed: int = 0, comm: Comm | None = None, frozen=None,
+                 tol: float = 0.0, verbose: int = 0):
+        self.n_clusters = int(n_clusters)
+        self.batch_size = int(batch_size)
+        self.max_iter = int(max_iter)
+        self.max_steps = max_steps
+        self.init = init
+        self.init_size = init_size
+        self.dtype = resolve_dtype(dtype)
+        self.device = device
+        self.seed = int(seed)
+        self.comm = comm
+        self.frozen = frozen
+        self.tol = float(tol)
+        self.verbose = verbose
+        self._eng = None
+
+    def _engine(self, D, device):
+        if self._eng is None:
+            comm = self.comm or get_comm()
+            self._eng = MiniBatchEngine(self.n_clusters, D, self.batch_size, dtype=self.dtype,
+                                        device=device, comm=comm, frozen=self.frozen)
+        return self._eng
+
+    def _init_centers(self, sample: torch.Tensor):
+        comm = self.comm or get_comm()
+        D = sample.shape[1]
+        n_global, start = _shard_info(sample.shape[0], comm, sample.device)
+        Xs = pad_columns(sample) if sample.is_cuda else sample
+        return resolve_init(self.init, Xs, D, self.n_clusters, n_global, start, comm, self.seed,
+                            None)[:, :D]
+
+    def fit(self, X):
+        """Fit on a tensor/array (random batches each step; ``max_iter`` epochs)."""
+        comm = self.comm or get_comm()
+        device = _default_device(self.device) if self.device is not None or comm.world == 1 else comm.device
+        Xt, was_numpy = _to_tensor(X, device, self.dtype)
+        self._numpy_io = was_numpy
+        n, D = Xt.shape
+        eng = self._engine(D, device)
+        g = torch.Generator(device="cpu").manual_seed(self.seed + 7919 * comm.rank)
+        init_n = min(n, self.init_size or max(3 * self.batch_size, 3 * self.n_clusters))
+        sample_idx = torch.randperm(n, generator=g)[:init_n].to(device)
+        eng.set_centers(self._init_centers(Xt[sample_idx]))
+        steps = self.max_steps or max(1, math.ceil(self.max_iter * n / self.batch_size))
+        for s in range(steps):
+            idx = torch.randint(0, n, (min(self.batch_size, n),), generator=g).to(device)
+            eng.partial_fit(Xt[idx])
+            if self.tol > 0 and (s + 1) % 10 == 0:
+                if float(eng.shift.sum()) <= self.tol:
+                    break
+        self._finish(eng)
+        self.labels_ = self.predict(X)
+        return self
+
+    def fit_stream(self, stream, steps: int, init_batch: torch.Tensor | None = None):
+        """Fit on an iterator of per-rank batches (e.g. :class:`~mikmeans.data.blobs.BlobStream`)."""
+        first = init_batch if init_batch is not None else next(iter(stream))
+        eng = self._engine(first.shape[1], first.device)
+        eng.set_centers(self._init_centers(first.to(self.dtype)))
+        for _ in range(steps):
+            eng.partial_fit(next(stream))
+        self._finish(eng)
+        return self
+
+    def partial_fit(self, Xb):
+        comm = self.comm or get_comm()
+        device = _default_device(self.device) if self.device is not None or comm.world == 1 else comm.device
+        Xt, _ = _to_tensor(Xb, device, self.dtype)
+        eng = self._engine(Xt.shape[1], device)
+        if not hasattr(self, "cluster_centers_"):
+            eng.set_centers(self._init_centers(Xt))
+        eng.partial_fit(Xt)
+        self._finish(eng)
+        return self
+
+    def _finish(self, eng):
+        self.cluster_centers_ = eng.centers.clone()
+        self.n_steps_ = eng.steps
+        self.counts_ = eng.vcount.clone()
+
+    def predict(self, X):
+        from . import ops
+
+        Xt, was_numpy = _to_tensor(X, self.cluster_centers_.device, self.dtype)
+        labels, _ = ops.assign(Xt, self.cluster_centers_, with_dist=False)
+        return labels.cpu().numpy() if was_numpy else labels
+
+    def score(self, X):
+        from . import ops
+
+        Xt, _ = _to_tensor(X, self.cluster_centers_.device, self.dtype)
+        _, mind = ops.assign(Xt, self.cluster_centers_, with_dist=True)
+        return -float(mind.double().sum())
+
+
+# ------------------------------------------------------------------ functional
+def fit(X, k: int, **kw):
+    """``fit(X, k) -> (centers, labels)`` — the north-star functional surface."""
+    km = KMeans(n_clusters=k, **kw).fit(X)
+    return km._out(km.cluster_centers_), km._out(km.labels_)
+
+
+def predict(X, centers, dtype="float32"):
+    """Nearest-centre labels of ``X`` for given ``centers``."""
+    from . import ops
+
+    was_numpy = not torch.is_tensor(X)
+    c = torch.as_tensor(np.asarray(centers) if not torch.is_tensor(centers) else centers, dtype=torch.float32)
+    dev = c.device if torch.is_tensor(centers) else _default_device(None)
+    Xt, _ = _to_tensor(X, dev, resolve_dtype(dtype))
+    labels, _ = ops.assign(Xt, c.to(dev), with_dist=False)
+    return labels.cpu().numpy() if was_numpy else labels
+
+
+def fit_predict(X, k: int, **kw):
+    return fit(X, k, **kw)[1]
+
+
+def kmeans_plusplus(X, n_clusters: int, *, seed: int = 0, n_local_trials=None, comm: Comm | None = None,
+                    dtype="float32", device=None):
+    """k-means++ seeding only; returns the ``[K, D]`` initial centres."""
+    comm = comm or get_comm()
+    dev = _default_device(device)
+    Xt, was_numpy = _to_tensor(X, dev, resolve_dtype(dtype))
+    D = Xt.shape[1]
+    Xp = pad_columns(Xt) if Xt.is_cuda else Xt
+    n_global, start = _shard_info(Xt.shape[0], comm, dev)
+    name = "greedy-k-means++" if (n_local_trials or 1) > 1 else "k-means++"
+    c = resolve_init(name, Xp, D, n_clusters, n_global, start, comm, seed, n_local_trials)
+    return c.cpu().numpy() if was_numpy else c

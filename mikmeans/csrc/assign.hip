@@ -1,0 +1,277 @@
+// mikmeans — K2: fused MFMA assignment kernel (Lloyd E-step) for gfx950.
+//
+// score[i,k] = |c_k|^2 - 2 x_i.c_k is computed as a GEMM on the matrix cores
+// (v_mfma_f32_32x32x16_bf16 for bf16 points, v_mfma_f32_32x32x2_f32 for exact
+// f32) with the argmin over k folded into the epilogue ("online argmin", the
+// k-means analogue of flash attention's online max over key blocks).
+//
+// Design (MI355X-first):
+//  * A workgroup (4 waves) owns NW*P*32 points.  Each wave keeps the B-operand
+//    fragments of its P*32 points in registers for the whole kernel: lane
+//    (r, h) holds x[p0+r][h*DPAD/2 .. +DPAD/2) -- one contiguous 64..512 B run
+//    per lane (the d-permutation used by both operands, see kernels.h).
+//  * Centroids are streamed as fragment-packed 16 KiB chunks through a 3-slot
+//    LDS ring by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction),
+//    one raw s_barrier per chunk and a counted vmcnt, so the next two chunks
+//    stay in flight while the current one feeds the MFMAs.  All of C is re-read
+//    from L2 by every workgroup; per point that is 2*K*D*2/(NW*P*32) bytes.
+//  * |c|^2 seeds the accumulator (C-in of the first MFMA), so the matrix core
+//    emits the score directly; no VALU add per element.
+//  * Epilogue per 32x32 tile: the register index r (0..15) is packed into the
+//    4 low mantissa bits of each score (v_and_or_b32), a v_min3_f32 tree gives
+//    the lane's best (score, r) in 8 instructions, and one compare/select pair
+//    tracks the best tile.  The two lane halves (rows 4h..) merge once at the
+//    end with a cross-lane shuffle.  Relative score resolution is 2^-19.
+//  * Outputs: labels (in place, counting changed labels), optional squared
+//    distance, and per-workgroup inertia / changed partials accumulated into
+//    256 f64 slots (reduced by launch_reduce, which also re-zeroes them).
+//
+// Reference parity: this replaces the reference's human drag-and-drop
+// assignment step (app.mjs:358-372 drop handler, :398-402 <select>); there the
+// "distance" is a person's judgement, here it is the squared L2 distance.
+#include "common.h"
+#include "kernels.h"
+
+namespace mk {
+
+// centroid tiles per LDS chunk: a chunk is 16 KiB (or one tile when a tile is larger)
+constexpr int chunk_tiles(int esize, int dpad) {
+  return (32 * dpad * esize) >= 16384 ? 1 : 16384 / (32 * dpad * esize);
+}
+
+template <typename T, int DPAD>
+struct AssignCfg {
+  static constexpr int NW = 4;                 // waves per workgroup
+  static constexpr int P = 2;                  // 32-point blocks per wave
+  static constexpr int V = Elem<T>::V;         // elements per 16-B piece
+  static constexpr int NQ = DPAD / 2 / V;      // pieces per lane per point
+  static constexpr int TILE_BYTES = NQ * 1024; // 32 centroids x DPAD
+  static constexpr int CT = chunk_tiles(sizeof(T), DPAD);  // tiles per chunk
+  static constexpr int CHUNK_BYTES = CT * TILE_BYTES;
+  static constexpr int PIECES = CHUNK_BYTES / 1024;
+  static constexpr int NPW = PIECES / NW;      // LDS-DMA instructions per wave per chunk
+  static constexpr int PTS = NW * P * 32;      // points per workgroup
+  static constexpr int NBUF = 3;
+  static_assert(NQ >= 1, "DPAD too small");
+  static_assert(PIECES % NW == 0, "chunk pieces must split evenly over waves");
+};
+
+__device__ __forceinline__ float pack_key(float s, int r) {
+  return __uint_as_float((__float_as_uint(s) & ~15u) | (unsigned)r);
+}
+
+template <typename T>
+struct MfmaOp;
+template <>
+struct MfmaOp<uint16_t> {
+  __device__ static __forceinline__ f32x16 run(const u32x4& a, const u32x4& b, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(short8, a),
+                                                   __builtin_bit_cast(short8, b), c, 0, 0, 0);
+  }
+};
+template <>
+struct MfmaOp<float> {
+  // one 16-B piece = 4 k-steps of the exact-f32 32x32x2 MFMA
+  __device__ static __forceinline__ f32x16 run(const u32x4& a, const u32x4& b, f32x16 c) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a[e]), __uint_as_float(b[e]), c, 0,
+                                               0, 0);
+    return c;
+  }
+};
+
+template <typename T, int DPAD>
+__global__ __launch_bounds__(256) void assign_kernel(AssignArgs a) {
+  using C = AssignCfg<T, DPAD>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
+  char* cn_lds = smem;
+  char* bufs = smem + cn_bytes;
+  const int nch = a.Kpad / (32 * C::CT);
+  const char* gC = (const char*)a.Cpack;
+
+  // ---- LDS-DMA prologue (|c|^2 table + chunk 0), then the point fragments
+  for (int p = wid; p < cn_bytes / 1024; p += C::NW)
+    glds16((const char*)a.cn + p * 1024 + lane * 16, (MK_LDS void*)(cn_lds + p * 1024));
+  auto issue_chunk = [&](int c) {
+    const char* src = gC + (int64_t)c * C::CHUNK_BYTES + lane * 16;
+    char* dst = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
+#pragma unroll
+    for (int i = 0; i < C::NPW; ++i) {
+      const int pc = wid + i * C::NW;
+      glds16(src + pc * 1024, (MK_LDS void*)(dst + pc * 1024));
+    }
+  };
+  issue_chunk(0);
+
+  // lane (r,h) of block p: contiguous DPAD/2 elements of point p0+r
+  const int64_t pbase = (int64_t)blockIdx.x * C::PTS + (int64_t)wid * (C::P * 32);
+  u32x4 xr[C::P][C::NQ];
+#pragma unroll
+  for (int p = 0; p < C::P; ++p) {
+    int64_t row = pbase + p * 32 + r;
+    row = row < a.N ? row : (a.N - 1);
+    const T* rp = (const T*)a.X + row * a.ldx + h * (DPAD / 2);
+#pragma unroll
+    for (int q = 0; q < C::NQ; ++q) {
+      const int col = h * (DPAD / 2) + q * C::V;
+      if (col < a.D) xr[p][q] = *(const u32x4*)(rp + q * C::V);
+      else xr[p][q] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  // Retire the fragments here, once: otherwise hipcc's waitcnt pass cannot
+  // count them across the LDS-DMA issued in the loop and drains vmcnt(0)
+  // before every chunk's first MFMA.
+  wait_vmcnt<0>();
+  if (nch > 1) issue_chunk(1);
+
+  float best[C::P];
+  int bt[C::P];
+#pragma unroll
+  for (int p = 0; p < C::P; ++p) { best[p] = 3.0e38f; bt[p] = 0; }
+
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
+    wait_lgkm0();
+    raw_barrier();  // chunk c visible to every wave; every wave done with chunk c-1
+    if (c + 2 < nch) issue_chunk(c + 2);
+    const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
+#pragma unroll
+    for (int t = 0; t < C::CT; ++t) {
+      const int tile = c * C::CT + t;
+      f32x16 ci;
+      const float* cnt = (const float*)cn_lds + tile * 32 + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *(const f32x4*)(cnt + 8 * g);
+        ci[4 * g + 0] = v[0]; ci[4 * g + 1] = v[1]; ci[4 * g + 2] = v[2]; ci[4 * g + 3] = v[3];
+      }
+      f32x16 acc[C::P];
+      const char* tl = buf + t * C::TILE_BYTES + lane * 16;
+      u32x4 aw[C::NQ];
+#pragma unroll
+      for (int q = 0; q < C::NQ; ++q) aw[q] = *(const u32x4*)(tl + q * 1024);
+#pragma unroll
+      for (int q = 0; q < C::NQ; ++q) {
+#pragma unroll
+        for (int p = 0; p < C::P; ++p) acc[p] = MfmaOp<T>::run(aw[q], xr[p][q], q == 0 ? ci : acc[p]);
+      }
+#pragma unroll
+      for (int p = 0; p < C::P; ++p) {
+        const f32x16& s = acc[p];
+        float m0 = min3f(pack_key(s[0], 0), pack_key(s[1], 1), pack_key(s[2], 2));
+        float m1 = min3f(pack_key(s[3], 3), pack_key(s[4], 4), pack_key(s[5], 5));
+        float m2 = min3f(pack_key(s[6], 6), pack_key(s[7], 7), pack_key(s[8], 8));
+        float m3 = min3f(pack_key(s[9], 9), pack_key(s[10], 10), pack_key(s[11], 11));
+        float m4 = min3f(pack_key(s[12], 12), pack_key(s[13], 13), pack_key(s[14], 14));
+        float m5 = min3f(m0, m1, m2);
+        float m6 = min3f(m3, m4, pack_key(s[15], 15));
+        float m = min3f(m5, m6, m6);
+        if (m < best[p]) { best[p] = m; bt[p] = tile; }
+      }
+    }
+  }
+
+  // ---- epilogue: merge lane halves, write labels / distances / partials
+  float inert = 0.f;
+  int changed = 0;
+#pragma unroll
+  for (int p = 0; p < C::P; ++p) {
+    const unsigned bits = __float_as_uint(best[p]);
+    int k = bt[p] * 32 + mfma32_row((int)(bits & 15u), h);
+    float v = __uint_as_float(bits & ~15u);
+    const float vo = __shfl_xor(v, 32, 64);
+    const int ko = __shfl_xor(k, 32, 64);
+    if (vo < v || (vo == v && ko < k)) { v = vo; k = ko; }
+    if ((p & 1) == h) {
+      const int64_t i = pbase + p * 32 + r;
+      if (i < a.N) {
+        if (a.track_changed) changed += (a.labels[i] != k);
+        a.labels[i] = k;
+        if (a.xn) {
+          const float d = fmaxf(a.xn[i] + v, 0.f);
+          inert += d;
+          if (a.mind) a.mind[i] = d;
+        }
+      }
+    }
+  }
+  if (a.slots) {
+    double di = wave_sum((double)inert);
+    int dc = wave_sum(changed);
+    // scratch after the ring (all LDS-DMA traffic retired at the last chunk's vmcnt(0))
+    double* red = (double*)(bufs + C::NBUF * C::CHUNK_BYTES);
+    if (lane == 0) { red[2 * wid] = di; red[2 * wid + 1] = (double)dc; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double si = 0, sc = 0;
+#pragma unroll
+      for (int w = 0; w < C::NW; ++w) { si += red[2 * w]; sc += red[2 * w + 1]; }
+      double* slot = a.slots + (blockIdx.x % NSLOT) * SLOT_STRIDE;
+      atomicAdd(slot + 0, si);
+      atomicAdd(slot + 1, sc);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+template <typename T, int DPAD>
+static hipError_t launch_t(const AssignArgs& a, hipStream_t s) {
+  using C = AssignCfg<T, DPAD>;
+  if (a.Kpad % (32 * C::CT) != 0) return hipErrorInvalidValue;
+  const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
+  const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)assign_kernel<T, DPAD>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
+  if (nblk <= 0) return hipSuccess;
+  hipLaunchKernelGGL((assign_kernel<T, DPAD>), dim3((unsigned)nblk), dim3(C::NW * 64), lds, s, a);
+  return hipGetLastError();
+}
+
+int assign_chunk_tiles(int dtype, int dpad) {
+  const bool ok = dtype == DT_BF16 ? (dpad == 16 || dpad == 32 || dpad == 64 || dpad == 128 || dpad == 256)
+                                   : (dpad == 8 || dpad == 16 || dpad == 32 || dpad == 64 || dpad == 128 || dpad == 256);
+  if (!ok) return 0;
+  return chunk_tiles(dtype == DT_BF16 ? 2 : 4, dpad);
+}
+int assign_kpad(int dtype, int dpad, int K) {
+  const int ct = assign_chunk_tiles(dtype, dpad);
+  if (ct <= 0) return 0;
+  const int m = 32 * ct;
+  return ((K + m - 1) / m) * m;
+}
+int assign_cn_len(int kpad) { return ((kpad + 255) / 256) * 256; }
+
+hipError_t launch_assign(int dtype, int dpad, const AssignArgs& a, hipStream_t s) {
+  if (dtype == DT_BF16) {
+    switch (dpad) {
+      case 16: return launch_t<uint16_t, 16>(a, s);
+      case 32: return launch_t<uint16_t, 32>(a, s);
+      case 64: return launch_t<uint16_t, 64>(a, s);
+      case 128: return launch_t<uint16_t, 128>(a, s);
+      case 256: return launch_t<uint16_t, 256>(a, s);
+    }
+  } else {
+    switch (dpad) {
+      case 8: return launch_t<float, 8>(a, s);
+      case 16: return launch_t<float, 16>(a, s);
+      case 32: return launch_t<float, 32>(a, s);
+      case 64: return launch_t<float, 64>(a, s);
+      case 128: return launch_t<float, 128>(a, s);
+      case 256: return launch_t<float, 256>(a, s);
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace mk

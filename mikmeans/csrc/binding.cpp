@@ -1,0 +1,332 @@
+// mikmeans — torch extension binding for the gfx950 kernels (+ native host helpers).
+//
+// Thin, allocation-free wrappers: every op takes pre-allocated tensors, checks
+// shapes/dtypes/devices on the host (a hand-written kernel must never see a
+// shape it does not assume), and launches on the current HIP stream.  Built by
+// hipcc directly (mikmeans/_build.py) -- no hipify, no CUDA compatibility layer.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <charconv>
+#include <cmath>
+#include <string>
+
+#include "kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+void hip_check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "mikmeans: ", what, " failed: ", hipGetErrorString(e));
+}
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dtype_of(const Tensor& X) {
+  if (X.scalar_type() == at::kBFloat16) return mk::DT_BF16;
+  TORCH_CHECK(X.scalar_type() == at::kFloat, "mikmeans: points must be bfloat16 or float32");
+  return mk::DT_F32;
+}
+int vec_of(int dt) { return dt == mk::DT_BF16 ? 8 : 4; }
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "mikmeans: ", name, " must be a GPU tensor");
+}
+void check_f32(const Tensor& t, const char* name, int64_t numel_min = 0) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous(), "mikmeans: ", name,
+              " must be contiguous float32");
+  TORCH_CHECK(t.numel() >= numel_min, "mikmeans: ", name, " too small (", t.numel(), " < ",
+              numel_min, ")");
+}
+void check_f64(const Tensor& t, const char* name, int64_t numel_min) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kDouble && t.is_contiguous(), "mikmeans: ", name,
+              " must be contiguous float64");
+  TORCH_CHECK(t.numel() >= numel_min, "mikmeans: ", name, " too small");
+}
+// Points: 2-D, unit column stride, 16-B aligned rows whose length is a multiple of 16 B.
+int64_t check_points(const Tensor& X, int dt) {
+  check_cuda(X, "X");
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "mikmeans: X must be 2-D with unit column stride");
+  const int v = vec_of(dt);
+  TORCH_CHECK(X.size(1) % v == 0, "mikmeans: D must be a multiple of ", v,
+              " for the vector path (pad the columns)");
+  TORCH_CHECK(X.size(0) <= 1 || X.stride(0) % v == 0, "mikmeans: row stride must be 16-B aligned");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0, "mikmeans: X must be 16-B aligned");
+  return X.size(0) <= 1 ? X.size(1) : X.stride(0);
+}
+template <typename T>
+T* opt_ptr(const c10::optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+// ----------------------------------------------------------------------------
+void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::optional<Tensor>& xn,
+            const Tensor& labels, const c10::optional<Tensor>& mind,
+            const c10::optional<Tensor>& slots, int64_t Kpad, int64_t dpad, bool track_changed) {
+  const int dt = dtype_of(X);
+  const int64_t ldx = check_points(X, dt);
+  const int64_t N = X.size(0);
+  const int D = (int)X.size(1);
+  TORCH_CHECK(D <= dpad, "mikmeans: D exceeds dpad");
+  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, (int)Kpad) == Kpad, "mikmeans: bad Kpad ", Kpad,
+              " for dpad ", dpad);
+  check_cuda(pack, "pack");
+  TORCH_CHECK(pack.is_contiguous() && pack.scalar_type() == X.scalar_type(),
+              "mikmeans: pack dtype must match X");
+  TORCH_CHECK(pack.numel() >= Kpad * dpad, "mikmeans: pack too small");
+  check_f32(cn, "cn", mk::assign_cn_len((int)Kpad));
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kInt && labels.is_contiguous() &&
+                  labels.numel() >= N,
+              "mikmeans: labels must be contiguous int32 [N]");
+  if (xn.has_value()) check_f32(*xn, "xn", N);
+  if (mind.has_value()) check_f32(*mind, "mind", N);
+  if (slots.has_value()) check_f64(*slots, "slots", mk::NSLOT * mk::SLOT_STRIDE);
+  TORCH_CHECK(!mind.has_value() || xn.has_value(), "mikmeans: mind needs xn");
+  mk::AssignArgs a;
+  a.X = X.data_ptr(); a.N = N; a.D = D; a.ldx = ldx;
+  a.Cpack = pack.data_ptr(); a.cn = cn.data_ptr<float>(); a.Kpad = (int)Kpad;
+  a.xn = opt_ptr<const float>(xn);
+  a.labels = labels.data_ptr<int32_t>();
+  a.mind = opt_ptr<float>(mind);
+  a.slots = opt_ptr<double>(slots);
+  a.track_changed = track_changed ? 1 : 0;
+  hip_check(mk::launch_assign(dt, (int)dpad, a, stream()), "assign");
+}
+
+void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab,
+            const Tensor& cnt_slab, int64_t n_chunks, const c10::optional<Tensor>& weights) {
+  const int dt = dtype_of(X);
+  const int64_t ldx = check_points(X, dt);
+  const int64_t N = X.size(0);
+  const int D = (int)X.size(1);
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kInt && labels.numel() >= N,
+              "mikmeans: labels must be int32 [N]");
+  const int sw = mk::update_slice_width(dt, (int)K, D);
+  TORCH_CHECK(sw == 0 ? n_chunks == 1 : n_chunks % 8 == 0, "mikmeans: bad n_chunks");
+  check_f32(slab, "slab", n_chunks * K * D);
+  check_f32(cnt_slab, "cnt_slab", n_chunks * K);
+  if (weights.has_value()) check_f32(*weights, "weights", N);
+  if (sw == 0) {  // global-atomic fallback accumulates into zeroed buffers
+    hip_check(hipMemsetAsync(slab.data_ptr(), 0, K * D * 4, stream()), "memset");
+    hip_check(hipMemsetAsync(cnt_slab.data_ptr(), 0, K * 4, stream()), "memset");
+  }
+  mk::UpdateArgs a;
+  a.X = X.data_ptr(); a.N = N; a.D = D; a.ldx = ldx;
+  a.labels = labels.data_ptr<int32_t>(); a.K = (int)K; a.n_chunks = (int)n_chunks;
+  a.slab = slab.data_ptr<float>(); a.cnt_slab = cnt_slab.data_ptr<float>();
+  a.weights = opt_ptr<const float>(weights);
+  hip_check(mk::launch_update(dt, a, stream()), "update");
+}
+
+void reduce(const Tensor& slab, const Tensor& cnt_slab, int64_t n_chunks, int64_t K, int64_t D,
+            const c10::optional<Tensor>& slots, const Tensor& packed) {
+  check_f32(slab, "slab", n_chunks * K * D);
+  check_f32(cnt_slab, "cnt_slab", n_chunks * K);
+  check_f64(packed, "packed", K * D + K + 2);
+  if (slots.has_value()) check_f64(*slots, "slots", mk::NSLOT * mk::SLOT_STRIDE);
+  hip_check(mk::launch_reduce(slab.data_ptr<float>(), cnt_slab.data_ptr<float>(), (int)n_chunks,
+                              (int)K, (int)D, opt_ptr<double>(slots), packed.data_ptr<double>(),
+                              stream()),
+            "reduce");
+}
+
+void finalize(int64_t mode, const c10::optional<Tensor>& packed, const Tensor& Cold,
+              const c10::optional<Tensor>& Cnew, const c10::optional<Tensor>& frozen,
+              const c10::optional<Tensor>& mb_counts, const Tensor& pack, const Tensor& cn,
+              const c10::optional<Tensor>& shift, const c10::optional<Tensor>& counts,
+              int64_t dpad, int64_t Kpad) {
+  check_f32(Cold, "C");
+  TORCH_CHECK(Cold.dim() == 2, "mikmeans: C must be [K, D]");
+  const int K = (int)Cold.size(0), D = (int)Cold.size(1);
+  const int dt = pack.scalar_type() == at::kBFloat16 ? mk::DT_BF16 : mk::DT_F32;
+  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, K) == Kpad, "mikmeans: bad Kpad");
+  TORCH_CHECK(D <= dpad, "mikmeans: D > dpad");
+  check_cuda(pack, "pack");
+  TORCH_CHECK(pack.is_contiguous() && pack.numel() >= Kpad * dpad, "mikmeans: pack too small");
+  check_f32(cn, "cn", mk::assign_cn_len((int)Kpad));
+  if (mode != mk::FIN_PACK_ONLY) {
+    TORCH_CHECK(packed.has_value(), "mikmeans: finalize needs the packed message");
+    check_f64(*packed, "packed", (int64_t)K * D + K + 2);
+  }
+  if (mode == mk::FIN_MINIBATCH) {
+    TORCH_CHECK(mb_counts.has_value(), "mikmeans: minibatch finalize needs counts");
+    check_f64(*mb_counts, "mb_counts", K);
+  }
+  if (Cnew.has_value()) check_f32(*Cnew, "Cnew", (int64_t)K * D);
+  if (shift.has_value()) check_f32(*shift, "shift", K);
+  if (counts.has_value()) check_f32(*counts, "counts", K);
+  if (frozen.has_value())
+    TORCH_CHECK(frozen->is_cuda() && frozen->scalar_type() == at::kByte && frozen->numel() >= K,
+                "mikmeans: frozen must be uint8 [K]");
+  mk::FinalizeArgs a;
+  a.packed = opt_ptr<const double>(packed);
+  a.Cold = Cold.data_ptr<float>(); a.Cnew = opt_ptr<float>(Cnew); a.K = K; a.D = D;
+  a.frozen = opt_ptr<const uint8_t>(frozen);
+  a.mb_counts = opt_ptr<double>(mb_counts);
+  a.dtype = dt; a.dpad = (int)dpad; a.Kpad = (int)Kpad;
+  a.pack = pack.data_ptr(); a.cn = cn.data_ptr<float>();
+  a.shift = opt_ptr<float>(shift); a.counts_out = opt_ptr<float>(counts);
+  a.mode = (int)mode;
+  hip_check(mk::launch_finalize(a, stream()), "finalize");
+}
+
+void row_sqnorm(const Tensor& X, const Tensor& out) {
+  const int dt = dtype_of(X);
+  const int64_t ldx = check_points(X, dt);
+  check_f32(out, "out", X.size(0));
+  hip_check(mk::launch_row_sqnorm(dt, X.data_ptr(), X.size(0), (int)X.size(1), ldx,
+                                  out.data_ptr<float>(), stream()),
+            "row_sqnorm");
+}
+
+void kpp_d2(const Tensor& X, const Tensor& c, bool first, const Tensor& d2, const Tensor& block_sums,
+            int64_t rows_per_block) {
+  const int dt = dtype_of(X);
+  const int64_t ldx = check_points(X, dt);
+  const int64_t N = X.size(0);
+  check_f32(c, "c", X.size(1));
+  check_f32(d2, "d2", N);
+  const int64_t nb = (N + rows_per_block - 1) / rows_per_block;
+  check_f64(block_sums, "block_sums", nb);
+  hip_check(mk::launch_kpp_d2(dt, X.data_ptr(), N, (int)X.size(1), ldx, c.data_ptr<float>(),
+                              first ? 1 : 0, d2.data_ptr<float>(), block_sums.data_ptr<double>(),
+                              rows_per_block, (int)nb, stream()),
+            "kpp_d2");
+}
+
+void kpp_sample(const Tensor& block_sums, const Tensor& d2, int64_t rows_per_block,
+                const Tensor& target, const Tensor& X, const Tensor& crow,
+                const c10::optional<Tensor>& idx_out) {
+  const int dt = dtype_of(X);
+  const int64_t ldx = check_points(X, dt);
+  const int64_t N = X.size(0);
+  const int64_t nb = (N + rows_per_block - 1) / rows_per_block;
+  check_f64(block_sums, "block_sums", nb);
+  check_f32(d2, "d2", N);
+  check_f64(target, "target", 1);
+  check_f32(crow, "crow", X.size(1));
+  if (idx_out.has_value())
+    TORCH_CHECK(idx_out->is_cuda() && idx_out->scalar_type() == at::kLong, "idx_out must be int64");
+  TORCH_CHECK(N > 0, "mikmeans: kpp_sample on an empty shard");
+  hip_check(mk::launch_kpp_sample(dt, block_sums.data_ptr<double>(), (int)nb, d2.data_ptr<float>(),
+                                  N, rows_per_block, target.data_ptr<double>(), X.data_ptr(),
+                                  (int)X.size(1), ldx, crow.data_ptr<float>(),
+                                  opt_ptr<int64_t>(idx_out), stream()),
+            "kpp_sample");
+}
+
+void blob_centers(const Tensor& centers, double box, int64_t seed) {
+  check_f32(centers, "centers");
+  TORCH_CHECK(centers.dim() == 2, "centers must be [C, D]");
+  hip_check(mk::launch_blob_centers(centers.data_ptr<float>(), (int)centers.size(0),
+                                    (int)centers.size(1), (float)box, (uint64_t)seed, stream()),
+            "blob_centers");
+}
+
+void blobs(const Tensor& X, int64_t i0, const Tensor& centers, double stddev, int64_t seed,
+           const c10::optional<Tensor>& y) {
+  const int dt = dtype_of(X);
+  check_cuda(X, "X");
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "X must be 2-D with unit column stride");
+  check_f32(centers, "centers");
+  TORCH_CHECK(centers.dim() == 2 && centers.size(1) == X.size(1), "centers must be [C, D]");
+  if (y.has_value())
+    TORCH_CHECK(y->is_cuda() && y->scalar_type() == at::kInt && y->numel() >= X.size(0),
+                "y must be int32 [n]");
+  const int64_t ldx = X.size(0) <= 1 ? X.size(1) : X.stride(0);
+  hip_check(mk::launch_blobs(dt, X.data_ptr(), i0, X.size(0), (int)X.size(1), ldx,
+                             centers.data_ptr<float>(), (int)centers.size(0), (float)stddev,
+                             (uint64_t)seed, opt_ptr<int32_t>(y), stream()),
+            "blobs");
+}
+
+// ----------------------------------------------------------------------------
+// ECMAScript Number::toString (what JSON.stringify emits for a finite number),
+// from the shortest round-trip digits.  NaN/Infinity -> "null" as in JSON.
+void js_number(double v, std::string& out) {
+  if (std::isnan(v) || std::isinf(v)) { out += "null"; return; }
+  if (v == 0.0) { out += '0'; return; }
+  if (v < 0) { out += '-'; v = -v; }
+  char buf[64];
+  auto res = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::scientific);
+  // buf = d[.ddd]e(+|-)XX
+  std::string digits;
+  char* p = buf;
+  int e10 = 0;
+  for (; p < res.ptr && *p != 'e'; ++p)
+    if (*p != '.') digits += *p;
+  if (p < res.ptr) e10 = std::atoi(p + 1);
+  const int k = (int)digits.size();
+  const int n = e10 + 1;  // value = 0.digits * 10^n
+  if (k <= n && n <= 21) {
+    out += digits;
+    out.append(n - k, '0');
+  } else if (0 < n && n <= 21) {
+    out.append(digits, 0, n);
+    out += '.';
+    out.append(digits, n, std::string::npos);
+  } else if (-6 < n && n <= 0) {
+    out += "0.";
+    out.append(-n, '0');
+    out += digits;
+  } else {
+    out += digits[0];
+    if (k > 1) { out += '.'; out.append(digits, 1, std::string::npos); }
+    out += 'e';
+    const int ee = n - 1;
+    out += ee >= 0 ? '+' : '-';
+    out += std::to_string(ee >= 0 ? ee : -ee);
+  }
+}
+
+std::string js_format(double v) {
+  std::string s;
+  js_number(v, s);
+  return s;
+}
+
+// Flat JSON array of a CPU float32/float64 tensor, each value widened to f64
+// (what JSON.stringify(Array.from(Float32Array)) prints), no spaces.
+std::string js_array(const Tensor& t) {
+  TORCH_CHECK(!t.is_cuda(), "js_array expects a CPU tensor");
+  Tensor c = t.contiguous().view(-1);
+  std::string s;
+  s.reserve((size_t)c.numel() * 12 + 2);
+  s += '[';
+  const int64_t n = c.numel();
+  if (c.scalar_type() == at::kFloat) {
+    const float* p = c.data_ptr<float>();
+    for (int64_t i = 0; i < n; ++i) { if (i) s += ','; js_number((double)p[i], s); }
+  } else {
+    TORCH_CHECK(c.scalar_type() == at::kDouble, "js_array: float32 or float64 only");
+    const double* p = c.data_ptr<double>();
+    for (int64_t i = 0; i < n; ++i) { if (i) s += ','; js_number(p[i], s); }
+  }
+  s += ']';
+  return s;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "mikmeans native ops (gfx950 HIP kernels + host helpers)";
+  m.def("assign", &assign, "fused MFMA distance + argmin (K2)");
+  m.def("update", &update, "LDS-privatised per-cluster sums/counts (K3)");
+  m.def("reduce", &reduce, "slab reduction into the packed f64 all-reduce message");
+  m.def("finalize", &finalize, "new centroids, shift, fragment re-pack (K4)");
+  m.def("row_sqnorm", &row_sqnorm, "row squared norms (K1)");
+  m.def("kpp_d2", &kpp_d2, "k-means++ D^2 update (K5)");
+  m.def("kpp_sample", &kpp_sample, "k-means++ D^2 sampling (K6)");
+  m.def("blob_centers", &blob_centers, "Philox blob centres");
+  m.def("blobs", &blobs, "Philox Gaussian blobs (K8)");
+  m.def("assign_kpad", [](int64_t dt, int64_t dpad, int64_t K) { return mk::assign_kpad((int)dt, (int)dpad, (int)K); });
+  m.def("assign_chunk_tiles", [](int64_t dt, int64_t dpad) { return mk::assign_chunk_tiles((int)dt, (int)dpad); });
+  m.def("assign_cn_len", [](int64_t kpad) { return mk::assign_cn_len((int)kpad); });
+  m.def("update_slice_width", [](int64_t dt, int64_t K, int64_t D) { return mk::update_slice_width((int)dt, (int)K, (int)D); });
+  m.def("update_n_chunks", [](int64_t dt, int64_t K, int64_t D, int64_t N) { return mk::update_n_chunks((int)dt, (int)K, (int)D, N); });
+  m.def("js_format", &js_format, "ECMAScript Number::toString of a double");
+  m.def("js_array", &js_array, "JSON array of a CPU float tensor with JS number formatting");
+  m.attr("NSLOT") = mk::NSLOT;
+  m.attr("SLOT_STRIDE") = mk::SLOT_STRIDE;
+}

@@ -1,0 +1,116 @@
+// mikmeans — shared device helpers for the CDNA4 (gfx950 / MI355X) kernels.
+//
+// Everything here is written for 64-lane wavefronts, the 32x32 MFMA C/D layout
+// (col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)) and LDS-DMA
+// (`global_load_lds_dwordx4`).  No CUDA shims, no dual paths.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mk {
+
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int WAVE = 64;
+// Score given to padded (non-existent) centroids: finite so that the packed
+// argmin key stays a valid float, large enough never to win.
+constexpr float PAD_SCORE = 1.0e30f;
+
+#define MK_LDS __attribute__((address_space(3)))
+
+// ---------------------------------------------------------------------------
+// bf16 <-> f32 (raw uint16 storage; RNE rounding, NaN stays NaN)
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+__device__ __forceinline__ float bf16lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float round_bf16(float f) { return bf16_to_f32(f32_to_bf16(f)); }
+
+// ---------------------------------------------------------------------------
+// Element traits: storage type, elements per 16-byte piece.
+template <typename T> struct Elem;
+template <> struct Elem<uint16_t> {  // bf16
+  static constexpr int V = 8;
+  __device__ static float to_f32(uint16_t v) { return bf16_to_f32(v); }
+  __device__ static uint16_t from_f32(float f) { return f32_to_bf16(f); }
+};
+template <> struct Elem<float> {
+  static constexpr int V = 4;
+  __device__ static float to_f32(float v) { return v; }
+  __device__ static float from_f32(float f) { return f; }
+};
+
+// Unpack a 16-byte piece into f32 values.
+__device__ __forceinline__ void unpack16(const u32x4& w, float* o, uint16_t*) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { o[2 * i] = bf16lo(w[i]); o[2 * i + 1] = bf16hi(w[i]); }
+}
+__device__ __forceinline__ void unpack16(const u32x4& w, float* o, float*) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = __uint_as_float(w[i]);
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA: each lane copies 16 B from its own global address to
+// lds_base + lane*16 (lds_base must be wave-uniform).
+__device__ __forceinline__ void glds16(const void* gsrc, MK_LDS void* lds_base) {
+  __builtin_amdgcn_global_load_lds(gsrc, lds_base, 16, 0, 0);
+}
+
+// s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] | vmcnt_hi[15:14],
+// expcnt[6:4]=7, lgkmcnt[11:8]=15).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+
+// Raw workgroup barrier that does NOT drain outstanding LDS-DMA (unlike
+// __syncthreads, whose fence emits vmcnt(0)).  The asm statement is a compiler
+// memory barrier so LDS reads are not hoisted above it.
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// v_min3_f32 without the canonicalisation hipcc inserts around fminf.
+__device__ __forceinline__ float min3f(float a, float b, float c) {
+  float d;
+  asm volatile("v_min3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+// ---------------------------------------------------------------------------
+// 64-lane reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Row index of accumulator register `reg` for lane half `h` in the 32x32 MFMA C/D map.
+__device__ __forceinline__ int mfma32_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+}  // namespace mk

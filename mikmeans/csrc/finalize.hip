@@ -1,0 +1,140 @@
+// mikmeans — K4 finalize (new centroids, shift, re-pack for the next E-step)
+// and K1 row squared norms, for gfx950.
+//
+// finalize runs once per iteration on the all-reduced f64 message
+// [K*D sums | K counts | inertia | changed]: C_new = sums / counts (empty or
+// frozen centres keep their position -- the frozen mask is the reference's
+// "locked" centroid, app.mjs:128 / :360), shift_k = |C_new - C_old|^2, and it
+// writes the fragment-packed -2*C (bf16 or f32) plus |C_q|^2 that the assign
+// kernel streams (layout in kernels.h).  One workgroup per 32-centroid tile.
+#include "common.h"
+#include "kernels.h"
+
+namespace mk {
+
+template <typename T>
+__device__ __forceinline__ void store_pack(void* pack, int dpad, int k, int d, float v) {
+  constexpr int V = Elem<T>::V;
+  const int nq = dpad / (2 * V);
+  const int t = k >> 5, r = k & 31;
+  const int hh = d / (dpad / 2), e = d % (dpad / 2);
+  const int64_t off = ((int64_t)(t * nq + e / V) * 64 + r + 32 * hh) * V + e % V;
+  ((T*)pack)[off] = Elem<T>::from_f32(v);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
+  const int kk = threadIdx.x >> 3, part = threadIdx.x & 7;
+  const int k = blockIdx.x * 32 + kk;
+  const int64_t KD = (int64_t)a.K * a.D;
+  float shift = 0.f, cn = 0.f, cnt = 0.f;
+  if (k < a.K) {
+    double c = 0.0;
+    bool upd = false;
+    double scale = 0.0, keep = 1.0;
+    if (a.mode != FIN_PACK_ONLY) {
+      c = a.packed[KD + k];
+      cnt = (float)c;
+      const bool frozen = a.frozen && a.frozen[k];
+      if (a.mode == FIN_LLOYD) {
+        upd = (c > 0.0) && !frozen;
+        scale = upd ? 1.0 / c : 0.0;
+        keep = 0.0;
+      } else {  // FIN_MINIBATCH: running weighted mean (Sculley 2010, batch form)
+        upd = (c > 0.0) && !frozen;
+        if (upd) {
+          const double v_old = a.mb_counts[k];
+          const double v_new = v_old + c;
+          scale = 1.0 / v_new;
+          keep = v_old / v_new;
+        }
+      }
+    }
+    for (int d = part; d < a.D; d += 8) {
+      const float old = a.Cold[(int64_t)k * a.D + d];
+      float nv = old;
+      if (upd) nv = (float)(keep * (double)old + scale * a.packed[(int64_t)k * a.D + d]);
+      if (a.Cnew) a.Cnew[(int64_t)k * a.D + d] = nv;
+      const float diff = nv - old;
+      shift += diff * diff;
+      const float q = (a.dtype == DT_BF16) ? round_bf16(nv) : nv;
+      cn += q * q;
+      if (a.dtype == DT_BF16) store_pack<uint16_t>(a.pack, a.dpad, k, d, -2.f * q);
+      else store_pack<float>(a.pack, a.dpad, k, d, -2.f * q);
+    }
+    for (int d = a.D + part; d < a.dpad; d += 8) {
+      if (a.dtype == DT_BF16) store_pack<uint16_t>(a.pack, a.dpad, k, d, 0.f);
+      else store_pack<float>(a.pack, a.dpad, k, d, 0.f);
+    }
+    if (a.mode == FIN_MINIBATCH && upd && part == 0) a.mb_counts[k] += c;
+  } else if (k < a.Kpad) {
+    for (int d = part; d < a.dpad; d += 8) {
+      if (a.dtype == DT_BF16) store_pack<uint16_t>(a.pack, a.dpad, k, d, 0.f);
+      else store_pack<float>(a.pack, a.dpad, k, d, 0.f);
+    }
+  }
+  // reduce over the 8 threads of a centroid
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    shift += __shfl_xor(shift, o, 64);
+    cn += __shfl_xor(cn, o, 64);
+  }
+  if (part == 0 && k < a.Kpad) {
+    a.cn[k] = (k < a.K) ? cn : PAD_SCORE;
+    if (k < a.K) {
+      if (a.shift) a.shift[k] = shift;
+      if (a.counts_out) a.counts_out[k] = cnt;
+    }
+  }
+}
+
+hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
+  const unsigned nb = (unsigned)((a.Kpad + 31) / 32);
+  if (a.dtype == DT_BF16) hipLaunchKernelGGL(finalize_kernel<uint16_t>, dim3(nb), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(finalize_kernel<float>, dim3(nb), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K1: xn[i] = sum_d x[i,d]^2 (f32 accumulate).  16 lanes per row, 16-B loads.
+template <typename T>
+__global__ __launch_bounds__(256) void row_sqnorm_kernel(const T* __restrict__ X, int64_t N, int D,
+                                                         int64_t ldx, float* __restrict__ out) {
+  constexpr int V = Elem<T>::V;
+  const int sub = threadIdx.x & 15;
+  const int64_t stride = (int64_t)gridDim.x * 16;
+  for (int64_t i = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); i < N; i += stride) {
+    const T* row = X + i * ldx;
+    float acc = 0.f;
+    if ((D % V) == 0) {
+      for (int c = sub * V; c < D; c += 16 * V) {
+        const u32x4 w = *(const u32x4*)(row + c);
+        float f[V];
+        unpack16(w, f, (T*)nullptr);
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc += f[e] * f[e];
+      }
+    } else {
+      for (int c = sub; c < D; c += 16) { const float f = Elem<T>::to_f32(row[c]); acc += f * f; }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (sub == 0) out[i] = acc;
+  }
+}
+
+hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t ldx, float* out,
+                             hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  int64_t nb = (N + 15) / 16;
+  if (nb > 8192) nb = 8192;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(row_sqnorm_kernel<uint16_t>, dim3((unsigned)nb), dim3(256), 0, s,
+                       (const uint16_t*)X, N, D, ldx, out);
+  else
+    hipLaunchKernelGGL(row_sqnorm_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s,
+                       (const float*)X, N, D, ldx, out);
+  return hipGetLastError();
+}
+
+}  // namespace mk

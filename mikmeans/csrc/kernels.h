@@ -1,0 +1,97 @@
+// mikmeans — host-side launcher declarations for the gfx950 kernels.
+//
+// Every launcher is stream-ordered (takes the hipStream_t it must launch on),
+// allocates nothing and never synchronises, so a caller may capture a whole
+// Lloyd iteration into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mk {
+
+enum DType : int { DT_F32 = 0, DT_BF16 = 1 };
+
+// Number of f64 accumulation slots the assign kernel spreads its per-workgroup
+// inertia / changed-label partials over (slot = blockIdx % NSLOT, 8 doubles each).
+constexpr int NSLOT = 256;
+constexpr int SLOT_STRIDE = 8;
+
+// ---- centroid packing -------------------------------------------------------
+// The assign kernel reads centroids from a "fragment-packed" array: for tile
+// t (32 centroids) and 16-byte piece q, the 64 lanes' MFMA A-operand fragments
+// are stored contiguously (1 KiB), so one LDS-DMA wave-instruction stages a
+// piece and one ds_read_b128 per lane fetches it conflict-free.
+//   element (k, d): t = k/32, r = k%32, h = d / (DPAD/2), e = d % (DPAD/2)
+//   offset = ((t*NQ + e/V)*64 + r + 32*h)*V + e%V,  V = 16/sizeof(T), NQ = DPAD/(2V)
+// The stored value is -2*c (exact in bf16/f32) and cn[k] = |c_q|^2 of the
+// quantised centroid, so the MFMA chain seeded with cn directly yields
+// score = |c|^2 - 2 x.c  (= |x-c|^2 - |x|^2).
+int assign_chunk_tiles(int dtype, int dpad);  // centroid tiles per LDS chunk (CT)
+int assign_kpad(int dtype, int dpad, int K);  // K rounded up to a multiple of 32*CT
+int assign_cn_len(int kpad);                  // cn array length (multiple of 256 floats)
+
+struct AssignArgs {
+  const void* X; int64_t N; int D; int64_t ldx;
+  const void* Cpack; const float* cn; int Kpad;
+  const float* xn;      // optional: |x|^2 per row, needed for mind/inertia
+  int32_t* labels;      // in/out (old labels read when track_changed)
+  float* mind;          // optional: squared distance to the chosen centroid
+  double* slots;        // optional: [NSLOT][SLOT_STRIDE] (+inertia, +changed)
+  int track_changed;
+};
+hipError_t launch_assign(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
+
+// ---- update (LDS-privatised scatter-add) -------------------------------------
+struct UpdateArgs {
+  const void* X; int64_t N; int D; int64_t ldx;
+  const int32_t* labels; int K;
+  int n_chunks;          // multiple of 8
+  float* slab;           // [n_chunks][K][D] partial sums
+  float* cnt_slab;       // [n_chunks][K] partial counts
+  const float* weights;  // optional per-row weights (sample_weight)
+};
+int update_slice_width(int dtype, int K, int D);  // columns per workgroup (0 = unsupported)
+int update_n_chunks(int dtype, int K, int D, int64_t N);
+hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s);
+
+// Reduce slabs (+ assign slots) into the packed f64 message
+// [K*D sums | K counts | inertia | n_changed] (length K*D + K + 2).
+hipError_t launch_reduce(const float* slab, const float* cnt_slab, int n_chunks, int K, int D,
+                         double* slots, double* packed, hipStream_t s);
+
+// ---- finalize (new centroids + shift + re-pack) -------------------------------
+enum FinalizeMode : int { FIN_PACK_ONLY = 0, FIN_LLOYD = 1, FIN_MINIBATCH = 2 };
+struct FinalizeArgs {
+  const double* packed;   // may be null for FIN_PACK_ONLY
+  const float* Cold; float* Cnew; int K; int D;
+  const uint8_t* frozen;  // optional
+  double* mb_counts;      // FIN_MINIBATCH running per-centre counts
+  int dtype; int dpad; int Kpad;
+  void* pack; float* cn;
+  float* shift;           // optional [K]
+  float* counts_out;      // optional [K]
+  int mode;
+};
+hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
+
+// ---- row squared norms -------------------------------------------------------
+hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t ldx, float* out,
+                             hipStream_t s);
+
+// ---- k-means++ ---------------------------------------------------------------
+hipError_t launch_kpp_d2(int dtype, const void* X, int64_t N, int D, int64_t ldx, const float* c,
+                         int first, float* d2, double* block_sums, int64_t rows_per_block,
+                         int nblocks, hipStream_t s);
+// target: device double (rank-local); if < 0 writes zeros to crow.
+hipError_t launch_kpp_sample(int dtype, const double* block_sums, int nblocks, const float* d2,
+                             int64_t N, int64_t rows_per_block, const double* target, const void* X,
+                             int D, int64_t ldx, float* crow, int64_t* idx_out, hipStream_t s);
+
+// ---- synthetic Gaussian blobs (counter-based Philox, deterministic by index) --
+hipError_t launch_blob_centers(float* centers, int n_centers, int D, float box, uint64_t seed,
+                               hipStream_t s);
+hipError_t launch_blobs(int dtype, void* X, int64_t i0, int64_t n, int D, int64_t ldx,
+                        const float* centers, int n_centers, float stddev, uint64_t seed,
+                        int32_t* y, hipStream_t s);
+
+}  // namespace mk

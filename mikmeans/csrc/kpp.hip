@@ -1,0 +1,293 @@
+// mikmeans — K5/K6 k-means++ seeding and K8 on-device Gaussian blobs (gfx950).
+//
+// k-means++ (Arthur & Vassilvitskii 2007) is K-1 dependent passes.  Each pass:
+//   K5 kpp_d2     d2[i] = min(d2[i], |x_i - c_new|^2) over fixed row blocks, plus an
+//                 f64 partial sum per block (memory-bound streaming pass).
+//   K6 kpp_sample one workgroup turns u*sum(d2) into an index with two
+//                 prefix-sum searches (blocks, then rows) and copies the chosen
+//                 row into C[k].  No host synchronisation anywhere, so all K-1
+//                 steps are enqueued back to back (and capturable in a hipGraph).
+// Multi-GPU: each rank's block sums are all-gathered and the
+// rank-local target is computed on device; the owner contributes the row to an
+// all-reduce (C4).
+//
+// K8 blobs: counter-based Philox4x32-10, so point i of a dataset is a pure
+// function of (seed, i) -- every rank generates exactly its global row range and
+// the dataset is identical for any world size.
+#include "common.h"
+#include "kernels.h"
+
+namespace mk {
+
+constexpr int KPP_NT = 256;
+
+template <typename T>
+__global__ __launch_bounds__(KPP_NT) void kpp_d2_kernel(const T* __restrict__ X, int64_t N, int D,
+                                                        int64_t ldx, const float* __restrict__ c,
+                                                        int first, float* __restrict__ d2,
+                                                        double* __restrict__ block_sums,
+                                                        int64_t rows_per_block) {
+  constexpr int V = Elem<T>::V;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* cs = (float*)smem;
+  for (int d = threadIdx.x; d < D; d += KPP_NT) cs[d] = c[d];
+  __syncthreads();
+  const int sub = threadIdx.x & 15;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  int64_t r1 = r0 + rows_per_block;
+  if (r1 > N) r1 = N;
+  double part = 0.0;
+  for (int64_t i = r0 + (threadIdx.x >> 4); i < r1; i += KPP_NT / 16) {
+    const T* row = X + i * ldx;
+    float acc = 0.f;
+    for (int cc = sub * V; cc < D; cc += 16 * V) {
+      const u32x4 w = *(const u32x4*)(row + cc);
+      float f[V];
+      unpack16(w, f, (T*)nullptr);
+#pragma unroll
+      for (int e = 0; e < V; ++e) { const float df = f[e] - cs[cc + e]; acc += df * df; }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (sub == 0) {
+      const float v = first ? acc : fminf(acc, d2[i]);
+      d2[i] = v;
+      part += v;
+    }
+  }
+  part = wave_sum(part);
+  __shared__ double red[KPP_NT / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = part;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0;
+    for (int w = 0; w < KPP_NT / 64; ++w) s += red[w];
+    block_sums[blockIdx.x] = s;
+  }
+}
+
+hipError_t launch_kpp_d2(int dtype, const void* X, int64_t N, int D, int64_t ldx, const float* c,
+                         int first, float* d2, double* block_sums, int64_t rows_per_block,
+                         int nblocks, hipStream_t s) {
+  const size_t lds = ((size_t)D * 4 + 15) / 16 * 16;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(kpp_d2_kernel<uint16_t>, dim3(nblocks), dim3(KPP_NT), lds, s,
+                       (const uint16_t*)X, N, D, ldx, c, first, d2, block_sums, rows_per_block);
+  else
+    hipLaunchKernelGGL(kpp_d2_kernel<float>, dim3(nblocks), dim3(KPP_NT), lds, s, (const float*)X,
+                       N, D, ldx, c, first, d2, block_sums, rows_per_block);
+  return hipGetLastError();
+}
+
+// Block-wide inclusive scan (1024 threads) of one double per thread.
+__device__ double block_scan_incl(double v, double* sh) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const double add = (t >= o) ? sh[t - o] : 0.0;
+    __syncthreads();
+    sh[t] += add;
+    __syncthreads();
+  }
+  return sh[t];
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void kpp_sample_kernel(const double* __restrict__ block_sums,
+                                                          int nblocks, const float* __restrict__ d2,
+                                                          int64_t N, int64_t rpb,
+                                                          const double* __restrict__ target_p,
+                                                          const T* __restrict__ X, int D,
+                                                          int64_t ldx, float* __restrict__ crow,
+                                                          int64_t* __restrict__ idx_out) {
+  __shared__ double sh[1024];
+  __shared__ int64_t sel;
+  __shared__ double base_sh;
+  const int t = threadIdx.x;
+  double target = *target_p;
+  if (!(target >= 0.0)) {  // not the owner rank (or NaN): contribute zeros
+    for (int d = t; d < D; d += 1024) crow[d] = 0.f;
+    if (t == 0 && idx_out) *idx_out = -1;
+    return;
+  }
+  // --- stage 1: which block
+  const int per = (nblocks + 1023) / 1024;
+  double segsum = 0.0;
+  for (int b = t * per; b < (t + 1) * per && b < nblocks; ++b) segsum += block_sums[b];
+  double incl = block_scan_incl(segsum, sh);
+  const double total = sh[1023];
+  if (target >= total) target = total * (1.0 - 1e-12);
+  if (t == 0) { sel = -1; base_sh = 0.0; }
+  __syncthreads();
+  {
+    const double excl = incl - segsum;
+    if (segsum > 0.0 && target >= excl && target < incl) {
+      double run = excl;
+      int64_t bsel = -1;
+      for (int b = t * per; b < (t + 1) * per && b < nblocks; ++b) {
+        const double bs = block_sums[b];
+        if (bs > 0.0 && target < run + bs) { bsel = b; break; }
+        run += bs;
+      }
+      if (bsel < 0) {  // rounding: last non-empty block of this segment
+        for (int b = (t + 1) * per - 1; b >= t * per; --b)
+          if (b < nblocks && block_sums[b] > 0.0) { bsel = b; break; }
+        run = excl;
+        for (int b = t * per; b < bsel; ++b) run += block_sums[b];
+      }
+      sel = bsel;
+      base_sh = run;
+    }
+  }
+  __syncthreads();
+  int64_t b = sel;
+  if (b < 0) {  // all-zero potential (duplicates): pick the last non-empty block, else row 0
+    if (t == 0) {
+      int64_t bb = -1;
+      for (int i = nblocks - 1; i >= 0; --i) if (block_sums[i] > 0.0) { bb = i; break; }
+      sel = bb;
+      base_sh = 0.0;
+      if (bb >= 0) for (int i = 0; i < bb; ++i) base_sh += block_sums[i];
+    }
+    __syncthreads();
+    b = sel;
+  }
+  int64_t chosen = 0;
+  if (b >= 0) {
+    // --- stage 2: which row inside block b
+    const double tb = target - base_sh;
+    const int64_t r0 = b * rpb;
+    int64_t r1 = r0 + rpb;
+    if (r1 > N) r1 = N;
+    const int64_t len = r1 - r0;
+    const int64_t per2 = (len + 1023) / 1024;
+    double s2 = 0.0;
+    const int64_t a0 = r0 + t * per2;
+    for (int64_t i = a0; i < a0 + per2 && i < r1; ++i) s2 += (double)d2[i];
+    const double inc2 = block_scan_incl(s2, sh);
+    __syncthreads();
+    if (t == 0) sel = -1;
+    __syncthreads();
+    const double ex2 = inc2 - s2;
+    if (s2 > 0.0 && tb >= ex2 && tb < inc2) {
+      double run = ex2;
+      int64_t isel = -1;
+      for (int64_t i = a0; i < a0 + per2 && i < r1; ++i) {
+        const double v = (double)d2[i];
+        if (v > 0.0 && tb < run + v) { isel = i; break; }
+        run += v;
+      }
+      if (isel < 0)
+        for (int64_t i = (a0 + per2 < r1 ? a0 + per2 : r1) - 1; i >= a0; --i)
+          if (d2[i] > 0.f) { isel = i; break; }
+      sel = isel;
+    }
+    __syncthreads();
+    if (sel < 0 && t == 0) {  // target beyond the block's float sum: last positive row
+      for (int64_t i = r1 - 1; i >= r0; --i) if (d2[i] > 0.f) { sel = i; break; }
+      if (sel < 0) sel = r0;
+    }
+    __syncthreads();
+    chosen = sel;
+  }
+  const T* row = X + chosen * ldx;
+  for (int d = t; d < D; d += 1024) crow[d] = Elem<T>::to_f32(row[d]);
+  if (t == 0 && idx_out) *idx_out = chosen;
+}
+
+hipError_t launch_kpp_sample(int dtype, const double* block_sums, int nblocks, const float* d2,
+                             int64_t N, int64_t rows_per_block, const double* target, const void* X,
+                             int D, int64_t ldx, float* crow, int64_t* idx_out, hipStream_t s) {
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(kpp_sample_kernel<uint16_t>, dim3(1), dim3(1024), 0, s, block_sums, nblocks,
+                       d2, N, rows_per_block, target, (const uint16_t*)X, D, ldx, crow, idx_out);
+  else
+    hipLaunchKernelGGL(kpp_sample_kernel<float>, dim3(1), dim3(1024), 0, s, block_sums, nblocks,
+                       d2, N, rows_per_block, target, (const float*)X, D, ldx, crow, idx_out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11)
+struct U4 { uint32_t x, y, z, w; };
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+__device__ __forceinline__ float u01_open0(uint32_t v) { return ((v >> 8) + 1) * (1.0f / 16777216.0f); }
+__device__ __forceinline__ float u01(uint32_t v) { return (v >> 8) * (1.0f / 16777216.0f); }
+
+constexpr uint32_t TAG_CID = 0xC1D0u, TAG_CTR = 0xCE27u, TAG_NRM = 0x4E52u;
+
+__global__ void blob_centers_kernel(float* centers, int n_centers, int D, float box, uint32_t k0,
+                                    uint32_t k1) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)n_centers * D) return;
+  const int c = (int)(e / D), d = (int)(e % D);
+  const U4 r = philox(U4{(uint32_t)c, (uint32_t)(d >> 2), TAG_CTR, 0u}, k0, k1);
+  const uint32_t v = (d & 3) == 0 ? r.x : (d & 3) == 1 ? r.y : (d & 3) == 2 ? r.z : r.w;
+  centers[e] = box * (2.f * u01(v) - 1.f);
+}
+
+hipError_t launch_blob_centers(float* centers, int n_centers, int D, float box, uint64_t seed,
+                               hipStream_t s) {
+  const int64_t tot = (int64_t)n_centers * D;
+  hipLaunchKernelGGL(blob_centers_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
+                     centers, n_centers, D, box, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return hipGetLastError();
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void blobs_kernel(T* X, int64_t i0, int64_t n, int D, int64_t ldx,
+                                                    const float* __restrict__ centers,
+                                                    int n_centers, float stddev, uint32_t k0,
+                                                    uint32_t k1, int32_t* y) {
+  const int G = (D + 3) / 4;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * G) return;
+  const int64_t il = e / G;
+  const int g = (int)(e % G);
+  const uint64_t gi = (uint64_t)(i0 + il);
+  const U4 rc = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), TAG_CID, 0u}, k0, k1);
+  const int cid = (int)__umulhi(rc.x, (uint32_t)n_centers);
+  if (y && g == 0) y[il] = cid;
+  const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
+  const float rad0 = sqrtf(-2.f * logf(u01_open0(r.x)));
+  const float rad1 = sqrtf(-2.f * logf(u01_open0(r.z)));
+  float s0, c0, s1, c1;
+  sincospif(2.f * u01(r.y), &s0, &c0);
+  sincospif(2.f * u01(r.w), &s1, &c1);
+  const float z[4] = {rad0 * c0, rad0 * s0, rad1 * c1, rad1 * s1};
+  const float* mu = centers + (int64_t)cid * D;
+  T* out = X + il * ldx;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int d = 4 * g + j;
+    if (d < D) out[d] = Elem<T>::from_f32(mu[d] + stddev * z[j]);
+  }
+}
+
+hipError_t launch_blobs(int dtype, void* X, int64_t i0, int64_t n, int D, int64_t ldx,
+                        const float* centers, int n_centers, float stddev, uint64_t seed,
+                        int32_t* y, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t tot = n * ((D + 3) / 4);
+  const unsigned nb = (unsigned)((tot + 255) / 256);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(blobs_kernel<uint16_t>, dim3(nb), dim3(256), 0, s, (uint16_t*)X, i0, n, D,
+                       ldx, centers, n_centers, stddev, (uint32_t)seed, (uint32_t)(seed >> 32), y);
+  else
+    hipLaunchKernelGGL(blobs_kernel<float>, dim3(nb), dim3(256), 0, s, (float*)X, i0, n, D, ldx,
+                       centers, n_centers, stddev, (uint32_t)seed, (uint32_t)(seed >> 32), y);
+  return hipGetLastError();
+}
+
+}  // namespace mk

@@ -1,0 +1,204 @@
+"""Centroid initialisation: uniform random rows, k-means++ (D^2 sampling), or user array.
+
+All schemes are defined on the *global* dataset and give the same centres for any
+world size given the same seed:
+
+* ``random``: K distinct global row indices by Floyd's algorithm (O(K), no
+  permutation of N), each owner rank contributes its rows to a SUM all-reduce.
+* ``k-means++``: Arthur & Vassilvitskii (2007).  The first centre is a uniform
+  global row; each next centre is drawn with probability proportional to
+  D^2(x) = min_j |x - c_j|^2.  On GPU the D^2 update (K5) and the sampling (K6)
+  are HIP kernels and the K-1 steps run without any host synchronisation; the
+  per-rank potential totals are all-gathered (C3) and the owner of the drawn row
+  contributes it to an all-reduce (C4).
+* ``greedy k-means++`` (``n_local_trials > 1``, sklearn's default 2+log K): each
+  step draws several candidates and keeps the one with the lowest potential.
+
+Reference parity: the reference seeds one fixed card (``JESSICA``,
+app.mjs:188-196) and leaves centroid placement to humans (addCentroid,
+app.mjs:126-129); here seeding is algorithmic and reproducible by seed.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..ops import native
+from ..parallel.comm import Comm
+
+
+def floyd_sample(n: int, k: int, rng: np.random.Generator) -> np.ndarray:
+    """k distinct integers from [0, n) in draw order (Floyd's algorithm)."""
+    if k > n:
+        raise ValueError(f"cannot draw {k} distinct rows from {n}")
+    chosen: dict[int, None] = {}
+    for j in range(n - k, n):
+        t = int(rng.integers(0, j + 1))
+        chosen[t if t not in chosen else j] = None
+    out = np.fromiter(chosen.keys(), dtype=np.int64, count=k)
+    rng.shuffle(out)
+    return out
+
+
+def gather_rows(X: torch.Tensor, D: int, global_idx: np.ndarray, start: int, comm: Comm) -> torch.Tensor:
+    """Rows ``global_idx`` of the sharded dataset, replicated on every rank (f32 [k, D])."""
+    k = len(global_idx)
+    out = torch.zeros((k, D), dtype=torch.float64, device=X.device)
+    n = X.shape[0]
+    loc = global_idx - start
+    mine = np.nonzero((loc >= 0) & (loc < n))[0]
+    if len(mine):
+        li = torch.as_tensor(loc[mine], device=X.device)
+        out[torch.as_tensor(mine, device=X.device)] = X[li][:, :D].to(torch.float64)
+    comm.allreduce_(out)
+    return out.to(torch.float32)
+
+
+def init_random(X, D, K, n_global, start, comm: Comm, seed: int) -> torch.Tensor:
+    rng = np.random.default_rng(seed)
+    idx = floyd_sample(n_global, K, rng)
+    return gather_rows(X, D, idx, start, comm)
+
+
+def init_kmeanspp(X: torch.Tensor, D: int, K: int, n_global: int, start: int, comm: Comm, seed: int,
+                  n_local_trials: int = 1, xn: torch.Tensor | None = None) -> torch.Tensor:
+    """k-means++ seeding; returns replicated f32 centres [K, D].
+
+    ``X`` may be column-padded (only the first ``D`` columns are real).
+    """
+    rng = np.random.default_rng(seed)
+    first = int(rng.integers(0, n_global))
+    centers = torch.zeros((K, X.shape[1]), dtype=torch.float32, device=X.device)
+    centers[0, :D] = gather_rows(X, D, np.array([first]), start, comm)[0]
+    if K == 1:
+        return centers[:, :D].contiguous()
+    L = max(1, int(n_local_trials))
+    # every random number up front: the GPU loop then never waits for the host
+    u = torch.as_tensor(rng.random((K - 1) * L), dtype=torch.float64)
+    if X.is_cuda:
+        _kpp_gpu(X, centers, K, comm, u.to(X.device), L)
+    else:
+        _kpp_cpu(X, centers, K, comm, u, L)
+    return centers[:, :D].contiguous()
+
+
+def _local_target(totals_all: torch.Tensor, u: torch.Tensor, rank: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """Given per-rank potentials [W] and u in [0,1): (rank-local target or -1, global total)."""
+    total = totals_all.sum()
+    target = u * total
+    cum = torch.cumsum(totals_all, 0)
+    before = cum[rank] - totals_all[rank]
+    local = target - before
+    owner = (local >= 0) & (local < totals_all[rank])
+    # fp edge: a target past the last rank's cumulative sum belongs to the last non-empty rank
+    nz = torch.nonzero(totals_all > 0).flatten()
+    last = nz[-1] if nz.numel() else torch.tensor(totals_all.numel() - 1, device=totals_all.device)
+    edge = (target >= cum[-1]) & (last == rank)
+    owner = owner | edge
+    local = torch.where(edge, totals_all[rank] * (1 - 1e-12), local)
+    return torch.where(owner, local, torch.full_like(local, -1.0)), total
+
+
+def _kpp_gpu(X, centers, K, comm: Comm, u, L):
+    C = native.require()
+    n = X.shape[0]
+    dev = X.device
+    D = X.shape[1]
+    rpb = max(256, -(-n // 2048)) if n else 256
+    nb = max(1, -(-n // rpb))
+    d2 = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+    bs = torch.zeros(nb, dtype=torch.float64, device=dev)
+    d2c = torch.empty_like(d2) if L > 1 else None
+    bsc = torch.zeros_like(bs) if L > 1 else None
+    crow = torch.empty(D, dtype=torch.float32, device=dev)
+    cand = torch.empty((L, D), dtype=torch.float32, device=dev)
+    if n:
+        C.kpp_d2(X, centers[0], True, d2, bs, rpb)
+    for k in range(1, K):
+        for t in range(L):
+            tot = bs.sum().reshape(1) if n else torch.zeros(1, dtype=torch.float64, device=dev)
+            allt = comm.all_gather(tot).reshape(-1)
+            target, _ = _local_target(allt, u[(k - 1) * L + t], comm.rank)
+            if n:
+                C.kpp_sample(bs, d2, rpb, target.reshape(1).contiguous(), X, crow, None)
+            else:
+                crow.zero_()
+            comm.allreduce_(crow)
+            cand[t] = crow
+        if L == 1:
+            centers[k] = cand[0]
+            if n:
+                C.kpp_d2(X, centers[k], False, d2, bs, rpb)
+            continue
+        # greedy: potential of each candidate, keep the best (ties -> first)
+        pots = torch.zeros(L, dtype=torch.float64, device=dev)
+        for t in range(L):
+            if n:
+                d2c.copy_(d2)
+                C.kpp_d2(X, cand[t], False, d2c, bsc, rpb)
+                pots[t] = bsc.sum()
+        comm.allreduce_(pots)
+        best = torch.argmin(pots)
+        centers[k] = cand[best]
+        if n:
+            C.kpp_d2(X, centers[k], False, d2, bs, rpb)
+
+
+def _kpp_cpu(X, centers, K, comm: Comm, u, L):
+    n = X.shape[0]
+    Xf = X.to(torch.float32)
+    D = X.shape[1]
+
+    def dist_to(c):
+        return ((Xf - c[None, :]) ** 2).sum(1)
+
+    d2 = dist_to(centers[0]) if n else torch.zeros(0)
+    for k in range(1, K):
+        cand = torch.zeros((L, D), dtype=torch.float32)
+        for t in range(L):
+            tot = d2.double().sum().reshape(1)
+            allt = comm.all_gather(tot).reshape(-1)
+            target, _ = _local_target(allt, u[(k - 1) * L + t], comm.rank)
+            row = torch.zeros(D, dtype=torch.float32)
+            tv = float(target.item())
+            if tv >= 0 and n:
+                cs = torch.cumsum(d2.double(), 0)
+                i = int(torch.searchsorted(cs, torch.tensor([tv], dtype=torch.float64), right=True).item())
+                if i >= n or d2[min(i, n - 1)] <= 0:
+                    pos = torch.nonzero(d2 > 0).flatten()
+                    i = int(pos[-1].item()) if pos.numel() else 0
+                row = Xf[i].clone()
+            comm.allreduce_(row)
+            cand[t] = row
+        if L == 1:
+            centers[k] = cand[0]
+        else:
+            pots = torch.tensor([float(torch.minimum(d2, dist_to(cand[t])).double().sum()) for t in range(L)],
+                                dtype=torch.float64)
+            comm.allreduce_(pots)
+            centers[k] = cand[int(torch.argmin(pots))]
+        if n:
+            d2 = torch.minimum(d2, dist_to(centers[k]))
+
+
+def default_local_trials(K: int) -> int:
+    return 2 + int(math.log(K)) if K > 1 else 1
+
+
+def resolve_init(init, X, D, K, n_global, start, comm: Comm, seed: int, n_local_trials=None):
+    if isinstance(init, str):
+        name = init.lower().replace("_", "-")
+        if name == "random":
+            return init_random(X, D, K, n_global, start, comm, seed)
+        if name in ("k-means++", "kmeans++", "kpp"):
+            return init_kmeanspp(X, D, K, n_global, start, comm, seed, n_local_trials or 1)
+        if name in ("greedy-k-means++", "greedy-kmeans++"):
+            return init_kmeanspp(X, D, K, n_global, start, comm, seed,
+                                 n_local_trials or default_local_trials(K))
+        raise ValueError(f"unknown init {init!r}")
+    c = torch.as_tensor(np.asarray(init) if not torch.is_tensor(init) else init, dtype=torch.float32)
+    if c.shape != (K, D):
+        raise ValueError(f"init array must be [{K}, {D}], got {tuple(c.shape)}")
+    return c.to(X.device)

@@ -1,0 +1,132 @@
+"""Mini-batch k-means (Sculley 2010) for datasets that do not fit in HBM.
+
+BASELINE config 5 (N=1e9, D=256, K=512) is 512 GB of bf16: more than one
+MI355X's 288 GB.  Each step takes a batch (a tensor slice, a random sample, or a
+device-generated :class:`~mikmeans.data.blobs.BlobStream` batch), runs the same
+K2 assign and K3 update kernels as Lloyd, all-reduces the per-batch sums/counts
+(C5), and applies the per-centre running-mean update in the K4 finalize kernel:
+
+    v_k <- v_k + b_k ;  c_k <- c_k + (s_k - b_k c_k) / v_k
+
+where b_k / s_k are the batch count / sum of centre k and v_k the running count.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import cpu as cpu_ops
+from ..ops import native, pad_columns
+from ..parallel.comm import Comm
+
+
+class MiniBatchEngine:
+    def __init__(self, n_clusters: int, D: int, batch_size: int, *, dtype=torch.float32,
+                 device="cpu", comm: Comm | None = None, frozen=None):
+        self.comm = comm or Comm.local(device)
+        self.K, self.D = int(n_clusters), int(D)
+        self.device = torch.device(device)
+        self.gpu = self.device.type == "cuda"
+        self.dtype = dtype
+        v = native.vec_elems(dtype)
+        self.Dp = (self.D + v - 1) // v * v if self.gpu else self.D
+        self.batch = int(batch_size)
+        self.C = torch.zeros((self.K, self.Dp), dtype=torch.float32, device=self.device)
+        self.Cnew = torch.zeros_like(self.C)
+        self.vcount = torch.zeros(self.K, dtype=torch.float64, device=self.device)
+        self.shift = torch.zeros(self.K, dtype=torch.float32, device=self.device)
+        self.counts = torch.zeros(self.K, dtype=torch.float32, device=self.device)
+        self.packed = torch.zeros(self.K * self.Dp + self.K + 2, dtype=torch.float64, device=self.device)
+        self.frozen = None
+        if frozen is not None:
+            self.frozen = torch.as_tensor(frozen, dtype=torch.uint8).reshape(-1).to(self.device)
+        self.steps = 0
+        self.batch_inertia = 0.0
+        if self.gpu:
+            C = native.require()
+            self._C = C
+            self.dt = native.dtype_code(dtype)
+            self.dpad = native.dpad_for(self.Dp, dtype)
+            if self.dpad == 0:
+                raise NotImplementedError("mikmeans: GPU mini-batch supports D <= 256")
+            self.Kpad = C.assign_kpad(self.dt, self.dpad, self.K)
+            dev = self.device
+            self.pack = torch.zeros(self.Kpad * self.dpad, dtype=dtype, device=dev)
+            self.cn = torch.zeros(C.assign_cn_len(self.Kpad), dtype=torch.float32, device=dev)
+            self.slots = torch.zeros(C.NSLOT * C.SLOT_STRIDE, dtype=torch.float64, device=dev)
+            self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, self.batch)
+            self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.float32, device=dev)
+            self.cnt_slab = torch.empty(self.n_chunks * self.K, dtype=torch.float32, device=dev)
+            self.labels = torch.empty(self.batch, dtype=torch.int32, device=dev)
+            self.xn = torch.empty(self.batch, dtype=torch.float32, device=dev)
+
+    def set_centers(self, centers: torch.Tensor, counts=None):
+        self.C.zero_()
+        self.C[:, : self.D] = centers.to(device=self.device, dtype=torch.float32)
+        self.vcount.zero_()
+        if counts is not None:
+            self.vcount.copy_(torch.as_tensor(counts, dtype=torch.float64))
+        if self.gpu:
+            self._C.finalize(0, None, self.C, None, None, None, self.pack, self.cn, None, None,
+                             self.dpad, self.Kpad)
+
+    @property
+    def centers(self):
+        return self.C[:, : self.D]
+
+    def partial_fit(self, Xb: torch.Tensor):
+        """One mini-batch step on this rank's batch ``Xb`` (may be empty)."""
+        if self.gpu:
+            self._step_gpu(Xb)
+        else:
+            self._step_cpu(Xb)
+        self.C, self.Cnew = self.Cnew, self.C
+        self.steps += 1
+
+    def _step_gpu(self, Xb):
+        C = self._C
+        Xb = pad_columns(Xb.to(self.device), self.dtype)
+        b = Xb.shape[0]
+        if b > self.batch:
+            raise ValueError(f"batch of {b} rows exceeds the engine's batch_size {self.batch}")
+        if b:
+            xn, lab = self.xn[:b], self.labels[:b]
+            C.row_sqnorm(Xb, xn)
+            C.assign(Xb, self.pack, self.cn, xn, lab, None, self.slots, self.Kpad, self.dpad, False)
+            C.update(Xb, lab, self.K, self.slab, self.cnt_slab, self.n_chunks, None)
+            C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed)
+        else:
+            self.packed.zero_()
+        self.comm.allreduce_(self.packed)
+        C.finalize(2, self.packed, self.C, self.Cnew, self.frozen, self.vcount, self.pack, self.cn,
+                   self.shift, self.counts, self.dpad, self.Kpad)
+
+    def _step_cpu(self, Xb):
+        K, Dp = self.K, self.Dp
+        KD = K * Dp
+        Xb = Xb.to(self.device)
+        if Xb.shape[0]:
+            lab, mind = cpu_ops.assign(Xb, self.C)
+            sums, counts = cpu_ops.cluster_sums(Xb, lab, K)
+            self.packed[:KD] = sums.reshape(-1)
+            self.packed[KD : KD + K] = counts
+            self.packed[KD + K] = mind.double().sum()
+            self.packed[KD + K + 1] = 0
+        else:
+            self.packed.zero_()
+        self.comm.allreduce_(self.packed)
+        s = self.packed[:KD].view(K, Dp)
+        b = self.packed[KD : KD + K]
+        upd = b > 0
+        if self.frozen is not None:
+            upd &= self.frozen == 0
+        vnew = self.vcount + b
+        new = torch.where(upd[:, None],
+                          ((self.vcount / vnew.clamp_min(1e-300))[:, None] * self.C.double()
+                           + s / vnew.clamp_min(1e-300)[:, None]).to(torch.float32), self.C)
+        self.vcount = torch.where(upd, vnew, self.vcount)
+        self.Cnew.copy_(new)
+        self.shift.copy_(((new - self.C) ** 2).sum(1))
+        self.counts.copy_(b.to(torch.float32))
+
+    def last_batch_inertia(self) -> float:
+        return float(self.packed[self.K * self.Dp + self.K].item())

@@ -1,0 +1,130 @@
+"""Op layer: natural-layout entry points over the gfx950 kernels.
+
+GPU tensors run the hand-written HIP kernels of ``mikmeans._C`` (fail loudly if
+the extension is missing); CPU tensors run :mod:`mikmeans.ops.cpu`, the plain
+PyTorch reference of the same op (the test oracle and the demo-parity path,
+BASELINE config 1).  There is no third backend.
+
+* :func:`row_sqnorm`   K1  |x_i|^2
+* :func:`assign`       K2  nearest centroid + squared distance (MFMA GEMM + argmin)
+* :func:`cluster_sums` K3  per-cluster sums / counts (LDS scatter-add + f64 slab reduce)
+* :class:`CentroidPack` K4 fragment-packed centroids for the assign kernel
+"""
+from __future__ import annotations
+
+import torch
+
+from . import cpu
+from .native import available, dpad_for, dtype_code, require, vec_elems
+
+__all__ = [
+    "available",
+    "require",
+    "dpad_for",
+    "vec_elems",
+    "pad_columns",
+    "row_sqnorm",
+    "assign",
+    "cluster_sums",
+    "CentroidPack",
+]
+
+
+def pad_columns(X: torch.Tensor, dtype: torch.dtype | None = None) -> torch.Tensor:
+    """Return ``X`` in ``dtype`` with columns zero-padded to a 16-byte multiple.
+
+    Zero columns change neither distances nor cluster sums; the GPU kernels need
+    16-byte rows.  No copy when ``X`` already qualifies.
+    """
+    dtype = dtype or X.dtype
+    v = vec_elems(dtype)
+    n, d = X.shape
+    dp = (d + v - 1) // v * v
+    ok = X.dtype == dtype and d == dp and X.stride(1) == 1 and (n <= 1 or X.stride(0) % v == 0)
+    if ok and X.data_ptr() % 16 == 0:
+        return X
+    out = torch.zeros((n, dp), dtype=dtype, device=X.device)
+    out[:, :d] = X.to(dtype)
+    return out
+
+
+def row_sqnorm(X: torch.Tensor) -> torch.Tensor:
+    if not X.is_cuda:
+        return cpu.row_sqnorm(X)
+    C = require()
+    Xp = pad_columns(X)
+    out = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)
+    C.row_sqnorm(Xp, out)
+    return out
+
+
+class CentroidPack:
+    """Centroids in the assign kernel's fragment-packed layout (see csrc/kernels.h).
+
+    ``pack`` holds ``-2*c`` (bf16 or f32, as the points) and ``cn`` holds
+    ``|c_q|^2`` of the quantised centroids, padded with a huge score for the
+    rows between K and Kpad.
+    """
+
+    def __init__(self, K: int, D: int, dtype: torch.dtype, device):
+        C = require()
+        self.K, self.D, self.dtype = K, D, dtype
+        self.dpad = dpad_for(D, dtype)
+        if self.dpad == 0:
+            raise NotImplementedError(f"mikmeans: GPU assign supports D <= 256 (got {D})")
+        self.dt = dtype_code(dtype)
+        self.Kpad = C.assign_kpad(self.dt, self.dpad, K)
+        self.pack = torch.zeros(self.Kpad * self.dpad, dtype=dtype, device=device)
+        self.cn = torch.zeros(C.assign_cn_len(self.Kpad), dtype=torch.float32, device=device)
+
+    def load(self, centers: torch.Tensor) -> "CentroidPack":
+        C = require()
+        c = centers.to(device=self.pack.device, dtype=torch.float32).contiguous()
+        assert c.shape == (self.K, self.D), (c.shape, self.K, self.D)
+        C.finalize(0, None, c, None, None, None, self.pack, self.cn, None, None, self.dpad, self.Kpad)
+        return self
+
+
+def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True):
+    """Nearest centroid of every row: returns ``(labels int32, sqdist float32 or None)``.
+
+    bf16 points are compared against bf16-quantised centroids (scores
+    accumulated in fp32 on the matrix cores); f32 points use the exact-f32 MFMA.
+    """
+    if not X.is_cuda:
+        return cpu.assign(X, centers, with_dist=with_dist)
+    C = require()
+    Xp = pad_columns(X)
+    D = Xp.shape[1]
+    cen = torch.zeros((centers.shape[0], D), dtype=torch.float32, device=X.device)
+    cen[:, : centers.shape[1]] = centers.to(device=X.device, dtype=torch.float32)
+    pk = CentroidPack(cen.shape[0], D, Xp.dtype, X.device).load(cen)
+    n = Xp.shape[0]
+    labels = torch.empty(n, dtype=torch.int32, device=X.device)
+    xn = mind = None
+    if with_dist:
+        xn = torch.empty(n, dtype=torch.float32, device=X.device)
+        C.row_sqnorm(Xp, xn)
+        mind = torch.empty(n, dtype=torch.float32, device=X.device)
+    C.assign(Xp, pk.pack, pk.cn, xn, labels, mind, None, pk.Kpad, pk.dpad, False)
+    return labels, mind
+
+
+def cluster_sums(X: torch.Tensor, labels: torch.Tensor, K: int, weights: torch.Tensor | None = None):
+    """Per-cluster f64 sums ``[K, D]`` and counts ``[K]`` (weighted when ``weights``)."""
+    if not X.is_cuda:
+        return cpu.cluster_sums(X, labels, K, weights)
+    C = require()
+    Xp = pad_columns(X)
+    n, D = Xp.shape
+    dt = dtype_code(Xp.dtype)
+    nch = C.update_n_chunks(dt, K, D, n)
+    slab = torch.empty(nch * K * D, dtype=torch.float32, device=X.device)
+    cnt = torch.empty(nch * K, dtype=torch.float32, device=X.device)
+    packed = torch.empty(K * D + K + 2, dtype=torch.float64, device=X.device)
+    lab = labels.to(torch.int32).contiguous()
+    w = weights.to(torch.float32).contiguous() if weights is not None else None
+    C.update(Xp, lab, K, slab, cnt, nch, w)
+    C.reduce(slab, cnt, nch, K, D, None, packed)
+    sums = packed[: K * D].view(K, D)[:, : X.shape[1]]
+    return sums, packed[K * D : K * D + K]

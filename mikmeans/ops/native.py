@@ -1,0 +1,78 @@
+"""Loader for the in-tree native extension ``mikmeans._C`` (gfx950 HIP kernels).
+
+The extension is built by :mod:`mikmeans._build` (``hipcc --offload-arch=gfx950``)
+and lives next to the package so it ships with the repository.  GPU code paths
+call :func:`require`, which fails loudly when the extension is missing: a GPU run
+must never silently fall back to eager PyTorch.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+import torch  # noqa: F401  (torch's HIP runtime must be loaded before _C)
+
+_mod = None
+_err: BaseException | None = None
+
+DT_F32 = 0
+DT_BF16 = 1
+
+
+def _load():
+    global _mod, _err
+    if _mod is not None or _err is not None:
+        return _mod
+    try:
+        _mod = importlib.import_module("mikmeans._C")
+    except BaseException as e:  # ImportError, OSError (missing symbols), ...
+        _err = e
+        if os.environ.get("MIKMEANS_AUTOBUILD", "0") == "1":
+            from .. import _build
+
+            _build.build(verbose=False)
+            _err = None
+            _mod = importlib.import_module("mikmeans._C")
+    return _mod
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def require():
+    """Return the native module or raise with the build instructions."""
+    m = _load()
+    if m is None:
+        raise RuntimeError(
+            "mikmeans native extension is not built (mikmeans/_C*.so missing or unloadable: "
+            f"{_err!r}). Build it with `python -m mikmeans._build` (hipcc, gfx950)."
+        )
+    return m
+
+
+def dtype_code(dtype: torch.dtype) -> int:
+    if dtype == torch.bfloat16:
+        return DT_BF16
+    if dtype == torch.float32:
+        return DT_F32
+    raise TypeError(f"mikmeans: unsupported compute dtype {dtype}")
+
+
+def vec_elems(dtype: torch.dtype) -> int:
+    """Elements per 16-byte piece: the column padding granule of the vector path."""
+    return 8 if dtype == torch.bfloat16 else 4
+
+
+def dpad_for(D: int, dtype: torch.dtype) -> int:
+    """Power-of-two padded feature width the assign kernel is instantiated for (0 = unsupported)."""
+    v = vec_elems(dtype)
+    d = 2 * v
+    while d < D:
+        d *= 2
+    return d if d <= 256 else 0
+
+
+def loaded_path() -> str | None:
+    m = _load()
+    return getattr(m, "__file__", None) if m is not None else None

@@ -1,0 +1,5 @@
+"""Distributed layer: process groups (RCCL over xGMI / gloo), shard planning, replication."""
+from .comm import Comm, get_comm, set_comm
+from .shard import ShardPlan, plan, shard_range, shard_sizes
+
+__all__ = ["Comm", "get_comm", "set_comm", "ShardPlan", "plan", "shard_range", "shard_sizes"]

@@ -1,0 +1,144 @@
+"""Process-group wrapper: one process per GPU, RCCL over xGMI (backend "nccl" on ROCm).
+
+This is the MI355X-native replacement of the reference's transport + replication
+layers (P2PT/WebRTC gossip of Yjs CRDT updates, app.mjs:35-121): instead of
+flooding state deltas to peers, every Lloyd iteration performs ONE bulk-synchronous
+all-reduce of the packed f64 message ``[sums | counts | inertia | changed]``
+(SURVEY.md §2.4 C1), which leaves every replica of the centroids bit-identical.
+Rendezvous is env:// (MASTER_ADDR/PORT, a TCPStore) -- the analogue of the
+reference's WebTorrent trackers (app.mjs:39-45); the run id plays the room code
+(app.mjs:15-19).
+
+The same code runs on CPU with the gloo backend (world_size > 1 in tests).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class Comm:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str | None = None
+    device: torch.device = torch.device("cpu")
+    owns_group: bool = False
+
+    # ---------------------------------------------------------------- setup
+    @staticmethod
+    def local(device=None) -> "Comm":
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        return Comm(device=dev)
+
+    @staticmethod
+    def from_env(device: str | None = None, timeout_s: float = 600.0) -> "Comm":
+        """Join (or create) the default process group described by torchrun's env vars.
+
+        ``device`` "cuda" binds LOCAL_RANK's GPU and uses RCCL; "cpu" uses gloo.
+        Without WORLD_SIZE>1 in the environment this returns a single-rank Comm.
+        """
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        if device.startswith("cuda"):
+            torch.cuda.set_device(local_rank)
+            dev = torch.device("cuda", local_rank)
+            backend = "nccl"
+        else:
+            dev = torch.device("cpu")
+            backend = "gloo"
+        if world <= 1 and not dist.is_initialized():
+            return Comm(device=dev, backend=None)
+        owns = False
+        if not dist.is_initialized():
+            kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kw["device_id"] = dev
+            dist.init_process_group(**kw)
+            owns = True
+        return Comm(
+            rank=dist.get_rank(),
+            world=dist.get_world_size(),
+            local_rank=local_rank,
+            backend=dist.get_backend(),
+            device=dev,
+            owns_group=owns,
+        )
+
+    def close(self):
+        if self.owns_group and dist.is_initialized():
+            dist.destroy_process_group()
+            self.owns_group = False
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+    # ---------------------------------------------------------- collectives
+    def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place SUM across ranks (no-op on one rank)."""
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t
+
+    def allreduce_max_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.world > 1:
+            dist.broadcast(t, src=src)
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """Stack ``t`` from every rank: shape ``[world, *t.shape]``."""
+        if self.world == 1:
+            return t.unsqueeze(0).clone()
+        out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous())
+        return out
+
+    def all_gather_object(self, obj):
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        dist.all_gather_object(out, obj)
+        return out
+
+    def broadcast_object(self, obj, src: int = 0):
+        if self.world == 1:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=src)
+        return box[0]
+
+    def barrier(self):
+        if self.world > 1:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+
+_default: Comm | None = None
+
+
+def get_comm() -> Comm:
+    global _default
+    if _default is None:
+        _default = Comm.local()
+    return _default
+
+
+def set_comm(c: Comm) -> None:
+    global _default
+    _default = c

@@ -1,0 +1,60 @@
+"""Data-parallel shard planning for 288 GB-HBM3E GPUs.
+
+Points are split into contiguous, balanced row ranges (rank r owns
+``[start_r, end_r)``); centroids are replicated.  :func:`plan` sizes the
+per-rank resident set (points + labels + norms + kernel workspace) against the
+HBM budget and tells the caller whether a full-batch Lloyd fit fits or whether
+the run must stream mini-batches (BASELINE config 5: N=1e9, D=256 bf16 is 512 GB,
+over one GPU's 288 GB but 64 GB per rank at W=8).
+"""
+from __future__ import annotations
+
+from dataclasses import asdict, dataclass
+
+HBM_BYTES = 288 * 10**9          # MI355X HBM3E per GPU (spec)
+HBM_USABLE_FRACTION = 0.90       # leave room for the runtime / RCCL buffers
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Balanced contiguous split: the first ``n % world`` ranks get one extra row."""
+    base, rem = divmod(n, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def shard_sizes(n: int, world: int) -> list[int]:
+    return [shard_range(n, r, world)[1] - shard_range(n, r, world)[0] for r in range(world)]
+
+
+@dataclass
+class ShardPlan:
+    n_global: int
+    world: int
+    rows_per_rank: int
+    bytes_points: int
+    bytes_aux: int
+    bytes_workspace: int
+    bytes_total: int
+    hbm_budget: int
+    fits: bool
+    batch_rows: int  # rows per streamed mini-batch when it does not fit (0 = full batch)
+
+    def as_dict(self):
+        return asdict(self)
+
+
+def plan(n: int, d: int, k: int, world: int = 1, itemsize: int = 2,
+         hbm_bytes: int = HBM_BYTES, usable: float = HBM_USABLE_FRACTION,
+         update_chunks: int = 64) -> ShardPlan:
+    rows = -(-n // world)
+    pts = rows * d * itemsize
+    aux = rows * (4 + 4 + 4)                      # labels + |x|^2 + distance
+    ws = update_chunks * k * d * 4 + k * d * 8 * 3 + (1 << 20)   # slabs + packed + centroids
+    total = pts + aux + ws
+    budget = int(hbm_bytes * usable)
+    fits = total <= budget
+    batch = 0
+    if not fits:
+        per_row = d * itemsize + 12
+        batch = max(1, (budget - ws) // (4 * per_row))   # 4 batches in flight worth of headroom
+    return ShardPlan(n, world, rows, pts, aux, ws, total, budget, fits, int(batch))

@@ -1,0 +1,28 @@
+#!/bin/bash
+# One gpurun session: smoke -> GPU tests -> bench -> rocprof.  Stops at the first
+# step that faults, aborts or times out (exit >= 124 or signal); a plain test
+# failure (pytest exit 1) does not stop the bench.
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+step() {  # step NAME TIMEOUT CMD...
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/session.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/session.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-smoke tests bench prof}; do
+  case $s in
+    smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step pytest_gpu 1200 python -m pytest tests -x -q -m gpu ;;
+    bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
+    bench2) step bench_cfg2 300 python bench.py --config cfg2 --steps 50 --warmup 5 ;;
+    prof) cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$OLDPWD}"
+          step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -- python3 bench.py --steps 5 --warmup 1 ;;
+  esac
+done
+exit 0

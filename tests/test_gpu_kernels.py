@@ -1,0 +1,179 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32/f64 reference (1 GPU)."""
+import numpy as np
+import pytest
+import torch
+
+import mikmeans
+from mikmeans import ops
+from mikmeans.data import blobs as B
+from mikmeans.ops import cpu as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _points(n, d, dtype, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(n, d, generator=g) * scale).to(dtype)
+
+
+def _check_assign(X, C, labels, mind, rel=2e-5):
+    """Tie-tolerant: the chosen centre must be (near-)optimal for every point."""
+    Xc = X.cpu()
+    sc = ref.scores(Xc, C.cpu())                       # |c|^2 - 2 x.c on quantised centres
+    best = sc.min(1).values
+    got = sc.gather(1, labels.cpu().long()[:, None])[:, 0]
+    scale = (Xc.float() ** 2).sum(1) + (ref.quantize_centers(C.cpu(), X.dtype) ** 2).sum(1).max()
+    bad = (got - best) > rel * scale + 1e-6
+    assert int(bad.sum()) == 0, f"{int(bad.sum())} suboptimal labels of {len(bad)}"
+    if mind is not None:
+        xn = (Xc.float() ** 2).sum(1)
+        exp = (xn + got).clamp_min(0)
+        torch.testing.assert_close(mind.cpu(), exp, rtol=1e-3, atol=1e-3 * float(scale.max()) ** 0.5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,d", [(1, 8), (1000, 2), (4097, 64), (20000, 128), (3000, 256), (777, 30)])
+def test_row_sqnorm(native, dtype, n, d):
+    X = _points(n, d, dtype, seed=n + d)
+    got = ops.row_sqnorm(X.to(DEV)).cpu()
+    torch.testing.assert_close(got, ref.row_sqnorm(X), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,d,k", [(1000, 2, 3), (513, 16, 37), (20000, 128, 256), (9000, 128, 1024),
+                                   (4096, 64, 4096), (3000, 256, 512), (255, 100, 70), (70000, 32, 9)])
+def test_assign_matches_reference(native, dtype, n, d, k):
+    X = _points(n, d, dtype, seed=k)
+    C = _points(k, d, torch.float32, seed=k + 1)
+    labels, mind = ops.assign(X.to(DEV), C.to(DEV), with_dist=True)
+    _check_assign(X, C, labels, mind, rel=2e-5 if dtype == torch.float32 else 3e-5)
+
+
+def test_assign_exact_f32_small_ints(native):
+    # integer data: scores are exact in f32, so labels must equal argmin exactly (lowest index on ties)
+    g = torch.Generator().manual_seed(3)
+    X = torch.randint(-8, 8, (5000, 64), generator=g).float()
+    C = torch.randint(-8, 8, (300, 64), generator=g).float()
+    C[17] = C[5]  # exact duplicate centre: index 5 must win
+    labels, _ = ops.assign(X.to(DEV), C.to(DEV), with_dist=False)
+    exp, _ = ref.assign(X, C)
+    sc = ref.scores(X, C)
+    tie = (sc == sc.min(1, keepdim=True).values).sum(1) > 1
+    assert torch.equal(labels.cpu()[~tie], exp[~tie])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,d,k", [(10000, 128, 1024), (50000, 64, 4096), (7000, 256, 512), (999, 8, 3),
+                                   (30000, 128, 256), (4000, 128, 20000)])
+def test_cluster_sums(native, dtype, n, d, k):
+    X = _points(n, d, dtype, seed=d)
+    g = torch.Generator().manual_seed(k)
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32)
+    sums, counts = ops.cluster_sums(X.to(DEV), lab.to(DEV), k)
+    es, ec = ref.cluster_sums(X, lab, k)
+    torch.testing.assert_close(counts.cpu(), ec, rtol=0, atol=0)
+    torch.testing.assert_close(sums.cpu(), es, rtol=1e-5, atol=1e-4)
+
+
+def test_cluster_sums_weighted(native):
+    X = _points(5000, 32, torch.float32)
+    lab = torch.randint(0, 50, (5000,), dtype=torch.int32)
+    w = torch.rand(5000)
+    sums, counts = ops.cluster_sums(X.to(DEV), lab.to(DEV), 50, w.to(DEV))
+    es, ec = ref.cluster_sums(X, lab, 50, w)
+    torch.testing.assert_close(counts.cpu(), ec, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(sums.cpu(), es, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_blobs_match_numpy_mirror(native, dtype):
+    Cg = B.blob_centers(16, 40, 10.0, seed=11, device=DEV)
+    Cn = B.blob_centers_np(16, 40, 10.0, seed=11)
+    np.testing.assert_allclose(Cg.cpu().numpy(), Cn, rtol=0, atol=0)
+    Xg, yg = B.make_blobs(5000, 40, 16, seed=11, i0=123456789, dtype=dtype, device=DEV,
+                          return_labels=True, centers=Cg)
+    Xn, yn = B.blobs_np(123456789, 5000, Cn, 1.0, 11, True)
+    assert np.array_equal(yg.cpu().numpy(), yn)
+    tol = 1e-4 if dtype == torch.float32 else 8e-2
+    np.testing.assert_allclose(Xg.float().cpu().numpy(), Xn, rtol=0, atol=tol)
+
+
+def test_lloyd_gpu_matches_cpu_engine(native):
+    from mikmeans.models.lloyd import LloydEngine
+
+    X = B.make_blobs(20000, 64, 50, seed=5)
+    C0 = X[:50].clone()
+    ec = LloydEngine(X, 50).set_centers(C0)
+    eg = LloydEngine(X.to(DEV), 50).set_centers(C0)
+    for _ in range(5):
+        ec.step()
+        eg.step()
+        sc, sg = ec.last_stats(), eg.last_stats()
+        assert sc.n_changed == sg.n_changed
+        assert abs(sc.inertia - sg.inertia) <= 1e-4 * abs(sc.inertia)
+    torch.testing.assert_close(eg.centers.cpu(), ec.centers, rtol=1e-4, atol=1e-4)
+    assert torch.equal(eg.labels.cpu(), ec.labels)
+
+
+def test_kmeans_fit_bf16_blobs(native):
+    from sklearn.metrics import adjusted_rand_score
+
+    X, y = B.make_blobs(200000, 128, 64, seed=2, dtype=torch.bfloat16, device=DEV, return_labels=True)
+    km = mikmeans.KMeans(64, init="k-means++", dtype="bfloat16", seed=0, max_iter=50).fit(X)
+    assert km.cluster_centers_.shape == (64, 128)
+    ari = adjusted_rand_score(y.cpu().numpy(), km.labels_.cpu().numpy())
+    assert ari > 0.95, ari
+    assert np.isfinite(km.inertia_)
+
+
+def test_kmeanspp_gpu_picks_data_rows(native):
+    X = B.make_blobs(30000, 32, 20, seed=9, device=DEV)
+    C = mikmeans.kmeans_plusplus(X, 20, seed=4)
+    d = torch.cdist(C.float(), X.float()).min(1).values
+    assert float(d.max()) == 0.0
+    # k-means++ on well separated blobs hits (almost) every blob
+    _, y = B.make_blobs(30000, 32, 20, seed=9, device=DEV, return_labels=True)
+    lab, _ = ops.assign(C, B.blob_centers(20, 32, 10.0, 9, device=DEV), with_dist=False)
+    assert len(set(lab.cpu().tolist())) >= 17
+
+
+def test_kmeanspp_gpu_cpu_same_seed_same_first_center(native):
+    X = B.make_blobs(5000, 16, 8, seed=1)
+    Cg = mikmeans.kmeans_plusplus(X.to(DEV), 8, seed=7).cpu()
+    Cc = mikmeans.kmeans_plusplus(X, 8, seed=7)
+    torch.testing.assert_close(Cg[0], Cc[0])
+
+
+def test_minibatch_gpu_vs_cpu(native):
+    from mikmeans.models.minibatch import MiniBatchEngine
+
+    X = B.make_blobs(8192, 32, 10, seed=3)
+    C0 = X[:10].clone()
+    ec = MiniBatchEngine(10, 32, 1024)
+    eg = MiniBatchEngine(10, 32, 1024, device=DEV)
+    ec.set_centers(C0)
+    eg.set_centers(C0)
+    for s in range(8):
+        xb = X[s * 1024 : (s + 1) * 1024]
+        ec.partial_fit(xb)
+        eg.partial_fit(xb.to(DEV))
+    torch.testing.assert_close(eg.centers.cpu(), ec.centers, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(eg.vcount.cpu(), ec.vcount)
+
+
+def test_frozen_centers_stay(native):
+    X = B.make_blobs(10000, 16, 4, seed=8, device=DEV)
+    C0 = X[:4].clone().float()
+    km = mikmeans.KMeans(4, init=C0, frozen=[1, 0, 0, 1], max_iter=10, tol=0).fit(X)
+    torch.testing.assert_close(km.cluster_centers_[0], C0[0])
+    torch.testing.assert_close(km.cluster_centers_[3], C0[3])
+
+
+def test_native_extension_is_loaded(native):
+    import sys
+
+    assert "mikmeans._C" in sys.modules
+    maps = open("/proc/self/maps").read()
+    hip = {l.split()[-1] for l in maps.splitlines() if "libamdhip64" in l}
+    assert len(hip) == 1, hip  # exactly one HIP runtime (torch's)
