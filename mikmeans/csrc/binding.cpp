@@ -94,8 +94,16 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
   hip_check(mk::launch_assign(dt, (int)dpad, a, stream()), "assign");
 }
 
+void check_i64(const Tensor& t, const char* name, int64_t numel_min) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kLong && t.is_contiguous(), "mikmeans: ", name,
+              " must be contiguous int64");
+  TORCH_CHECK(t.numel() >= numel_min, "mikmeans: ", name, " too small");
+}
+
 void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab,
-            const Tensor& cnt_slab, int64_t n_chunks, const c10::optional<Tensor>& weights) {
+            const Tensor& cnt_slab, int64_t n_chunks, const c10::optional<Tensor>& weights,
+            int64_t sum_exp, int64_t cnt_exp) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   const int64_t N = X.size(0);
@@ -104,30 +112,33 @@ void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab
               "mikmeans: labels must be int32 [N]");
   const int sw = mk::update_slice_width(dt, (int)K, D);
   TORCH_CHECK(sw == 0 ? n_chunks == 1 : n_chunks % 8 == 0, "mikmeans: bad n_chunks");
-  check_f32(slab, "slab", n_chunks * K * D);
-  check_f32(cnt_slab, "cnt_slab", n_chunks * K);
+  check_i64(slab, "slab", n_chunks * K * D);
+  check_i64(cnt_slab, "cnt_slab", n_chunks * K);
   if (weights.has_value()) check_f32(*weights, "weights", N);
   if (sw == 0) {  // global-atomic fallback accumulates into zeroed buffers
-    hip_check(hipMemsetAsync(slab.data_ptr(), 0, K * D * 4, stream()), "memset");
-    hip_check(hipMemsetAsync(cnt_slab.data_ptr(), 0, K * 4, stream()), "memset");
+    hip_check(hipMemsetAsync(slab.data_ptr(), 0, K * D * 8, stream()), "memset");
+    hip_check(hipMemsetAsync(cnt_slab.data_ptr(), 0, K * 8, stream()), "memset");
   }
   mk::UpdateArgs a;
   a.X = X.data_ptr(); a.N = N; a.D = D; a.ldx = ldx;
   a.labels = labels.data_ptr<int32_t>(); a.K = (int)K; a.n_chunks = (int)n_chunks;
-  a.slab = slab.data_ptr<float>(); a.cnt_slab = cnt_slab.data_ptr<float>();
+  a.slab = (long long*)slab.data_ptr<int64_t>(); a.cnt_slab = (long long*)cnt_slab.data_ptr<int64_t>();
   a.weights = opt_ptr<const float>(weights);
+  a.sum_exp = (int)sum_exp; a.cnt_exp = (int)cnt_exp;
   hip_check(mk::launch_update(dt, a, stream()), "update");
 }
 
 void reduce(const Tensor& slab, const Tensor& cnt_slab, int64_t n_chunks, int64_t K, int64_t D,
-            const c10::optional<Tensor>& slots, const Tensor& packed) {
-  check_f32(slab, "slab", n_chunks * K * D);
-  check_f32(cnt_slab, "cnt_slab", n_chunks * K);
+            const c10::optional<Tensor>& slots, const Tensor& packed, int64_t sum_exp,
+            int64_t cnt_exp) {
+  check_i64(slab, "slab", n_chunks * K * D);
+  check_i64(cnt_slab, "cnt_slab", n_chunks * K);
   check_f64(packed, "packed", K * D + K + 2);
   if (slots.has_value()) check_f64(*slots, "slots", mk::NSLOT * mk::SLOT_STRIDE);
-  hip_check(mk::launch_reduce(slab.data_ptr<float>(), cnt_slab.data_ptr<float>(), (int)n_chunks,
-                              (int)K, (int)D, opt_ptr<double>(slots), packed.data_ptr<double>(),
-                              stream()),
+  hip_check(mk::launch_reduce((const long long*)slab.data_ptr<int64_t>(),
+                              (const long long*)cnt_slab.data_ptr<int64_t>(), (int)n_chunks, (int)K,
+                              (int)D, (int)sum_exp, (int)cnt_exp, opt_ptr<double>(slots),
+                              packed.data_ptr<double>(), stream()),
             "reduce");
 }
 
@@ -325,6 +336,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("assign_cn_len", [](int64_t kpad) { return mk::assign_cn_len((int)kpad); });
   m.def("update_slice_width", [](int64_t dt, int64_t K, int64_t D) { return mk::update_slice_width((int)dt, (int)K, (int)D); });
   m.def("update_n_chunks", [](int64_t dt, int64_t K, int64_t D, int64_t N) { return mk::update_n_chunks((int)dt, (int)K, (int)D, N); });
+  m.def("fixed_exp", [](double maxabs) { return mk::fixed_exp(maxabs); },
+        "fixed-point exponent e with maxabs * 2^e <= 2^30 (M-step accumulators)");
   m.def("js_format", &js_format, "ECMAScript Number::toString of a double");
   m.def("js_array", &js_array, "JSON array of a CPU float tensor with JS number formatting");
   m.attr("NSLOT") = mk::NSLOT;

