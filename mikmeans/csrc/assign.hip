@@ -39,10 +39,10 @@ constexpr int chunk_tiles(int esize, int dpad) {
   return (32 * dpad * esize) >= 16384 ? 1 : 16384 / (32 * dpad * esize);
 }
 
-template <typename T, int DPAD>
+template <typename T, int DPAD, int P_>
 struct AssignCfg {
   static constexpr int NW = 4;                 // waves per workgroup
-  static constexpr int P = 2;                  // 32-point blocks per wave
+  static constexpr int P = P_;                 // 32-point blocks per wave
   static constexpr int V = Elem<T>::V;         // elements per 16-B piece
   static constexpr int NQ = DPAD / 2 / V;      // pieces per lane per point
   static constexpr int TILE_BYTES = NQ * 1024; // 32 centroids x DPAD
@@ -81,9 +81,9 @@ struct MfmaOp<float> {
   }
 };
 
-template <typename T, int DPAD>
+template <typename T, int DPAD, int P>
 __global__ __launch_bounds__(256) void assign_kernel(AssignArgs a) {
-  using C = AssignCfg<T, DPAD>;
+  using C = AssignCfg<T, DPAD, P>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -219,23 +219,38 @@ __global__ __launch_bounds__(256) void assign_kernel(AssignArgs a) {
 }
 
 // ----------------------------------------------------------------------------
-template <typename T, int DPAD>
+template <typename T, int DPAD, int P>
 static hipError_t launch_t(const AssignArgs& a, hipStream_t s) {
-  using C = AssignCfg<T, DPAD>;
+  using C = AssignCfg<T, DPAD, P>;
   if (a.Kpad % (32 * C::CT) != 0) return hipErrorInvalidValue;
   const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
   const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)assign_kernel<T, DPAD>,
+    hipFuncSetAttribute((const void*)assign_kernel<T, DPAD, P>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
   if (nblk <= 0) return hipSuccess;
-  hipLaunchKernelGGL((assign_kernel<T, DPAD>), dim3((unsigned)nblk), dim3(C::NW * 64), lds, s, a);
+  hipLaunchKernelGGL((assign_kernel<T, DPAD, P>), dim3((unsigned)nblk), dim3(C::NW * 64), lds, s, a);
   return hipGetLastError();
+}
+
+// Points per wave = 32*P.  P=2 by default; tunable for A/B experiments
+// (set_assign_points_per_wave) -- larger P halves the LDS/L2 centroid traffic per
+// FLOP at the price of registers.
+static int g_assign_p = 0;
+void set_assign_p(int p) { g_assign_p = p; }
+int get_assign_p() { return g_assign_p; }
+
+template <typename T, int DPAD>
+static hipError_t launch_p(const AssignArgs& a, hipStream_t s) {
+  const int p = g_assign_p ? g_assign_p : 2;
+  if (p == 1) return launch_t<T, DPAD, 1>(a, s);
+  if (p == 4 && DPAD * sizeof(T) <= 256) return launch_t<T, DPAD, 4>(a, s);
+  return launch_t<T, DPAD, 2>(a, s);
 }
 
 int assign_chunk_tiles(int dtype, int dpad) {
@@ -255,20 +270,20 @@ int assign_cn_len(int kpad) { return ((kpad + 255) / 256) * 256; }
 hipError_t launch_assign(int dtype, int dpad, const AssignArgs& a, hipStream_t s) {
   if (dtype == DT_BF16) {
     switch (dpad) {
-      case 16: return launch_t<uint16_t, 16>(a, s);
-      case 32: return launch_t<uint16_t, 32>(a, s);
-      case 64: return launch_t<uint16_t, 64>(a, s);
-      case 128: return launch_t<uint16_t, 128>(a, s);
-      case 256: return launch_t<uint16_t, 256>(a, s);
+      case 16: return launch_p<uint16_t, 16>(a, s);
+      case 32: return launch_p<uint16_t, 32>(a, s);
+      case 64: return launch_p<uint16_t, 64>(a, s);
+      case 128: return launch_p<uint16_t, 128>(a, s);
+      case 256: return launch_p<uint16_t, 256>(a, s);
     }
   } else {
     switch (dpad) {
-      case 8: return launch_t<float, 8>(a, s);
-      case 16: return launch_t<float, 16>(a, s);
-      case 32: return launch_t<float, 32>(a, s);
-      case 64: return launch_t<float, 64>(a, s);
-      case 128: return launch_t<float, 128>(a, s);
-      case 256: return launch_t<float, 256>(a, s);
+      case 8: return launch_p<float, 8>(a, s);
+      case 16: return launch_p<float, 16>(a, s);
+      case 32: return launch_p<float, 32>(a, s);
+      case 64: return launch_p<float, 64>(a, s);
+      case 128: return launch_p<float, 128>(a, s);
+      case 256: return launch_p<float, 256>(a, s);
     }
   }
   return hipErrorInvalidValue;

@@ -336,6 +336,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("assign_cn_len", [](int64_t kpad) { return mk::assign_cn_len((int)kpad); });
   m.def("update_slice_width", [](int64_t dt, int64_t K, int64_t D) { return mk::update_slice_width((int)dt, (int)K, (int)D); });
   m.def("update_n_chunks", [](int64_t dt, int64_t K, int64_t D, int64_t N) { return mk::update_n_chunks((int)dt, (int)K, (int)D, N); });
+  m.def("set_assign_p", [](int64_t p) { mk::set_assign_p((int)p); }, "tuning: points blocks per wave");
+  m.def("get_assign_p", []() { return mk::get_assign_p(); });
   m.def("fixed_exp", [](double maxabs) { return mk::fixed_exp(maxabs); },
         "fixed-point exponent e with maxabs * 2^e <= 2^30 (M-step accumulators)");
   m.def("js_format", &js_format, "ECMAScript Number::toString of a double");

@@ -40,6 +40,8 @@ struct AssignArgs {
   int track_changed;
 };
 hipError_t launch_assign(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
+void set_assign_p(int p);  // 32-point blocks per wave (0 = default)
+int get_assign_p();
 
 // ---- update (LDS-privatised scatter-add) -------------------------------------
 // Sums are accumulated in FIXED POINT: every contribution x*w is rounded to a
