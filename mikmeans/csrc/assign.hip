@@ -56,10 +56,6 @@ struct AssignCfg {
   static_assert(PIECES % NW == 0, "chunk pieces must split evenly over waves");
 };
 
-__device__ __forceinline__ float pack_key(float s, int r) {
-  return __uint_as_float((__float_as_uint(s) & ~15u) | (unsigned)r);
-}
-
 template <typename T>
 struct MfmaOp;
 template <>
@@ -259,10 +255,10 @@ int assign_chunk_tiles(int dtype, int dpad) {
   if (!ok) return 0;
   return chunk_tiles(dtype == DT_BF16 ? 2 : 4, dpad);
 }
-int assign_kpad(int dtype, int dpad, int K) {
-  const int ct = assign_chunk_tiles(dtype, dpad);
+int assign_kpad(int dtype, int dpad, int K, int layout) {
+  const int ct = layout == 16 ? assign16_chunk_tiles(dtype, dpad) : assign_chunk_tiles(dtype, dpad);
   if (ct <= 0) return 0;
-  const int m = 32 * ct;
+  const int m = layout * ct;
   return ((K + m - 1) / m) * m;
 }
 int assign_cn_len(int kpad) { return ((kpad + 255) / 256) * 256; }

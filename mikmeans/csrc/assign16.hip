@@ -1,0 +1,271 @@
+// mikmeans — K2 variant: assignment on 16x16 MFMA tiles (v_mfma_f32_16x16x32_bf16 /
+// v_mfma_f32_16x16x4_f32) for gfx950.
+//
+// Same algorithm and pipeline as assign.hip (fragment-packed centroid chunks in a
+// 3-slot LDS ring fed by LDS-DMA, |c|^2 seeding the accumulators, packed-index
+// v_min3 argmin), re-tiled for the 16x16 matrix-core shape:
+//  * lane (r = l&15, g = l>>4) holds the B fragment of point p0+r, feature
+//    quarter g: x[p0+r][g*DPAD/4 .. +DPAD/4) (contiguous), and the A fragment of
+//    centroid r of the tile, same quarter;
+//  * output D[row = 4g+reg][col = r]: each lane holds 4 centroid scores of its
+//    point per tile; GT consecutive tiles are reduced together (4-bit index =
+//    tile-in-group * 4 + reg), the 4 lane groups g merge once at the end.
+// On MI355X the chip holds a higher clock on the 16x16 shape under load
+// (MI355X_MICROARCH.md, DVFS give-back item 7), which is why this variant exists;
+// scripts/ab_kernels.py picks the faster one per shape.
+//
+// Layout "16" of the packed centroids (csrc/kernels.h describes layout "32"):
+//   element (k, d): t = k/16, r = k%16, g = d / (DPAD/4), e = d % (DPAD/4)
+//   offset = ((t*NQ + e/V)*64 + r + 16*g)*V + e%V,  NQ = DPAD/(4V)
+#include "common.h"
+#include "kernels.h"
+
+namespace mk {
+
+constexpr int chunk_tiles16(int esize, int dpad) {
+  return (16 * dpad * esize) >= 16384 ? 1 : 16384 / (16 * dpad * esize);
+}
+
+template <typename T, int DPAD, int P_, int GT_>
+struct Assign16Cfg {
+  static constexpr int NW = 4;
+  static constexpr int P = P_;                  // 16-point blocks per wave
+  static constexpr int GT = GT_;                // tiles reduced per epilogue
+  static constexpr int V = Elem<T>::V;
+  static constexpr int NQ = DPAD / 4 / V;       // 16-B pieces per lane per point
+  static constexpr int TILE_BYTES = NQ * 1024;  // 16 centroids x DPAD
+  static constexpr int CT = chunk_tiles16(sizeof(T), DPAD);
+  static constexpr int CHUNK_BYTES = CT * TILE_BYTES;
+  static constexpr int PIECES = CHUNK_BYTES / 1024;
+  static constexpr int NPW = PIECES / NW;
+  static constexpr int PTS = NW * P * 16;
+  static constexpr int NBUF = 3;
+  static_assert(NQ >= 1, "DPAD too small for the 16x16 layout");
+  static_assert(CT % GT == 0, "tile group must divide the chunk");
+  static_assert(GT * 4 <= 16, "4-bit packed index");
+  static_assert(PIECES % NW == 0, "chunk pieces must split evenly over waves");
+};
+
+template <typename T> struct Mfma16;
+template <> struct Mfma16<uint16_t> {
+  __device__ static __forceinline__ f32x4 run(const u32x4& a, const u32x4& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(short8, a),
+                                                   __builtin_bit_cast(short8, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfma16<float> {
+  __device__ static __forceinline__ f32x4 run(const u32x4& a, const u32x4& b, f32x4 c) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[e]), __uint_as_float(b[e]), c, 0, 0, 0);
+    return c;
+  }
+};
+
+template <typename T, int DPAD, int P, int GT>
+__global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
+  using C = Assign16Cfg<T, DPAD, P, GT>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
+  char* cn_lds = smem;
+  char* bufs = smem + cn_bytes;
+  const int nch = a.Kpad / (16 * C::CT);
+  const char* gC = (const char*)a.Cpack;
+
+  for (int p = wid; p < cn_bytes / 1024; p += C::NW)
+    glds16((const char*)a.cn + p * 1024 + lane * 16, (MK_LDS void*)(cn_lds + p * 1024));
+  auto issue_chunk = [&](int c) {
+    const char* src = gC + (int64_t)c * C::CHUNK_BYTES + lane * 16;
+    char* dst = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
+#pragma unroll
+    for (int i = 0; i < C::NPW; ++i) {
+      const int pc = wid + i * C::NW;
+      glds16(src + pc * 1024, (MK_LDS void*)(dst + pc * 1024));
+    }
+  };
+  issue_chunk(0);
+
+  const int64_t pbase = (int64_t)blockIdx.x * C::PTS + (int64_t)wid * (C::P * 16);
+  u32x4 xr[C::P][C::NQ];
+#pragma unroll
+  for (int p = 0; p < C::P; ++p) {
+    int64_t row = pbase + p * 16 + r;
+    row = row < a.N ? row : (a.N - 1);
+    const T* rp = (const T*)a.X + row * a.ldx + g * (DPAD / 4);
+#pragma unroll
+    for (int q = 0; q < C::NQ; ++q) {
+      const int col = g * (DPAD / 4) + q * C::V;
+      if (col < a.D) xr[p][q] = *(const u32x4*)(rp + q * C::V);
+      else xr[p][q] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  wait_vmcnt<0>();  // see assign.hip: retire the fragments before the LDS-DMA loop
+  if (nch > 1) issue_chunk(1);
+
+  float best[C::P];
+  int bg[C::P];
+#pragma unroll
+  for (int p = 0; p < C::P; ++p) { best[p] = 3.0e38f; bg[p] = 0; }
+
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
+    wait_lgkm0();
+    raw_barrier();
+    if (c + 2 < nch) issue_chunk(c + 2);
+    const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
+#pragma unroll
+    for (int tg = 0; tg < C::CT / GT; ++tg) {
+      f32x4 acc[C::P][GT];
+#pragma unroll
+      for (int t = 0; t < GT; ++t) {
+        const int tl_i = tg * GT + t;
+        const int tile = c * C::CT + tl_i;
+        const f32x4 ci = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
+        const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
+        u32x4 aw[C::NQ];
+#pragma unroll
+        for (int q = 0; q < C::NQ; ++q) aw[q] = *(const u32x4*)(tl + q * 1024);
+#pragma unroll
+        for (int q = 0; q < C::NQ; ++q) {
+#pragma unroll
+          for (int p = 0; p < C::P; ++p)
+            acc[p][t] = Mfma16<T>::run(aw[q], xr[p][q], q == 0 ? ci : acc[p][t]);
+        }
+      }
+      const int grp = c * (C::CT / GT) + tg;
+#pragma unroll
+      for (int p = 0; p < C::P; ++p) {
+        float m;
+        if constexpr (GT == 1) {
+          const f32x4& s = acc[p][0];
+          m = min3f(min3f(pack_key(s[0], 0), pack_key(s[1], 1), pack_key(s[2], 2)), pack_key(s[3], 3),
+                    pack_key(s[3], 3));
+        } else if constexpr (GT == 2) {
+          const f32x4& s0 = acc[p][0];
+          const f32x4& s1 = acc[p][1];
+          const float m0 = min3f(pack_key(s0[0], 0), pack_key(s0[1], 1), pack_key(s0[2], 2));
+          const float m1 = min3f(pack_key(s0[3], 3), pack_key(s1[0], 4), pack_key(s1[1], 5));
+          m = min3f(min3f(m0, m1, pack_key(s1[2], 6)), pack_key(s1[3], 7), pack_key(s1[3], 7));
+        } else {
+          float k[16];
+#pragma unroll
+          for (int t = 0; t < GT; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) k[4 * t + e] = pack_key(acc[p][t][e], 4 * t + e);
+          const float m0 = min3f(k[0], k[1], k[2]), m1 = min3f(k[3], k[4], k[5]);
+          const float m2 = min3f(k[6], k[7], k[8]), m3 = min3f(k[9], k[10], k[11]);
+          const float m4 = min3f(k[12], k[13], k[14]);
+          m = min3f(min3f(m0, m1, m2), min3f(m3, m4, k[15]), min3f(m3, m4, k[15]));
+        }
+        if (m < best[p]) { best[p] = m; bg[p] = grp; }
+      }
+    }
+  }
+
+  float inert = 0.f;
+  int changed = 0;
+#pragma unroll
+  for (int p = 0; p < C::P; ++p) {
+    const unsigned bits = __float_as_uint(best[p]);
+    const int idx = (int)(bits & 15u);
+    int k = (bg[p] * GT + (idx >> 2)) * 16 + 4 * g + (idx & 3);
+    float v = __uint_as_float(bits & ~15u);
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+      const float vo = __shfl_xor(v, o, 64);
+      const int ko = __shfl_xor(k, o, 64);
+      if (vo < v || (vo == v && ko < k)) { v = vo; k = ko; }
+    }
+    if ((p & 3) == g) {
+      const int64_t i = pbase + p * 16 + r;
+      if (i < a.N) {
+        if (a.track_changed) changed += (a.labels[i] != k);
+        a.labels[i] = k;
+        if (a.xn) {
+          const float d = fmaxf(a.xn[i] + v, 0.f);
+          inert += d;
+          if (a.mind) a.mind[i] = d;
+        }
+      }
+    }
+  }
+  if (a.slots) {
+    double di = wave_sum((double)inert);
+    int dc = wave_sum(changed);
+    double* red = (double*)(bufs + C::NBUF * C::CHUNK_BYTES);
+    if (lane == 0) { red[2 * wid] = di; red[2 * wid + 1] = (double)dc; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double si = 0, sc = 0;
+#pragma unroll
+      for (int w = 0; w < C::NW; ++w) { si += red[2 * w]; sc += red[2 * w + 1]; }
+      double* slot = a.slots + (blockIdx.x % NSLOT) * SLOT_STRIDE;
+      atomicAdd(slot + 0, si);
+      atomicAdd(slot + 1, sc);
+    }
+  }
+}
+
+template <typename T, int DPAD, int P, int GT>
+static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
+  using C = Assign16Cfg<T, DPAD, P, GT>;
+  if (a.Kpad % (16 * C::CT) != 0) return hipErrorInvalidValue;
+  const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
+  const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
+  if (nblk <= 0) return hipSuccess;
+  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT>), dim3((unsigned)nblk), dim3(C::NW * 64), lds, s, a);
+  return hipGetLastError();
+}
+
+static int g_assign16_gt = 0;
+void set_assign16_gt(int gt) { g_assign16_gt = gt; }
+
+template <typename T, int DPAD>
+static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
+  constexpr int CT = chunk_tiles16(sizeof(T), DPAD);
+  constexpr int NQ = DPAD / 4 / Elem<T>::V;
+  constexpr int P = NQ >= 8 ? 2 : 4;  // keep the point fragments within ~64-128 VGPRs
+  const int want = g_assign16_gt ? g_assign16_gt : 2;
+  if (want >= 4 && CT % 4 == 0) return launch16_t<T, DPAD, P, (CT % 4 == 0 ? 4 : 1)>(a, s);
+  if (want >= 2 && CT % 2 == 0) return launch16_t<T, DPAD, P, (CT % 2 == 0 ? 2 : 1)>(a, s);
+  return launch16_t<T, DPAD, P, 1>(a, s);
+}
+
+int assign16_chunk_tiles(int dtype, int dpad) {
+  const bool ok = dtype == DT_BF16 ? (dpad == 32 || dpad == 64 || dpad == 128 || dpad == 256)
+                                   : (dpad == 16 || dpad == 32 || dpad == 64 || dpad == 128 || dpad == 256);
+  return ok ? chunk_tiles16(dtype == DT_BF16 ? 2 : 4, dpad) : 0;
+}
+
+hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s) {
+  if (dtype == DT_BF16) {
+    switch (dpad) {
+      case 32: return launch16_d<uint16_t, 32>(a, s);
+      case 64: return launch16_d<uint16_t, 64>(a, s);
+      case 128: return launch16_d<uint16_t, 128>(a, s);
+      case 256: return launch16_d<uint16_t, 256>(a, s);
+    }
+  } else {
+    switch (dpad) {
+      case 16: return launch16_d<float, 16>(a, s);
+      case 32: return launch16_d<float, 32>(a, s);
+      case 64: return launch16_d<float, 64>(a, s);
+      case 128: return launch16_d<float, 128>(a, s);
+      case 256: return launch16_d<float, 256>(a, s);
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace mk

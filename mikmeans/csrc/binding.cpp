@@ -63,14 +63,16 @@ T* opt_ptr(const c10::optional<Tensor>& t) {
 // ----------------------------------------------------------------------------
 void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::optional<Tensor>& xn,
             const Tensor& labels, const c10::optional<Tensor>& mind,
-            const c10::optional<Tensor>& slots, int64_t Kpad, int64_t dpad, bool track_changed) {
+            const c10::optional<Tensor>& slots, int64_t Kpad, int64_t dpad, bool track_changed,
+            int64_t layout) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   const int64_t N = X.size(0);
   const int D = (int)X.size(1);
+  TORCH_CHECK(layout == 32 || layout == 16, "mikmeans: layout must be 32 or 16");
   TORCH_CHECK(D <= dpad, "mikmeans: D exceeds dpad");
-  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, (int)Kpad) == Kpad, "mikmeans: bad Kpad ", Kpad,
-              " for dpad ", dpad);
+  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, (int)Kpad, (int)layout) == Kpad, "mikmeans: bad Kpad ",
+              Kpad, " for dpad ", dpad, " layout ", layout);
   check_cuda(pack, "pack");
   TORCH_CHECK(pack.is_contiguous() && pack.scalar_type() == X.scalar_type(),
               "mikmeans: pack dtype must match X");
@@ -91,7 +93,8 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
   a.mind = opt_ptr<float>(mind);
   a.slots = opt_ptr<double>(slots);
   a.track_changed = track_changed ? 1 : 0;
-  hip_check(mk::launch_assign(dt, (int)dpad, a, stream()), "assign");
+  if (layout == 16) hip_check(mk::launch_assign16(dt, (int)dpad, a, stream()), "assign16");
+  else hip_check(mk::launch_assign(dt, (int)dpad, a, stream()), "assign");
 }
 
 void check_i64(const Tensor& t, const char* name, int64_t numel_min) {
@@ -146,12 +149,13 @@ void finalize(int64_t mode, const c10::optional<Tensor>& packed, const Tensor& C
               const c10::optional<Tensor>& Cnew, const c10::optional<Tensor>& frozen,
               const c10::optional<Tensor>& mb_counts, const Tensor& pack, const Tensor& cn,
               const c10::optional<Tensor>& shift, const c10::optional<Tensor>& counts,
-              int64_t dpad, int64_t Kpad) {
+              int64_t dpad, int64_t Kpad, int64_t layout) {
   check_f32(Cold, "C");
   TORCH_CHECK(Cold.dim() == 2, "mikmeans: C must be [K, D]");
   const int K = (int)Cold.size(0), D = (int)Cold.size(1);
   const int dt = pack.scalar_type() == at::kBFloat16 ? mk::DT_BF16 : mk::DT_F32;
-  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, K) == Kpad, "mikmeans: bad Kpad");
+  TORCH_CHECK(layout == 32 || layout == 16, "mikmeans: layout must be 32 or 16");
+  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, K, (int)layout) == Kpad, "mikmeans: bad Kpad");
   TORCH_CHECK(D <= dpad, "mikmeans: D > dpad");
   check_cuda(pack, "pack");
   TORCH_CHECK(pack.is_contiguous() && pack.numel() >= Kpad * dpad, "mikmeans: pack too small");
@@ -179,6 +183,7 @@ void finalize(int64_t mode, const c10::optional<Tensor>& packed, const Tensor& C
   a.pack = pack.data_ptr(); a.cn = cn.data_ptr<float>();
   a.shift = opt_ptr<float>(shift); a.counts_out = opt_ptr<float>(counts);
   a.mode = (int)mode;
+  a.layout = (int)layout;
   hip_check(mk::launch_finalize(a, stream()), "finalize");
 }
 
@@ -331,7 +336,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("kpp_sample", &kpp_sample, "k-means++ D^2 sampling (K6)");
   m.def("blob_centers", &blob_centers, "Philox blob centres");
   m.def("blobs", &blobs, "Philox Gaussian blobs (K8)");
-  m.def("assign_kpad", [](int64_t dt, int64_t dpad, int64_t K) { return mk::assign_kpad((int)dt, (int)dpad, (int)K); });
+  m.def("assign_kpad", [](int64_t dt, int64_t dpad, int64_t K, int64_t layout) {
+    return mk::assign_kpad((int)dt, (int)dpad, (int)K, (int)layout); });
+  m.def("assign16_supported", [](int64_t dt, int64_t dpad) { return mk::assign16_chunk_tiles((int)dt, (int)dpad) > 0; });
+  m.def("set_assign16_gt", [](int64_t gt) { mk::set_assign16_gt((int)gt); }, "tuning: 16x16 epilogue tile group");
   m.def("assign_chunk_tiles", [](int64_t dt, int64_t dpad) { return mk::assign_chunk_tiles((int)dt, (int)dpad); });
   m.def("assign_cn_len", [](int64_t kpad) { return mk::assign_cn_len((int)kpad); });
   m.def("update_slice_width", [](int64_t dt, int64_t K, int64_t D) { return mk::update_slice_width((int)dt, (int)K, (int)D); });

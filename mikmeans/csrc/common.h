@@ -110,6 +110,12 @@ __device__ __forceinline__ int wave_sum(int v) {
   return v;
 }
 
+// argmin key: a score with a 4-bit index in its low mantissa bits (relative
+// resolution 2^-19), so one v_min3_f32 tree yields (min score, index).
+__device__ __forceinline__ float pack_key(float s, int r) {
+  return __uint_as_float((__float_as_uint(s) & ~15u) | (unsigned)r);
+}
+
 // Row index of accumulator register `reg` for lane half `h` in the 32x32 MFMA C/D map.
 __device__ __forceinline__ int mfma32_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 

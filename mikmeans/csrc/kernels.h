@@ -26,8 +26,12 @@ constexpr int SLOT_STRIDE = 8;
 // The stored value is -2*c (exact in bf16/f32) and cn[k] = |c_q|^2 of the
 // quantised centroid, so the MFMA chain seeded with cn directly yields
 // score = |c|^2 - 2 x.c  (= |x-c|^2 - |x|^2).
-int assign_chunk_tiles(int dtype, int dpad);  // centroid tiles per LDS chunk (CT)
-int assign_kpad(int dtype, int dpad, int K);  // K rounded up to a multiple of 32*CT
+// Layout "16" (assign16.hip) is the same idea on 16-centroid tiles for the
+// 16x16 MFMA shape.  The layout is chosen per fit and must match between the
+// finalize (packing) and assign launches.
+int assign_chunk_tiles(int dtype, int dpad);  // centroid tiles per LDS chunk (CT), layout 32
+int assign16_chunk_tiles(int dtype, int dpad);  // layout 16 (0 = unsupported)
+int assign_kpad(int dtype, int dpad, int K, int layout = 32);  // K rounded to a chunk multiple
 int assign_cn_len(int kpad);                  // cn array length (multiple of 256 floats)
 
 struct AssignArgs {
@@ -40,6 +44,8 @@ struct AssignArgs {
   int track_changed;
 };
 hipError_t launch_assign(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
+hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
+void set_assign16_gt(int gt);  // tiles per epilogue group of the 16x16 variant (0 = default)
 void set_assign_p(int p);  // 32-point blocks per wave (0 = default)
 int get_assign_p();
 
@@ -82,6 +88,7 @@ struct FinalizeArgs {
   float* shift;           // optional [K]
   float* counts_out;      // optional [K]
   int mode;
+  int layout;             // 32 or 16 (packed-centroid layout of the assign variant)
 };
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 

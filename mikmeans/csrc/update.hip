@@ -31,8 +31,11 @@
 
 namespace mk {
 
-constexpr int UPD_NT = 512;
-constexpr int UPD_UNROLL = 4;
+// One workgroup per CU (LDS-bound): 16 waves x 8 rows in flight per lane keeps
+// ~128 KiB of loads outstanding per CU (PMC: 8 waves x 4 rows left the kernel
+// waiting on memory 56% of its wave-cycles).
+constexpr int UPD_NT = 1024;
+constexpr int UPD_UNROLL = 8;
 constexpr size_t UPD_LDS_MAX = 160 * 1024;
 
 template <int BYTES> struct LoadT;

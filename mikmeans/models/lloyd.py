@@ -97,16 +97,15 @@ class LloydEngine:
 
     # ------------------------------------------------------------------ setup
     def _init_gpu(self):
+        from ..ops import CentroidPack
+
         C = native.require()
         self._C = C
         self.dt = native.dtype_code(self.dtype)
-        self.dpad = native.dpad_for(self.Dp, self.dtype)
-        if self.dpad == 0:
+        if native.dpad_for(self.Dp, self.dtype) == 0:
             raise NotImplementedError(f"mikmeans: the GPU engine supports D <= 256 (got {self.D})")
-        self.Kpad = C.assign_kpad(self.dt, self.dpad, self.K)
         dev = self.device
-        self.pack = torch.zeros(self.Kpad * self.dpad, dtype=self.dtype, device=dev)
-        self.cn = torch.zeros(C.assign_cn_len(self.Kpad), dtype=torch.float32, device=dev)
+        self.pk = CentroidPack(self.K, self.Dp, self.dtype, dev)
         self.slots = torch.zeros(C.NSLOT * C.SLOT_STRIDE, dtype=torch.float64, device=dev)
         self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, max(self.n, 1))
         self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.int64, device=dev)
@@ -128,8 +127,7 @@ class LloydEngine:
         self.C.zero_()
         self.C[:, : self.D] = c
         if self.gpu:
-            self._C.finalize(0, None, self.C, None, None, None, self.pack, self.cn, None, None,
-                             self.dpad, self.Kpad)
+            self.pk.finalize(0, None, self.C)
         return self
 
     @property
@@ -150,8 +148,7 @@ class LloydEngine:
         C = self._C
         KD = self.K * self.Dp
         if self.n:
-            C.assign(self.X, self.pack, self.cn, self.xn, self.labels, self.mind, self.slots,
-                     self.Kpad, self.dpad, True)
+            self.pk.assign(self.X, self.xn, self.labels, self.mind, self.slots, True)
             C.update(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks, self.weights,
                      self.sum_exp, self.cnt_exp)
             C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
@@ -162,8 +159,7 @@ class LloydEngine:
             self.packed.zero_()
         self.comm.allreduce_(self.packed)
         self._relocate_empty()
-        C.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.pack, self.cn,
-                   self.shift, self.counts, self.dpad, self.Kpad)
+        self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts)
 
     def _step_cpu(self):
         K, Dp = self.K, self.Dp
@@ -228,7 +224,7 @@ class LloydEngine:
 
     def _assign_into(self, mind):
         labels = torch.empty_like(self.labels)
-        self._C.assign(self.X, self.pack, self.cn, self.xn, labels, mind, None, self.Kpad, self.dpad, False)
+        self.pk.assign(self.X, self.xn, labels, mind)
 
     def last_stats(self) -> IterStats:
         """Host read of the last iteration's scalars (one small D2H copy)."""
@@ -268,8 +264,7 @@ class LloydEngine:
             mind = torch.empty(self.n, dtype=torch.float32, device=self.device) if with_dist else None
             if self.n:
                 xn = self.xn if with_dist else None
-                self._C.assign(self.X, self.pack, self.cn, xn, labels, mind, None, self.Kpad,
-                               self.dpad, False)
+                self.pk.assign(self.X, xn, labels, mind)
             return labels, mind
         return cpu_ops.assign(self.X, self.C, with_dist=with_dist, xn=self.xn)
 

@@ -46,13 +46,12 @@ class MiniBatchEngine:
             C = native.require()
             self._C = C
             self.dt = native.dtype_code(dtype)
-            self.dpad = native.dpad_for(self.Dp, dtype)
-            if self.dpad == 0:
+            if native.dpad_for(self.Dp, dtype) == 0:
                 raise NotImplementedError("mikmeans: GPU mini-batch supports D <= 256")
-            self.Kpad = C.assign_kpad(self.dt, self.dpad, self.K)
+            from ..ops import CentroidPack
+
             dev = self.device
-            self.pack = torch.zeros(self.Kpad * self.dpad, dtype=dtype, device=dev)
-            self.cn = torch.zeros(C.assign_cn_len(self.Kpad), dtype=torch.float32, device=dev)
+            self.pk = CentroidPack(self.K, self.Dp, dtype, dev)
             self.slots = torch.zeros(C.NSLOT * C.SLOT_STRIDE, dtype=torch.float64, device=dev)
             self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, self.batch)
             self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.int64, device=dev)
@@ -69,8 +68,7 @@ class MiniBatchEngine:
         if counts is not None:
             self.vcount.copy_(torch.as_tensor(counts, dtype=torch.float64))
         if self.gpu:
-            self._C.finalize(0, None, self.C, None, None, None, self.pack, self.cn, None, None,
-                             self.dpad, self.Kpad)
+            self.pk.finalize(0, None, self.C)
 
     @property
     def centers(self):
@@ -102,15 +100,15 @@ class MiniBatchEngine:
         if b:
             xn, lab = self.xn[:b], self.labels[:b]
             C.row_sqnorm(Xb, xn)
-            C.assign(Xb, self.pack, self.cn, xn, lab, None, self.slots, self.Kpad, self.dpad, False)
+            self.pk.assign(Xb, xn, lab, None, self.slots, False)
             C.update(Xb, lab, self.K, self.slab, self.cnt_slab, self.n_chunks, None, self.sum_exp, 0)
             C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
                      self.sum_exp, 0)
         else:
             self.packed.zero_()
         self.comm.allreduce_(self.packed)
-        C.finalize(2, self.packed, self.C, self.Cnew, self.frozen, self.vcount, self.pack, self.cn,
-                   self.shift, self.counts, self.dpad, self.Kpad)
+        self.pk.finalize(2, self.packed, self.C, self.Cnew, self.frozen, self.vcount, self.shift,
+                         self.counts)
 
     def _step_cpu(self, Xb):
         K, Dp = self.K, self.Dp

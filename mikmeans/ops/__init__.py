@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 
 from . import cpu
-from .native import available, dpad_for, dtype_code, require, vec_elems
+from .native import available, dpad_for, dtype_code, preferred_layout, require, vec_elems
 
 __all__ = [
     "available",
@@ -66,26 +66,39 @@ class CentroidPack:
     rows between K and Kpad.
     """
 
-    def __init__(self, K: int, D: int, dtype: torch.dtype, device):
+    def __init__(self, K: int, D: int, dtype: torch.dtype, device, layout: int | None = None):
         C = require()
+        self._C = C
         self.K, self.D, self.dtype = K, D, dtype
         self.dpad = dpad_for(D, dtype)
         if self.dpad == 0:
             raise NotImplementedError(f"mikmeans: GPU assign supports D <= 256 (got {D})")
         self.dt = dtype_code(dtype)
-        self.Kpad = C.assign_kpad(self.dt, self.dpad, K)
+        self.layout = layout or preferred_layout(dtype, self.dpad)
+        self.Kpad = C.assign_kpad(self.dt, self.dpad, K, self.layout)
         self.pack = torch.zeros(self.Kpad * self.dpad, dtype=dtype, device=device)
         self.cn = torch.zeros(C.assign_cn_len(self.Kpad), dtype=torch.float32, device=device)
 
     def load(self, centers: torch.Tensor) -> "CentroidPack":
-        C = require()
         c = centers.to(device=self.pack.device, dtype=torch.float32).contiguous()
         assert c.shape == (self.K, self.D), (c.shape, self.K, self.D)
-        C.finalize(0, None, c, None, None, None, self.pack, self.cn, None, None, self.dpad, self.Kpad)
+        self.finalize(0, None, c)
         return self
 
+    def finalize(self, mode: int, packed, Cold, Cnew=None, frozen=None, mb_counts=None, shift=None,
+                 counts=None):
+        """K4: new centres from the all-reduced message (mode 1 Lloyd, 2 mini-batch) or
+        pack-only (mode 0); always re-packs ``-2c`` / ``|c|^2`` for the next assign."""
+        self._C.finalize(mode, packed, Cold, Cnew, frozen, mb_counts, self.pack, self.cn, shift, counts,
+                         self.dpad, self.Kpad, self.layout)
 
-def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True):
+    def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False):
+        """K2 on these centres (``X`` column-padded, 16-B rows)."""
+        self._C.assign(X, self.pack, self.cn, xn, labels, mind, slots, self.Kpad, self.dpad,
+                       track_changed, self.layout)
+
+
+def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True, layout: int | None = None):
     """Nearest centroid of every row: returns ``(labels int32, sqdist float32 or None)``.
 
     bf16 points are compared against bf16-quantised centroids (scores
@@ -98,7 +111,7 @@ def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True):
     D = Xp.shape[1]
     cen = torch.zeros((centers.shape[0], D), dtype=torch.float32, device=X.device)
     cen[:, : centers.shape[1]] = centers.to(device=X.device, dtype=torch.float32)
-    pk = CentroidPack(cen.shape[0], D, Xp.dtype, X.device).load(cen)
+    pk = CentroidPack(cen.shape[0], D, Xp.dtype, X.device, layout=layout).load(cen)
     n = Xp.shape[0]
     labels = torch.empty(n, dtype=torch.int32, device=X.device)
     xn = mind = None
@@ -106,7 +119,7 @@ def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True):
         xn = torch.empty(n, dtype=torch.float32, device=X.device)
         C.row_sqnorm(Xp, xn)
         mind = torch.empty(n, dtype=torch.float32, device=X.device)
-    C.assign(Xp, pk.pack, pk.cn, xn, labels, mind, None, pk.Kpad, pk.dpad, False)
+    pk.assign(Xp, xn, labels, mind)
     return labels, mind
 
 

@@ -73,6 +73,20 @@ def dpad_for(D: int, dtype: torch.dtype) -> int:
     return d if d <= 256 else 0
 
 
+def preferred_layout(dtype: torch.dtype, dpad: int) -> int:
+    """Assign-kernel variant (MFMA tile rows): 32 (32x32 MFMA, assign.hip) or 16
+    (16x16 MFMA, assign16.hip).  ``MIKMEANS_ASSIGN_LAYOUT`` overrides."""
+    env = os.environ.get("MIKMEANS_ASSIGN_LAYOUT")
+    m = require()
+    ok16 = m.assign16_supported(dtype_code(dtype), dpad)
+    if env in ("16", "32"):
+        return 16 if env == "16" and ok16 else 32
+    return DEFAULT_LAYOUT if (DEFAULT_LAYOUT == 32 or ok16) else 32
+
+
+DEFAULT_LAYOUT = 32
+
+
 def loaded_path() -> str | None:
     m = _load()
     return getattr(m, "__file__", None) if m is not None else None

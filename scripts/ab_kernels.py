@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="2,4")
+    ap.add_argument("--variants", default="32p2,32p4,16g1,16g2,16g4")
     a = ap.parse_args()
 
     from mikmeans.data.blobs import make_blobs
@@ -36,21 +36,34 @@ def main():
     eng = LloydEngine(X, a.k).set_centers(X[: a.k].float())
     eng.step()
     torch.cuda.synchronize()
-    variants = [int(v) for v in a.variants.split(",")]
-    res = {f"assign_p{v}": [] for v in variants}
+    # variants: "32pP" = 32x32 MFMA with P point-blocks per wave; "16gG" = 16x16 MFMA, G tiles/epilogue
+    from mikmeans.ops import CentroidPack
+
+    variants = a.variants.split(",")
+    packs = {}
+    for v in variants:
+        lay = 16 if v.startswith("16") else 32
+        if lay not in packs:
+            packs[lay] = CentroidPack(a.k, eng.Dp, dt, "cuda", layout=lay).load(eng.C[:, : eng.Dp])
+    res = {f"assign_{v}": [] for v in variants}
     res["update"] = []
     res["step"] = []
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     for _ in range(a.rounds):
         for v in variants:
-            C.set_assign_p(v)
+            lay = 16 if v.startswith("16") else 32
+            if lay == 32:
+                C.set_assign_p(int(v.split("p")[1]))
+            else:
+                C.set_assign16_gt(int(v.split("g")[1]))
             e0, e1 = ev(), ev()
             e0.record()
-            C.assign(eng.X, eng.pack, eng.cn, eng.xn, eng.labels, None, eng.slots, eng.Kpad, eng.dpad, True)
+            packs[lay].assign(eng.X, eng.xn, eng.labels, None, eng.slots, True)
             e1.record()
             torch.cuda.synchronize()
-            res[f"assign_p{v}"].append(e0.elapsed_time(e1))
+            res[f"assign_{v}"].append(e0.elapsed_time(e1))
         C.set_assign_p(0)
+        C.set_assign16_gt(0)
         e0, e1 = ev(), ev()
         e0.record()
         C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks, None, eng.sum_exp, 0)

@@ -43,11 +43,27 @@ def test_row_sqnorm(native, dtype, n, d):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n,d,k", [(1000, 2, 3), (513, 16, 37), (20000, 128, 256), (9000, 128, 1024),
                                    (4096, 64, 4096), (3000, 256, 512), (255, 100, 70), (70000, 32, 9)])
-def test_assign_matches_reference(native, dtype, n, d, k):
+@pytest.mark.parametrize("layout", [32, 16])
+def test_assign_matches_reference(native, dtype, n, d, k, layout):
     X = _points(n, d, dtype, seed=k)
     C = _points(k, d, torch.float32, seed=k + 1)
-    labels, mind = ops.assign(X.to(DEV), C.to(DEV), with_dist=True)
+    dp = ops.dpad_for(ops.pad_columns(X[:1]).shape[1], dtype)
+    if layout == 16 and not native.assign16_supported(ops.dtype_code(dtype), dp):
+        pytest.skip("16x16 variant needs DPAD/4 >= one 16-byte piece")
+    labels, mind = ops.assign(X.to(DEV), C.to(DEV), with_dist=True, layout=layout)
     _check_assign(X, C, labels, mind, rel=2e-5 if dtype == torch.float32 else 3e-5)
+
+
+@pytest.mark.parametrize("gt", [1, 2, 4])
+def test_assign16_tile_groups(native, gt):
+    X = _points(7000, 128, torch.bfloat16, seed=gt)
+    C = _points(1000, 128, torch.float32, seed=gt + 7)
+    native.set_assign16_gt(gt)
+    try:
+        labels, mind = ops.assign(X.to(DEV), C.to(DEV), with_dist=True, layout=16)
+    finally:
+        native.set_assign16_gt(0)
+    _check_assign(X, C, labels, mind, rel=3e-5)
 
 
 def test_assign_exact_f32_small_ints(native):
