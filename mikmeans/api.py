@@ -32,9 +32,12 @@ from .parallel.comm import Comm, get_comm
 from .utils import metrics as mmetrics
 
 
-def _default_device(device):
+def _default_device(device, X=None):
+    """Explicit device > the input tensor's device > cuda when available > cpu."""
     if device is not None:
         return torch.device(device)
+    if X is not None and torch.is_tensor(X):
+        return X.device
     return torch.device("cuda" if torch.cuda.is_available() else "cpu")
 
 
@@ -107,7 +110,7 @@ class KMeans:
     # ------------------------------------------------------------------- fit
     def fit(self, X, y=None, sample_weight=None, *, resume_from=None):
         comm = self.comm or get_comm()
-        device = _default_device(self.device) if self.device is not None or comm.world == 1 else comm.device
+        device = _default_device(self.device, X) if self.device is not None or comm.world == 1 else comm.device
         Xt, was_numpy = _to_tensor(X, device, self.dtype)
         self._numpy_io = was_numpy
         D = Xt.shape[1]
@@ -297,7 +300,7 @@ class MiniBatchKMeans:
     def fit(self, X):
         """Fit on a tensor/array (random batches each step; ``max_iter`` epochs)."""
         comm = self.comm or get_comm()
-        device = _default_device(self.device) if self.device is not None or comm.world == 1 else comm.device
+        device = _default_device(self.device, X) if self.device is not None or comm.world == 1 else comm.device
         Xt, was_numpy = _to_tensor(X, device, self.dtype)
         self._numpy_io = was_numpy
         n, D = Xt.shape
@@ -329,7 +332,7 @@ class MiniBatchKMeans:
 
     def partial_fit(self, Xb):
         comm = self.comm or get_comm()
-        device = _default_device(self.device) if self.device is not None or comm.world == 1 else comm.device
+        device = _default_device(self.device, Xb) if self.device is not None or comm.world == 1 else comm.device
         Xt, _ = _to_tensor(Xb, device, self.dtype)
         eng = self._engine(Xt.shape[1], device)
         if not hasattr(self, "cluster_centers_"):
@@ -385,7 +388,7 @@ def kmeans_plusplus(X, n_clusters: int, *, seed: int = 0, n_local_trials=None, c
                     dtype="float32", device=None):
     """k-means++ seeding only; returns the ``[K, D]`` initial centres."""
     comm = comm or get_comm()
-    dev = _default_device(device)
+    dev = _default_device(device, X)
     Xt, was_numpy = _to_tensor(X, dev, resolve_dtype(dtype))
     D = Xt.shape[1]
     Xp = pad_columns(Xt) if Xt.is_cuda else Xt

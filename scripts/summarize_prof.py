@@ -12,7 +12,7 @@ from collections import defaultdict
 
 
 def kernel_stats(d):
-    fs = sorted(glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True))
+    fs = sorted(glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True), key=os.path.getmtime)
     if not fs:
         return None
     rows = list(csv.DictReader(open(fs[-1])))
@@ -24,7 +24,7 @@ def kernel_stats(d):
 
 
 def pmc(d):
-    fs = sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True))
+    fs = sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True), key=os.path.getmtime)
     if not fs:
         return None
     agg = defaultdict(lambda: defaultdict(float))
