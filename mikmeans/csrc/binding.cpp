@@ -265,7 +265,8 @@ void js_number(double v, std::string& out) {
   if (v == 0.0) { out += '0'; return; }
   if (v < 0) { out += '-'; v = -v; }
   char buf[64];
-  auto res = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::scientific);
+  auto res = std::to_chars(buf, buf + sizeof(buf) - 1, v, std::chars_format::scientific);
+  *res.ptr = '\0';  // atoi below must stop at the exponent's last digit
   // buf = d[.ddd]e(+|-)XX
   std::string digits;
   char* p = buf;

@@ -103,9 +103,9 @@ class Comm:
         """Stack ``t`` from every rank: shape ``[world, *t.shape]``."""
         if self.world == 1:
             return t.unsqueeze(0).clone()
-        out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous())
-        return out
+        flat = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(flat, t.contiguous().reshape(-1))  # gloo wants flat buffers
+        return flat.view(self.world, *t.shape)
 
     def all_gather_object(self, obj):
         if self.world == 1:

@@ -1,0 +1,179 @@
+"""CPU path: Lloyd / k-means++ / mini-batch / API against scikit-learn and invariants."""
+import numpy as np
+import pytest
+import torch
+
+import mikmeans
+from mikmeans.data import blobs as B
+from mikmeans.models.init import floyd_sample, init_kmeanspp
+from mikmeans.models.lloyd import LloydEngine, tol_to_abs
+from mikmeans.parallel import Comm, plan, shard_range, shard_sizes
+
+sk_cluster = pytest.importorskip("sklearn.cluster")
+
+
+def blobs(n=3000, d=8, k=5, seed=1):
+    return B.make_blobs(n, d, k, seed=seed, return_labels=True)
+
+
+def test_config1_parity_with_sklearn():
+    """BASELINE config 1: N=1000, D=2, K=3 fp32 on the CPU path."""
+    X, _ = blobs(1000, 2, 3, seed=3)
+    init = X[:3].numpy()
+    km = mikmeans.KMeans(3, init=init, max_iter=100, tol=1e-4, device="cpu").fit(X.numpy())
+    sk = sk_cluster.KMeans(3, init=init, n_init=1, max_iter=100, tol=1e-4, algorithm="lloyd").fit(X.numpy())
+    assert np.array_equal(km.labels_, sk.labels_)
+    np.testing.assert_allclose(km.cluster_centers_.numpy(), sk.cluster_centers_, rtol=1e-5, atol=1e-5)
+    assert km.inertia_ == pytest.approx(sk.inertia_, rel=1e-5)
+    assert isinstance(km.labels_, np.ndarray) or torch.is_tensor(km.labels_)
+
+
+def test_lloyd_engine_matches_sklearn_iterates():
+    X, _ = blobs(5000, 16, 20, seed=5)
+    init = X[:20].numpy().copy()
+    eng = LloydEngine(X, 20).set_centers(torch.from_numpy(init))
+    eng.run(7, tol=-1, check_every=1)
+    sk = sk_cluster.KMeans(20, init=init, n_init=1, max_iter=7, tol=0, algorithm="lloyd").fit(X.numpy())
+    np.testing.assert_allclose(eng.centers.numpy(), sk.cluster_centers_, rtol=1e-5, atol=1e-5)
+
+
+def test_functional_fit_predict_numpy_io():
+    X, y = blobs()
+    C, lab = mikmeans.fit(X.numpy(), 5, device="cpu", seed=0)
+    assert isinstance(C, np.ndarray) and C.shape == (5, 8)
+    lab2 = mikmeans.predict(X.numpy(), C)
+    assert isinstance(lab2, np.ndarray)
+    assert np.array_equal(lab, lab2)
+    from sklearn.metrics import adjusted_rand_score
+
+    assert adjusted_rand_score(y.numpy(), lab) > 0.99
+
+
+def test_kmeans_methods_and_metrics():
+    X, _ = blobs()
+    km = mikmeans.KMeans(5, device="cpu", seed=0).fit(X)
+    assert km.predict(X).dtype == torch.int32
+    d = km.transform(X[:10])
+    assert d.shape == (10, 5)
+    assert km.score(X) == pytest.approx(-km.inertia_, rel=1e-5)
+    m = km.metrics()
+    assert m["k"] == 5 and sum(m["counts"]) == 3000 and m["balance"]["gap"] == max(m["counts"]) - min(m["counts"])
+    assert km.n_iter_ >= 1 and km.converged_
+
+
+def test_sample_weight_matches_sklearn():
+    X, _ = blobs(2000, 4, 4, seed=9)
+    w = np.random.default_rng(0).uniform(0.1, 2.0, 2000).astype(np.float32)
+    init = X[:4].numpy()
+    km = mikmeans.KMeans(4, init=init, max_iter=50, tol=0, device="cpu").fit(X.numpy(), sample_weight=w)
+    sk = sk_cluster.KMeans(4, init=init, n_init=1, max_iter=50, tol=0, algorithm="lloyd").fit(
+        X.numpy(), sample_weight=w)
+    np.testing.assert_allclose(km.cluster_centers_.numpy(), sk.cluster_centers_, rtol=1e-4, atol=1e-4)
+    assert km.inertia_ == pytest.approx(sk.inertia_, rel=1e-4)
+
+
+def test_frozen_and_empty_policies():
+    X, _ = blobs(1000, 2, 2, seed=2)
+    far = np.array([[1e4, 1e4]], dtype=np.float32)
+    init = np.concatenate([X[:2].numpy(), far])
+    km = mikmeans.KMeans(3, init=init, frozen=[0, 0, 1], max_iter=20, device="cpu").fit(X)
+    np.testing.assert_array_equal(km.cluster_centers_[2].numpy(), far[0])
+    keep = mikmeans.KMeans(3, init=init, max_iter=20, device="cpu").fit(X)
+    assert keep.counts_[2] == 0  # empty centre stays put
+    np.testing.assert_array_equal(keep.cluster_centers_[2].numpy(), far[0])
+    moved = mikmeans.KMeans(3, init=init, max_iter=20, empty_cluster="farthest", device="cpu").fit(X)
+    assert moved.counts_.min() > 0
+
+
+def test_n_init_keeps_best():
+    X, _ = blobs(3000, 4, 8, seed=4)
+    one = mikmeans.KMeans(8, init="random", n_init=1, seed=0, device="cpu").fit(X)
+    many = mikmeans.KMeans(8, init="random", n_init=5, seed=0, device="cpu").fit(X)
+    assert many.inertia_ <= one.inertia_ + 1e-6
+
+
+def test_floyd_sample_distinct_and_deterministic():
+    rng = np.random.default_rng(3)
+    s = floyd_sample(10**9, 1000, rng)
+    assert len(set(s.tolist())) == 1000 and s.min() >= 0 and s.max() < 10**9
+    assert np.array_equal(s, floyd_sample(10**9, 1000, np.random.default_rng(3)))
+    with pytest.raises(ValueError):
+        floyd_sample(5, 6, rng)
+
+
+@pytest.mark.parametrize("trials", [1, 3])
+def test_kmeanspp_cpu(trials):
+    X, _ = blobs(4000, 8, 10, seed=6)
+    C = init_kmeanspp(X, 8, 10, 4000, 0, Comm.local(), seed=5, n_local_trials=trials)
+    d = ((C[:, None, :] - X[None]) ** 2).sum(-1).min(1).values
+    assert float(d.max()) == 0.0          # every centre is a data row
+    assert len(set(map(tuple, C.numpy().round(4).tolist()))) == 10
+    C2 = init_kmeanspp(X, 8, 10, 4000, 0, Comm.local(), seed=5, n_local_trials=trials)
+    assert torch.equal(C, C2)
+
+
+def test_kmeanspp_beats_random_on_blobs():
+    X, _ = blobs(6000, 8, 30, seed=8)
+    a = mikmeans.KMeans(30, init="k-means++", max_iter=1, tol=-1, seed=0, device="cpu").fit(X).inertia_
+    b = mikmeans.KMeans(30, init="random", max_iter=1, tol=-1, seed=0, device="cpu").fit(X).inertia_
+    assert a < b
+
+
+def test_minibatch_cpu_converges():
+    X, y = blobs(20000, 8, 6, seed=10)
+    mb = mikmeans.MiniBatchKMeans(6, batch_size=1024, max_iter=5, device="cpu", seed=0).fit(X)
+    full = mikmeans.KMeans(6, device="cpu", seed=0).fit(X)
+    assert mb.score(X) >= 1.05 * full.score(X)   # scores are negative inertias
+    assert mb.n_steps_ > 0 and float(mb.counts_.sum()) == pytest.approx(mb.n_steps_ * 1024)
+
+
+def test_minibatch_partial_fit_stream():
+    stream = B.BlobStream(10**6, 8, 5, 512, seed=1)
+    mb = mikmeans.MiniBatchKMeans(5, batch_size=512, device="cpu")
+    mb.fit_stream(stream, steps=20)
+    X, _ = blobs(2000, 8, 5, seed=1)
+    assert np.isfinite(mb.score(X))
+
+
+def test_tol_scaling():
+    X, _ = blobs(1000, 4, 3)
+    var = X.double().var(0, unbiased=False).mean().item()
+    assert tol_to_abs(1e-4, X, Comm.local(), 1000) == pytest.approx(1e-4 * var, rel=1e-6)
+    assert tol_to_abs(-1, X, Comm.local(), 1000) == float("-inf")
+
+
+def test_blobs_shard_invariance():
+    C = B.blob_centers_np(7, 5, 10.0, 3)
+    whole = B.blobs_np(0, 1000, C, 1.0, 3)
+    parts = np.concatenate([B.blobs_np(s, e - s, C, 1.0, 3) for s, e in (shard_range(1000, r, 3) for r in range(3))])
+    assert np.array_equal(whole, parts)
+
+
+def test_shard_plan():
+    assert shard_sizes(10, 3) == [4, 3, 3]
+    assert [shard_range(10, r, 3) for r in range(3)] == [(0, 4), (4, 7), (7, 10)]
+    p = plan(10**8, 128, 1024, world=1, itemsize=2)
+    assert p.fits and p.bytes_points == 25_600_000_000
+    big = plan(10**9, 256, 512, world=1, itemsize=2)
+    assert not big.fits and big.batch_rows > 0
+    assert plan(10**9, 256, 512, world=8, itemsize=2).fits
+
+
+def test_config_roundtrip_and_argparse():
+    import argparse
+
+    cfg = mikmeans.KMeansConfig(n_clusters=7, dtype="bf16", max_iter=3)
+    km = mikmeans.KMeans.from_config(cfg)
+    assert km.n_clusters == 7 and km.dtype == torch.bfloat16
+    ap = mikmeans.KMeansConfig.add_arguments(argparse.ArgumentParser())
+    ns = ap.parse_args(["--n-clusters", "4", "--init", "random", "--tol", "0"])
+    c2 = mikmeans.KMeansConfig.from_args(ns)
+    assert c2.n_clusters == 4 and c2.init == "random" and c2.tol == 0.0
+    assert mikmeans.KMeansConfig.from_dict(c2.to_dict()) == c2
+
+
+def test_bf16_cpu_path_quantises_like_kernel():
+    X, _ = blobs(2000, 8, 4, seed=12)
+    km = mikmeans.KMeans(4, dtype="bfloat16", device="cpu", seed=0).fit(X)
+    assert km.cluster_centers_.dtype == torch.float32
+    assert np.isfinite(km.inertia_)

@@ -1,0 +1,136 @@
+"""Data-parallel correctness on CPU ranks (gloo): W ranks must reproduce the 1-rank result.
+
+Same code paths as the RCCL/xGMI GPU job (packed f64 all-reduce per iteration,
+k-means++ owner selection, checkpoint broadcast), only the backend differs.
+"""
+import numpy as np
+import pytest
+import torch
+
+from mikmeans.parallel import shard_range
+from mikmeans.parallel.launch import spawn_local
+
+N, D, K = 6000, 8, 12
+
+
+def _data():
+    from mikmeans.data import blobs as B
+
+    return B.make_blobs(N, D, K, seed=21)
+
+
+def _lloyd(comm, init, iters):
+    from mikmeans.models.init import resolve_init
+    from mikmeans.models.lloyd import LloydEngine
+
+    X = _data()
+    s, e = shard_range(N, comm.rank, comm.world)
+    Xl = X[s:e]
+    C0 = resolve_init(init, Xl, D, K, N, s, comm, seed=3)
+    eng = LloydEngine(Xl, K, comm=comm).set_centers(C0)
+    eng.run(iters, tol=-1, check_every=1)
+    st = eng.last_stats()
+    return {"C0": C0, "C": eng.centers.clone(), "labels": eng.labels.clone(), "inertia": st.inertia,
+            "changed": st.n_changed, "counts": eng.counts.clone()}
+
+
+def _single(init, iters):
+    from mikmeans.parallel import Comm
+
+    return _lloyd(Comm.local(), init, iters)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("init", ["random", "k-means++"])
+def test_lloyd_dp_equals_single_rank(world, init):
+    ref = _single(init, 6)
+    outs = spawn_local(_lloyd, world, init, 6)
+    for o in outs:  # centroids are replicated bit-identically on every rank
+        assert torch.equal(o["C"], outs[0]["C"])
+        assert torch.equal(o["C0"], ref["C0"])
+    torch.testing.assert_close(outs[0]["C"], ref["C"], rtol=1e-5, atol=1e-5)
+    assert torch.equal(torch.cat([o["labels"] for o in outs]), ref["labels"])
+    assert outs[0]["inertia"] == pytest.approx(ref["inertia"], rel=1e-9)
+    assert outs[0]["changed"] == ref["changed"]
+    assert torch.equal(outs[0]["counts"], ref["counts"])
+
+
+def _fit_api(comm):
+    import mikmeans
+
+    X = _data()
+    s, e = shard_range(N, comm.rank, comm.world)
+    km = mikmeans.KMeans(K, comm=comm, device="cpu", seed=1, max_iter=50).fit(X[s:e])
+    return {"C": km.cluster_centers_, "inertia": km.inertia_, "n_iter": km.n_iter_, "labels": km.labels_}
+
+
+def test_kmeans_api_distributed():
+    from mikmeans.parallel import Comm
+    import mikmeans
+
+    X = _data()
+    ref = mikmeans.KMeans(K, comm=Comm.local(), device="cpu", seed=1, max_iter=50).fit(X)
+    outs = spawn_local(_fit_api, 2)
+    torch.testing.assert_close(outs[0]["C"], ref.cluster_centers_, rtol=1e-5, atol=1e-5)
+    assert outs[0]["inertia"] == pytest.approx(ref.inertia_, rel=1e-7)
+    assert outs[0]["n_iter"] == ref.n_iter_
+    assert torch.equal(torch.cat([o["labels"] for o in outs]), ref.labels_)
+
+
+def _minibatch(comm, steps):
+    from mikmeans.data.blobs import BlobStream
+    from mikmeans.models.minibatch import MiniBatchEngine
+
+    b = 256 // comm.world
+    stream = BlobStream(10**6, D, K, b, seed=4, rank=comm.rank, world=comm.world)
+    eng = MiniBatchEngine(K, D, b, comm=comm)
+    from mikmeans.data.blobs import blob_centers
+
+    eng.set_centers(blob_centers(K, D, 10.0, 4) + 0.5)
+    for _ in range(steps):
+        eng.partial_fit(next(stream))
+    return {"C": eng.centers.clone(), "v": eng.vcount.clone()}
+
+
+def test_minibatch_dp_equals_single_rank():
+    from mikmeans.parallel import Comm
+
+    ref = _minibatch(Comm.local(), 10)
+    outs = spawn_local(_minibatch, 2, 10)
+    torch.testing.assert_close(outs[0]["C"], ref["C"], rtol=1e-5, atol=1e-5)
+    assert torch.equal(outs[0]["v"], ref["v"])
+
+
+def _ckpt(comm, path):
+    from mikmeans.utils.checkpoint import load_checkpoint, save_checkpoint
+
+    C = torch.arange(12, dtype=torch.float32).reshape(3, 4) * (1 + comm.rank)  # only rank 0's is saved
+    save_checkpoint(path, C, 7, {"n_clusters": 3}, comm=comm)
+    st = load_checkpoint(path, comm=comm)
+    return {"C": st["centers"], "it": st["iteration"], "world": st["world_size"]}
+
+
+def test_checkpoint_broadcast(tmp_path):
+    outs = spawn_local(_ckpt, 2, str(tmp_path / "ck"))
+    for o in outs:
+        assert torch.equal(o["C"], torch.arange(12, dtype=torch.float32).reshape(3, 4))
+        assert o["it"] == 7 and o["world"] == 2
+
+
+def _collectives(comm):
+    t = torch.tensor([float(comm.rank + 1)], dtype=torch.float64)
+    comm.allreduce_(t)
+    m = torch.tensor([float(comm.rank)])
+    comm.allreduce_max_(m)
+    g = comm.all_gather(torch.tensor([comm.rank, 10 * comm.rank]))
+    o = comm.all_gather_object({"r": comm.rank})
+    b = comm.broadcast_object("hello" if comm.rank == 0 else None)
+    comm.barrier()
+    return {"sum": t.item(), "max": m.item(), "g": g, "o": [x["r"] for x in o], "b": b}
+
+
+def test_comm_collectives_world4():
+    outs = spawn_local(_collectives, 4)
+    for o in outs:
+        assert o["sum"] == 10 and o["max"] == 3 and o["b"] == "hello"
+        assert o["g"].tolist() == [[0, 0], [1, 10], [2, 20], [3, 30]] and o["o"] == [0, 1, 2, 3]
