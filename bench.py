@@ -105,6 +105,8 @@ def main(argv=None):
             mfma_tflops=2.0 * N * K * D * value / 1e12,
             inertia=st.inertia,
             n_changed=st.n_changed,
+            phase_ms=_phase_breakdown(eng),  # one extra, untimed, event-instrumented iteration
+            assign_layout=eng.pk.layout,
         )
     if comm.rank == 0:
         out = {
@@ -133,6 +135,28 @@ def main(argv=None):
         }
         print(json.dumps(out), flush=True)
     comm.close()
+
+
+def _phase_breakdown(eng) -> dict:
+    """Per-phase device time of one Lloyd iteration (rank-local; after the timed region)."""
+    C = eng._C
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    ev[0].record()
+    eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True)
+    ev[1].record()
+    C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks, eng.weights, eng.sum_exp,
+             eng.cnt_exp)
+    ev[2].record()
+    C.reduce(eng.slab, eng.cnt_slab, eng.n_chunks, eng.K, eng.Dp, eng.slots, eng.packed, eng.sum_exp,
+             eng.cnt_exp)
+    ev[3].record()
+    eng.comm.allreduce_(eng.packed)
+    ev[4].record()
+    eng.pk.finalize(1, eng.packed, eng.C, eng.Cnew, eng.frozen, None, eng.shift, eng.counts)
+    ev[5].record()
+    torch.cuda.synchronize()
+    names = ["assign", "update", "reduce", "allreduce", "finalize"]
+    return {n: round(ev[i].elapsed_time(ev[i + 1]), 4) for i, n in enumerate(names)}
 
 
 def _bench_minibatch(args, cfg, comm, dtype):
