@@ -26,7 +26,9 @@ constexpr int chunk_tiles16(int esize, int dpad) {
   return (16 * dpad * esize) >= 16384 ? 1 : 16384 / (16 * dpad * esize);
 }
 
-template <typename T, int DPAD, int P_, int GT_>
+// CT_: tiles per LDS chunk (0 = the 16 KiB default, which also fixes Kpad's
+// granule); NBUF_: ring slots (prefetch depth NBUF-1).
+template <typename T, int DPAD, int P_, int GT_, int CT_ = 0, int NBUF_ = 3>
 struct Assign16Cfg {
   static constexpr int NW = 4;
   static constexpr int P = P_;                  // 16-point blocks per wave
@@ -34,12 +36,14 @@ struct Assign16Cfg {
   static constexpr int V = Elem<T>::V;
   static constexpr int NQ = DPAD / 4 / V;       // 16-B pieces per lane per point
   static constexpr int TILE_BYTES = NQ * 1024;  // 16 centroids x DPAD
-  static constexpr int CT = chunk_tiles16(sizeof(T), DPAD);
+  static constexpr int CT = CT_ ? CT_ : chunk_tiles16(sizeof(T), DPAD);
   static constexpr int CHUNK_BYTES = CT * TILE_BYTES;
   static constexpr int PIECES = CHUNK_BYTES / 1024;
   static constexpr int NPW = PIECES / NW;
   static constexpr int PTS = NW * P * 16;
-  static constexpr int NBUF = 3;
+  static constexpr int NBUF = NBUF_;
+  static_assert(NBUF == 2 || NBUF == 3, "ring depth");
+  static_assert(chunk_tiles16(sizeof(T), DPAD) % CT == 0, "chunk must divide the Kpad granule");
   static_assert(NQ >= 1, "DPAD too small for the 16x16 layout");
   static_assert(CT % GT == 0, "tile group must divide the chunk");
   static_assert(GT * 4 <= 16, "4-bit packed index");
@@ -62,9 +66,9 @@ template <> struct Mfma16<float> {
   }
 };
 
-template <typename T, int DPAD, int P, int GT>
+template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3>
 __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
-  using C = Assign16Cfg<T, DPAD, P, GT>;
+  using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -103,7 +107,7 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
     }
   }
   wait_vmcnt<0>();  // see assign.hip: retire the fragments before the LDS-DMA loop
-  if (nch > 1) issue_chunk(1);
+  if (C::NBUF == 3 && nch > 1) issue_chunk(1);
 
   float best[C::P];
   int bg[C::P];
@@ -111,10 +115,11 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
   for (int p = 0; p < C::P; ++p) { best[p] = 3.0e38f; bg[p] = 0; }
 
   for (int c = 0; c < nch; ++c) {
-    if (c + 1 < nch) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
+    // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
+    if (C::NBUF == 3 && c + 1 < nch) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
     wait_lgkm0();
-    raw_barrier();
-    if (c + 2 < nch) issue_chunk(c + 2);
+    raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
+    if (c + C::NBUF - 1 < nch) issue_chunk(c + C::NBUF - 1);
     const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
 #pragma unroll
     for (int tg = 0; tg < C::CT / GT; ++tg) {
@@ -209,33 +214,49 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
   }
 }
 
-template <typename T, int DPAD, int P, int GT>
+template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3>
 static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
-  using C = Assign16Cfg<T, DPAD, P, GT>;
+  using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_>;
   if (a.Kpad % (16 * C::CT) != 0) return hipErrorInvalidValue;
   const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
   const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT>,
+    hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT, CT_, NBUF_>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
   if (nblk <= 0) return hipSuccess;
-  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT>), dim3((unsigned)nblk), dim3(C::NW * 64), lds, s, a);
+  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT, CT_, NBUF_>), dim3((unsigned)nblk),
+                     dim3(C::NW * 64), lds, s, a);
   return hipGetLastError();
 }
 
 static int g_assign16_gt = 0;
+static int g_assign16_cfg = 0;  // tuned-shape pipeline variant (A/B), 0 = default
 void set_assign16_gt(int gt) { g_assign16_gt = gt; }
+void set_assign16_cfg(int v) { g_assign16_cfg = v; }
 
 template <typename T, int DPAD>
 static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   constexpr int CT = chunk_tiles16(sizeof(T), DPAD);
   constexpr int NQ = DPAD / 4 / Elem<T>::V;
   constexpr int P = NQ >= 8 ? 2 : 4;  // keep the point fragments within ~64-128 VGPRs
+  if constexpr (sizeof(T) == 2 && DPAD == 128) {
+    // pipeline variants of the headline shape (occupancy vs barrier frequency):
+    //   1: GT1, 16 KiB chunks, 2 slots (36 KiB LDS at K=1024 -> 4 WGs/CU at <=128 VGPRs)
+    //   2: GT1,  8 KiB chunks, 3 slots (28 KiB)     3: GT2, 16 KiB chunks, 2 slots
+    //   4: GT2,  8 KiB chunks, 3 slots
+    switch (g_assign16_cfg) {
+      case 1: return launch16_t<T, DPAD, P, 1, 4, 2>(a, s);
+      case 2: return launch16_t<T, DPAD, P, 1, 2, 3>(a, s);
+      case 3: return launch16_t<T, DPAD, P, 2, 4, 2>(a, s);
+      case 4: return launch16_t<T, DPAD, P, 2, 2, 3>(a, s);
+      default: break;
+    }
+  }
   const int want = g_assign16_gt ? g_assign16_gt : 2;
   if (want >= 4 && CT % 4 == 0) return launch16_t<T, DPAD, P, (CT % 4 == 0 ? 4 : 1)>(a, s);
   if (want >= 2 && CT % 2 == 0) return launch16_t<T, DPAD, P, (CT % 2 == 0 ? 2 : 1)>(a, s);

@@ -46,6 +46,7 @@ struct AssignArgs {
 hipError_t launch_assign(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 void set_assign16_gt(int gt);  // tiles per epilogue group of the 16x16 variant (0 = default)
+void set_assign16_cfg(int v);  // pipeline variant of the bf16 D=128 shape (0 = default)
 void set_assign_p(int p);  // 32-point blocks per wave (0 = default)
 int get_assign_p();
 

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="32p2,32p4,16g1,16g2,16g4")
+    ap.add_argument("--variants", default="32p2,16g2,16g1v1,16g1v2,16g2v3,16g2v4")
     a = ap.parse_args()
 
     from mikmeans.data.blobs import make_blobs
@@ -55,7 +55,9 @@ def main():
             if lay == 32:
                 C.set_assign_p(int(v.split("p")[1]))
             else:
-                C.set_assign16_gt(int(v.split("g")[1]))
+                gpart = v.split("g")[1]
+                C.set_assign16_gt(int(gpart.split("v")[0]))
+                C.set_assign16_cfg(int(gpart.split("v")[1]) if "v" in gpart else 0)
             e0, e1 = ev(), ev()
             e0.record()
             packs[lay].assign(eng.X, eng.xn, eng.labels, None, eng.slots, True)
@@ -64,6 +66,7 @@ def main():
             res[f"assign_{v}"].append(e0.elapsed_time(e1))
         C.set_assign_p(0)
         C.set_assign16_gt(0)
+        C.set_assign16_cfg(0)
         e0, e1 = ev(), ev()
         e0.record()
         C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks, None, eng.sum_exp, 0)
