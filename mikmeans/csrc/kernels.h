@@ -69,6 +69,7 @@ struct UpdateArgs {
 int update_slice_width(int dtype, int K, int D);  // columns per workgroup (0 = global fallback)
 int update_n_chunks(int dtype, int K, int D, int64_t N);
 int fixed_exp(double maxabs);                     // largest e with maxabs * 2^e <= 2^30
+void set_update_max_sw(int sw);                   // cap the slice width (0 = none)
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s);
 
 // Reduce slabs (+ assign slots) into the packed f64 message

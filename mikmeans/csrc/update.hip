@@ -163,6 +163,12 @@ static int esize(int dtype) { return dtype == DT_BF16 ? 2 : 4; }
 static size_t upd_lds(int K, int sw, bool pad) { return (size_t)K * ((pad ? sw + 1 : sw) + 1) * 8; }
 
 // returns slice width; *pad says whether the padded LDS stride fits
+// Cap on the slice width (0 = none).  A smaller slice shrinks the LDS footprint
+// so an update workgroup can be co-resident with assign workgroups when the
+// engine overlaps the two kernels on separate streams.
+static int g_update_max_sw = 0;
+void set_update_max_sw(int sw) { g_update_max_sw = sw; }
+
 static int choose_sw(int dtype, int K, int D, bool* pad) {
   const int es = esize(dtype);
   if ((D * es) % 4) return 0;
@@ -170,6 +176,7 @@ static int choose_sw(int dtype, int K, int D, bool* pad) {
   while (dp < D) dp *= 2;
   for (int sw = 64; sw >= 2; sw /= 2) {
     if (sw > dp && sw > 2) continue;
+    if (g_update_max_sw && sw > g_update_max_sw) continue;
     if (upd_lds(K, sw, true) <= UPD_LDS_MAX) { *pad = true; return sw; }
     if (upd_lds(K, sw, false) <= UPD_LDS_MAX) { *pad = false; return sw; }
   }

@@ -60,9 +60,12 @@ class LloydEngine:
 
     def __init__(self, X: torch.Tensor, n_clusters: int, *, comm: Comm | None = None,
                  sample_weight: torch.Tensor | None = None, frozen=None,
-                 empty_policy: str = "keep", n_features: int | None = None):
+                 empty_policy: str = "keep", n_features: int | None = None, segments: int = 1,
+                 overlap_sw: int = 8):
         from ..ops import pad_columns
 
+        self.segments = max(1, int(segments))
+        self.overlap_sw = overlap_sw
         self.comm = comm or Comm.local(X.device)
         self.K = int(n_clusters)
         self.D = int(n_features or X.shape[1])   # real features (X may be column-padded)
@@ -107,7 +110,24 @@ class LloydEngine:
         dev = self.device
         self.pk = CentroidPack(self.K, self.Dp, self.dtype, dev)
         self.slots = torch.zeros(C.NSLOT * C.SLOT_STRIDE, dtype=torch.float64, device=dev)
-        self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, max(self.n, 1))
+        if self.segments > 1 and self.n >= 2 * self.segments:
+            # Overlapped M-step: segment s is scattered on a side stream while the
+            # matrix cores assign segment s+1.  Narrow slices keep the update's LDS
+            # small enough to share a CU with assign workgroups.
+            from ..parallel.shard import shard_range
+
+            self.seg_ranges = [shard_range(self.n, s, self.segments) for s in range(self.segments)]
+            C.set_update_max_sw(self.overlap_sw)
+            seg_rows = max(e - s for s, e in self.seg_ranges)
+            self.seg_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, seg_rows)
+            C.set_update_max_sw(0)
+            self.n_chunks = self.seg_chunks * self.segments
+            self.side = torch.cuda.Stream(device=dev)
+            self.seg_events = [torch.cuda.Event() for _ in range(self.segments)]
+            self.side_done = torch.cuda.Event()
+        else:
+            self.segments = 1
+            self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, max(self.n, 1))
         self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.int64, device=dev)
         self.cnt_slab = torch.empty(self.n_chunks * self.K, dtype=torch.int64, device=dev)
         self.xn = torch.empty(self.n, dtype=torch.float32, device=dev)
@@ -147,7 +167,13 @@ class LloydEngine:
     def _step_gpu(self):
         C = self._C
         KD = self.K * self.Dp
-        if self.n:
+        if self.n and self.segments > 1:
+            self._assign_update_overlapped()
+            C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
+                     self.sum_exp, self.cnt_exp)
+            if self.weights is not None:
+                self.packed[KD + self.K] = (self.mind.double() * self.weights.double()).sum()
+        elif self.n:
             self.pk.assign(self.X, self.xn, self.labels, self.mind, self.slots, True)
             C.update(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks, self.weights,
                      self.sum_exp, self.cnt_exp)
@@ -160,6 +186,28 @@ class LloydEngine:
         self.comm.allreduce_(self.packed)
         self._relocate_empty()
         self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts)
+
+    def _assign_update_overlapped(self):
+        C = self._C
+        main = torch.cuda.current_stream(self.device)
+        self.side.wait_stream(main)  # slab / labels of the previous iteration are free
+        kd, nc = self.K * self.Dp, self.seg_chunks
+        for s, (r0, r1) in enumerate(self.seg_ranges):
+            mind = self.mind[r0:r1] if self.mind is not None else None
+            self.pk.assign(self.X[r0:r1], self.xn[r0:r1], self.labels[r0:r1], mind, self.slots, True)
+            self.seg_events[s].record(main)
+        C.set_update_max_sw(self.overlap_sw)
+        try:
+            with torch.cuda.stream(self.side):
+                for s, (r0, r1) in enumerate(self.seg_ranges):
+                    self.side.wait_event(self.seg_events[s])
+                    w = self.weights[r0:r1] if self.weights is not None else None
+                    C.update(self.X[r0:r1], self.labels[r0:r1], self.K, self.slab[s * nc * kd:],
+                             self.cnt_slab[s * nc * self.K:], nc, w, self.sum_exp, self.cnt_exp)
+                self.side_done.record(self.side)
+        finally:
+            C.set_update_max_sw(0)
+        main.wait_event(self.side_done)
 
     def _step_cpu(self):
         K, Dp = self.K, self.Dp
