@@ -1,0 +1,201 @@
+"""Command line: ``python -m mikmeans <command>`` (or ``torchrun ... -m mikmeans fit`` for DP).
+
+Commands (the reference's top-bar controls, app.mjs:240-288, as a CLI):
+
+* ``fit``      -- k-means on a file (.npy/.safetensors/.csv) or synthetic blobs; writes a
+                  checkpoint (safetensors + JSON), the flat-float ``centroids.json`` and labels
+* ``predict``  -- labels of a dataset under a saved model
+* ``blobs``    -- write a synthetic Gaussian-blob dataset
+* ``room``     -- the trait-card game headless: seed/populate/auto-assign/dashboard/export/import
+* ``bench``    -- the headline benchmark (same as ``python bench.py``)
+* ``info``     -- device, native extension and build information
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+
+def _comm(device):
+    from .parallel import Comm, set_comm
+
+    c = Comm.from_env(device)
+    set_comm(c)
+    return c
+
+
+def cmd_fit(a) -> int:
+    from . import KMeans, MiniBatchKMeans
+    from .config import KMeansConfig, resolve_dtype
+    from .utils.io import load_points
+    from .utils.jsjson import centroids_to_json
+
+    cfg = KMeansConfig.from_args(a)
+    device = cfg.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    comm = _comm(device)
+    dtype = resolve_dtype(cfg.dtype)
+    if a.input:
+        X, n, start = load_points(a.input, comm.rank, comm.world)
+    else:
+        from .data.blobs import make_blobs
+        from .parallel import shard_range
+
+        n, d, c = (int(v) for v in a.blobs.split(","))
+        start, end = shard_range(n, comm.rank, comm.world)
+        X = make_blobs(end - start, d, c, seed=cfg.seed, i0=start, device=comm.device, dtype=dtype)
+    if cfg.batch_size > 0:
+        km = MiniBatchKMeans(cfg.n_clusters, batch_size=cfg.batch_size, max_iter=cfg.max_iter, init=cfg.init,
+                             dtype=dtype, device=comm.device, seed=cfg.seed, comm=comm)
+    else:
+        km = KMeans.from_config(cfg, comm=comm)
+        km.device = comm.device
+    km.fit(X)
+    out = Path(a.output) if a.output else None
+    if comm.rank == 0:
+        rec = {"n_samples": n, "n_clusters": cfg.n_clusters, "world": comm.world}
+        if hasattr(km, "inertia_"):
+            rec.update(inertia=km.inertia_, n_iter=km.n_iter_, fit_time_s=round(km.fit_time_s_, 4),
+                       metrics=km.metrics())
+        print(json.dumps(rec, default=str))
+    if out is not None:
+        if isinstance(km, KMeans):
+            km.save(out)
+        elif comm.rank == 0:
+            out.mkdir(parents=True, exist_ok=True)
+            (out / "centroids.json").write_text(centroids_to_json(km.cluster_centers_))
+        if a.save_labels and hasattr(km, "labels_"):
+            lab = km.labels_
+            lab = lab.cpu().numpy() if torch.is_tensor(lab) else lab
+            np.save(out / f"labels.rank{comm.rank}.npy", lab.astype(np.int32), allow_pickle=False)
+    comm.close()
+    return 0
+
+
+def cmd_predict(a) -> int:
+    from . import KMeans
+    from .utils.io import load_points
+
+    comm = _comm(a.device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    km = KMeans.load(a.model, device=comm.device)
+    X, n, start = load_points(a.input, comm.rank, comm.world)
+    lab = km.predict(X.to(comm.device))
+    lab = lab.cpu().numpy().astype(np.int32)
+    if a.output:
+        np.save(Path(a.output).with_suffix(f".rank{comm.rank}.npy") if comm.world > 1 else a.output, lab,
+                allow_pickle=False)
+    if comm.rank == 0:
+        print(json.dumps({"n_samples": n, "counts": np.bincount(lab, minlength=km.n_clusters).tolist()}))
+    comm.close()
+    return 0
+
+
+def cmd_blobs(a) -> int:
+    from .data.blobs import make_blobs
+    from .utils.io import save_points
+
+    X, y = make_blobs(a.n, a.d, a.centers, std=a.std, seed=a.seed, return_labels=True)
+    save_points(a.output, X)
+    if a.labels:
+        np.save(a.labels, y.numpy(), allow_pickle=False)
+    print(json.dumps({"output": str(a.output), "shape": list(X.shape)}))
+    return 0
+
+
+def cmd_room(a) -> int:
+    from .models.room import Room
+
+    r = Room.from_json(Path(a.load).read_text(), a.room) if a.load else Room(a.room, seed=a.seed)
+    if a.populate:
+        r.populate_test_data()
+    for name in a.centroid or []:
+        r.add_centroid(name)
+    if a.auto:
+        r.auto_assign(seed=a.seed)
+    if a.iteration is not None:
+        r.set_iteration(a.iteration)
+    if a.export:
+        Path(a.export).write_text(r.export_json())
+    d = r.dashboard()
+    print("\n".join(d["chips"] + [" ".join(x for x in (row["name"], f"{row['bar_pct']}%", row["cohesion"],
+                                                             row["top"], row["suggested"])) for row in d["rows"]]))
+    return 0
+
+
+def cmd_bench(a, rest) -> int:
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root))
+    import bench  # noqa: E402
+
+    bench.main(rest)
+    return 0
+
+
+def cmd_info(a) -> int:
+    from .ops import native
+
+    info = {"torch": torch.__version__, "hip": getattr(torch.version, "hip", None),
+            "gpu": torch.cuda.is_available(), "native": native.available(), "native_path": native.loaded_path()}
+    if torch.cuda.is_available():
+        p = torch.cuda.get_device_properties(0)
+        info.update(device=p.name, arch=getattr(p, "gcnArchName", None), cus=p.multi_processor_count,
+                    hbm_gb=round(p.total_memory / 1e9, 1), n_gpus=torch.cuda.device_count())
+    print(json.dumps(info))
+    return 0
+
+
+def build_parser():
+    from .config import KMeansConfig
+
+    ap = argparse.ArgumentParser(prog="mikmeans", description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    f = sub.add_parser("fit", help="fit k-means")
+    src = f.add_mutually_exclusive_group(required=True)
+    src.add_argument("--input", help=".npy / .safetensors / .csv point matrix")
+    src.add_argument("--blobs", help="synthetic data N,D,CENTERS (generated on device, per rank)")
+    f.add_argument("--output", help="checkpoint directory")
+    f.add_argument("--save-labels", action="store_true")
+    KMeansConfig.add_arguments(f)
+    p = sub.add_parser("predict", help="assign points with a saved model")
+    p.add_argument("--model", required=True)
+    p.add_argument("--input", required=True)
+    p.add_argument("--output")
+    p.add_argument("--device")
+    b = sub.add_parser("blobs", help="write a synthetic dataset")
+    b.add_argument("--n", type=int, required=True)
+    b.add_argument("--d", type=int, required=True)
+    b.add_argument("--centers", type=int, required=True)
+    b.add_argument("--std", type=float, default=1.0)
+    b.add_argument("--seed", type=int, default=0)
+    b.add_argument("--output", required=True)
+    b.add_argument("--labels")
+    r = sub.add_parser("room", help="headless trait-card room")
+    r.add_argument("--room")
+    r.add_argument("--load", help="import a room JSON export")
+    r.add_argument("--populate", action="store_true", help="add the 11 test cards")
+    r.add_argument("--centroid", action="append", help="add a centroid (repeatable, max 3)")
+    r.add_argument("--auto", action="store_true", help="assign cards by numeric k-means")
+    r.add_argument("--iteration", type=int)
+    r.add_argument("--export", help="write kmeans-room JSON here")
+    r.add_argument("--seed", type=int, default=0)
+    sub.add_parser("bench", help="headline benchmark (args forwarded to bench.py)", add_help=False)
+    sub.add_parser("info", help="environment / build info")
+    return ap
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if argv and argv[0] == "bench":
+        return cmd_bench(None, argv[1:])
+    a = build_parser().parse_args(argv)
+    return {"fit": cmd_fit, "predict": cmd_predict, "blobs": cmd_blobs, "room": cmd_room,
+            "info": cmd_info}[a.cmd](a)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

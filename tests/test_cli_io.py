@@ -1,0 +1,74 @@
+"""CLI, dataset IO and checkpoint/resume (CPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, cwd):
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-m", "mikmeans", *args], cwd=cwd, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r.stdout
+
+
+@pytest.mark.parametrize("ext", [".npy", ".safetensors", ".csv"])
+def test_io_roundtrip_and_shards(tmp_path, ext):
+    from mikmeans.utils.io import load_points, num_rows, save_points
+
+    X = torch.randn(103, 5)
+    p = save_points(tmp_path / f"x{ext}", X)
+    assert num_rows(p) == (103, 5)
+    parts = [load_points(p, r, 4) for r in range(4)]
+    assert all(n == 103 for _, n, _ in parts)
+    assert [s for _, _, s in parts] == sorted(s for _, _, s in parts)
+    full = torch.cat([x for x, _, _ in parts])
+    tol = 1e-6 if ext == ".csv" else 0.0
+    assert torch.allclose(full, X, atol=tol, rtol=tol)
+
+
+def test_cli_fit_predict_room(tmp_path):
+    out = _run(["blobs", "--n", "3000", "--d", "4", "--centers", "3", "--output", "p.npy", "--labels", "y.npy"],
+               tmp_path)
+    assert json.loads(out)["shape"] == [3000, 4]
+    rec = json.loads(_run(["fit", "--input", "p.npy", "--n-clusters", "3", "--output", "m", "--save-labels",
+                           "--device", "cpu"], tmp_path).strip().splitlines()[-1])
+    assert sum(rec["metrics"]["counts"]) == 3000
+    for f in ("centroids.json", "centroids.safetensors", "state.json", "labels.rank0.npy"):
+        assert (tmp_path / "m" / f).exists()
+    pred = json.loads(_run(["predict", "--model", "m", "--input", "p.npy", "--output", "pred.npy", "--device",
+                            "cpu"], tmp_path).strip().splitlines()[-1])
+    assert pred["counts"] == rec["metrics"]["counts"]
+    assert np.array_equal(np.load(tmp_path / "pred.npy"), np.load(tmp_path / "m" / "labels.rank0.npy"))
+    from sklearn.metrics import adjusted_rand_score
+
+    assert adjusted_rand_score(np.load(tmp_path / "y.npy"), np.load(tmp_path / "pred.npy")) > 0.99
+    txt = _run(["room", "--populate", "--centroid", "A", "--centroid", "B", "--auto", "--export", "r.json"],
+               tmp_path)
+    assert txt.startswith("k = 2")
+    js = json.loads((tmp_path / "r.json").read_text())
+    assert set(js) == {"cards", "centroids", "meta"} and len(js["cards"]) == 12
+    again = _run(["room", "--load", "r.json"], tmp_path)
+    assert again.splitlines()[:4] == txt.splitlines()[:4]
+
+
+def test_resume_matches_uninterrupted(tmp_path):
+    from mikmeans import KMeans
+    from mikmeans.data.blobs import make_blobs
+
+    X = make_blobs(4000, 6, 12, std=3.0, seed=3)
+    kw = dict(init="random", seed=5, tol=-1.0, device="cpu")
+    full = KMeans(12, max_iter=9, **kw).fit(X)
+    part = KMeans(12, max_iter=4, checkpoint_every=2, checkpoint_dir=str(tmp_path / "ck"), **kw).fit(X)
+    assert part.n_iter_ == 4
+    res = KMeans(12, max_iter=9, **kw).fit(X, resume_from=str(tmp_path / "ck"))
+    if full.n_iter_ > 4:
+        assert torch.equal(res.cluster_centers_, full.cluster_centers_)
+        assert res.inertia_ == full.inertia_
