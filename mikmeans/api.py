@@ -66,7 +66,7 @@ class KMeans:
                  random_state: int | None = None, comm: Comm | None = None, frozen=None,
                  empty_cluster: str = "keep", check_every: int = 1, n_local_trials=None,
                  verbose: int = 0, mode: str = "learn", run_id: str | None = None,
-                 checkpoint_every: int = 0, checkpoint_dir: str | None = None):
+                 checkpoint_every: int = 0, checkpoint_dir: str | None = None, metrics_path: str | None = None):
         self.n_clusters = int(n_clusters)
         self.init = init
         self.n_init = int(n_init)
@@ -85,6 +85,7 @@ class KMeans:
         self.run_id = run_id
         self.checkpoint_every = int(checkpoint_every)
         self.checkpoint_dir = checkpoint_dir
+        self.metrics_path = metrics_path
         self.history_: list[dict] = []
 
     # ---------------------------------------------------------------- config
@@ -95,7 +96,7 @@ class KMeans:
                    empty_cluster=cfg.empty_cluster, check_every=cfg.check_every,
                    n_local_trials=cfg.n_local_trials, verbose=cfg.verbose, mode=cfg.mode,
                    run_id=cfg.run_id, checkpoint_every=cfg.checkpoint_every,
-                   checkpoint_dir=cfg.checkpoint_dir, **kw)
+                   checkpoint_dir=cfg.checkpoint_dir, metrics_path=cfg.metrics_path, **kw)
 
     def get_config(self) -> KMeansConfig:
         return KMeansConfig(n_clusters=self.n_clusters, init=self.init if isinstance(self.init, str) else "array",
@@ -105,7 +106,7 @@ class KMeans:
                             empty_cluster=self.empty_cluster, check_every=self.check_every,
                             n_local_trials=self.n_local_trials, mode=self.mode, run_id=self.run_id,
                             verbose=self.verbose, checkpoint_every=self.checkpoint_every,
-                            checkpoint_dir=self.checkpoint_dir)
+                            checkpoint_dir=self.checkpoint_dir, metrics_path=self.metrics_path)
 
     # ------------------------------------------------------------------- fit
     def fit(self, X, y=None, sample_weight=None, *, resume_from=None):
@@ -142,11 +143,16 @@ class KMeans:
             eng.set_centers(centers[:, :D])
             eng.iteration = start_iter
             hist = []
+            mlog = mmetrics.MetricsLogger(self.metrics_path, rank=comm.rank, world=comm.world,
+                                          n_points=n_global, run_id=self.run_id) if self.metrics_path else None
 
-            def cb(st, _eng=eng, _hist=hist):
+            def cb(st, _eng=eng, _hist=hist, _mlog=mlog):
                 rec = st.as_dict()
-                rec["counts"] = _eng.counts.tolist() if self.verbose > 1 else None
+                counts = _eng.counts.tolist() if (self.verbose > 1 or _mlog is not None) else None
+                rec["counts"] = counts if self.verbose > 1 else None
                 _hist.append(rec)
+                if _mlog is not None:
+                    _mlog.log(st, counts)
                 if self.verbose and comm.rank == 0:
                     print(f"[mikmeans] iter {st.iteration} inertia {st.inertia:.6g} "
                           f"shift {st.shift:.3g} changed {st.n_changed}", flush=True)
@@ -158,6 +164,8 @@ class KMeans:
 
             remaining = max(0, self.max_iter - start_iter)
             n_iter, converged, _ = eng.run(remaining, tol_abs, check_every=self.check_every, callback=cb)
+            if mlog is not None:
+                mlog.close()
             labels, mind = eng.assign(True)
             wt = eng.weights.double() if eng.weights is not None else 1.0
             inert = (mind.double() * wt).sum().reshape(1) if eng.n else torch.zeros(1, dtype=torch.float64,

@@ -55,6 +55,7 @@ class KMeansConfig:
     mode: str = "learn"              # free-form metadata, as in the reference
     run_id: str | None = None
     verbose: int = 0
+    metrics_path: str | None = None  # per-iteration JSONL (rank 0)
 
     def to_dict(self):
         return asdict(self)

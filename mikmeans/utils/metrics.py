@@ -78,3 +78,52 @@ def iteration_record(it: int, counts, *, inertia=None, shift=None, n_changed=Non
         if n_points is not None and time_ms > 0:
             rec["assign_per_s"] = n_points * 1000.0 / time_ms
     return rec
+
+
+class MetricsLogger:
+    """Per-iteration JSONL records on rank 0.
+
+    One line per checked iteration: ``iter, inertia, shift, max_shift, n_changed,
+    counts, balance, time_ms, iters_per_s, assign_per_s, world``.  It is the
+    numeric counterpart of the reference dashboard, which recomputes
+    ``snapshotMetrics`` on every change (app.mjs:481-496, :498-508).
+    """
+
+    def __init__(self, path, *, rank: int = 0, world: int = 1, n_points: int = 0, run_id=None):
+        import time
+
+        self._time = time.perf_counter
+        self.rank, self.world, self.n_points, self.run_id = rank, world, n_points, run_id
+        self.f = open(path, "a", encoding="utf-8") if (path and rank == 0) else None
+        self._t = self._time()
+        self._it = None
+
+    def log(self, stats, counts=None):
+        now = self._time()
+        it = stats.iteration
+        steps = it - self._it if self._it is not None else max(it, 1)
+        dt = (now - self._t) / max(steps, 1)
+        self._t, self._it = now, it
+        if self.f is None:
+            return None
+        rec = dict(stats.as_dict())
+        if counts is not None:
+            counts = [int(c) if float(c).is_integer() else float(c) for c in counts]
+            rec["counts"] = counts
+            rec["balance"] = balance(counts)
+            if math.isinf(rec["balance"]["ratio"]):
+                rec["balance"]["ratio"] = "Infinity"
+        rec.update(time_ms=dt * 1e3, iters_per_s=1.0 / dt if dt > 0 else None,
+                   assign_per_s=self.n_points / dt if dt > 0 else None, world=self.world)
+        if self.run_id:
+            rec["run_id"] = self.run_id
+        import json
+
+        self.f.write(json.dumps(rec) + "\n")
+        self.f.flush()
+        return rec
+
+    def close(self):
+        if self.f is not None:
+            self.f.close()
+            self.f = None

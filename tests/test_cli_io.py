@@ -72,3 +72,18 @@ def test_resume_matches_uninterrupted(tmp_path):
     if full.n_iter_ > 4:
         assert torch.equal(res.cluster_centers_, full.cluster_centers_)
         assert res.inertia_ == full.inertia_
+
+
+def test_metrics_jsonl(tmp_path):
+    from mikmeans import KMeans
+    from mikmeans.data.blobs import make_blobs
+
+    X = make_blobs(2000, 3, 5, seed=1)
+    p = tmp_path / "m.jsonl"
+    km = KMeans(5, max_iter=6, tol=-1.0, device="cpu", metrics_path=str(p), run_id="ABCD").fit(X)
+    recs = [json.loads(line) for line in p.read_text().splitlines()]
+    assert len(recs) == km.n_iter_
+    assert [r["iter"] for r in recs] == list(range(1, km.n_iter_ + 1))
+    for r in recs:
+        assert sum(r["counts"]) == 2000 and r["balance"]["gap"] == max(r["counts"]) - min(r["counts"])
+        assert r["world"] == 1 and r["run_id"] == "ABCD" and r["time_ms"] > 0
