@@ -121,6 +121,31 @@ class Comm:
         dist.broadcast_object_list(box, src=src)
         return box[0]
 
+    def all_gather_bytes(self, data: bytes) -> list[bytes]:
+        """Variable-length byte strings from every rank, as two tensor collectives
+        (lengths, then a padded uint8 gather) -- no pickling of peer payloads."""
+        if self.world == 1:
+            return [bytes(data)]
+        n = torch.tensor([len(data)], dtype=torch.int64, device=self.device)
+        lens = self.all_gather(n).reshape(-1).tolist()
+        buf = torch.zeros(max(max(lens), 1), dtype=torch.uint8)
+        if data:
+            buf[: len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        allb = self.all_gather(buf.to(self.device)).cpu()
+        return [allb[r, : lens[r]].numpy().tobytes() for r in range(self.world)]
+
+    def broadcast_bytes(self, data: bytes | None, src: int = 0) -> bytes:
+        if self.world == 1:
+            return bytes(data or b"")
+        n = torch.tensor([len(data) if self.rank == src else 0], dtype=torch.int64, device=self.device)
+        self.broadcast_(n, src)
+        buf = torch.zeros(max(int(n.item()), 1), dtype=torch.uint8)
+        if self.rank == src and data:
+            buf[: len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        buf = buf.to(self.device)
+        self.broadcast_(buf, src)
+        return buf.cpu()[: int(n.item())].numpy().tobytes()
+
     def barrier(self):
         if self.world > 1:
             if self.backend == "nccl":
