@@ -29,6 +29,7 @@ from .models.minibatch import MiniBatchEngine
 from .ops import cpu as cpu_ops
 from .ops import pad_columns
 from .parallel.comm import Comm, get_comm
+from .utils import faults
 from .utils import metrics as mmetrics
 
 
@@ -153,6 +154,7 @@ class KMeans:
                 _hist.append(rec)
                 if _mlog is not None:
                     _mlog.log(st, counts)
+                faults.maybe_fail(comm.rank, st.iteration)
                 if self.verbose and comm.rank == 0:
                     print(f"[mikmeans] iter {st.iteration} inertia {st.inertia:.6g} "
                           f"shift {st.shift:.3g} changed {st.n_changed}", flush=True)

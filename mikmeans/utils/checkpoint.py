@@ -74,8 +74,13 @@ def load_checkpoint(path, comm=None, device=None) -> dict:
         t = load_file(str(path / CKPT_TENSORS))["centers"]
         state = {**meta, "centers": t}
     if comm is not None and comm.world > 1:
-        meta = comm.broadcast_object({k: v for k, v in (state or {}).items() if k != "centers"}, 0)
-        shape = comm.broadcast_object(tuple(state["centers"].shape) if state else None, 0)
+        blob = None
+        if state is not None:
+            hdr = {k: v for k, v in state.items() if k != "centers"}
+            hdr["_shape"] = list(state["centers"].shape)
+            blob = json.dumps(hdr).encode()
+        meta = json.loads(comm.broadcast_bytes(blob, 0).decode())   # JSON, never unpickled
+        shape = meta.pop("_shape")
         buf = (state["centers"] if state else torch.zeros(shape)).to(comm.device)
         comm.broadcast_(buf, 0)
         state = {**meta, "centers": buf.cpu()}
