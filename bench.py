@@ -144,10 +144,10 @@ def _phase_breakdown(eng) -> dict:
     ev[0].record()
     eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True)
     ev[1].record()
-    C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks, eng.weights, eng.sum_exp,
-             eng.cnt_exp)
+    C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks, eng.weights, eng.col_exp,
+             eng.cnt_exp, False)
     ev[2].record()
-    C.reduce(eng.slab, eng.cnt_slab, eng.n_chunks, eng.K, eng.Dp, eng.slots, eng.packed, eng.sum_exp,
+    C.reduce(eng.slab, eng.cnt_slab, eng.n_chunks, eng.K, eng.Dp, eng.slots, eng.packed, eng.col_exp,
              eng.cnt_exp)
     ev[3].record()
     eng.comm.allreduce_(eng.packed)

@@ -38,6 +38,12 @@ void check_f32(const Tensor& t, const char* name, int64_t numel_min = 0) {
   TORCH_CHECK(t.numel() >= numel_min, "mikmeans: ", name, " too small (", t.numel(), " < ",
               numel_min, ")");
 }
+void check_i32(const Tensor& t, const char* name, int64_t numel_min) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kInt && t.is_contiguous(), "mikmeans: ", name,
+              " must be contiguous int32");
+  TORCH_CHECK(t.numel() >= numel_min, "mikmeans: ", name, " too small");
+}
 void check_f64(const Tensor& t, const char* name, int64_t numel_min) {
   check_cuda(t, name);
   TORCH_CHECK(t.scalar_type() == at::kDouble && t.is_contiguous(), "mikmeans: ", name,
@@ -106,7 +112,7 @@ void check_i64(const Tensor& t, const char* name, int64_t numel_min) {
 
 void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab,
             const Tensor& cnt_slab, int64_t n_chunks, const c10::optional<Tensor>& weights,
-            int64_t sum_exp, int64_t cnt_exp) {
+            const Tensor& col_exp, int64_t cnt_exp, bool clamp) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   const int64_t N = X.size(0);
@@ -118,6 +124,7 @@ void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab
   check_i64(slab, "slab", n_chunks * K * D);
   check_i64(cnt_slab, "cnt_slab", n_chunks * K);
   if (weights.has_value()) check_f32(*weights, "weights", N);
+  check_i32(col_exp, "col_exp", D);
   if (sw == 0) {  // global-atomic fallback accumulates into zeroed buffers
     hip_check(hipMemsetAsync(slab.data_ptr(), 0, K * D * 8, stream()), "memset");
     hip_check(hipMemsetAsync(cnt_slab.data_ptr(), 0, K * 8, stream()), "memset");
@@ -127,20 +134,21 @@ void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab
   a.labels = labels.data_ptr<int32_t>(); a.K = (int)K; a.n_chunks = (int)n_chunks;
   a.slab = (long long*)slab.data_ptr<int64_t>(); a.cnt_slab = (long long*)cnt_slab.data_ptr<int64_t>();
   a.weights = opt_ptr<const float>(weights);
-  a.sum_exp = (int)sum_exp; a.cnt_exp = (int)cnt_exp;
+  a.col_exp = col_exp.data_ptr<int32_t>(); a.cnt_exp = (int)cnt_exp; a.clamp = clamp ? 1 : 0;
   hip_check(mk::launch_update(dt, a, stream()), "update");
 }
 
 void reduce(const Tensor& slab, const Tensor& cnt_slab, int64_t n_chunks, int64_t K, int64_t D,
-            const c10::optional<Tensor>& slots, const Tensor& packed, int64_t sum_exp,
+            const c10::optional<Tensor>& slots, const Tensor& packed, const Tensor& col_exp,
             int64_t cnt_exp) {
   check_i64(slab, "slab", n_chunks * K * D);
   check_i64(cnt_slab, "cnt_slab", n_chunks * K);
   check_f64(packed, "packed", K * D + K + 2);
   if (slots.has_value()) check_f64(*slots, "slots", mk::NSLOT * mk::SLOT_STRIDE);
+  check_i32(col_exp, "col_exp", D);
   hip_check(mk::launch_reduce((const long long*)slab.data_ptr<int64_t>(),
                               (const long long*)cnt_slab.data_ptr<int64_t>(), (int)n_chunks, (int)K,
-                              (int)D, (int)sum_exp, (int)cnt_exp, opt_ptr<double>(slots),
+                              (int)D, col_exp.data_ptr<int32_t>(), (int)cnt_exp, opt_ptr<double>(slots),
                               packed.data_ptr<double>(), stream()),
             "reduce");
 }

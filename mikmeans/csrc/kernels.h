@@ -63,19 +63,20 @@ struct UpdateArgs {
   long long* slab;       // [n_chunks][K][D] fixed-point partial sums
   long long* cnt_slab;   // [n_chunks][K] fixed-point partial counts
   const float* weights;  // optional per-row weights (sample_weight)
-  int sum_exp;           // sums scale 2^sum_exp
+  const int* col_exp;    // [D] column d's contributions are rne(x * w * 2^col_exp[d]), |.| <= 2^20
   int cnt_exp;           // counts scale 2^cnt_exp (0 when unweighted)
+  int clamp;             // saturate contributions outside +-2^21 (streamed data)
 };
 int update_slice_width(int dtype, int K, int D);  // columns per workgroup (0 = global fallback)
 int update_n_chunks(int dtype, int K, int D, int64_t N);
-int fixed_exp(double maxabs);                     // largest e with maxabs * 2^e <= 2^30
+int fixed_exp(double maxabs);                     // largest e with maxabs * 2^e <= 2^20
 void set_update_max_sw(int sw);                   // cap the slice width (0 = none)
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s);
 
 // Reduce slabs (+ assign slots) into the packed f64 message
 // [K*D sums | K counts | inertia | n_changed] (length K*D + K + 2).
 hipError_t launch_reduce(const long long* slab, const long long* cnt_slab, int n_chunks, int K,
-                         int D, int sum_exp, int cnt_exp, double* slots, double* packed,
+                         int D, const int* col_exp, int cnt_exp, double* slots, double* packed,
                          hipStream_t s);
 
 // ---- finalize (new centroids + shift + re-pack) -------------------------------

@@ -6,20 +6,28 @@
 //  * global float atomics run at ~1.3 TB/s of added bytes chip-wide, so a direct
 //    scatter of N=1e8 x D=128 f32 adds (51 GB) would take ~40 ms per iteration;
 //  * LDS ds_add_f32 costs ~169 cycles per wave-instruction whatever the bank
-//    pattern, ds_add_f64 ~23, but the INTEGER ds_add_u64 only ~8.4.
-// So every workgroup privatises a [K][SW] slice of the sums in LDS as 64-bit
-// FIXED-POINT integers: each contribution is rounded to an int32 at scale
-// 2^sum_exp (chosen per fit from max|x*w| so it cannot overflow) and added with
-// ds_add_u64.  Integer addition is exact and associative: the M-step result is
-// bitwise identical for any atomic order, and its error (<= 2^-31 max|x| per
-// point, unbiased rounding) is far below an f32 accumulator's.
+//    pattern; integer LDS adds are ~20x faster and are bound by moving their
+//    address + data dwords from VGPRs to the LDS (2 cycles per dword).
+// So every workgroup privatises a [K][SW] slice of the sums in LDS as FIXED-POINT
+// integers, TWO columns per 64-bit cell: a contribution q = rne(x * w * 2^e_col)
+// (|q| <= 2^20, per-column exponent e_col from the global column max) is formed
+// by ONE fma against the magic constant 1.5*2^23, whose result's bit pattern is
+// 0x4B400000 + q; the bit patterns of two adjacent columns are added as one
+// ds_add_u64 (3 dwords for 2 elements).  Modulo 2^64 the cell then holds
+//   sum(q_a) + sum(q_b) * 2^32 + n * 0x4B400000 * (1 + 2^32)
+// where n is the number of adds since the last flush (counted per label), and as
+// long as |sum(q)| < 2^31 for both columns the two sums decode exactly.  Each
+// label's add count is tracked; before any can reach 2^11 the workgroup flushes
+// its slice (decode, add into its int64 slab rows, zero) and carries on.
+// Integer addition is exact and associative: the M-step is bitwise identical for
+// any atomic order, chunking or world size; the quantisation error per point is
+// <= 2^-21 max|x_col|.
 //
-// D is split into column slices so the slice fits LDS; every workgroup streams
-// its contiguous chunk of rows with 4..16-byte loads and flushes its slice once,
-// with plain coalesced stores, into an int64 slab that launch_reduce sums in f64.
-// Grid mapping is XCD-aware: blocks b and b+8 share an XCD on MI355X, so the
-// n_slices workgroups that read the same rows (different column slices of the
-// same lines) get block ids congruent mod 8 and meet in one 4 MB L2.
+// D is split into column slices so a slice fits LDS; every workgroup streams its
+// contiguous chunk of rows with 4..16-byte loads.  Grid mapping is XCD-aware:
+// blocks b and b+8 share an XCD on MI355X, so the n_slices workgroups that read
+// the same rows (different column slices of the same lines) get block ids
+// congruent mod 8 and meet in one 4 MB L2.
 //
 // Reference parity: the reference's "update step" is re-deriving the dashboard
 // after humans move cards (app.mjs:481-496 snapshotMetrics counts); counts here
@@ -31,12 +39,14 @@
 
 namespace mk {
 
-// One workgroup per CU (LDS-bound).  Measured (N=2e7, D=128, K=1024, bf16):
-// 512 threads x 4 rows 1.56 ms, 1024 x 8 rows 1.69 ms -- the LDS atomics and
-// their bank conflicts, not memory latency, bound this kernel.
-constexpr int UPD_NT = 512;
-constexpr int UPD_UNROLL = 8;
+constexpr int UPD_NT = 512;                 // one LDS-filling workgroup per CU
 constexpr size_t UPD_LDS_MAX = 160 * 1024;
+constexpr int FX_BITS = 20;                 // |q| <= 2^20 per contribution
+constexpr int FX_LIM = (1 << (30 - FX_BITS)) * 2 - 1;  // adds per flush: 2047 * 2^20 < 2^31
+constexpr float FX_MAGIC = 12582912.0f;     // 1.5 * 2^23, bits 0x4B400000
+constexpr unsigned long long FX_MM = 0x4B4000004B400000ull;
+constexpr int UPD_MAX_PERIOD = 1024;        // rows between flush checks
+constexpr int UPD_NBUF = 3;                 // period buffers in the prefetch ring
 
 template <int BYTES> struct LoadT;
 template <> struct LoadT<16> { typedef u32x4 type; };
@@ -59,87 +69,277 @@ __device__ __forceinline__ void unpack_any(const typename LoadT<BYTES>::type& w,
   }
 }
 
-__device__ __forceinline__ long long to_fixed(float v, float scale) {
-  return (long long)__float2int_rn(v * scale);
+// bits of (1.5*2^23 + rne(v * sc)); exact while |v * sc| <= 2^22.  CLAMP saturates
+// out-of-range contributions (streams whose scale came from an earlier batch).
+template <bool CLAMP>
+__device__ __forceinline__ uint32_t fx_bits(float v, float sc) {
+  float r = __builtin_fmaf(v, sc, FX_MAGIC);
+  if constexpr (CLAMP) r = __builtin_amdgcn_fmed3f(r, FX_MAGIC - 2097152.f, FX_MAGIC + 2097152.f);
+  return __float_as_uint(r);
 }
 
-template <typename T, int SW, bool PAD>
+__device__ __forceinline__ long long fx_q(float v, float sc) {
+  return (long long)(int)(fx_bits<true>(v, sc) - 0x4B400000u);
+}
+
+// LDS: cells [K+1][ldc] u64 (row K is a sink for rows outside the chunk, so the hot
+// loop has no per-row branch) | weighted counts [K+1] i64 | add counts [K+1] u32 | flag
+struct UpdLayout {
+  int K, LDc;
+  __device__ unsigned long long* cells(char* m) const { return (unsigned long long*)m; }
+  __device__ long long* wcnt(char* m) const { return (long long*)m + (size_t)(K + 1) * LDc; }
+  __device__ unsigned* nadd(char* m) const { return (unsigned*)(wcnt(m) + K + 1); }
+  __device__ int* flag(char* m) const { return (int*)(nadd(m) + K + 1); }
+};
+
+// nadd[k]: adds since label k's last flush in bits 0..30; bit 31 = "k's slab row
+// already holds a partial sum" (then a flush adds instead of storing).
+constexpr unsigned NADD_MASK = 0x7fffffffu, NADD_WRITTEN = 0x80000000u;
+
+// Decode label k's cells, store/add them into this workgroup's slab row, reset them.
+template <int SW>
+__device__ __forceinline__ void upd_flush_label(const UpdateArgs& a, const UpdLayout& L, char* m,
+                                                int slice, int chunk, int k) {
+  constexpr int NP = SW / 2;
+  unsigned long long* cells = L.cells(m) + k * L.LDc;
+  const unsigned na = L.nadd(m)[k];
+  const unsigned long long n = na & NADD_MASK;
+  const bool add = na & NADD_WRITTEN;
+  const int cols = (a.D - slice * SW) < SW ? (a.D - slice * SW) : SW;
+  long long* dst = a.slab + (int64_t)chunk * a.K * a.D + (int64_t)k * a.D + slice * SW;
+#pragma unroll 4
+  for (int p = 0; p < NP; ++p) {
+    const unsigned long long T = cells[p] - n * FX_MM;
+    cells[p] = 0;
+    const int lo = (int)(uint32_t)T;
+    const long long hi = (long long)(T - (unsigned long long)(long long)lo) >> 32;
+    if (2 * p < cols) {
+      if (add) { dst[2 * p] += lo; dst[2 * p + 1] += hi; }
+      else { dst[2 * p] = lo; dst[2 * p + 1] = hi; }
+    }
+  }
+  if (slice == 0) {
+    long long* w = L.wcnt(m) + k;
+    const long long c = a.weights ? *w : (long long)n;
+    long long* cd = a.cnt_slab + (int64_t)chunk * a.K + k;
+    if (add) *cd += c; else *cd = c;
+  }
+  L.wcnt(m)[k] = 0;
+  L.nadd(m)[k] = NADD_WRITTEN;
+}
+
+// Mid-chunk flush: only labels whose add count reached `thresh` (one thread per
+// label; hot labels are few).  Called by all threads after an LDS barrier.
+template <int SW>
+__device__ void upd_flush_hot(const UpdateArgs& a, const UpdLayout& L, char* m, int slice, int chunk,
+                              unsigned thresh) {
+  for (int k = threadIdx.x; k < a.K; k += UPD_NT)
+    if ((L.nadd(m)[k] & NADD_MASK) >= thresh) upd_flush_label<SW>(a, L, m, slice, chunk, k);
+  if (threadIdx.x == 0) *L.flag(m) = 0;
+  __syncthreads();
+}
+
+// Final flush of every label, one (label, cell) per thread so the slab writes coalesce.
+template <int SW>
+__device__ void upd_flush_all(const UpdateArgs& a, const UpdLayout& L, char* m, int slice, int chunk) {
+  constexpr int NP = SW / 2;
+  unsigned long long* cells = L.cells(m);
+  const unsigned* nadd = L.nadd(m);
+  __syncthreads();
+  long long* slab = a.slab + (int64_t)chunk * a.K * a.D + slice * SW;
+  const int cols = (a.D - slice * SW) < SW ? (a.D - slice * SW) : SW;
+  for (int e = threadIdx.x; e < a.K * NP; e += UPD_NT) {
+    const int k = e / NP, p = e % NP;
+    const unsigned na = nadd[k];
+    const unsigned long long T = cells[k * L.LDc + p] - (unsigned long long)(na & NADD_MASK) * FX_MM;
+    const int lo = (int)(uint32_t)T;
+    const long long hi = (long long)(T - (unsigned long long)(long long)lo) >> 32;
+    if (2 * p < cols) {
+      long long* dst = slab + (int64_t)k * a.D + 2 * p;
+      if (na & NADD_WRITTEN) { dst[0] += lo; dst[1] += hi; }
+      else { dst[0] = lo; dst[1] = hi; }
+    }
+  }
+  if (slice == 0) {
+    const long long* wcnt = L.wcnt(m);
+    for (int k = threadIdx.x; k < a.K; k += UPD_NT) {
+      const unsigned na = nadd[k];
+      const long long c = a.weights ? wcnt[k] : (long long)(na & NADD_MASK);
+      long long* dst = a.cnt_slab + (int64_t)chunk * a.K + k;
+      if (na & NADD_WRITTEN) *dst += c; else *dst = c;
+    }
+  }
+}
+
+enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2 };
+
+template <typename T, int SW, int MODE>
 __global__ __launch_bounds__(UPD_NT) void update_kernel(UpdateArgs a, int n_slices,
                                                         int64_t rows_per_chunk) {
+  constexpr bool CLAMP = MODE & UPD_CLAMP;
+  constexpr bool W = MODE & UPD_WEIGHTED;
   constexpr int ES = sizeof(T);
   constexpr int PB = (SW * ES >= 16) ? 16 : SW * ES;  // bytes per lane load
-  constexpr int V = PB / ES;                           // elements per lane load
+  constexpr int V = PB / ES;                           // elements per lane load (even)
   constexpr int LPR = SW / V;                          // lanes per row
   constexpr int RPP = UPD_NT / LPR;                    // rows per pass
-  constexpr int LD = PAD ? SW + 1 : SW;                // LDS row stride (int64 cells)
+  constexpr int UNR = (UPD_MAX_PERIOD / RPP) < 8 ? (UPD_MAX_PERIOD / RPP) : 8;
+  constexpr int PERIOD = RPP * UNR;
+  constexpr unsigned THRESH = FX_LIM - PERIOD + 1;     // flush before any label passes FX_LIM
+  constexpr int LDC = SW / 2 + 1;                      // odd cell stride
+  static_assert(V % 2 == 0 && UNR >= 1 && FX_LIM >= PERIOD, "update tiling");
   typedef typename LoadT<PB>::type LT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  long long* s = (long long*)smem;
-  long long* cnt = s + (size_t)a.K * LD;
+  const UpdLayout L{a.K, LDC};
+  unsigned long long* cells = L.cells(smem);
+  long long* wcnt = L.wcnt(smem);
+  unsigned* nadd = L.nadd(smem);
 
   const int b = blockIdx.x;
   const int j = b >> 3;
   const int slice = j % n_slices;
   const int chunk = (j / n_slices) * 8 + (b & 7);
 
-  for (int e = threadIdx.x; e < a.K * (LD + 1); e += UPD_NT) s[e] = 0;
-  __syncthreads();
+  {
+    unsigned long long* z = cells;
+    const int nz = (int)(((size_t)(a.K + 1) * LDC * 8 + (size_t)(a.K + 1) * 12 + 16) / 8);
+    for (int e = threadIdx.x; e < nz; e += UPD_NT) z[e] = 0;
+  }
 
-  const float scale = ldexpf(1.f, a.sum_exp);
-  const float cscale = ldexpf(1.f, a.cnt_exp);
   const int64_t row0 = (int64_t)chunk * rows_per_chunk;
   int64_t row1 = row0 + rows_per_chunk;
   if (row1 > a.N) row1 = a.N;
   const int lr = threadIdx.x / LPR, lp = threadIdx.x % LPR;
   const int col = slice * SW + lp * V;
   const bool colok = col < a.D;
-  const bool counter = (slice == 0) && (lp == 0);
+  const bool all_cols = (a.D % SW) == 0;               // kernel-uniform
+  const int colc = colok ? col : 0;
+  const bool counter = lp == 0;
+  const bool wcounter = W && counter && slice == 0;
+  const float cscale = ldexpf(1.f, a.cnt_exp);
+  float sc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) sc[e] = (col + e < a.D) ? ldexpf(1.f, a.col_exp[col + e]) : 0.f;
 
-  for (int64_t base = row0; base < row1; base += (int64_t)RPP * UPD_UNROLL) {
-    LT w[UPD_UNROLL];
-    int lab[UPD_UNROLL];
-    float wt[UPD_UNROLL];
+  // Row mapping: in a period starting at `base`, lane (lr, lp) owns the UNR
+  // consecutive rows base + lr*UNR + u, so runs of equal labels (sorted or
+  // converged data) merge in registers before they reach the LDS, and the loads
+  // of one lane are one address plus immediate offsets.
+  const T* xrow = (const T*)a.X + (row0 + (int64_t)lr * UNR) * a.ldx + colc;
+  const int* lrow = a.labels + row0 + lr * UNR;
+  const float* wrow = W ? a.weights + row0 + lr * UNR : nullptr;
+  auto load = [&](int64_t base, LT* w_, int* lab_, float* wt_) {
+    const int64_t off = base - row0;
+    if (base + PERIOD <= row1) {                       // whole period (all but the last)
+      const T* p = xrow + off * a.ldx;
 #pragma unroll
-    for (int u = 0; u < UPD_UNROLL; ++u) {
-      const int64_t i = base + (int64_t)u * RPP + lr;
-      const bool ok = i < row1;
-      const int l = ok ? a.labels[i] : -1;
-      lab[u] = ((unsigned)l < (unsigned)a.K) ? l : -1;  // never index LDS out of range
-      wt[u] = (ok && a.weights) ? a.weights[i] : 1.f;
-      if (ok && colok) w[u] = *(const LT*)((const T*)a.X + i * a.ldx + col);
-      else w[u] = LT{};
+      for (int u = 0; u < UNR; ++u) {
+        const int l = lrow[off + u];
+        lab_[u] = ((unsigned)l < (unsigned)a.K) ? l : a.K;
+        if constexpr (W) wt_[u] = wrow[off + u];
+        w_[u] = *(const LT*)(p + u * a.ldx);
+      }
+    } else {                                           // clamp rows past the chunk -> sink row K
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int64_t i0 = base + (int64_t)lr * UNR + u;
+        const int64_t i = i0 < row1 ? i0 : row1 - 1;
+        const int l = a.labels[i];
+        lab_[u] = (i0 < row1 && (unsigned)l < (unsigned)a.K) ? l : a.K;
+        if constexpr (W) wt_[u] = a.weights[i];
+        w_[u] = *(const LT*)((const T*)a.X + i * a.ldx + colc);
+      }
     }
+    if (!all_cols && !colok) {
 #pragma unroll
-    for (int u = 0; u < UPD_UNROLL; ++u) {
-      if (lab[u] < 0) continue;
+      for (int u = 0; u < UNR; ++u) w_[u] = LT{};
+    }
+  };
+
+  // Accumulate one period; sets the flush flag when a label's add count nears FX_LIM.
+  auto accumulate = [&](const LT* w_, const int* lab_, const float* wt_) {
+    unsigned seen = 0;
+    unsigned long long acc[V / 2];
+    int cur = lab_[0];
+    unsigned run = 0;
+    auto emit = [&]() {
+      unsigned long long* dst = cells + cur * LDC + lp * (V / 2);
+#pragma unroll
+      for (int c = 0; c < V / 2; ++c)
+        __hip_atomic_fetch_add(dst + c, acc[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (counter) {
+        const unsigned old = __hip_atomic_fetch_add(nadd + cur, run, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP) & NADD_MASK;
+        if (cur < a.K) seen = old + run > seen ? old + run : seen;  // the sink never flushes
+      }
+    };
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
       float f[V];
-      unpack_any<T, PB>(w[u], f);
-      long long* dst = s + lab[u] * LD + lp * V;
-      const float sc = a.weights ? wt[u] * scale : scale;
+      unpack_any<T, PB>(w_[u], f);
+      unsigned long long v[V / 2];
 #pragma unroll
-      for (int e = 0; e < V; ++e)
-        __hip_atomic_fetch_add(dst + e, to_fixed(f[e], sc), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (counter)
-        __hip_atomic_fetch_add(cnt + lab[u], a.weights ? to_fixed(wt[u], cscale) : 1ll,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int e = 0; e < V; e += 2) {
+        const float s0 = W ? sc[e] * wt_[u] : sc[e];
+        const float s1 = W ? sc[e + 1] * wt_[u] : sc[e + 1];
+        v[e / 2] = (unsigned long long)fx_bits<CLAMP>(f[e], s0) |
+                   ((unsigned long long)fx_bits<CLAMP>(f[e + 1], s1) << 32);
+      }
+      if constexpr (W)
+        if (wcounter)  // weighted counts: one add per row (slice 0 only)
+          __hip_atomic_fetch_add(wcnt + lab_[u], (long long)__float2int_rn(wt_[u] * cscale),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (u == 0) {
+#pragma unroll
+        for (int c = 0; c < V / 2; ++c) acc[c] = v[c];
+        run = 1;
+      } else {
+        if (lab_[u] != cur) {  // label changes: emit the run so far
+          emit();
+          cur = lab_[u];
+          run = 0;
+#pragma unroll
+          for (int c = 0; c < V / 2; ++c) acc[c] = 0;
+        }
+#pragma unroll
+        for (int c = 0; c < V / 2; ++c) acc[c] += v[c];
+        ++run;
+      }
+    }
+    emit();
+    if (seen >= THRESH) *L.flag(smem) = 1;
+    // LDS-only barrier: the prefetched global loads stay in flight
+    wait_lgkm0();
+    raw_barrier();
+  };
+
+  // NB-deep ring of period buffers: NB-1 periods of loads in flight while one accumulates
+  constexpr int NB = UPD_NBUF;
+  LT wb[NB][UNR];
+  int lb[NB][UNR];
+  float tb[NB][UNR];
+#pragma unroll
+  for (int s = 0; s < NB - 1; ++s)
+    if (row0 + (int64_t)s * PERIOD < row1) load(row0 + (int64_t)s * PERIOD, wb[s], lb[s], tb[s]);
+  __syncthreads();
+  for (int64_t base = row0; base < row1; base += (int64_t)NB * PERIOD) {
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+      const int64_t pb = base + (int64_t)s * PERIOD;
+      if (pb < row1) {
+        const int64_t nb = pb + (int64_t)(NB - 1) * PERIOD;
+        const int ns = (s + NB - 1) % NB;  // static after unrolling
+        if (nb < row1) load(nb, wb[ns], lb[ns], tb[ns]);
+        accumulate(wb[s], lb[s], tb[s]);
+        if (*L.flag(smem)) upd_flush_hot<SW>(a, L, smem, slice, chunk, THRESH);
+      }
     }
   }
-  __syncthreads();
-
-  // flush this slice: slab[chunk][k][slice*SW + c]
-  const int cols = (a.D - slice * SW) < SW ? (a.D - slice * SW) : SW;
-  long long* slab = a.slab + (int64_t)chunk * a.K * a.D + slice * SW;
-  for (int e = threadIdx.x; e < a.K * SW; e += UPD_NT) {
-    const int k = e / SW, c = e % SW;
-    if (c < cols) slab[(int64_t)k * a.D + c] = s[k * LD + c];
-  }
-  if (slice == 0)
-    for (int k = threadIdx.x; k < a.K; k += UPD_NT) a.cnt_slab[(int64_t)chunk * a.K + k] = cnt[k];
+  upd_flush_all<SW>(a, L, smem, slice, chunk);
 }
 
 // Fallback for K too large to privatise even 2 columns: direct int64 global atomics
-// (same fixed-point arithmetic, so results match the LDS path bit for bit).
+// (same fixed-point contributions, so results match the LDS path bit for bit).
 template <typename T>
 __global__ __launch_bounds__(256) void update_global_kernel(UpdateArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -148,51 +348,51 @@ __global__ __launch_bounds__(256) void update_global_kernel(UpdateArgs a) {
   const int k = a.labels[i];
   if ((unsigned)k >= (unsigned)a.K) return;
   const float wt = a.weights ? a.weights[i] : 1.f;
-  const float sc = ldexpf(1.f, a.sum_exp) * wt;
   const T* xr = (const T*)a.X + i * a.ldx;
   for (int d = lane; d < a.D; d += 64)
     atomicAdd((unsigned long long*)(a.slab + (int64_t)k * a.D + d),
-              (unsigned long long)to_fixed(Elem<T>::to_f32(xr[d]), sc));
+              (unsigned long long)fx_q(Elem<T>::to_f32(xr[d]), ldexpf(1.f, a.col_exp[d]) * wt));
   if (lane == 0)
     atomicAdd((unsigned long long*)(a.cnt_slab + k),
-              (unsigned long long)(a.weights ? to_fixed(wt, ldexpf(1.f, a.cnt_exp)) : 1ll));
+              (unsigned long long)(a.weights ? (long long)__float2int_rn(wt * ldexpf(1.f, a.cnt_exp))
+                                             : 1ll));
 }
 
 static int esize(int dtype) { return dtype == DT_BF16 ? 2 : 4; }
 
-static size_t upd_lds(int K, int sw, bool pad) { return (size_t)K * ((pad ? sw + 1 : sw) + 1) * 8; }
+// LDS bytes: cells [K+1][ldc] u64 + weighted counts [K+1] i64 + add counts [K+1] u32 + flag
+static size_t upd_lds(int K, int ldc) { return (size_t)(K + 1) * ldc * 8 + (size_t)(K + 1) * 12 + 16; }
 
-// returns slice width; *pad says whether the padded LDS stride fits
 // Cap on the slice width (0 = none).  A smaller slice shrinks the LDS footprint
 // so an update workgroup can be co-resident with assign workgroups when the
 // engine overlaps the two kernels on separate streams.
 static int g_update_max_sw = 0;
 void set_update_max_sw(int sw) { g_update_max_sw = sw; }
 
-static int choose_sw(int dtype, int K, int D, bool* pad) {
+// slice width (columns per workgroup, 0 = global fallback) and LDS cell stride
+static int choose_sw(int dtype, int K, int D, int* ldc) {
   const int es = esize(dtype);
-  if ((D * es) % 4) return 0;
-  int dp = 1;
+  if ((D * es) % 4 || D % 2) return 0;
+  int dp = 2;
   while (dp < D) dp *= 2;
   for (int sw = 64; sw >= 2; sw /= 2) {
-    if (sw > dp && sw > 2) continue;
+    if (sw > dp) continue;
     if (g_update_max_sw && sw > g_update_max_sw) continue;
-    if (upd_lds(K, sw, true) <= UPD_LDS_MAX) { *pad = true; return sw; }
-    if (upd_lds(K, sw, false) <= UPD_LDS_MAX) { *pad = false; return sw; }
+    if (upd_lds(K, sw / 2 + 1) <= UPD_LDS_MAX) { *ldc = sw / 2 + 1; return sw; }  // odd stride
   }
   return 0;
 }
 
 int update_slice_width(int dtype, int K, int D) {
-  bool pad;
-  return choose_sw(dtype, K, D, &pad);
+  int ldc;
+  return choose_sw(dtype, K, D, &ldc);
 }
 
 int update_n_chunks(int dtype, int K, int D, int64_t N) {
   const int sw = update_slice_width(dtype, K, D);
   if (sw == 0) return 1;
   const int n_slices = (D + sw - 1) / sw;
-  // LDS-bound: one resident workgroup per CU; aim for ~1-2 waves of the 256 CUs
+  // LDS-bound: one resident workgroup per CU; aim for one wave of the 256 CUs
   int nc = (256 + n_slices - 1) / n_slices;
   nc = ((nc + 7) / 8) * 8;
   const int64_t rows = (N + nc - 1) / nc;
@@ -206,41 +406,48 @@ int update_n_chunks(int dtype, int K, int D, int64_t N) {
 
 int fixed_exp(double maxabs) {
   if (!(maxabs > 0) || !isfinite(maxabs)) return 0;
-  int e = 30 - (int)ceil(log2(maxabs));
-  while (e > -1000 && ldexp(maxabs, e) > 1073741824.0) --e;  // guard rounding of log2
+  int e = FX_BITS - (int)ceil(log2(maxabs));
+  while (e > -1000 && ldexp(maxabs, e) > ldexp(1.0, FX_BITS)) --e;  // guard rounding of log2
+  if (e > 126) e = 126;     // 2^e must stay a normal float
+  if (e < -126) e = -126;
   return e;
 }
 
-template <typename T, int SW, bool PAD>
-static hipError_t launch_sw(const UpdateArgs& a, hipStream_t s) {
+template <typename T, int SW, int MODE>
+static hipError_t launch_sw(const UpdateArgs& a, int ldc, hipStream_t s) {
   const int n_slices = (a.D + SW - 1) / SW;
   const int64_t rows_per_chunk = (a.N + a.n_chunks - 1) / a.n_chunks;
-  const size_t lds = upd_lds(a.K, SW, PAD);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)update_kernel<T, SW, PAD>,
+    hipFuncSetAttribute((const void*)update_kernel<T, SW, MODE>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)UPD_LDS_MAX);
     attr = true;
   }
-  hipLaunchKernelGGL((update_kernel<T, SW, PAD>), dim3(a.n_chunks * n_slices), dim3(UPD_NT), lds,
-                     s, a, n_slices, rows_per_chunk);
+  hipLaunchKernelGGL((update_kernel<T, SW, MODE>), dim3(a.n_chunks * n_slices), dim3(UPD_NT),
+                     upd_lds(a.K, ldc), s, a, n_slices, rows_per_chunk);
   return hipGetLastError();
 }
 
 template <typename T, int SW>
-static hipError_t launch_pad(const UpdateArgs& a, hipStream_t s, bool pad) {
-  return pad ? launch_sw<T, SW, true>(a, s) : launch_sw<T, SW, false>(a, s);
+static hipError_t launch_clamp(const UpdateArgs& a, int ldc, hipStream_t s) {
+  const int mode = (a.clamp ? UPD_CLAMP : 0) | (a.weights ? UPD_WEIGHTED : 0);
+  switch (mode) {
+    case 0: return launch_sw<T, SW, 0>(a, ldc, s);
+    case 1: return launch_sw<T, SW, 1>(a, ldc, s);
+    case 2: return launch_sw<T, SW, 2>(a, ldc, s);
+    default: return launch_sw<T, SW, 3>(a, ldc, s);
+  }
 }
 
 template <typename T>
-static hipError_t launch_update_t(const UpdateArgs& a, hipStream_t s, int sw, bool pad) {
+static hipError_t launch_update_t(const UpdateArgs& a, hipStream_t s, int sw, int ldc) {
   switch (sw) {
-    case 64: return launch_pad<T, 64>(a, s, pad);
-    case 32: return launch_pad<T, 32>(a, s, pad);
-    case 16: return launch_pad<T, 16>(a, s, pad);
-    case 8: return launch_pad<T, 8>(a, s, pad);
-    case 4: return launch_pad<T, 4>(a, s, pad);
-    case 2: return launch_pad<T, 2>(a, s, pad);
+    case 64: return launch_clamp<T, 64>(a, ldc, s);
+    case 32: return launch_clamp<T, 32>(a, ldc, s);
+    case 16: return launch_clamp<T, 16>(a, ldc, s);
+    case 8: return launch_clamp<T, 8>(a, ldc, s);
+    case 4: return launch_clamp<T, 4>(a, ldc, s);
+    case 2: return launch_clamp<T, 2>(a, ldc, s);
     case 0:
       // caller zeroed slab[K*D] + cnt_slab[K] (n_chunks == 1)
       hipLaunchKernelGGL((update_global_kernel<T>), dim3((unsigned)((a.N + 3) / 4)), dim3(256), 0,
@@ -252,19 +459,21 @@ static hipError_t launch_update_t(const UpdateArgs& a, hipStream_t s, int sw, bo
 
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s) {
   if (a.N <= 0) return hipSuccess;
-  bool pad = true;
-  const int sw = choose_sw(dtype, a.K, a.D, &pad);
+  int ldc = 0;
+  const int sw = choose_sw(dtype, a.K, a.D, &ldc);
   if (sw > 0 && a.n_chunks % 8) return hipErrorInvalidValue;
-  return dtype == DT_BF16 ? launch_update_t<uint16_t>(a, s, sw, pad)
-                          : launch_update_t<float>(a, s, sw, pad);
+  return dtype == DT_BF16 ? launch_update_t<uint16_t>(a, s, sw, ldc)
+                          : launch_update_t<float>(a, s, sw, ldc);
 }
 
 // ---------------------------------------------------------------------------
-// launch_reduce: packed[e] = 2^-exp * sum_c slab[c][e] (f64), counts likewise,
+// launch_reduce: packed[k*D+d] = 2^-exp[d] * sum_c slab[c][k][d] (f64, exact: every
+// partial is an integer below 2^53), counts likewise,
 // plus the assign kernel's inertia / changed slots (which it then re-zeroes).
 __global__ __launch_bounds__(256) void reduce_kernel(const long long* __restrict__ slab,
                                                      const long long* __restrict__ cnt_slab,
-                                                     int n_chunks, int K, int D, double inv_s,
+                                                     int n_chunks, int K, int D,
+                                                     const int* __restrict__ col_exp,
                                                      double inv_c, double* slots, double* packed) {
   const int64_t KD = (int64_t)K * D;
   const int64_t total = KD + K;
@@ -273,7 +482,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(const long long* __restrict
     double acc = 0.0;
     if (e < KD) {
       for (int c = 0; c < n_chunks; ++c) acc += (double)slab[(int64_t)c * KD + e];
-      acc *= inv_s;
+      acc = ldexp(acc, -col_exp[e % D]);
     } else {
       const int64_t k = e - KD;
       for (int c = 0; c < n_chunks; ++c) acc += (double)cnt_slab[(int64_t)c * K + k];
@@ -304,12 +513,12 @@ __global__ __launch_bounds__(256) void reduce_kernel(const long long* __restrict
 }
 
 hipError_t launch_reduce(const long long* slab, const long long* cnt_slab, int n_chunks, int K,
-                         int D, int sum_exp, int cnt_exp, double* slots, double* packed,
+                         int D, const int* col_exp, int cnt_exp, double* slots, double* packed,
                          hipStream_t s) {
   const int64_t total = (int64_t)K * D + K;
   const unsigned nb = (unsigned)((total + 255) / 256);
   hipLaunchKernelGGL(reduce_kernel, dim3(nb), dim3(256), 0, s, slab, cnt_slab, n_chunks, K, D,
-                     ldexp(1.0, -sum_exp), ldexp(1.0, -cnt_exp), slots, packed);
+                     col_exp, ldexp(1.0, -cnt_exp), slots, packed);
   return hipGetLastError();
 }
 

@@ -136,7 +136,8 @@ class LloydEngine:
         # fixed-point scale of the M-step accumulators (X is static for the fit)
         from ..ops import fixed_exps
 
-        self.sum_exp, self.cnt_exp = fixed_exps(self.X, self.weights) if self.n else (0, 0)
+        # (global column maxima: every rank uses the same scale -> exact, world-size independent sums)
+        self.col_exp, self.cnt_exp = fixed_exps(self.X, self.weights, comm=self.comm)
         if self.weights is not None:
             self.mind = torch.empty(self.n, dtype=torch.float32, device=dev)
 
@@ -170,15 +171,15 @@ class LloydEngine:
         if self.n and self.segments > 1:
             self._assign_update_overlapped()
             C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
-                     self.sum_exp, self.cnt_exp)
+                     self.col_exp, self.cnt_exp)
             if self.weights is not None:
                 self.packed[KD + self.K] = (self.mind.double() * self.weights.double()).sum()
         elif self.n:
             self.pk.assign(self.X, self.xn, self.labels, self.mind, self.slots, True)
             C.update(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks, self.weights,
-                     self.sum_exp, self.cnt_exp)
+                     self.col_exp, self.cnt_exp, False)
             C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
-                     self.sum_exp, self.cnt_exp)
+                     self.col_exp, self.cnt_exp)
             if self.weights is not None:
                 self.packed[KD + self.K] = (self.mind.double() * self.weights.double()).sum()
         else:
@@ -203,7 +204,7 @@ class LloydEngine:
                     self.side.wait_event(self.seg_events[s])
                     w = self.weights[r0:r1] if self.weights is not None else None
                     C.update(self.X[r0:r1], self.labels[r0:r1], self.K, self.slab[s * nc * kd:],
-                             self.cnt_slab[s * nc * self.K:], nc, w, self.sum_exp, self.cnt_exp)
+                             self.cnt_slab[s * nc * self.K:], nc, w, self.col_exp, self.cnt_exp, False)
                 self.side_done.record(self.side)
         finally:
             C.set_update_max_sw(0)

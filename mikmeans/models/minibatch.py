@@ -56,7 +56,7 @@ class MiniBatchEngine:
             self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, self.batch)
             self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.int64, device=dev)
             self.cnt_slab = torch.empty(self.n_chunks * self.K, dtype=torch.int64, device=dev)
-            self.sum_exp = None  # fixed-point scale, set from the first batch (x8 headroom)
+            self.col_exp = None  # fixed-point scales, set from the first batch (x8 headroom)
             self.value_bound = value_bound
             self.labels = torch.empty(self.batch, dtype=torch.int32, device=dev)
             self.xn = torch.empty(self.batch, dtype=torch.float32, device=dev)
@@ -89,21 +89,23 @@ class MiniBatchEngine:
         b = Xb.shape[0]
         if b > self.batch:
             raise ValueError(f"batch of {b} rows exceeds the engine's batch_size {self.batch}")
-        if self.sum_exp is None:
-            # one host read for the whole stream: |x| <= 8 x (first batch's max) or the given bound
-            from ..ops import max_abs
+        if self.col_exp is None:
+            # one host read for the whole stream: per column |x| <= 8 x (first batch's max) or the
+            # given bound; contributions beyond it saturate (clamp) instead of wrapping
+            from ..ops import col_max_abs, fixed_exps
 
-            bound = self.value_bound if self.value_bound is not None else 8.0 * max(max_abs(Xb), 1e-30)
-            t = torch.tensor([bound], dtype=torch.float64, device=self.device)
-            self.comm.allreduce_max_(t)
-            self.sum_exp = C.fixed_exp(float(t.item()))
+            if self.value_bound is not None:
+                bound = torch.full((self.Dp,), float(self.value_bound), dtype=torch.float64)
+            else:
+                bound = 8.0 * col_max_abs(Xb).clamp_min(1e-30)
+            self.col_exp, _ = fixed_exps(Xb, None, comm=self.comm, bound=bound)
         if b:
             xn, lab = self.xn[:b], self.labels[:b]
             C.row_sqnorm(Xb, xn)
             self.pk.assign(Xb, xn, lab, None, self.slots, False)
-            C.update(Xb, lab, self.K, self.slab, self.cnt_slab, self.n_chunks, None, self.sum_exp, 0)
+            C.update(Xb, lab, self.K, self.slab, self.cnt_slab, self.n_chunks, None, self.col_exp, 0, True)
             C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
-                     self.sum_exp, 0)
+                     self.col_exp, 0)
         else:
             self.packed.zero_()
         self.comm.allreduce_(self.packed)

@@ -131,15 +131,34 @@ def max_abs(X: torch.Tensor) -> float:
     return max(abs(float(mn)), abs(float(mx)))
 
 
-def fixed_exps(X: torch.Tensor, weights: torch.Tensor | None = None, maxabs: float | None = None):
-    """Fixed-point exponents ``(sum_exp, cnt_exp)`` of the M-step accumulators (csrc/update.hip):
-    every contribution ``x*w * 2^sum_exp`` is guaranteed to fit in 30 bits."""
+def col_max_abs(X: torch.Tensor) -> torch.Tensor:
+    """Per-column max |x| as float64 ``[D]`` (no |X| temporary)."""
+    if X.shape[0] == 0:
+        return torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
+    mn, mx = torch.aminmax(X, dim=0)
+    return torch.maximum(mn.double().abs(), mx.double().abs())
+
+
+def fixed_exps(X: torch.Tensor, weights: torch.Tensor | None = None, comm=None, bound=None):
+    """Fixed-point exponents of the M-step accumulators (csrc/update.hip).
+
+    Returns ``(col_exp, cnt_exp)``: an int32 device tensor ``[D]`` such that every
+    contribution ``|x[:, d] * w| * 2^col_exp[d] <= 2^20``, and the exponent of the
+    weighted counts.  ``bound`` (per-column float64 ``[D]``) overrides the data's
+    column maxima; with ``comm`` the maxima are all-reduced so every rank uses the
+    same scale (exact, world-size independent sums)."""
     C = require()
-    m = max_abs(X) if maxabs is None else float(maxabs)
-    if weights is None:
-        return C.fixed_exp(m), 0
-    wm = max_abs(weights)
-    return C.fixed_exp(m * wm), C.fixed_exp(wm)
+    m = col_max_abs(X) if bound is None else bound.to(device=X.device, dtype=torch.float64)
+    wm = torch.zeros(1, dtype=torch.float64, device=X.device)
+    if weights is not None and weights.numel():
+        wm[0] = max_abs(weights)
+    if comm is not None:
+        comm.allreduce_max_(m)
+        comm.allreduce_max_(wm)
+    w = float(wm.item()) if weights is not None else 1.0
+    exps = [C.fixed_exp(v * w) for v in m.cpu().tolist()]
+    col_exp = torch.tensor(exps, dtype=torch.int32, device=X.device)
+    return col_exp, (C.fixed_exp(w) if weights is not None else 0)
 
 
 def cluster_sums(X: torch.Tensor, labels: torch.Tensor, K: int, weights: torch.Tensor | None = None):
@@ -156,8 +175,8 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, K: int, weights: torch.T
     packed = torch.empty(K * D + K + 2, dtype=torch.float64, device=X.device)
     lab = labels.to(torch.int32).contiguous()
     w = weights.to(torch.float32).contiguous() if weights is not None else None
-    se, ce = fixed_exps(Xp, w)
-    C.update(Xp, lab, K, slab, cnt, nch, w, se, ce)
-    C.reduce(slab, cnt, nch, K, D, None, packed, se, ce)
+    ce_col, ce = fixed_exps(Xp, w)
+    C.update(Xp, lab, K, slab, cnt, nch, w, ce_col, ce, False)
+    C.reduce(slab, cnt, nch, K, D, None, packed, ce_col, ce)
     sums = packed[: K * D].view(K, D)[:, : X.shape[1]]
     return sums, packed[K * D : K * D + K]

@@ -69,7 +69,7 @@ def main():
         C.set_assign16_cfg(0)
         e0, e1 = ev(), ev()
         e0.record()
-        C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks, None, eng.sum_exp, 0)
+        C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks, None, eng.col_exp, 0, False)
         e1.record()
         torch.cuda.synchronize()
         res["update"].append(e0.elapsed_time(e1))

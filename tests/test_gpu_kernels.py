@@ -102,6 +102,40 @@ def test_cluster_sums_weighted(native):
     torch.testing.assert_close(sums.cpu(), es, rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("case", ["one_label", "two_labels", "uniform", "wide_range"])
+def test_cluster_sums_fixed_point_bound(native, case):
+    """Packed-pair fixed point (csrc/update.hip): every sum within count * 2^-20 * colmax of
+    the f64 sum, bitwise reproducible, including labels that force a flush every period."""
+    n, d, k = 300_000, 40, 64
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(n, d, generator=g)
+    if case == "wide_range":
+        X = X * torch.logspace(-6, 6, d)            # per-column exponents must cope
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32)
+    if case == "one_label":
+        lab.zero_()                                   # every period hits the flush threshold
+    elif case == "two_labels":
+        lab = (lab % 2).to(torch.int32)
+    Xd, ld = X.to(DEV), lab.to(DEV)
+    sums, counts = ops.cluster_sums(Xd, ld, k)
+    es, ec = ref.cluster_sums(X, lab, k)
+    assert torch.equal(counts.cpu(), ec)
+    colmax = X.abs().amax(0).double()
+    bound = ec[:, None] * colmax[None, :] * 2.0 ** -20
+    assert bool(((sums.cpu() - es).abs() <= bound).all())
+    again, _ = ops.cluster_sums(Xd, ld, k)          # atomics in another order: same bits
+    assert torch.equal(again, sums)
+
+
+def test_cluster_sums_integer_data_exact(native):
+    g = torch.Generator().manual_seed(5)
+    X = torch.randint(-1000, 1000, (100_000, 64), generator=g).float()
+    lab = torch.randint(0, 300, (100_000,), generator=g, dtype=torch.int32)
+    sums, counts = ops.cluster_sums(X.to(DEV), lab.to(DEV), 300)
+    es, ec = ref.cluster_sums(X, lab, 300)
+    assert torch.equal(sums.cpu(), es) and torch.equal(counts.cpu(), ec)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_blobs_match_numpy_mirror(native, dtype):
     Cg = B.blob_centers(16, 40, 10.0, seed=11, device=DEV)
