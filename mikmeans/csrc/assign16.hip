@@ -66,7 +66,10 @@ template <> struct Mfma16<float> {
   }
 };
 
-template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3>
+// DBG (diagnostic builds for A/B only, never the default): 1 = epilogue replaced by
+// one add per tile (MFMA + LDS pipeline alone), 2 = no ring refills / waits (MFMA +
+// epilogue alone on whatever the LDS holds).
+template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0>
 __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -109,17 +112,23 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
   wait_vmcnt<0>();  // see assign.hip: retire the fragments before the LDS-DMA loop
   if (C::NBUF == 3 && nch > 1) issue_chunk(1);
 
-  float best[C::P];
+  float best[C::P], seg_best[C::P];
   int bg[C::P];
 #pragma unroll
-  for (int p = 0; p < C::P; ++p) { best[p] = 3.0e38f; bg[p] = 0; }
+  for (int p = 0; p < C::P; ++p) { best[p] = 3.0e38f; seg_best[p] = 3.0e38f; bg[p] = 0; }
+  const int last_grp = nch * (C::CT / GT) - 1;
+  const unsigned kmask = key6_mask();
 
+  float dbg_sink = 0.f;
+  if constexpr (DBG == 2) { wait_vmcnt<0>(); raw_barrier(); }
   for (int c = 0; c < nch; ++c) {
-    // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
-    if (C::NBUF == 3 && c + 1 < nch) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
-    wait_lgkm0();
-    raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
-    if (c + C::NBUF - 1 < nch) issue_chunk(c + C::NBUF - 1);
+    if constexpr (DBG != 2) {
+      // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
+      if (C::NBUF == 3 && c + 1 < nch) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
+      wait_lgkm0();
+      raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
+      if (c + C::NBUF - 1 < nch) issue_chunk(c + C::NBUF - 1);
+    }
     const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
 #pragma unroll
     for (int tg = 0; tg < C::CT / GT; ++tg) {
@@ -141,14 +150,48 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
         }
       }
       const int grp = c * (C::CT / GT) + tg;
+      if constexpr (DBG == 1) {
+#pragma unroll
+        for (int p = 0; p < C::P; ++p) dbg_sink += acc[p][0][0];
+        continue;
+      }
+      if constexpr (GT == 1) {
+        // 6-bit keys over a segment of 16 tiles (tile-in-segment * 4 + reg): 4 key
+        // packs + 2 v_min3 per tile and point block; the running best is merged
+        // with its segment id once per segment.
+        // the four indices as opaque SGPRs, so each key is one v_and_or_b32
+        const unsigned tis = (unsigned)(grp & 15) << 2;
+        unsigned t0, t1, t2, t3;
+        asm volatile("s_mov_b32 %0, %4\n\ts_or_b32 %1, %4, 1\n\ts_or_b32 %2, %4, 2\n\ts_or_b32 %3, %4, 3"
+                     : "=s"(t0), "=s"(t1), "=s"(t2), "=s"(t3) : "s"(tis));
+#pragma unroll
+        for (int p = 0; p < C::P; ++p) {
+          const f32x4& sv = acc[p][0];
+          const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
+          const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
+          if constexpr (DBG == 3) {
+            seg_best[p] = min3f_v(min3f_v(k0, k1, k2), k3, seg_best[p]);
+          } else {
+            seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
+          }
+        }
+        if ((grp & 15) == 15 || grp == last_grp) {
+#pragma unroll
+          for (int p = 0; p < C::P; ++p) {
+            // compare values only: on equal (truncated) values the earlier segment keeps
+            // the lower centroid index
+            const float sv = __uint_as_float(__float_as_uint(seg_best[p]) & ~63u);
+            const float bv = __uint_as_float(__float_as_uint(best[p]) & ~63u);
+            if (sv < bv) { best[p] = seg_best[p]; bg[p] = grp >> 4; }
+            seg_best[p] = 3.0e38f;
+          }
+        }
+        continue;
+      }
 #pragma unroll
       for (int p = 0; p < C::P; ++p) {
         float m;
-        if constexpr (GT == 1) {
-          const f32x4& s = acc[p][0];
-          m = min3f(min3f(pack_key(s[0], 0), pack_key(s[1], 1), pack_key(s[2], 2)), pack_key(s[3], 3),
-                    pack_key(s[3], 3));
-        } else if constexpr (GT == 2) {
+        if constexpr (GT == 2) {
           const f32x4& s0 = acc[p][0];
           const f32x4& s1 = acc[p][1];
           const float m0 = min3f(pack_key(s0[0], 0), pack_key(s0[1], 1), pack_key(s0[2], 2));
@@ -170,14 +213,23 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
     }
   }
 
+  if constexpr (DBG == 1) best[0] = fminf(best[0], dbg_sink);
   float inert = 0.f;
   int changed = 0;
 #pragma unroll
   for (int p = 0; p < C::P; ++p) {
     const unsigned bits = __float_as_uint(best[p]);
-    const int idx = (int)(bits & 15u);
-    int k = (bg[p] * GT + (idx >> 2)) * 16 + 4 * g + (idx & 3);
-    float v = __uint_as_float(bits & ~15u);
+    int k;
+    float v;
+    if constexpr (GT == 1) {  // bg = segment of 16 tiles, 6-bit key
+      const int idx = (int)(bits & 63u);
+      k = (bg[p] * 16 + (idx >> 2)) * 16 + 4 * g + (idx & 3);
+      v = __uint_as_float(bits & ~63u);
+    } else {
+      const int idx = (int)(bits & 15u);
+      k = (bg[p] * GT + (idx >> 2)) * 16 + 4 * g + (idx & 3);
+      v = __uint_as_float(bits & ~15u);
+    }
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) {
       const float vo = __shfl_xor(v, o, 64);
@@ -214,7 +266,7 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
   }
 }
 
-template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3>
+template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0>
 static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_>;
   if (a.Kpad % (16 * C::CT) != 0) return hipErrorInvalidValue;
@@ -223,13 +275,13 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT, CT_, NBUF_>,
+    hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
   if (nblk <= 0) return hipSuccess;
-  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT, CT_, NBUF_>), dim3((unsigned)nblk),
+  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG>), dim3((unsigned)nblk),
                      dim3(C::NW * 64), lds, s, a);
   return hipGetLastError();
 }
@@ -254,15 +306,28 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
       case 2: return launch16_t<T, DPAD, P, 1, 2, 3>(a, s);
       case 3: return launch16_t<T, DPAD, P, 2, 4, 2>(a, s);
       case 4: return launch16_t<T, DPAD, P, 2, 2, 3>(a, s);
+      case 10: return launch16_t<T, DPAD, P, 1, 2, 3, 1>(a, s);   // diagnostics of the default
+      case 11: return launch16_t<T, DPAD, P, 1, 2, 3, 2>(a, s);
+      case 12: return launch16_t<T, DPAD, 8, 1, 2, 3>(a, s);      // 8 point-blocks per wave
+      case 13: return launch16_t<T, DPAD, 2, 1, 2, 3>(a, s);      // 2 point-blocks per wave
+      case 14: return launch16_t<T, DPAD, P, 1, 2, 3, 3>(a, s);   // volatile min3 (sched barrier)
+      case 15: return launch16_t<T, DPAD, P, 1, 4, 2, 3>(a, s);
+      case 16: return launch16_t<T, DPAD, P, 1, 4, 2>(a, s);
+      case 17: return launch16_t<T, DPAD, P, 1, 4, 3>(a, s);
+      case 18: return launch16_t<T, DPAD, P, 1, 1, 3>(a, s);
+      case 19: return launch16_t<T, DPAD, P, 1, 1, 2>(a, s);
+      case 20: return launch16_t<T, DPAD, P, 1, 4, 3, 3>(a, s);
+      case 21: return launch16_t<T, DPAD, 2, 1, 4, 2>(a, s);
+      case 22: return launch16_t<T, DPAD, 8, 1, 4, 2>(a, s);
       default: break;
     }
   }
   if (g_assign16_gt == 0) {
-    // Default (A/B on MI355X, N=2e7 D=128 K=1024 bf16: 1340 TF/s vs 1286 for the 16 KiB /
-    // 2-tile-group form): 1-tile epilogue + half-size chunks keep the kernel at <=128 VGPRs
-    // and ~28 KiB LDS, i.e. 4 waves per SIMD, which hides the per-chunk barrier better.
-    constexpr int CTH = CT >= 2 ? CT / 2 : 1;
-    return launch16_t<T, DPAD, P, 1, CTH, 3>(a, s);
+    // Default: 1-tile epilogue with segmented 6-bit keys (1.5 VALU per score), 16 KiB
+    // chunks in a 2-slot ring.  A/B on MI355X at N=2e7 D=128 K=1024 bf16 (scripts/
+    // ab_kernels.py, one process, interleaved rounds): 1279-1317 TF/s vs 1218-1265 for
+    // 4/8 KiB chunks with 3 slots, 1099 / 1250 for 2 / 8 point blocks per wave.
+    return launch16_t<T, DPAD, P, 1, CT, 2>(a, s);
   }
   const int want = g_assign16_gt;
   if (want >= 4 && CT % 4 == 0) return launch16_t<T, DPAD, P, (CT % 4 == 0 ? 4 : 1)>(a, s);

@@ -348,6 +348,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("assign_kpad", [](int64_t dt, int64_t dpad, int64_t K, int64_t layout) {
     return mk::assign_kpad((int)dt, (int)dpad, (int)K, (int)layout); });
   m.def("assign16_supported", [](int64_t dt, int64_t dpad) { return mk::assign16_chunk_tiles((int)dt, (int)dpad) > 0; });
+  m.def("set_update_nt", [](int64_t nt) { mk::set_update_nt((int)nt); }, "update threads/WG (A/B)");
   m.def("set_update_max_sw", [](int64_t sw) { mk::set_update_max_sw((int)sw); },
         "cap the M-step slice width (smaller LDS footprint for overlap with assign)");
   m.def("set_assign16_cfg", [](int64_t v) { mk::set_assign16_cfg((int)v); }, "tuning: 16x16 pipeline variant");

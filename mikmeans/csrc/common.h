@@ -85,10 +85,17 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// v_min3_f32 without the canonicalisation hipcc inserts around fminf.
-__device__ __forceinline__ float min3f(float a, float b, float c) {
+// Volatile form: also a scheduling barrier, which keeps MFMA groups contiguous.
+__device__ __forceinline__ float min3f_v(float a, float b, float c) {
   float d;
   asm volatile("v_min3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+// v_min3_f32 without the canonicalisation hipcc inserts around fminf.  Not
+// volatile: a pure instruction the scheduler may interleave with the MFMAs.
+__device__ __forceinline__ float min3f(float a, float b, float c) {
+  float d;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
   return d;
 }
 
@@ -114,6 +121,19 @@ __device__ __forceinline__ int wave_sum(int v) {
 // resolution 2^-19), so one v_min3_f32 tree yields (min score, index).
 __device__ __forceinline__ float pack_key(float s, int r) {
   return __uint_as_float((__float_as_uint(s) & ~15u) | (unsigned)r);
+}
+// 6-bit variant (relative resolution 2^-17): one key space spans 64 candidates.
+// `mask` must be ~63u held in a VGPR (see key6_mask): -64 is no inline constant and a
+// gfx9 VOP3 takes no literal, so with the index in an SGPR this is ONE v_and_or_b32.
+// Plain C++ (not inline asm): the first reader of an MFMA result must be an
+// instruction the compiler's hazard recognizer sees, or it reads the register early.
+__device__ __forceinline__ float pack_key6(float s, unsigned mask, unsigned r) {
+  return __uint_as_float((__float_as_uint(s) & mask) | r);
+}
+__device__ __forceinline__ unsigned key6_mask() {
+  unsigned m;
+  asm volatile("v_mov_b32 %0, 0xffffffc0" : "=v"(m));  // opaque VGPR constant
+  return m;
 }
 
 // Row index of accumulator register `reg` for lane half `h` in the 32x32 MFMA C/D map.

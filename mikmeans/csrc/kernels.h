@@ -72,6 +72,7 @@ int update_n_chunks(int dtype, int K, int D, int64_t N);
 int fixed_exp(double maxabs);                     // largest e with maxabs * 2^e <= 2^20
 void set_update_max_sw(int sw);                   // cap the slice width (0 = none)
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s);
+void set_update_nt(int nt);                       // A/B knob: threads per workgroup
 
 // Reduce slabs (+ assign slots) into the packed f64 message
 // [K*D sums | K counts | inertia | n_changed] (length K*D + K + 2).

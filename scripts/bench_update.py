@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--patterns", default="random,mod,sorted,one")
+    ap.add_argument("--nts", default="0", help="threads/WG variants to A/B (0 = default)")
     a = ap.parse_args()
     from mikmeans.ops import fixed_exps, native
 
@@ -44,17 +45,24 @@ def main():
            "slice_width": C.update_slice_width(native.dtype_code(dt), a.k, a.d)}
     for p in a.patterns.split(","):
         lab = pats[p]()
-        C.update(X, lab, a.k, slab, cnt, nch, None, col_exp, 0, False)
-        ts = []
-        for _ in range(a.reps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
+        ts = {nt: [] for nt in a.nts.split(",")}
+        for nt in ts:
+            C.set_update_nt(int(nt))
             C.update(X, lab, a.k, slab, cnt, nch, None, col_exp, 0, False)
-            e1.record()
-            torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1))
-        ms = statistics.median(ts)
-        out[p] = {"ms": round(ms, 4), "read_GBps": round(X.numel() * X.element_size() / ms / 1e6, 1)}
+        for _ in range(a.reps):
+            for nt in ts:
+                C.set_update_nt(int(nt))
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                C.update(X, lab, a.k, slab, cnt, nch, None, col_exp, 0, False)
+                e1.record()
+                torch.cuda.synchronize()
+                ts[nt].append(e0.elapsed_time(e1))
+        C.set_update_nt(0)
+        for nt, v in ts.items():
+            ms = statistics.median(v)
+            key = p if nt == "0" else f"{p}_nt{nt}"
+            out[key] = {"ms": round(ms, 4), "read_GBps": round(X.numel() * X.element_size() / ms / 1e6, 1)}
     # reference point: a plain streaming read of X (column sums in f32)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     X.sum(0, dtype=torch.float32)
