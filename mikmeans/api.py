@@ -195,6 +195,14 @@ class KMeans:
         return self.fit(X, sample_weight=sample_weight)._out(self.labels_)
 
     # --------------------------------------------------------------- predict
+    def reset(self):
+        """Forget the fit (the reference's hard reset, app.mjs:225-237); keeps the config."""
+        for k in ("cluster_centers_", "labels_", "inertia_", "n_iter_", "converged_", "counts_",
+                  "n_features_in_", "fit_time_s_", "_engine"):
+            self.__dict__.pop(k, None)
+        self.history_ = []
+        return self
+
     def _check_fitted(self):
         if not hasattr(self, "cluster_centers_"):
             raise RuntimeError("KMeans instance is not fitted yet; call fit() first")
@@ -204,13 +212,19 @@ class KMeans:
             return t.cpu().numpy()
         return t
 
-    def predict(self, X):
+    def predict(self, X, *, unassign_nonfinite: bool = False):
+        """Nearest-centre labels.  ``unassign_nonfinite`` gives rows with NaN/inf
+        coordinates the label -1 ("unassigned", the reference's unassigned list,
+        app.mjs:421-433); the M-step ignores such labels."""
         self._check_fitted()
         from . import ops
 
         device = self.cluster_centers_.device
         Xt, was_numpy = _to_tensor(X, device, self.dtype)
         labels, _ = ops.assign(Xt, self.cluster_centers_, with_dist=False)
+        if unassign_nonfinite:
+            bad = ~torch.isfinite(Xt).all(dim=1)
+            labels = labels.masked_fill(bad, -1)
         return labels.cpu().numpy() if was_numpy else labels
 
     def transform(self, X):

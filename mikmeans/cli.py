@@ -7,6 +7,8 @@ Commands (the reference's top-bar controls, app.mjs:240-288, as a CLI):
 * ``predict``  -- labels of a dataset under a saved model
 * ``blobs``    -- write a synthetic Gaussian-blob dataset
 * ``room``     -- the trait-card game headless: seed/populate/auto-assign/dashboard/export/import
+* ``export``   -- checkpoint -> flat-float centroid JSON or room-export JSON (app.mjs:263-267)
+* ``import``   -- room-export JSON -> numeric checkpoint of trait vectors (app.mjs:268-282)
 * ``bench``    -- the headline benchmark (same as ``python bench.py``)
 * ``info``     -- device, native extension and build information
 """
@@ -126,6 +128,60 @@ def cmd_room(a) -> int:
     return 0
 
 
+def cmd_export(a) -> int:
+    """Checkpoint -> flat-float centroid JSON, or a room-export JSON whose centroids
+    are the model's clusters (named by their top features when a vocabulary exists)."""
+    from .utils.checkpoint import load_checkpoint
+    from .utils.jsjson import centroids_to_json
+
+    ck = load_checkpoint(a.model)
+    C = ck["centers"]
+    if a.format == "flat":
+        Path(a.output).write_text(centroids_to_json(C))
+    else:
+        from .models.room import Room
+
+        r = Room(a.room or ck.get("config", {}).get("run_id"), seed_jessica=False, seed=0)
+        vocab = ck.get("vocab")
+        names = None
+        if vocab:
+            from .utils.traits import label_clusters
+
+            names = label_clusters(C.numpy(), [1] * C.shape[0], vocab)
+        r.max_centroids = max(r.max_centroids, C.shape[0])
+        for k in range(C.shape[0]):
+            r.add_centroid((names[k] if names and names[k] else None) or f"Centroid {k + 1}",
+                           cid=f"c:{k}")
+        r.set_iteration(int(ck["iteration"]))
+        Path(a.output).write_text(r.export_json())
+    print(json.dumps({"output": a.output, "format": a.format, "k": int(C.shape[0])}))
+    return 0
+
+
+def cmd_import(a) -> int:
+    """Room-export JSON -> numeric model: cards become multi-hot trait vectors, the
+    room's centroids seed k-means (auto_assign), the result is saved as a checkpoint."""
+    from .models.room import Room
+    from .utils.checkpoint import save_checkpoint
+    from .utils.traits import encode_traits
+
+    r = Room.from_json(Path(a.room).read_text())
+    dash = r.auto_assign(seed=a.seed) if a.assign else r.dashboard()
+    X, vocab = encode_traits(r.cards)
+    cents = []
+    for c in r.centroids:
+        members = [i for i, card in enumerate(r.cards) if card.get("assignedTo") == c["id"]]
+        cents.append(X[members].mean(0) if members else np.zeros(X.shape[1], dtype=np.float32))
+    C = torch.from_numpy(np.stack(cents).astype(np.float32)) if cents else torch.zeros(0, X.shape[1])
+    save_checkpoint(a.output, C, int(r.meta.get("iteration") or 0), {"run_id": r.room, "mode": r.meta.get("mode")},
+                    extra={"vocab": vocab, "centroid_ids": [c["id"] for c in r.centroids],
+                           "centroid_names": [c["name"] for c in r.centroids]})
+    if a.save_room:
+        Path(a.save_room).write_text(r.export_json())
+    print("\n".join(dash["chips"]))
+    return 0
+
+
 def cmd_bench(a, rest) -> int:
     root = Path(__file__).resolve().parent.parent
     sys.path.insert(0, str(root))
@@ -183,6 +239,17 @@ def build_parser():
     r.add_argument("--iteration", type=int)
     r.add_argument("--export", help="write kmeans-room JSON here")
     r.add_argument("--seed", type=int, default=0)
+    e = sub.add_parser("export", help="checkpoint -> flat centroid JSON or room-export JSON")
+    e.add_argument("--model", required=True)
+    e.add_argument("--format", choices=["flat", "room"], default="flat")
+    e.add_argument("--room", help="room code for --format room")
+    e.add_argument("--output", required=True)
+    i = sub.add_parser("import", help="room-export JSON -> numeric checkpoint (trait vectors)")
+    i.add_argument("--room", required=True, help="kmeans-room-*.json")
+    i.add_argument("--output", required=True, help="checkpoint directory")
+    i.add_argument("--assign", action="store_true", help="re-assign cards by numeric k-means first")
+    i.add_argument("--save-room", help="also write the (re-assigned) room JSON")
+    i.add_argument("--seed", type=int, default=0)
     sub.add_parser("bench", help="headline benchmark (args forwarded to bench.py)", add_help=False)
     sub.add_parser("info", help="environment / build info")
     return ap
@@ -194,7 +261,7 @@ def main(argv=None) -> int:
         return cmd_bench(None, argv[1:])
     a = build_parser().parse_args(argv)
     return {"fit": cmd_fit, "predict": cmd_predict, "blobs": cmd_blobs, "room": cmd_room,
-            "info": cmd_info}[a.cmd](a)
+            "export": cmd_export, "import": cmd_import, "info": cmd_info}[a.cmd](a)
 
 
 if __name__ == "__main__":

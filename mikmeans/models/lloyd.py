@@ -141,6 +141,12 @@ class LloydEngine:
         if self.weights is not None:
             self.mind = torch.empty(self.n, dtype=torch.float32, device=dev)
 
+    def reset_labels(self):
+        """Unassign every point (the reference's Restart, app.mjs:167-178); the next
+        step re-assigns from the current centres and counts every point as changed."""
+        self.labels.fill_(-1)
+        return self
+
     def set_centers(self, centers: torch.Tensor):
         c = centers.to(device=self.device, dtype=torch.float32)
         if c.shape != (self.K, self.D):

@@ -78,6 +78,16 @@ class Comm:
             dist.destroy_process_group()
             self.owns_group = False
 
+    def identity(self) -> dict:
+        """Who this rank is (the reference's presence name + roster, app.mjs:22-27, :95)."""
+        import socket
+
+        dev = str(self.device)
+        if self.device.type == "cuda" and torch.cuda.is_available():
+            dev = f"{dev} ({torch.cuda.get_device_name(self.device)})"
+        return {"host": socket.gethostname(), "pid": os.getpid(), "rank": self.rank, "world": self.world,
+                "local_rank": self.local_rank, "backend": self.backend, "device": dev}
+
     @property
     def distributed(self) -> bool:
         return self.world > 1

@@ -87,3 +87,36 @@ def test_metrics_jsonl(tmp_path):
     for r in recs:
         assert sum(r["counts"]) == 2000 and r["balance"]["gap"] == max(r["counts"]) - min(r["counts"])
         assert r["world"] == 1 and r["run_id"] == "ABCD" and r["time_ms"] > 0
+
+
+def test_cli_export_import_roundtrip(tmp_path):
+    _run(["room", "--populate", "--centroid", "Sweet", "--centroid", "Fresh", "--auto", "--export", "r.json"],
+         tmp_path)
+    out = _run(["import", "--room", "r.json", "--output", "ck", "--assign", "--save-room", "r2.json"], tmp_path)
+    assert out.startswith("k = 2")
+    st = json.loads((tmp_path / "ck" / "state.json").read_text())
+    assert st["n_clusters"] == 2 and st["vocab"] and len(st["centroid_names"]) == 2
+    _run(["export", "--model", "ck", "--format", "room", "--output", "r3.json"], tmp_path)
+    r3 = json.loads((tmp_path / "r3.json").read_text())
+    assert [c["id"] for c in r3["centroids"]] == ["c:0", "c:1"] and r3["cards"] == []
+    _run(["export", "--model", "ck", "--format", "flat", "--output", "flat.json"], tmp_path)
+    flat = json.loads((tmp_path / "flat.json").read_text())
+    assert len(flat) == 2 * st["n_features"]
+
+
+def test_init_reset_and_unassigned_predict():
+    import mikmeans
+    from mikmeans import KMeans
+
+    comm = mikmeans.init("cpu")
+    assert comm.world == 1 and comm.identity()["rank"] == 0
+    X = np.random.default_rng(0).normal(size=(300, 3)).astype(np.float32)
+    km = KMeans(3, device="cpu").fit(X)
+    Y = X.copy()
+    Y[5, 0] = np.nan
+    Y[7, 2] = np.inf
+    lab = km.predict(Y, unassign_nonfinite=True)
+    assert lab[5] == -1 and lab[7] == -1 and (lab[[0, 1, 2]] >= 0).all()
+    km.reset()
+    with pytest.raises(RuntimeError):
+        km.predict(X)
