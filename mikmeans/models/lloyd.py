@@ -21,7 +21,9 @@ counter advances per Lloyd step and every step yields the same metric record
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -29,6 +31,15 @@ import torch
 from ..ops import cpu as cpu_ops
 from ..ops import native
 from ..parallel.comm import Comm
+from ..utils import profiling
+
+# roctx ranges around each phase (rocprofv3 --marker-trace); off by default: a range
+# push/pop is a host call per phase per iteration.
+_TRACE = os.environ.get("MIKMEANS_ROCTX", "0") not in ("", "0")
+
+
+def _phase(name: str):
+    return profiling.range(name) if _TRACE else contextlib.nullcontext()
 
 
 @dataclass
@@ -181,18 +192,22 @@ class LloydEngine:
             if self.weights is not None:
                 self.packed[KD + self.K] = (self.mind.double() * self.weights.double()).sum()
         elif self.n:
-            self.pk.assign(self.X, self.xn, self.labels, self.mind, self.slots, True)
-            C.update(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks, self.weights,
-                     self.col_exp, self.cnt_exp, False)
-            C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
-                     self.col_exp, self.cnt_exp)
+            with _phase("mikmeans.assign"):
+                self.pk.assign(self.X, self.xn, self.labels, self.mind, self.slots, True)
+            with _phase("mikmeans.update"):
+                C.update(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks, self.weights,
+                         self.col_exp, self.cnt_exp, False)
+                C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
+                         self.col_exp, self.cnt_exp)
             if self.weights is not None:
                 self.packed[KD + self.K] = (self.mind.double() * self.weights.double()).sum()
         else:
             self.packed.zero_()
-        self.comm.allreduce_(self.packed)
-        self._relocate_empty()
-        self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts)
+        with _phase("mikmeans.allreduce"):
+            self.comm.allreduce_(self.packed)
+        with _phase("mikmeans.finalize"):
+            self._relocate_empty()
+            self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts)
 
     def _assign_update_overlapped(self):
         C = self._C
