@@ -66,7 +66,7 @@ template <> struct Mfma16<float> {
   }
 };
 
-// DBG (diagnostic builds for A/B only, never the default): 1 = epilogue replaced by
+// DBG bit flags (diagnostic builds for A/B; 4 is a pipeline option): 1 = epilogue replaced by
 // one add per tile (MFMA + LDS pipeline alone), 2 = no ring refills / waits (MFMA +
 // epilogue alone on whatever the LDS holds).
 template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0>
@@ -120,9 +120,9 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
   const unsigned kmask = key6_mask();
 
   float dbg_sink = 0.f;
-  if constexpr (DBG == 2) { wait_vmcnt<0>(); raw_barrier(); }
+  if constexpr ((DBG & 2) != 0) { wait_vmcnt<0>(); raw_barrier(); }
   for (int c = 0; c < nch; ++c) {
-    if constexpr (DBG != 2) {
+    if constexpr ((DBG & 2) == 0) {
       // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
       if (C::NBUF == 3 && c + 1 < nch) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
       wait_lgkm0();
@@ -130,18 +130,34 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
       if (c + C::NBUF - 1 < nch) issue_chunk(c + C::NBUF - 1);
     }
     const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
+    // A fragments + |c|^2 of one tile from the LDS ring
+    auto load_tile = [&](int tl_i, u32x4* aw_, f32x4& ci_) {
+      const int tile = c * C::CT + tl_i;
+      ci_ = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
+      const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
+#pragma unroll
+      for (int q = 0; q < C::NQ; ++q) aw_[q] = *(const u32x4*)(tl + q * 1024);
+    };
+    // DBG & 4: prefetch the next tile's fragments before this tile's MFMAs (GT == 1)
+    u32x4 awn[C::NQ];
+    f32x4 cin;
+    if constexpr ((DBG & 4) != 0 && GT == 1) load_tile(0, awn, cin);
 #pragma unroll
     for (int tg = 0; tg < C::CT / GT; ++tg) {
       f32x4 acc[C::P][GT];
 #pragma unroll
       for (int t = 0; t < GT; ++t) {
         const int tl_i = tg * GT + t;
-        const int tile = c * C::CT + tl_i;
-        const f32x4 ci = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
-        const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
         u32x4 aw[C::NQ];
+        f32x4 ci;
+        if constexpr ((DBG & 4) != 0 && GT == 1) {
 #pragma unroll
-        for (int q = 0; q < C::NQ; ++q) aw[q] = *(const u32x4*)(tl + q * 1024);
+          for (int q = 0; q < C::NQ; ++q) aw[q] = awn[q];
+          ci = cin;
+          if (tl_i + 1 < C::CT) load_tile(tl_i + 1, awn, cin);
+        } else {
+          load_tile(tl_i, aw, ci);
+        }
 #pragma unroll
         for (int q = 0; q < C::NQ; ++q) {
 #pragma unroll
@@ -150,7 +166,7 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
         }
       }
       const int grp = c * (C::CT / GT) + tg;
-      if constexpr (DBG == 1) {
+      if constexpr ((DBG & 1) != 0) {
 #pragma unroll
         for (int p = 0; p < C::P; ++p) dbg_sink += acc[p][0][0];
         continue;
@@ -169,7 +185,7 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
           const f32x4& sv = acc[p][0];
           const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
           const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
-          if constexpr (DBG == 3) {
+          if constexpr ((DBG & 8) != 0) {
             seg_best[p] = min3f_v(min3f_v(k0, k1, k2), k3, seg_best[p]);
           } else {
             seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
@@ -213,7 +229,7 @@ __global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
     }
   }
 
-  if constexpr (DBG == 1) best[0] = fminf(best[0], dbg_sink);
+  if constexpr ((DBG & 1) != 0) best[0] = fminf(best[0], dbg_sink);
   float inert = 0.f;
   int changed = 0;
 #pragma unroll
@@ -310,13 +326,18 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
       case 11: return launch16_t<T, DPAD, P, 1, 2, 3, 2>(a, s);
       case 12: return launch16_t<T, DPAD, 8, 1, 2, 3>(a, s);      // 8 point-blocks per wave
       case 13: return launch16_t<T, DPAD, 2, 1, 2, 3>(a, s);      // 2 point-blocks per wave
-      case 14: return launch16_t<T, DPAD, P, 1, 2, 3, 3>(a, s);   // volatile min3 (sched barrier)
-      case 15: return launch16_t<T, DPAD, P, 1, 4, 2, 3>(a, s);
+      case 14: return launch16_t<T, DPAD, P, 1, 2, 3, 8>(a, s);   // volatile min3 (sched barrier)
+      case 15: return launch16_t<T, DPAD, P, 1, 4, 2, 8>(a, s);
       case 16: return launch16_t<T, DPAD, P, 1, 4, 2>(a, s);
       case 17: return launch16_t<T, DPAD, P, 1, 4, 3>(a, s);
       case 18: return launch16_t<T, DPAD, P, 1, 1, 3>(a, s);
       case 19: return launch16_t<T, DPAD, P, 1, 1, 2>(a, s);
-      case 20: return launch16_t<T, DPAD, P, 1, 4, 3, 3>(a, s);
+      case 20: return launch16_t<T, DPAD, P, 1, 4, 3, 8>(a, s);
+      case 23: return launch16_t<T, DPAD, P, 1, 4, 2, 3>(a, s);   // no epilogue, no ring
+      case 24: return launch16_t<T, DPAD, P, 1, 4, 2, 4>(a, s);   // A prefetch
+      case 25: return launch16_t<T, DPAD, P, 1, 4, 2, 5>(a, s);   // A prefetch, no epilogue
+      case 26: return launch16_t<T, DPAD, P, 1, 4, 2, 1>(a, s);   // no epilogue
+      case 27: return launch16_t<T, DPAD, P, 1, 4, 2, 2>(a, s);   // no ring
       case 21: return launch16_t<T, DPAD, 2, 1, 4, 2>(a, s);
       case 22: return launch16_t<T, DPAD, 8, 1, 4, 2>(a, s);
       default: break;
