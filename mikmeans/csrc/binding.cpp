@@ -221,7 +221,8 @@ void kpp_d2(const Tensor& X, const Tensor& c, bool first, const Tensor& d2, cons
 
 void kpp_sample(const Tensor& block_sums, const Tensor& d2, int64_t rows_per_block,
                 const Tensor& target, const Tensor& X, const Tensor& crow,
-                const c10::optional<Tensor>& idx_out) {
+                const c10::optional<Tensor>& idx_out, int64_t mode,
+                const c10::optional<Tensor>& totals_all, int64_t rank) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   const int64_t N = X.size(0);
@@ -233,10 +234,19 @@ void kpp_sample(const Tensor& block_sums, const Tensor& d2, int64_t rows_per_blo
   if (idx_out.has_value())
     TORCH_CHECK(idx_out->is_cuda() && idx_out->scalar_type() == at::kLong, "idx_out must be int64");
   TORCH_CHECK(N > 0, "mikmeans: kpp_sample on an empty shard");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "mikmeans: kpp_sample mode");
+  int world = 1;
+  if (mode == 2) {
+    TORCH_CHECK(totals_all.has_value(), "mikmeans: mode 2 needs totals_all");
+    check_f64(*totals_all, "totals_all", 1);
+    world = (int)totals_all->numel();
+    TORCH_CHECK(rank >= 0 && rank < world, "mikmeans: bad rank");
+  }
   hip_check(mk::launch_kpp_sample(dt, block_sums.data_ptr<double>(), (int)nb, d2.data_ptr<float>(),
                                   N, rows_per_block, target.data_ptr<double>(), X.data_ptr(),
                                   (int)X.size(1), ldx, crow.data_ptr<float>(),
-                                  opt_ptr<int64_t>(idx_out), stream()),
+                                  opt_ptr<int64_t>(idx_out), (int)mode, opt_ptr<double>(totals_all),
+                                  world, (int)rank, stream()),
             "kpp_sample");
 }
 

@@ -104,10 +104,13 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
 hipError_t launch_kpp_d2(int dtype, const void* X, int64_t N, int D, int64_t ldx, const float* c,
                          int first, float* d2, double* block_sums, int64_t rows_per_block,
                          int nblocks, hipStream_t s);
-// target: device double (rank-local); if < 0 writes zeros to crow.
+// mode 0: target = device double (rank-local; < 0 writes zeros to crow); mode 1: target
+// holds u, scaled by this rank's total; mode 2: target holds u, totals_all[world] decide
+// the owner rank and its local target on device.
 hipError_t launch_kpp_sample(int dtype, const double* block_sums, int nblocks, const float* d2,
                              int64_t N, int64_t rows_per_block, const double* target, const void* X,
-                             int D, int64_t ldx, float* crow, int64_t* idx_out, hipStream_t s);
+                             int D, int64_t ldx, float* crow, int64_t* idx_out, int mode,
+                             const double* totals_all, int world, int rank, hipStream_t s);
 
 // ---- synthetic Gaussian blobs (counter-based Philox, deterministic by index) --
 hipError_t launch_blob_centers(float* centers, int n_centers, int D, float box, uint64_t seed,

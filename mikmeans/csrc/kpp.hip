@@ -21,38 +21,54 @@ namespace mk {
 
 constexpr int KPP_NT = 256;
 
-template <typename T>
+// LPR lanes per row (each 16 B per pass over the row), UNR rows in flight per lane group.
+template <typename T, int LPR>
 __global__ __launch_bounds__(KPP_NT) void kpp_d2_kernel(const T* __restrict__ X, int64_t N, int D,
                                                         int64_t ldx, const float* __restrict__ c,
                                                         int first, float* __restrict__ d2,
                                                         double* __restrict__ block_sums,
                                                         int64_t rows_per_block) {
   constexpr int V = Elem<T>::V;
+  constexpr int UNR = 4;
+  constexpr int RPW = KPP_NT / LPR;  // rows per pass of the workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* cs = (float*)smem;
   for (int d = threadIdx.x; d < D; d += KPP_NT) cs[d] = c[d];
   __syncthreads();
-  const int sub = threadIdx.x & 15;
+  const int sub = threadIdx.x % LPR;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   int64_t r1 = r0 + rows_per_block;
   if (r1 > N) r1 = N;
   double part = 0.0;
-  for (int64_t i = r0 + (threadIdx.x >> 4); i < r1; i += KPP_NT / 16) {
-    const T* row = X + i * ldx;
-    float acc = 0.f;
-    for (int cc = sub * V; cc < D; cc += 16 * V) {
-      const u32x4 w = *(const u32x4*)(row + cc);
-      float f[V];
-      unpack16(w, f, (T*)nullptr);
+  for (int64_t base = r0 + threadIdx.x / LPR; base < r1; base += (int64_t)RPW * UNR) {
+    float acc[UNR];
 #pragma unroll
-      for (int e = 0; e < V; ++e) { const float df = f[e] - cs[cc + e]; acc += df * df; }
+    for (int u = 0; u < UNR; ++u) acc[u] = 0.f;
+    for (int cc = sub * V; cc < D; cc += LPR * V) {
+      u32x4 w[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int64_t i = base + (int64_t)u * RPW;
+        w[u] = i < r1 ? *(const u32x4*)(X + i * ldx + cc) : u32x4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        float f[V];
+        unpack16(w[u], f, (T*)nullptr);
+#pragma unroll
+        for (int e = 0; e < V; ++e) { const float df = f[e] - cs[cc + e]; acc[u] += df * df; }
+      }
     }
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
-    if (sub == 0) {
-      const float v = first ? acc : fminf(acc, d2[i]);
-      d2[i] = v;
-      part += v;
+    for (int u = 0; u < UNR; ++u) {
+#pragma unroll
+      for (int o = 1; o < LPR; o <<= 1) acc[u] += __shfl_xor(acc[u], o, 64);
+      const int64_t i = base + (int64_t)u * RPW;
+      if (sub == 0 && i < r1) {
+        const float v = first ? acc[u] : fminf(acc[u], d2[i]);
+        d2[i] = v;
+        part += v;
+      }
     }
   }
   part = wave_sum(part);
@@ -66,16 +82,31 @@ __global__ __launch_bounds__(KPP_NT) void kpp_d2_kernel(const T* __restrict__ X,
   }
 }
 
+template <typename T>
+static void launch_kpp_d2_t(const void* X, int64_t N, int D, int64_t ldx, const float* c, int first,
+                            float* d2, double* block_sums, int64_t rows_per_block, int nblocks,
+                            size_t lds, hipStream_t s) {
+  const int pieces = (D * (int)sizeof(T) + 15) / 16;  // 16-byte pieces per row
+  const T* Xt = (const T*)X;
+#define MK_KPP_LAUNCH(L)                                                                        \
+  hipLaunchKernelGGL((kpp_d2_kernel<T, L>), dim3(nblocks), dim3(KPP_NT), lds, s, Xt, N, D, ldx, c, \
+                     first, d2, block_sums, rows_per_block)
+  if (pieces >= 16) MK_KPP_LAUNCH(16);
+  else if (pieces >= 8) MK_KPP_LAUNCH(8);
+  else if (pieces >= 4) MK_KPP_LAUNCH(4);
+  else if (pieces >= 2) MK_KPP_LAUNCH(2);
+  else MK_KPP_LAUNCH(1);
+#undef MK_KPP_LAUNCH
+}
+
 hipError_t launch_kpp_d2(int dtype, const void* X, int64_t N, int D, int64_t ldx, const float* c,
                          int first, float* d2, double* block_sums, int64_t rows_per_block,
                          int nblocks, hipStream_t s) {
   const size_t lds = ((size_t)D * 4 + 15) / 16 * 16;
   if (dtype == DT_BF16)
-    hipLaunchKernelGGL(kpp_d2_kernel<uint16_t>, dim3(nblocks), dim3(KPP_NT), lds, s,
-                       (const uint16_t*)X, N, D, ldx, c, first, d2, block_sums, rows_per_block);
+    launch_kpp_d2_t<uint16_t>(X, N, D, ldx, c, first, d2, block_sums, rows_per_block, nblocks, lds, s);
   else
-    hipLaunchKernelGGL(kpp_d2_kernel<float>, dim3(nblocks), dim3(KPP_NT), lds, s, (const float*)X,
-                       N, D, ldx, c, first, d2, block_sums, rows_per_block);
+    launch_kpp_d2_t<float>(X, N, D, ldx, c, first, d2, block_sums, rows_per_block, nblocks, lds, s);
   return hipGetLastError();
 }
 
@@ -93,6 +124,10 @@ __device__ double block_scan_incl(double v, double* sh) {
   return sh[t];
 }
 
+// mode 0: *target_p is this rank's target (< 0: not the owner, write zeros).
+// mode 1: *target_p is u in [0,1); target = u * (this rank's total potential) -- one rank.
+// mode 2: *target_p is u; totals_all[world] are the gathered per-rank potentials: the
+//         owner rank and its local target are derived here (no host round trip).
 template <typename T>
 __global__ __launch_bounds__(1024) void kpp_sample_kernel(const double* __restrict__ block_sums,
                                                           int nblocks, const float* __restrict__ d2,
@@ -100,12 +135,30 @@ __global__ __launch_bounds__(1024) void kpp_sample_kernel(const double* __restri
                                                           const double* __restrict__ target_p,
                                                           const T* __restrict__ X, int D,
                                                           int64_t ldx, float* __restrict__ crow,
-                                                          int64_t* __restrict__ idx_out) {
+                                                          int64_t* __restrict__ idx_out, int mode,
+                                                          const double* __restrict__ totals_all,
+                                                          int world, int rank) {
   __shared__ double sh[1024];
   __shared__ int64_t sel;
   __shared__ double base_sh;
   const int t = threadIdx.x;
   double target = *target_p;
+  if (mode == 2) {
+    double tot = 0.0, before = 0.0;
+    int last = -1;
+    for (int r = 0; r < world; ++r) {
+      const double v = totals_all[r];
+      tot += v;
+      if (r < rank) before += v;
+      if (v > 0.0) last = r;
+    }
+    const double tgt = target * tot;
+    const double mine = totals_all[rank];
+    double local = tgt - before;
+    bool owner = local >= 0.0 && local < mine;
+    if (tgt >= tot && last == rank) { owner = true; local = mine * (1.0 - 1e-12); }
+    target = owner ? local : -1.0;
+  }
   if (!(target >= 0.0)) {  // not the owner rank (or NaN): contribute zeros
     for (int d = t; d < D; d += 1024) crow[d] = 0.f;
     if (t == 0 && idx_out) *idx_out = -1;
@@ -117,6 +170,7 @@ __global__ __launch_bounds__(1024) void kpp_sample_kernel(const double* __restri
   for (int b = t * per; b < (t + 1) * per && b < nblocks; ++b) segsum += block_sums[b];
   double incl = block_scan_incl(segsum, sh);
   const double total = sh[1023];
+  if (mode == 1) target *= total;
   if (target >= total) target = total * (1.0 - 1e-12);
   if (t == 0) { sel = -1; base_sh = 0.0; }
   __syncthreads();
@@ -198,13 +252,16 @@ __global__ __launch_bounds__(1024) void kpp_sample_kernel(const double* __restri
 
 hipError_t launch_kpp_sample(int dtype, const double* block_sums, int nblocks, const float* d2,
                              int64_t N, int64_t rows_per_block, const double* target, const void* X,
-                             int D, int64_t ldx, float* crow, int64_t* idx_out, hipStream_t s) {
+                             int D, int64_t ldx, float* crow, int64_t* idx_out, int mode,
+                             const double* totals_all, int world, int rank, hipStream_t s) {
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(kpp_sample_kernel<uint16_t>, dim3(1), dim3(1024), 0, s, block_sums, nblocks,
-                       d2, N, rows_per_block, target, (const uint16_t*)X, D, ldx, crow, idx_out);
+                       d2, N, rows_per_block, target, (const uint16_t*)X, D, ldx, crow, idx_out,
+                       mode, totals_all, world, rank);
   else
     hipLaunchKernelGGL(kpp_sample_kernel<float>, dim3(1), dim3(1024), 0, s, block_sums, nblocks,
-                       d2, N, rows_per_block, target, (const float*)X, D, ldx, crow, idx_out);
+                       d2, N, rows_per_block, target, (const float*)X, D, ldx, crow, idx_out,
+                       mode, totals_all, world, rank);
   return hipGetLastError();
 }
 

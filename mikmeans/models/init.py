@@ -116,19 +116,27 @@ def _kpp_gpu(X, centers, K, comm: Comm, u, L):
     cand = torch.empty((L, D), dtype=torch.float32, device=dev)
     if n:
         C.kpp_d2(X, centers[0], True, d2, bs, rpb)
+    W = comm.world
     for k in range(1, K):
         for t in range(L):
-            tot = bs.sum().reshape(1) if n else torch.zeros(1, dtype=torch.float64, device=dev)
-            allt = comm.all_gather(tot).reshape(-1)
-            target, _ = _local_target(allt, u[(k - 1) * L + t], comm.rank)
-            if n:
-                C.kpp_sample(bs, d2, rpb, target.reshape(1).contiguous(), X, crow, None)
+            uk = u[(k - 1) * L + t: (k - 1) * L + t + 1]
+            # the sampled row lands straight in centers[k] on one rank (L == 1)
+            row = centers[k] if (L == 1 and W == 1) else crow
+            if W == 1:
+                C.kpp_sample(bs, d2, rpb, uk, X, row, None, 1, None, 0)  # target = u * total, on device
             else:
-                crow.zero_()
-            comm.allreduce_(crow)
-            cand[t] = crow
+                tot = bs.sum().reshape(1) if n else torch.zeros(1, dtype=torch.float64, device=dev)
+                allt = comm.all_gather(tot).reshape(-1).contiguous()
+                if n:
+                    C.kpp_sample(bs, d2, rpb, uk, X, row, None, 2, allt, comm.rank)
+                else:
+                    row.zero_()
+                comm.allreduce_(row)
+            if L > 1:
+                cand[t] = row
+            elif row is not centers[k]:
+                centers[k] = row
         if L == 1:
-            centers[k] = cand[0]
             if n:
                 C.kpp_d2(X, centers[k], False, d2, bs, rpb)
             continue
