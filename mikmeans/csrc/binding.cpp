@@ -119,7 +119,7 @@ void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab
   const int D = (int)X.size(1);
   TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kInt && labels.numel() >= N,
               "mikmeans: labels must be int32 [N]");
-  const int sw = mk::update_slice_width(dt, (int)K, D);
+  const int sw = mk::update_slice_width(dt, (int)K, D, weights.has_value());
   TORCH_CHECK(sw == 0 ? n_chunks == 1 : n_chunks % 8 == 0, "mikmeans: bad n_chunks");
   check_i64(slab, "slab", n_chunks * K * D);
   check_i64(cnt_slab, "cnt_slab", n_chunks * K);
@@ -365,8 +365,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_assign16_gt", [](int64_t gt) { mk::set_assign16_gt((int)gt); }, "tuning: 16x16 epilogue tile group");
   m.def("assign_chunk_tiles", [](int64_t dt, int64_t dpad) { return mk::assign_chunk_tiles((int)dt, (int)dpad); });
   m.def("assign_cn_len", [](int64_t kpad) { return mk::assign_cn_len((int)kpad); });
-  m.def("update_slice_width", [](int64_t dt, int64_t K, int64_t D) { return mk::update_slice_width((int)dt, (int)K, (int)D); });
-  m.def("update_n_chunks", [](int64_t dt, int64_t K, int64_t D, int64_t N) { return mk::update_n_chunks((int)dt, (int)K, (int)D, N); });
+  m.def("update_slice_width", [](int64_t dt, int64_t K, int64_t D, bool w) { return mk::update_slice_width((int)dt, (int)K, (int)D, w); },
+        py::arg("dtype"), py::arg("K"), py::arg("D"), py::arg("weighted") = false);
+  m.def("update_n_chunks", [](int64_t dt, int64_t K, int64_t D, int64_t N, bool w) { return mk::update_n_chunks((int)dt, (int)K, (int)D, N, w); },
+        py::arg("dtype"), py::arg("K"), py::arg("D"), py::arg("N"), py::arg("weighted") = false);
   m.def("set_assign_p", [](int64_t p) { mk::set_assign_p((int)p); }, "tuning: points blocks per wave");
   m.def("get_assign_p", []() { return mk::get_assign_p(); });
   m.def("fixed_exp", [](double maxabs) { return mk::fixed_exp(maxabs); },

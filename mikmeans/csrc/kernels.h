@@ -67,8 +67,8 @@ struct UpdateArgs {
   int cnt_exp;           // counts scale 2^cnt_exp (0 when unweighted)
   int clamp;             // saturate contributions outside +-2^21 (streamed data)
 };
-int update_slice_width(int dtype, int K, int D);  // columns per workgroup (0 = global fallback)
-int update_n_chunks(int dtype, int K, int D, int64_t N);
+int update_slice_width(int dtype, int K, int D, bool weighted = false);  // 0 = global fallback
+int update_n_chunks(int dtype, int K, int D, int64_t N, bool weighted = false);
 int fixed_exp(double maxabs);                     // largest e with maxabs * 2^e <= 2^20
 void set_update_max_sw(int sw);                   // cap the slice width (0 = none)
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s);

@@ -82,14 +82,22 @@ __device__ __forceinline__ long long fx_q(float v, float sc) {
   return (long long)(int)(fx_bits<true>(v, sc) - 0x4B400000u);
 }
 
-// LDS: cells [K+1][ldc] u64 (row K is a sink for rows outside the chunk, so the hot
-// loop has no per-row branch) | weighted counts [K+1] i64 | add counts [K+1] u32 | flag
+// LDS: cells [K+1][LDc] u64 (row K is a sink for rows outside the chunk, so the hot
+// loop has no per-row branch) | add counts [K+1] u32 | flag | weighted counts [K+1] i64
+// (weighted fits only).  With an odd stride (LDc = SW/2 + 1) rows start on scattered
+// banks; where only LDc = SW/2 fits, the pair index is XOR-swizzled by label bits
+// instead (swz), which scatters the banks of one instruction the same way.
 struct UpdLayout {
-  int K, LDc;
+  int K, LDc, np, ksh;
+  bool swz;
   __device__ unsigned long long* cells(char* m) const { return (unsigned long long*)m; }
-  __device__ long long* wcnt(char* m) const { return (long long*)m + (size_t)(K + 1) * LDc; }
-  __device__ unsigned* nadd(char* m) const { return (unsigned*)(wcnt(m) + K + 1); }
+  __device__ unsigned* nadd(char* m) const { return (unsigned*)(cells(m) + (size_t)(K + 1) * LDc); }
   __device__ int* flag(char* m) const { return (int*)(nadd(m) + K + 1); }
+  __device__ long long* wcnt(char* m) const {
+    return (long long*)(((uintptr_t)(flag(m) + 1) + 7) & ~(uintptr_t)7);
+  }
+  // cell position of pair p of label k
+  __device__ int pos(int k, int p) const { return swz ? (p ^ ((k >> ksh) & (np - 1))) : p; }
 };
 
 // nadd[k]: adds since label k's last flush in bits 0..30; bit 31 = "k's slab row
@@ -109,8 +117,9 @@ __device__ __forceinline__ void upd_flush_label(const UpdateArgs& a, const UpdLa
   long long* dst = a.slab + (int64_t)chunk * a.K * a.D + (int64_t)k * a.D + slice * SW;
 #pragma unroll 4
   for (int p = 0; p < NP; ++p) {
-    const unsigned long long T = cells[p] - n * FX_MM;
-    cells[p] = 0;
+    const int q = L.pos(k, p);
+    const unsigned long long T = cells[q] - n * FX_MM;
+    cells[q] = 0;
     const int lo = (int)(uint32_t)T;
     const long long hi = (long long)(T - (unsigned long long)(long long)lo) >> 32;
     if (2 * p < cols) {
@@ -119,12 +128,11 @@ __device__ __forceinline__ void upd_flush_label(const UpdateArgs& a, const UpdLa
     }
   }
   if (slice == 0) {
-    long long* w = L.wcnt(m) + k;
-    const long long c = a.weights ? *w : (long long)n;
+    const long long c = a.weights ? L.wcnt(m)[k] : (long long)n;
     long long* cd = a.cnt_slab + (int64_t)chunk * a.K + k;
     if (add) *cd += c; else *cd = c;
   }
-  L.wcnt(m)[k] = 0;
+  if (a.weights) L.wcnt(m)[k] = 0;
   L.nadd(m)[k] = NADD_WRITTEN;
 }
 
@@ -151,7 +159,7 @@ __device__ void upd_flush_all(const UpdateArgs& a, const UpdLayout& L, char* m, 
   for (int e = threadIdx.x; e < a.K * NP; e += blockDim.x) {
     const int k = e / NP, p = e % NP;
     const unsigned na = nadd[k];
-    const unsigned long long T = cells[k * L.LDc + p] - (unsigned long long)(na & NADD_MASK) * FX_MM;
+    const unsigned long long T = cells[k * L.LDc + L.pos(k, p)] - (unsigned long long)(na & NADD_MASK) * FX_MM;
     const int lo = (int)(uint32_t)T;
     const long long hi = (long long)(T - (unsigned long long)(long long)lo) >> 32;
     if (2 * p < cols) {
@@ -161,23 +169,30 @@ __device__ void upd_flush_all(const UpdateArgs& a, const UpdLayout& L, char* m, 
     }
   }
   if (slice == 0) {
-    const long long* wcnt = L.wcnt(m);
     for (int k = threadIdx.x; k < a.K; k += blockDim.x) {
       const unsigned na = nadd[k];
-      const long long c = a.weights ? wcnt[k] : (long long)(na & NADD_MASK);
+      const long long c = a.weights ? L.wcnt(m)[k] : (long long)(na & NADD_MASK);
       long long* dst = a.cnt_slab + (int64_t)chunk * a.K + k;
       if (na & NADD_WRITTEN) *dst += c; else *dst = c;
     }
   }
 }
 
-enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2 };
+enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4 };
+
+constexpr int upd_ksh(int np) { return np >= 32 ? 0 : np == 16 ? 1 : np == 8 ? 2 : np == 4 ? 3 : np == 2 ? 4 : 5; }
+__host__ __device__ static inline size_t upd_lds_bytes(int K, int ldc, bool weighted) {
+  size_t b = (size_t)(K + 1) * ldc * 8 + (size_t)(K + 1) * 4 + 4;
+  b = (b + 7) & ~(size_t)7;
+  return b + (weighted ? (size_t)(K + 1) * 8 : 0);
+}
 
 template <typename T, int SW, int MODE, int NT = UPD_NT>
 __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
                                                         int64_t rows_per_chunk) {
   constexpr bool CLAMP = MODE & UPD_CLAMP;
   constexpr bool W = MODE & UPD_WEIGHTED;
+  constexpr bool SWZ = MODE & UPD_SWZ;
   constexpr int ES = sizeof(T);
   constexpr int PB = (SW * ES >= 16) ? 16 : SW * ES;  // bytes per lane load
   constexpr int V = PB / ES;                           // elements per lane load (even)
@@ -186,11 +201,13 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   constexpr int UNR = (UPD_MAX_PERIOD / RPP) < 8 ? (UPD_MAX_PERIOD / RPP) : 8;
   constexpr int PERIOD = RPP * UNR;
   constexpr unsigned THRESH = FX_LIM - PERIOD + 1;     // flush before any label passes FX_LIM
-  constexpr int LDC = SW / 2 + 1;                      // odd cell stride
+  constexpr int NP = SW / 2;
+  constexpr int LDC = SWZ ? NP : NP + 1;                // unpadded + swizzle, or odd stride
+  constexpr int KSH = upd_ksh(NP);
   static_assert(V % 2 == 0 && UNR >= 1 && FX_LIM >= PERIOD, "update tiling");
   typedef typename LoadT<PB>::type LT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const UpdLayout L{a.K, LDC};
+  const UpdLayout L{a.K, LDC, NP, KSH, SWZ};
   unsigned long long* cells = L.cells(smem);
   long long* wcnt = L.wcnt(smem);
   unsigned* nadd = L.nadd(smem);
@@ -202,7 +219,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
 
   {
     unsigned long long* z = cells;
-    const int nz = (int)(((size_t)(a.K + 1) * LDC * 8 + (size_t)(a.K + 1) * 12 + 16) / 8);
+    const int nz = (int)((upd_lds_bytes(a.K, LDC, W) + 7) / 8);
     for (int e = threadIdx.x; e < nz; e += NT) z[e] = 0;
   }
 
@@ -263,10 +280,19 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
     int cur = lab_[0];
     unsigned run = 0;
     auto emit = [&]() {
-      unsigned long long* dst = cells + cur * LDC + lp * (V / 2);
+      unsigned long long* dst = cells + cur * LDC;
+      if constexpr (SWZ) {
+        const int f = (cur >> KSH) & (NP - 1);
 #pragma unroll
-      for (int c = 0; c < V / 2; ++c)
-        __hip_atomic_fetch_add(dst + c, acc[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int c = 0; c < V / 2; ++c)
+          __hip_atomic_fetch_add(dst + ((lp * (V / 2) + c) ^ f), acc[c], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+#pragma unroll
+        for (int c = 0; c < V / 2; ++c)
+          __hip_atomic_fetch_add(dst + lp * (V / 2) + c, acc[c], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       if (counter) {
         const unsigned old = __hip_atomic_fetch_add(nadd + cur, run, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_WORKGROUP) & NADD_MASK;
@@ -360,8 +386,7 @@ __global__ __launch_bounds__(256) void update_global_kernel(UpdateArgs a) {
 
 static int esize(int dtype) { return dtype == DT_BF16 ? 2 : 4; }
 
-// LDS bytes: cells [K+1][ldc] u64 + weighted counts [K+1] i64 + add counts [K+1] u32 + flag
-static size_t upd_lds(int K, int ldc) { return (size_t)(K + 1) * ldc * 8 + (size_t)(K + 1) * 12 + 16; }
+
 
 // Cap on the slice width (0 = none).  A smaller slice shrinks the LDS footprint
 // so an update workgroup can be co-resident with assign workgroups when the
@@ -369,8 +394,9 @@ static size_t upd_lds(int K, int ldc) { return (size_t)(K + 1) * ldc * 8 + (size
 static int g_update_max_sw = 0;
 void set_update_max_sw(int sw) { g_update_max_sw = sw; }
 
-// slice width (columns per workgroup, 0 = global fallback) and LDS cell stride
-static int choose_sw(int dtype, int K, int D, int* ldc) {
+// slice width (columns per workgroup, 0 = global fallback) and LDS cell stride: the
+// widest slice that fits, odd stride preferred, else unpadded + swizzle
+static int choose_sw(int dtype, int K, int D, bool weighted, int* ldc) {
   const int es = esize(dtype);
   if ((D * es) % 4 || D % 2) return 0;
   int dp = 2;
@@ -378,18 +404,19 @@ static int choose_sw(int dtype, int K, int D, int* ldc) {
   for (int sw = 64; sw >= 2; sw /= 2) {
     if (sw > dp) continue;
     if (g_update_max_sw && sw > g_update_max_sw) continue;
-    if (upd_lds(K, sw / 2 + 1) <= UPD_LDS_MAX) { *ldc = sw / 2 + 1; return sw; }  // odd stride
+    if (upd_lds_bytes(K, sw / 2 + 1, weighted) <= UPD_LDS_MAX) { *ldc = sw / 2 + 1; return sw; }
+    if (upd_lds_bytes(K, sw / 2, weighted) <= UPD_LDS_MAX) { *ldc = sw / 2; return sw; }
   }
   return 0;
 }
 
-int update_slice_width(int dtype, int K, int D) {
+int update_slice_width(int dtype, int K, int D, bool weighted) {
   int ldc;
-  return choose_sw(dtype, K, D, &ldc);
+  return choose_sw(dtype, K, D, weighted, &ldc);
 }
 
-int update_n_chunks(int dtype, int K, int D, int64_t N) {
-  const int sw = update_slice_width(dtype, K, D);
+int update_n_chunks(int dtype, int K, int D, int64_t N, bool weighted) {
+  const int sw = update_slice_width(dtype, K, D, weighted);
   if (sw == 0) return 1;
   const int n_slices = (D + sw - 1) / sw;
   // LDS-bound: one resident workgroup per CU; aim for one wave of the 256 CUs
@@ -428,7 +455,7 @@ static hipError_t launch_nt(const UpdateArgs& a, int ldc, hipStream_t s) {
     attr = true;
   }
   hipLaunchKernelGGL((update_kernel<T, SW, MODE, NT>), dim3(a.n_chunks * n_slices), dim3(NT),
-                     upd_lds(a.K, ldc), s, a, n_slices, rows_per_chunk);
+                     upd_lds_bytes(a.K, ldc, (MODE & UPD_WEIGHTED) != 0), s, a, n_slices, rows_per_chunk);
   return hipGetLastError();
 }
 
@@ -450,12 +477,17 @@ static hipError_t launch_sw(const UpdateArgs& a, int ldc, hipStream_t s) {
 
 template <typename T, int SW>
 static hipError_t launch_clamp(const UpdateArgs& a, int ldc, hipStream_t s) {
-  const int mode = (a.clamp ? UPD_CLAMP : 0) | (a.weights ? UPD_WEIGHTED : 0);
+  const int mode = (a.clamp ? UPD_CLAMP : 0) | (a.weights ? UPD_WEIGHTED : 0) |
+                   (ldc == SW / 2 ? UPD_SWZ : 0);
   switch (mode) {
     case 0: return launch_sw<T, SW, 0>(a, ldc, s);
     case 1: return launch_sw<T, SW, 1>(a, ldc, s);
     case 2: return launch_sw<T, SW, 2>(a, ldc, s);
-    default: return launch_sw<T, SW, 3>(a, ldc, s);
+    case 3: return launch_sw<T, SW, 3>(a, ldc, s);
+    case 4: return launch_sw<T, SW, 4>(a, ldc, s);
+    case 5: return launch_sw<T, SW, 5>(a, ldc, s);
+    case 6: return launch_sw<T, SW, 6>(a, ldc, s);
+    default: return launch_sw<T, SW, 7>(a, ldc, s);
   }
 }
 
@@ -480,7 +512,7 @@ static hipError_t launch_update_t(const UpdateArgs& a, hipStream_t s, int sw, in
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s) {
   if (a.N <= 0) return hipSuccess;
   int ldc = 0;
-  const int sw = choose_sw(dtype, a.K, a.D, &ldc);
+  const int sw = choose_sw(dtype, a.K, a.D, a.weights != nullptr, &ldc);
   if (sw > 0 && a.n_chunks % 8) return hipErrorInvalidValue;
   return dtype == DT_BF16 ? launch_update_t<uint16_t>(a, s, sw, ldc)
                           : launch_update_t<float>(a, s, sw, ldc);

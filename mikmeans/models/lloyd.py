@@ -130,7 +130,7 @@ class LloydEngine:
             self.seg_ranges = [shard_range(self.n, s, self.segments) for s in range(self.segments)]
             C.set_update_max_sw(self.overlap_sw)
             seg_rows = max(e - s for s, e in self.seg_ranges)
-            self.seg_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, seg_rows)
+            self.seg_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, seg_rows, self.weights is not None)
             C.set_update_max_sw(0)
             self.n_chunks = self.seg_chunks * self.segments
             self.side = torch.cuda.Stream(device=dev)
@@ -138,7 +138,7 @@ class LloydEngine:
             self.side_done = torch.cuda.Event()
         else:
             self.segments = 1
-            self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, max(self.n, 1))
+            self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, max(self.n, 1), self.weights is not None)
         self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.int64, device=dev)
         self.cnt_slab = torch.empty(self.n_chunks * self.K, dtype=torch.int64, device=dev)
         self.xn = torch.empty(self.n, dtype=torch.float32, device=dev)

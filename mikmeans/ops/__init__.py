@@ -169,7 +169,7 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, K: int, weights: torch.T
     Xp = pad_columns(X)
     n, D = Xp.shape
     dt = dtype_code(Xp.dtype)
-    nch = C.update_n_chunks(dt, K, D, n)
+    nch = C.update_n_chunks(dt, K, D, n, weights is not None)
     slab = torch.empty(nch * K * D, dtype=torch.int64, device=X.device)
     cnt = torch.empty(nch * K, dtype=torch.int64, device=X.device)
     packed = torch.empty(K * D + K + 2, dtype=torch.float64, device=X.device)

@@ -127,6 +127,25 @@ def test_cluster_sums_fixed_point_bound(native, case):
     assert torch.equal(again, sums)
 
 
+@pytest.mark.parametrize("k,weighted", [(4096, False), (3500, True), (2048, False), (9000, True)])
+def test_cluster_sums_large_k_layouts(native, k, weighted):
+    """Unpadded + swizzled LDS layout (and the weighted-count variant) at large K."""
+    n, d = 200_000, 64
+    g = torch.Generator().manual_seed(k)
+    X = torch.randn(n, d, generator=g).to(torch.bfloat16)
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32)
+    w = torch.rand(n, generator=g) if weighted else None
+    sums, counts = ops.cluster_sums(X.to(DEV), lab.to(DEV), k, w.to(DEV) if weighted else None)
+    es, ec = ref.cluster_sums(X, lab, k, w)
+    if weighted:
+        torch.testing.assert_close(counts.cpu(), ec, rtol=1e-5, atol=1e-4)
+        torch.testing.assert_close(sums.cpu(), es, rtol=1e-5, atol=1e-3)
+    else:
+        assert torch.equal(counts.cpu(), ec)
+        colmax = X.float().abs().amax(0).double()
+        assert bool(((sums.cpu() - es).abs() <= ec[:, None] * colmax[None, :] * 2.0 ** -20).all())
+
+
 def test_cluster_sums_integer_data_exact(native):
     g = torch.Generator().manual_seed(5)
     X = torch.randint(-1000, 1000, (100_000, 64), generator=g).float()
