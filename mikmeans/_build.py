@@ -87,6 +87,9 @@ def _compile(src: Path, flags, verbose: bool) -> Path:
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
     os.replace(str(obj) + ".tmp", obj)
+    for old in BUILD.glob(f"{src.stem}.*.o"):  # keep only the current object per source
+        if old != obj:
+            old.unlink(missing_ok=True)
     return obj
 
 

@@ -67,7 +67,8 @@ class KMeans:
                  random_state: int | None = None, comm: Comm | None = None, frozen=None,
                  empty_cluster: str = "keep", check_every: int = 1, n_local_trials=None,
                  verbose: int = 0, mode: str = "learn", run_id: str | None = None,
-                 checkpoint_every: int = 0, checkpoint_dir: str | None = None, metrics_path: str | None = None):
+                 checkpoint_every: int = 0, checkpoint_dir: str | None = None, metrics_path: str | None = None,
+                 graph: bool = False):
         self.n_clusters = int(n_clusters)
         self.init = init
         self.n_init = int(n_init)
@@ -87,6 +88,7 @@ class KMeans:
         self.checkpoint_every = int(checkpoint_every)
         self.checkpoint_dir = checkpoint_dir
         self.metrics_path = metrics_path
+        self.graph = bool(graph)
         self.history_: list[dict] = []
 
     # ---------------------------------------------------------------- config
@@ -97,7 +99,7 @@ class KMeans:
                    empty_cluster=cfg.empty_cluster, check_every=cfg.check_every,
                    n_local_trials=cfg.n_local_trials, verbose=cfg.verbose, mode=cfg.mode,
                    run_id=cfg.run_id, checkpoint_every=cfg.checkpoint_every,
-                   checkpoint_dir=cfg.checkpoint_dir, metrics_path=cfg.metrics_path, **kw)
+                   checkpoint_dir=cfg.checkpoint_dir, metrics_path=cfg.metrics_path, graph=cfg.graph, **kw)
 
     def get_config(self) -> KMeansConfig:
         return KMeansConfig(n_clusters=self.n_clusters, init=self.init if isinstance(self.init, str) else "array",
@@ -107,7 +109,8 @@ class KMeans:
                             empty_cluster=self.empty_cluster, check_every=self.check_every,
                             n_local_trials=self.n_local_trials, mode=self.mode, run_id=self.run_id,
                             verbose=self.verbose, checkpoint_every=self.checkpoint_every,
-                            checkpoint_dir=self.checkpoint_dir, metrics_path=self.metrics_path)
+                            checkpoint_dir=self.checkpoint_dir, metrics_path=self.metrics_path,
+                            graph=self.graph)
 
     # ------------------------------------------------------------------- fit
     def fit(self, X, y=None, sample_weight=None, *, resume_from=None):
@@ -164,6 +167,8 @@ class KMeans:
                     save_checkpoint(self.checkpoint_dir, _eng.centers, st.iteration, self.get_config(),
                                     history=_hist, comm=comm)
 
+            if self.graph:
+                eng.capture()
             remaining = max(0, self.max_iter - start_iter)
             n_iter, converged, _ = eng.run(remaining, tol_abs, check_every=self.check_every, callback=cb)
             if mlog is not None:

@@ -56,6 +56,7 @@ class KMeansConfig:
     run_id: str | None = None
     verbose: int = 0
     metrics_path: str | None = None  # per-iteration JSONL (rank 0)
+    graph: bool = False              # replay each Lloyd iteration as one captured hipGraph
 
     def to_dict(self):
         return asdict(self)

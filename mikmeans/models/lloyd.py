@@ -175,12 +175,50 @@ class LloydEngine:
     # ------------------------------------------------------------- iteration
     def step(self):
         """One Lloyd iteration (E-step on the current centres, M-step, all-reduce, finalize)."""
-        if self.gpu:
+        graphs = getattr(self, "_graphs", None)
+        if graphs is not None:
+            graphs[self._gphase].replay()   # one hipGraph launch for the whole iteration
+            self._gphase ^= 1
+        elif self.gpu:
             self._step_gpu()
         else:
             self._step_cpu()
         self.C, self.Cnew = self.Cnew, self.C
         self.iteration += 1
+
+    def capture(self):
+        """Record one Lloyd iteration as a hipGraph (two, one per centre-buffer parity) so
+        each later :meth:`step` is a single graph launch instead of ~6 kernel launches and
+        the RCCL call.  Needs the sync-free path: GPU, empty policy 'keep', no segment
+        overlap.  The graphs replay exactly the kernels :meth:`step` would launch."""
+        if not self.gpu or self.empty_policy != "keep" or self.segments > 1 or not self.n:
+            return self
+        if getattr(self, "_graphs", None) is not None:
+            return self
+        # eager warm-up on a side stream: kernel attributes, RCCL communicator, allocator
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        C0 = self.C.clone()
+        lab0 = self.labels.clone()
+        with torch.cuda.stream(side):
+            self._step_gpu()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        graphs = []
+        for _ in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                self._step_gpu()
+            graphs.append(g)
+            self.C, self.Cnew = self.Cnew, self.C
+        # the warm-up changed labels / slots: restore the pre-capture state
+        self.C.copy_(C0)
+        self.labels.copy_(lab0)
+        self.pk.finalize(0, None, self.C)
+        if self.slots is not None:
+            self.slots.zero_()
+        self._graphs = graphs
+        self._gphase = 0
+        return self
 
     def _step_gpu(self):
         C = self._C

@@ -253,3 +253,28 @@ def test_native_extension_is_loaded(native):
     maps = open("/proc/self/maps").read()
     hip = {l.split()[-1] for l in maps.splitlines() if "libamdhip64" in l}
     assert len(hip) == 1, hip  # exactly one HIP runtime (torch's)
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_lloyd_graph_replay_matches_eager(native, weighted):
+    """hipGraph-captured iterations (LloydEngine.capture) are bitwise the eager ones."""
+    from mikmeans.models.lloyd import LloydEngine
+
+    X = B.make_blobs(50_000, 64, 40, seed=9, dtype=torch.bfloat16, device=DEV)
+    w = torch.rand(50_000, device=DEV) if weighted else None
+    C0 = X[:40].float()
+    ea = LloydEngine(X, 40, sample_weight=w).set_centers(C0)
+    eb = LloydEngine(X, 40, sample_weight=w).set_centers(C0).capture()
+    assert eb._graphs is not None
+    for _ in range(5):
+        ea.step()
+        eb.step()
+        torch.cuda.synchronize()
+        assert torch.equal(ea.centers, eb.centers)
+        sa, sb = ea.last_stats(), eb.last_stats()
+        assert sa.n_changed == sb.n_changed and sa.inertia == sb.inertia
+    eb.set_centers(C0)
+    ea.set_centers(C0)
+    ea.step()
+    eb.step()
+    assert torch.equal(ea.centers, eb.centers)
