@@ -167,17 +167,17 @@ def _bench_minibatch(args, cfg, comm, dtype):
     N, D, K = cfg["n"], cfg["d"], cfg["k"]
     b = args.batch
     stream = BlobStream(N, D, K, b, seed=args.seed, dtype=dtype, device=comm.device, rank=comm.rank,
-                        world=comm.world)
+                        world=comm.world, with_norms=True)  # row norms fused into the generator
     eng = MiniBatchEngine(K, D, b, dtype=dtype, device=comm.device, comm=comm)
     first = next(stream)
     eng.set_centers(init_random(first, D, K, b * comm.world, comm.rank * b, comm, args.seed))
     for _ in range(args.warmup):
-        eng.partial_fit(next(stream))
+        eng.partial_fit(next(stream), stream.last_norms)
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.partial_fit(next(stream))  # includes on-device generation of the batch
+        eng.partial_fit(next(stream), stream.last_norms)  # includes on-device generation of the batch
     torch.cuda.synchronize()
     comm.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=comm.device)

@@ -355,7 +355,8 @@ class MiniBatchKMeans:
         eng = self._engine(first.shape[1], first.device)
         eng.set_centers(self._init_centers(first.to(self.dtype)))
         for _ in range(steps):
-            eng.partial_fit(next(stream))
+            Xb = next(stream)
+            eng.partial_fit(Xb, getattr(stream, "last_norms", None))
         self._finish(eng)
         return self
 

@@ -259,7 +259,7 @@ void blob_centers(const Tensor& centers, double box, int64_t seed) {
 }
 
 void blobs(const Tensor& X, int64_t i0, const Tensor& centers, double stddev, int64_t seed,
-           const c10::optional<Tensor>& y) {
+           const c10::optional<Tensor>& y, const c10::optional<Tensor>& xn) {
   const int dt = dtype_of(X);
   check_cuda(X, "X");
   TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "X must be 2-D with unit column stride");
@@ -268,10 +268,11 @@ void blobs(const Tensor& X, int64_t i0, const Tensor& centers, double stddev, in
   if (y.has_value())
     TORCH_CHECK(y->is_cuda() && y->scalar_type() == at::kInt && y->numel() >= X.size(0),
                 "y must be int32 [n]");
+  if (xn.has_value()) check_f32(*xn, "xn", X.size(0));
   const int64_t ldx = X.size(0) <= 1 ? X.size(1) : X.stride(0);
   hip_check(mk::launch_blobs(dt, X.data_ptr(), i0, X.size(0), (int)X.size(1), ldx,
                              centers.data_ptr<float>(), (int)centers.size(0), (float)stddev,
-                             (uint64_t)seed, opt_ptr<int32_t>(y), stream()),
+                             (uint64_t)seed, opt_ptr<int32_t>(y), opt_ptr<float>(xn), stream()),
             "blobs");
 }
 

@@ -117,6 +117,6 @@ hipError_t launch_blob_centers(float* centers, int n_centers, int D, float box, 
                                hipStream_t s);
 hipError_t launch_blobs(int dtype, void* X, int64_t i0, int64_t n, int D, int64_t ldx,
                         const float* centers, int n_centers, float stddev, uint64_t seed,
-                        int32_t* y, hipStream_t s);
+                        int32_t* y, float* xn, hipStream_t s);
 
 }  // namespace mk

@@ -302,48 +302,98 @@ hipError_t launch_blob_centers(float* centers, int n_centers, int D, float box, 
   return hipGetLastError();
 }
 
-template <typename T>
+// TPR threads per row (power of two); thread t generates the 4-element groups
+// g = t, t + TPR, ... so each store instruction of the row's threads is contiguous.
+// The row's blob id is drawn once (lane t == 0) and broadcast; the squared norm of
+// the stored (rounded) values is reduced across the row's lanes when xn is given, so
+// a streamed mini-batch needs no separate row-norm pass.
+template <typename T, int TPR>
 __global__ __launch_bounds__(256) void blobs_kernel(T* X, int64_t i0, int64_t n, int D, int64_t ldx,
                                                     const float* __restrict__ centers,
                                                     int n_centers, float stddev, uint32_t k0,
-                                                    uint32_t k1, int32_t* y) {
+                                                    uint32_t k1, int32_t* y, float* xn, int vec) {
   const int G = (D + 3) / 4;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= n * G) return;
-  const int64_t il = e / G;
-  const int g = (int)(e % G);
-  const uint64_t gi = (uint64_t)(i0 + il);
-  const U4 rc = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), TAG_CID, 0u}, k0, k1);
-  const int cid = (int)__umulhi(rc.x, (uint32_t)n_centers);
-  if (y && g == 0) y[il] = cid;
-  const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
-  const float rad0 = sqrtf(-2.f * logf(u01_open0(r.x)));
-  const float rad1 = sqrtf(-2.f * logf(u01_open0(r.z)));
-  float s0, c0, s1, c1;
-  sincospif(2.f * u01(r.y), &s0, &c0);
-  sincospif(2.f * u01(r.w), &s1, &c1);
-  const float z[4] = {rad0 * c0, rad0 * s0, rad1 * c1, rad1 * s1};
-  const float* mu = centers + (int64_t)cid * D;
-  T* out = X + il * ldx;
+  const int64_t il = e / TPR;
+  const int t = (int)(e % TPR);
+  const bool row_ok = il < n;
+  const uint64_t gi = (uint64_t)(i0 + (row_ok ? il : 0));
+  int cid = 0;
+  if (t == 0) {
+    const U4 rc = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), TAG_CID, 0u}, k0, k1);
+    cid = (int)__umulhi(rc.x, (uint32_t)n_centers);
+  }
+  cid = __shfl(cid, (int)(threadIdx.x & 63) & ~(TPR - 1), 64);
+  float sq = 0.f;
+  if (row_ok) {
+    if (y && t == 0) y[il] = cid;
+    const float* mu = centers + (int64_t)cid * D;
+    T* out = X + il * ldx;
+    for (int g = t; g < G; g += TPR) {
+      const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
+      const float rad0 = sqrtf(-2.f * logf(u01_open0(r.x)));
+      const float rad1 = sqrtf(-2.f * logf(u01_open0(r.z)));
+      float s0, c0, s1, c1;
+      sincospif(2.f * u01(r.y), &s0, &c0);
+      sincospif(2.f * u01(r.w), &s1, &c1);
+      const float z[4] = {rad0 * c0, rad0 * s0, rad1 * c1, rad1 * s1};
+      T v[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int d = 4 * g + j;
-    if (d < D) out[d] = Elem<T>::from_f32(mu[d] + stddev * z[j]);
+      for (int j = 0; j < 4; ++j) {
+        const int d = 4 * g + j;
+        v[j] = Elem<T>::from_f32(d < D ? mu[d] + stddev * z[j] : 0.f);
+        const float f = Elem<T>::to_f32(v[j]);
+        if (d < D) sq += f * f;
+      }
+      if (vec && 4 * g + 3 < D) {  // one 8-byte (bf16) / 16-byte (f32) store
+        if constexpr (sizeof(T) == 2) {
+          uint2 w;
+          w.x = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
+          w.y = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
+          *(uint2*)(out + 4 * g) = w;
+        } else {
+          *(f32x4*)(out + 4 * g) = f32x4{v[0], v[1], v[2], v[3]};
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (4 * g + j < D) out[4 * g + j] = v[j];
+      }
+    }
+  }
+  if (xn) {
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
+    if (row_ok && t == 0) xn[il] = sq;
   }
 }
 
 hipError_t launch_blobs(int dtype, void* X, int64_t i0, int64_t n, int D, int64_t ldx,
                         const float* centers, int n_centers, float stddev, uint64_t seed,
-                        int32_t* y, hipStream_t s) {
+                        int32_t* y, float* xn, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  const int64_t tot = n * ((D + 3) / 4);
+  const int G = (D + 3) / 4;
+  const int es = dtype == DT_BF16 ? 2 : 4;
+  const int vec = ((uintptr_t)X % (4 * es) == 0 && (ldx * es) % (4 * es) == 0) ? 1 : 0;
+  int tpr = 1;
+  while (tpr < G && tpr < 16) tpr *= 2;
+  const int64_t tot = n * tpr;
   const unsigned nb = (unsigned)((tot + 255) / 256);
-  if (dtype == DT_BF16)
-    hipLaunchKernelGGL(blobs_kernel<uint16_t>, dim3(nb), dim3(256), 0, s, (uint16_t*)X, i0, n, D,
-                       ldx, centers, n_centers, stddev, (uint32_t)seed, (uint32_t)(seed >> 32), y);
-  else
-    hipLaunchKernelGGL(blobs_kernel<float>, dim3(nb), dim3(256), 0, s, (float*)X, i0, n, D, ldx,
-                       centers, n_centers, stddev, (uint32_t)seed, (uint32_t)(seed >> 32), y);
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#define MK_BLOBS(TT, TP)                                                                         \
+  hipLaunchKernelGGL((blobs_kernel<TT, TP>), dim3(nb), dim3(256), 0, s, (TT*)X, i0, n, D, ldx,   \
+                     centers, n_centers, stddev, k0, k1, y, xn, vec)
+#define MK_BLOBS_T(TT)                                                                           \
+  switch (tpr) {                                                                                 \
+    case 1: MK_BLOBS(TT, 1); break;                                                              \
+    case 2: MK_BLOBS(TT, 2); break;                                                              \
+    case 4: MK_BLOBS(TT, 4); break;                                                              \
+    case 8: MK_BLOBS(TT, 8); break;                                                              \
+    default: MK_BLOBS(TT, 16); break;                                                            \
+  }
+  if (dtype == DT_BF16) { MK_BLOBS_T(uint16_t) } else { MK_BLOBS_T(float) }
+#undef MK_BLOBS_T
+#undef MK_BLOBS
   return hipGetLastError();
 }
 

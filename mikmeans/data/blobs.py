@@ -90,11 +90,13 @@ def blob_centers(n_centers: int, d: int, box: float = 10.0, seed: int = 0, devic
 
 def make_blobs(n: int, d: int, n_centers: int, *, std: float = 1.0, box: float = 10.0, seed: int = 0,
                i0: int = 0, dtype=torch.float32, device="cpu", return_labels: bool = False,
-               centers: torch.Tensor | None = None, out: torch.Tensor | None = None):
+               centers: torch.Tensor | None = None, out: torch.Tensor | None = None,
+               norms: torch.Tensor | None = None):
     """Rows ``[i0, i0+n)`` of the ``(seed, n_centers, d)`` blob dataset.
 
     On a GPU device the rows are generated in place by the HIP kernel (``out``
-    may be a preallocated ``[n, ldx>=d]`` view, e.g. column-padded).
+    may be a preallocated ``[n, ldx>=d]`` view, e.g. column-padded); ``norms``
+    (float32 ``[n]``) receives the squared row norms of the stored values.
     """
     device = torch.device(device)
     if centers is None:
@@ -104,7 +106,7 @@ def make_blobs(n: int, d: int, n_centers: int, *, std: float = 1.0, box: float =
         X = out if out is not None else torch.empty((n, d), dtype=dtype, device=device)
         y = torch.empty(n, dtype=torch.int32, device=device) if return_labels else None
         C.blobs(X, int(i0), centers.to(device=device, dtype=torch.float32).contiguous(), float(std),
-                int(seed), y)
+                int(seed), y, norms)
         return (X, y) if return_labels else X
     res = blobs_np(i0, n, centers.cpu().numpy().astype(np.float32), std, seed, return_labels)
     Xn, y = (res if return_labels else (res, None))
@@ -112,6 +114,8 @@ def make_blobs(n: int, d: int, n_centers: int, *, std: float = 1.0, box: float =
     if out is not None:
         out.copy_(X)
         X = out
+    if norms is not None:
+        norms.copy_(X.float().pow(2).sum(1))
     return (X, torch.from_numpy(y)) if return_labels else X
 
 
@@ -123,13 +127,17 @@ class BlobStream:
     """
 
     def __init__(self, n_total: int, d: int, n_centers: int, batch: int, *, std=1.0, box=10.0,
-                 seed=0, dtype=torch.float32, device="cpu", rank=0, world=1, offset=0):
+                 seed=0, dtype=torch.float32, device="cpu", rank=0, world=1, offset=0,
+                 with_norms: bool = False):
         self.n_total, self.d, self.batch = n_total, d, batch
         self.std, self.seed, self.dtype = std, seed, dtype
         self.device = torch.device(device)
         self.rank, self.world, self.offset = rank, world, offset
         self.centers = blob_centers(n_centers, d, box, seed, device=self.device)
         self._buf = None
+        self.with_norms = with_norms
+        self._nbuf = None
+        self.last_norms = None   # squared row norms of the last batch (with_norms=True)
         self.step = 0
 
     def __iter__(self):
@@ -147,5 +155,11 @@ class BlobStream:
         if self._buf is None or self._buf.shape[0] < self.batch:
             self._buf = torch.empty((self.batch, self.d), dtype=self.dtype, device=self.device)
         X = self._buf[:n]
+        nrm = None
+        if self.with_norms:
+            if self._nbuf is None or self._nbuf.shape[0] < self.batch:
+                self._nbuf = torch.empty(self.batch, dtype=torch.float32, device=self.device)
+            nrm = self._nbuf[:n]
+        self.last_norms = nrm
         return make_blobs(n, self.d, 0, std=self.std, seed=self.seed, i0=start, dtype=self.dtype,
-                          device=self.device, centers=self.centers, out=X)
+                          device=self.device, centers=self.centers, out=X, norms=nrm)

@@ -74,16 +74,18 @@ class MiniBatchEngine:
     def centers(self):
         return self.C[:, : self.D]
 
-    def partial_fit(self, Xb: torch.Tensor):
-        """One mini-batch step on this rank's batch ``Xb`` (may be empty)."""
+    def partial_fit(self, Xb: torch.Tensor, norms: torch.Tensor | None = None):
+        """One mini-batch step on this rank's batch ``Xb`` (may be empty).  ``norms``:
+        precomputed squared row norms (e.g. fused into the blob generator); the GPU
+        path otherwise runs a row-norm pass for the batch inertia."""
         if self.gpu:
-            self._step_gpu(Xb)
+            self._step_gpu(Xb, norms)
         else:
             self._step_cpu(Xb)
         self.C, self.Cnew = self.Cnew, self.C
         self.steps += 1
 
-    def _step_gpu(self, Xb):
+    def _step_gpu(self, Xb, norms=None):
         C = self._C
         Xb = pad_columns(Xb.to(self.device), self.dtype)
         b = Xb.shape[0]
@@ -100,8 +102,12 @@ class MiniBatchEngine:
                 bound = 8.0 * col_max_abs(Xb).clamp_min(1e-30)
             self.col_exp, _ = fixed_exps(Xb, None, comm=self.comm, bound=bound)
         if b:
-            xn, lab = self.xn[:b], self.labels[:b]
-            C.row_sqnorm(Xb, xn)
+            lab = self.labels[:b]
+            if norms is not None and norms.shape[0] >= b and norms.dtype == torch.float32 and norms.is_cuda:
+                xn = norms[:b].contiguous()
+            else:
+                xn = self.xn[:b]
+                C.row_sqnorm(Xb, xn)
             self.pk.assign(Xb, xn, lab, None, self.slots, False)
             C.update(Xb, lab, self.K, self.slab, self.cnt_slab, self.n_chunks, None, self.col_exp, 0, True)
             C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,

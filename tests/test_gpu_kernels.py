@@ -166,6 +166,12 @@ def test_blobs_match_numpy_mirror(native, dtype):
     assert np.array_equal(yg.cpu().numpy(), yn)
     tol = 1e-4 if dtype == torch.float32 else 8e-2
     np.testing.assert_allclose(Xg.float().cpu().numpy(), Xn, rtol=0, atol=tol)
+    # fused squared norms of the stored values, strided (non-16-byte) output rows too
+    nrm = torch.empty(5000, dtype=torch.float32, device=DEV)
+    Xs = torch.empty((5000, 41), dtype=dtype, device=DEV)[:, :40]
+    B.make_blobs(5000, 40, 16, seed=11, i0=123456789, dtype=dtype, device=DEV, centers=Cg, out=Xs, norms=nrm)
+    assert torch.equal(Xs, Xg)
+    torch.testing.assert_close(nrm, Xg.float().pow(2).sum(1), rtol=1e-5, atol=1e-3)
 
 
 def test_lloyd_gpu_matches_cpu_engine(native):
