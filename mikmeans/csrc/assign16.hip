@@ -66,11 +66,12 @@ template <> struct Mfma16<float> {
   }
 };
 
-// DBG bit flags (diagnostic builds for A/B; 4 is a pipeline option): 1 = epilogue replaced by
+// DBG bit flags (diagnostic builds for A/B; 4 and 16 are pipeline options; 16 = at
+// least 4 waves per SIMD, i.e. <= 128 VGPRs): 1 = epilogue replaced by
 // one add per tile (MFMA + LDS pipeline alone), 2 = no ring refills / waits (MFMA +
 // epilogue alone on whatever the LDS holds).
 template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0>
-__global__ __launch_bounds__(256) void assign16_kernel(AssignArgs a) {
+__global__ __launch_bounds__(256, (DBG & 16) ? 4 : 1) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -338,6 +339,9 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
       case 25: return launch16_t<T, DPAD, P, 1, 4, 2, 5>(a, s);   // A prefetch, no epilogue
       case 26: return launch16_t<T, DPAD, P, 1, 4, 2, 1>(a, s);   // no epilogue
       case 27: return launch16_t<T, DPAD, P, 1, 4, 2, 2>(a, s);   // no ring
+      case 29: return launch16_t<T, DPAD, P, 1, 4, 2, 16>(a, s);  // <= 128 VGPRs (4 waves/SIMD)
+      case 30: return launch16_t<T, DPAD, P, 1, 2, 3, 16>(a, s);
+      case 31: return launch16_t<T, DPAD, P, 1, 4, 3, 16>(a, s);
       case 21: return launch16_t<T, DPAD, 2, 1, 4, 2>(a, s);
       case 22: return launch16_t<T, DPAD, 8, 1, 4, 2>(a, s);
       default: break;
@@ -348,7 +352,10 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
     // chunks in a 2-slot ring.  A/B on MI355X at N=2e7 D=128 K=1024 bf16 (scripts/
     // ab_kernels.py, one process, interleaved rounds): 1279-1317 TF/s vs 1218-1265 for
     // 4/8 KiB chunks with 3 slots, 1099 / 1250 for 2 / 8 point blocks per wave.
-    return launch16_t<T, DPAD, P, 1, CT, 2>(a, s);
+    // bf16: at most 128 VGPRs (4 waves per SIMD; <= 5 spilled registers): +2.5 % at the
+    // headline shape (1339 vs 1306 TF/s).  f32 would spill heavily under that bound.
+    constexpr int WB = sizeof(T) == 2 ? 16 : 0;
+    return launch16_t<T, DPAD, P, 1, CT, 2, WB>(a, s);
   }
   const int want = g_assign16_gt;
   if (want >= 4 && CT % 4 == 0) return launch16_t<T, DPAD, P, (CT % 4 == 0 ? 4 : 1)>(a, s);
