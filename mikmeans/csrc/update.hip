@@ -94,7 +94,12 @@ struct UpdLayout {
   __device__ unsigned* nadd(char* m) const { return (unsigned*)(cells(m) + (size_t)(K + 1) * LDc); }
   __device__ int* flag(char* m) const { return (int*)(nadd(m) + K + 1); }
   __device__ long long* wcnt(char* m) const {
-    return (long long*)(((uintptr_t)(flag(m) + 1) + 7) & ~(uintptr_t)7);
+    return (long long*)(((uintptr_t)(flag(m) + 2) + 7) & ~(uintptr_t)7);
+  }
+  __device__ int* nhot(char* m) const { return flag(m) + 1; }
+  // list of labels being flushed (u16), after the weighted counts when present
+  __device__ unsigned short* hot(char* m, bool weighted) const {
+    return (unsigned short*)(wcnt(m) + (weighted ? K + 1 : 0));
   }
   // cell position of pair p of label k
   __device__ int pos(int k, int p) const { return swz ? (p ^ ((k >> ksh) & (np - 1))) : p; }
@@ -104,45 +109,50 @@ struct UpdLayout {
 // already holds a partial sum" (then a flush adds instead of storing).
 constexpr unsigned NADD_MASK = 0x7fffffffu, NADD_WRITTEN = 0x80000000u;
 
-// Decode label k's cells, store/add them into this workgroup's slab row, reset them.
+// Mid-chunk flush of every label whose add count reached `thresh`: list them, then
+// decode their cells with one (label, pair) per thread so the slab read-modify-writes
+// of a label are contiguous across lanes.  Called by all threads after an LDS barrier.
 template <int SW>
-__device__ __forceinline__ void upd_flush_label(const UpdateArgs& a, const UpdLayout& L, char* m,
-                                                int slice, int chunk, int k) {
+__device__ void upd_flush_hot(const UpdateArgs& a, const UpdLayout& L, char* m, int slice, int chunk,
+                              unsigned thresh) {
   constexpr int NP = SW / 2;
-  unsigned long long* cells = L.cells(m) + k * L.LDc;
-  const unsigned na = L.nadd(m)[k];
-  const unsigned long long n = na & NADD_MASK;
-  const bool add = na & NADD_WRITTEN;
+  const bool W = a.weights != nullptr;
+  unsigned* nadd = L.nadd(m);
+  unsigned short* hot = L.hot(m, W);
+  if (threadIdx.x == 0) *L.nhot(m) = 0;
+  __syncthreads();
+  for (int k = threadIdx.x; k < a.K; k += blockDim.x)
+    if ((nadd[k] & NADD_MASK) >= thresh) hot[atomicAdd(L.nhot(m), 1)] = (unsigned short)k;
+  __syncthreads();
+  const int nh = *L.nhot(m);
   const int cols = (a.D - slice * SW) < SW ? (a.D - slice * SW) : SW;
-  long long* dst = a.slab + (int64_t)chunk * a.K * a.D + (int64_t)k * a.D + slice * SW;
-#pragma unroll 4
-  for (int p = 0; p < NP; ++p) {
-    const int q = L.pos(k, p);
-    const unsigned long long T = cells[q] - n * FX_MM;
+  unsigned long long* cells = L.cells(m);
+  for (int e = threadIdx.x; e < nh * NP; e += blockDim.x) {
+    const int k = hot[e / NP], p = e % NP;
+    const unsigned na = nadd[k];
+    const int q = k * L.LDc + L.pos(k, p);
+    const unsigned long long T = cells[q] - (unsigned long long)(na & NADD_MASK) * FX_MM;
     cells[q] = 0;
     const int lo = (int)(uint32_t)T;
     const long long hi = (long long)(T - (unsigned long long)(long long)lo) >> 32;
     if (2 * p < cols) {
-      if (add) { dst[2 * p] += lo; dst[2 * p + 1] += hi; }
-      else { dst[2 * p] = lo; dst[2 * p + 1] = hi; }
+      long long* dst = a.slab + (int64_t)chunk * a.K * a.D + (int64_t)k * a.D + slice * SW + 2 * p;
+      if (na & NADD_WRITTEN) { dst[0] += lo; dst[1] += hi; }
+      else { dst[0] = lo; dst[1] = hi; }
     }
   }
-  if (slice == 0) {
-    const long long c = a.weights ? L.wcnt(m)[k] : (long long)n;
-    long long* cd = a.cnt_slab + (int64_t)chunk * a.K + k;
-    if (add) *cd += c; else *cd = c;
+  __syncthreads();
+  for (int i = threadIdx.x; i < nh; i += blockDim.x) {
+    const int k = hot[i];
+    const unsigned na = nadd[k];
+    if (slice == 0) {
+      const long long c = W ? L.wcnt(m)[k] : (long long)(na & NADD_MASK);
+      long long* cd = a.cnt_slab + (int64_t)chunk * a.K + k;
+      if (na & NADD_WRITTEN) *cd += c; else *cd = c;
+    }
+    if (W) L.wcnt(m)[k] = 0;
+    nadd[k] = NADD_WRITTEN;
   }
-  if (a.weights) L.wcnt(m)[k] = 0;
-  L.nadd(m)[k] = NADD_WRITTEN;
-}
-
-// Mid-chunk flush: only labels whose add count reached `thresh` (one thread per
-// label; hot labels are few).  Called by all threads after an LDS barrier.
-template <int SW>
-__device__ void upd_flush_hot(const UpdateArgs& a, const UpdLayout& L, char* m, int slice, int chunk,
-                              unsigned thresh) {
-  for (int k = threadIdx.x; k < a.K; k += blockDim.x)
-    if ((L.nadd(m)[k] & NADD_MASK) >= thresh) upd_flush_label<SW>(a, L, m, slice, chunk, k);
   if (threadIdx.x == 0) *L.flag(m) = 0;
   __syncthreads();
 }
@@ -182,9 +192,10 @@ enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4 };
 
 constexpr int upd_ksh(int np) { return np >= 32 ? 0 : np == 16 ? 1 : np == 8 ? 2 : np == 4 ? 3 : np == 2 ? 4 : 5; }
 __host__ __device__ static inline size_t upd_lds_bytes(int K, int ldc, bool weighted) {
-  size_t b = (size_t)(K + 1) * ldc * 8 + (size_t)(K + 1) * 4 + 4;
+  size_t b = (size_t)(K + 1) * ldc * 8 + (size_t)(K + 1) * 4 + 8;  // cells, nadd, flag, nhot
   b = (b + 7) & ~(size_t)7;
-  return b + (weighted ? (size_t)(K + 1) * 8 : 0);
+  b += weighted ? (size_t)(K + 1) * 8 : 0;                          // weighted counts
+  return b + ((size_t)(K + 1) * 2 + 7) / 8 * 8;                     // hot-label list (u16)
 }
 
 template <typename T, int SW, int MODE, int NT = UPD_NT>
@@ -357,7 +368,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
         const int ns = (s + NB - 1) % NB;  // static after unrolling
         if (nb < row1) load(nb, wb[ns], lb[ns], tb[ns]);
         accumulate(wb[s], lb[s], tb[s]);
-        if (*L.flag(smem)) upd_flush_hot<SW>(a, L, smem, slice, chunk, THRESH);
+        if (*L.flag(smem)) upd_flush_hot<SW>(a, L, smem, slice, chunk, THRESH / 2);  // batch near-hot labels too
       }
     }
   }
