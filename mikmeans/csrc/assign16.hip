@@ -28,9 +28,9 @@ constexpr int chunk_tiles16(int esize, int dpad) {
 
 // CT_: tiles per LDS chunk (0 = the 16 KiB default, which also fixes Kpad's
 // granule); NBUF_: ring slots (prefetch depth NBUF-1).
-template <typename T, int DPAD, int P_, int GT_, int CT_ = 0, int NBUF_ = 3>
+template <typename T, int DPAD, int P_, int GT_, int CT_ = 0, int NBUF_ = 3, int NW_ = 4>
 struct Assign16Cfg {
-  static constexpr int NW = 4;
+  static constexpr int NW = NW_;                // waves per workgroup sharing the ring
   static constexpr int P = P_;                  // 16-point blocks per wave
   static constexpr int GT = GT_;                // tiles reduced per epilogue
   static constexpr int V = Elem<T>::V;
@@ -70,9 +70,9 @@ template <> struct Mfma16<float> {
 // least 4 waves per SIMD, i.e. <= 128 VGPRs): 1 = epilogue replaced by
 // one add per tile (MFMA + LDS pipeline alone), 2 = no ring refills / waits (MFMA +
 // epilogue alone on whatever the LDS holds).
-template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0>
-__global__ __launch_bounds__(256, (DBG & 16) ? 4 : 1) void assign16_kernel(AssignArgs a) {
-  using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_>;
+template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0, int NW_ = 4>
+__global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : 1) void assign16_kernel(AssignArgs a) {
+  using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_, NW_>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -283,22 +283,22 @@ __global__ __launch_bounds__(256, (DBG & 16) ? 4 : 1) void assign16_kernel(Assig
   }
 }
 
-template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0>
+template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0, int NW_ = 4>
 static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
-  using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_>;
+  using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_, NW_>;
   if (a.Kpad % (16 * C::CT) != 0) return hipErrorInvalidValue;
   const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
   const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG>,
+    hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
   if (nblk <= 0) return hipSuccess;
-  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG>), dim3((unsigned)nblk),
+  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_>), dim3((unsigned)nblk),
                      dim3(C::NW * 64), lds, s, a);
   return hipGetLastError();
 }
@@ -342,6 +342,9 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
       case 29: return launch16_t<T, DPAD, P, 1, 4, 2, 16>(a, s);  // <= 128 VGPRs (4 waves/SIMD)
       case 30: return launch16_t<T, DPAD, P, 1, 2, 3, 16>(a, s);
       case 31: return launch16_t<T, DPAD, P, 1, 4, 3, 16>(a, s);
+      case 32: return launch16_t<T, DPAD, P, 1, 4, 2, 16, 8>(a, s);  // 8 waves share the ring
+      case 33: return launch16_t<T, DPAD, P, 1, 4, 3, 16, 8>(a, s);
+      case 34: return launch16_t<T, DPAD, P, 1, 2, 3, 16, 8>(a, s);
       case 21: return launch16_t<T, DPAD, 2, 1, 4, 2>(a, s);
       case 22: return launch16_t<T, DPAD, 8, 1, 4, 2>(a, s);
       default: break;

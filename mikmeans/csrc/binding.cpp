@@ -67,17 +67,21 @@ T* opt_ptr(const c10::optional<Tensor>& t) {
 }
 
 // ----------------------------------------------------------------------------
+void check_i64(const Tensor& t, const char* name, int64_t numel_min);
+
 void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::optional<Tensor>& xn,
             const Tensor& labels, const c10::optional<Tensor>& mind,
             const c10::optional<Tensor>& slots, int64_t Kpad, int64_t dpad, bool track_changed,
-            int64_t layout) {
+            int64_t layout, const c10::optional<Tensor>& keys) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   const int64_t N = X.size(0);
   const int D = (int)X.size(1);
-  TORCH_CHECK(layout == 32 || layout == 16, "mikmeans: layout must be 32 or 16");
+  // layout: 32 (assign.hip), 16 (assign16.hip), 116 (assign_res.hip; packs like 16)
+  TORCH_CHECK(layout == 32 || layout == 16 || layout == 116, "mikmeans: layout must be 32, 16 or 116");
+  const int pack_layout = layout == 32 ? 32 : 16;
   TORCH_CHECK(D <= dpad, "mikmeans: D exceeds dpad");
-  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, (int)Kpad, (int)layout) == Kpad, "mikmeans: bad Kpad ",
+  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, (int)Kpad, pack_layout) == Kpad, "mikmeans: bad Kpad ",
               Kpad, " for dpad ", dpad, " layout ", layout);
   check_cuda(pack, "pack");
   TORCH_CHECK(pack.is_contiguous() && pack.scalar_type() == X.scalar_type(),
@@ -99,8 +103,23 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
   a.mind = opt_ptr<float>(mind);
   a.slots = opt_ptr<double>(slots);
   a.track_changed = track_changed ? 1 : 0;
-  if (layout == 16) hip_check(mk::launch_assign16(dt, (int)dpad, a, stream()), "assign16");
-  else hip_check(mk::launch_assign(dt, (int)dpad, a, stream()), "assign");
+  if (layout == 116) {
+    const int passes = mk::assign_res_passes(dt, (int)dpad, (int)Kpad);
+    TORCH_CHECK(passes >= 1, "mikmeans: resident assign does not support this shape");
+    if (passes > 1) {
+      TORCH_CHECK(keys.has_value(), "mikmeans: resident assign over ", passes, " passes needs keys");
+      check_i64(*keys, "keys", N);
+    }
+    hip_check(mk::launch_assign_res(dt, (int)dpad, a,
+                                    keys.has_value() ? (unsigned long long*)keys->data_ptr<int64_t>()
+                                                     : nullptr,
+                                    stream()),
+              "assign_res");
+  } else if (layout == 16) {
+    hip_check(mk::launch_assign16(dt, (int)dpad, a, stream()), "assign16");
+  } else {
+    hip_check(mk::launch_assign(dt, (int)dpad, a, stream()), "assign");
+  }
 }
 
 void check_i64(const Tensor& t, const char* name, int64_t numel_min) {
@@ -359,6 +378,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("assign_kpad", [](int64_t dt, int64_t dpad, int64_t K, int64_t layout) {
     return mk::assign_kpad((int)dt, (int)dpad, (int)K, (int)layout); });
   m.def("assign16_supported", [](int64_t dt, int64_t dpad) { return mk::assign16_chunk_tiles((int)dt, (int)dpad) > 0; });
+  m.def("assign_res_passes", [](int64_t dt, int64_t dpad, int64_t Kpad) {
+          return mk::assign_res_passes((int)dt, (int)dpad, (int)Kpad); },
+        "passes of the LDS-resident assign (0 = unsupported)");
+  m.def("set_assign_res_grid", [](int64_t g) { mk::set_assign_res_grid((int)g); }, "A/B knob");
   m.def("set_update_nt", [](int64_t nt) { mk::set_update_nt((int)nt); }, "update threads/WG (A/B)");
   m.def("set_update_max_sw", [](int64_t sw) { mk::set_update_max_sw((int)sw); },
         "cap the M-step slice width (smaller LDS footprint for overlap with assign)");

@@ -45,6 +45,12 @@ struct AssignArgs {
 };
 hipError_t launch_assign(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
+// LDS-resident centroids, persistent workgroups; K split into passes that chain a per-point
+// best key through `keys` (u64 [N], needed when assign_res_passes > 1).
+hipError_t launch_assign_res(int dtype, int dpad, const AssignArgs& a, unsigned long long* keys,
+                             hipStream_t s);
+int assign_res_passes(int dtype, int dpad, int Kpad);
+void set_assign_res_grid(int g);
 void set_assign16_gt(int gt);  // tiles per epilogue group of the 16x16 variant (0 = default)
 void set_assign16_cfg(int v);  // pipeline variant of the bf16 D=128 shape (0 = default)
 void set_assign_p(int p);  // 32-point blocks per wave (0 = default)

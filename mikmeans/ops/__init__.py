@@ -74,8 +74,10 @@ class CentroidPack:
         if self.dpad == 0:
             raise NotImplementedError(f"mikmeans: GPU assign supports D <= 256 (got {D})")
         self.dt = dtype_code(dtype)
-        self.layout = layout or preferred_layout(dtype, self.dpad)
-        self.Kpad = C.assign_kpad(self.dt, self.dpad, K, self.layout)
+        self.layout = layout or preferred_layout(dtype, self.dpad, K)
+        self.pack_layout = 32 if self.layout == 32 else 16      # 116 (resident) packs like 16
+        self.Kpad = C.assign_kpad(self.dt, self.dpad, K, self.pack_layout)
+        self._keys = None
         self.pack = torch.zeros(self.Kpad * self.dpad, dtype=dtype, device=device)
         self.cn = torch.zeros(C.assign_cn_len(self.Kpad), dtype=torch.float32, device=device)
 
@@ -90,12 +92,17 @@ class CentroidPack:
         """K4: new centres from the all-reduced message (mode 1 Lloyd, 2 mini-batch) or
         pack-only (mode 0); always re-packs ``-2c`` / ``|c|^2`` for the next assign."""
         self._C.finalize(mode, packed, Cold, Cnew, frozen, mb_counts, self.pack, self.cn, shift, counts,
-                         self.dpad, self.Kpad, self.layout)
+                         self.dpad, self.Kpad, self.pack_layout)
 
     def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False):
         """K2 on these centres (``X`` column-padded, 16-B rows)."""
+        keys = None
+        if self.layout == 116 and self._C.assign_res_passes(self.dt, self.dpad, self.Kpad) > 1:
+            if self._keys is None or self._keys.numel() < X.shape[0]:
+                self._keys = torch.empty(max(X.shape[0], 1), dtype=torch.int64, device=X.device)
+            keys = self._keys
         self._C.assign(X, self.pack, self.cn, xn, labels, mind, slots, self.Kpad, self.dpad,
-                       track_changed, self.layout)
+                       track_changed, self.layout, keys)
 
 
 def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True, layout: int | None = None):

@@ -73,15 +73,18 @@ def dpad_for(D: int, dtype: torch.dtype) -> int:
     return d if d <= 256 else 0
 
 
-def preferred_layout(dtype: torch.dtype, dpad: int) -> int:
-    """Assign-kernel variant (MFMA tile rows): 32 (32x32 MFMA, assign.hip) or 16
-    (16x16 MFMA, assign16.hip).  ``MIKMEANS_ASSIGN_LAYOUT`` overrides."""
+def preferred_layout(dtype: torch.dtype, dpad: int, K: int | None = None) -> int:
+    """Assign-kernel variant: 32 (32x32 MFMA, assign.hip), 16 (16x16 MFMA with an LDS
+    ring, assign16.hip) or 116 (16x16 MFMA, LDS-resident centroids, assign_res.hip).
+    ``MIKMEANS_ASSIGN_LAYOUT`` overrides."""
     env = os.environ.get("MIKMEANS_ASSIGN_LAYOUT")
     m = require()
     ok16 = m.assign16_supported(dtype_code(dtype), dpad)
-    if env in ("16", "32"):
-        return 16 if env == "16" and ok16 else 32
-    return DEFAULT_LAYOUT if (DEFAULT_LAYOUT == 32 or ok16) else 32
+    if env in ("16", "32", "116"):
+        return int(env) if (env == "32" or ok16) else 32
+    if not ok16:
+        return 32
+    return DEFAULT_LAYOUT
 
 
 # Measured on MI355X (scripts/ab_kernels.py, N=2e7, D=128, K=1024, bf16): the 16x16

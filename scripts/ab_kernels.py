@@ -42,7 +42,7 @@ def main():
     variants = a.variants.split(",")
     packs = {}
     for v in variants:
-        lay = 16 if v.startswith("16") else 32
+        lay = 116 if v.startswith("res") else (16 if v.startswith("16") else 32)
         if lay not in packs:
             packs[lay] = CentroidPack(a.k, eng.Dp, dt, "cuda", layout=lay).load(eng.C[:, : eng.Dp])
     res = {f"assign_{v}": [] for v in variants}
@@ -51,8 +51,10 @@ def main():
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     for _ in range(a.rounds):
         for v in variants:
-            lay = 16 if v.startswith("16") else 32
-            if lay == 32:
+            lay = 116 if v.startswith("res") else (16 if v.startswith("16") else 32)
+            if lay == 116:
+                C.set_assign_res_grid(int(v[3:]) if len(v) > 3 else 0)   # "res" or "res<grid>"
+            elif lay == 32:
                 C.set_assign_p(int(v.split("p")[1]))
             else:
                 gpart = v.split("g")[1]
@@ -65,6 +67,7 @@ def main():
             torch.cuda.synchronize()
             res[f"assign_{v}"].append(e0.elapsed_time(e1))
         C.set_assign_p(0)
+        C.set_assign_res_grid(0)
         C.set_assign16_gt(0)
         C.set_assign16_cfg(0)
         e0, e1 = ev(), ev()

@@ -43,12 +43,12 @@ def test_row_sqnorm(native, dtype, n, d):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n,d,k", [(1000, 2, 3), (513, 16, 37), (20000, 128, 256), (9000, 128, 1024),
                                    (4096, 64, 4096), (3000, 256, 512), (255, 100, 70), (70000, 32, 9)])
-@pytest.mark.parametrize("layout", [32, 16])
+@pytest.mark.parametrize("layout", [32, 16, 116])
 def test_assign_matches_reference(native, dtype, n, d, k, layout):
     X = _points(n, d, dtype, seed=k)
     C = _points(k, d, torch.float32, seed=k + 1)
     dp = ops.dpad_for(ops.pad_columns(X[:1]).shape[1], dtype)
-    if layout == 16 and not native.assign16_supported(ops.dtype_code(dtype), dp):
+    if layout in (16, 116) and not native.assign16_supported(ops.dtype_code(dtype), dp):
         pytest.skip("16x16 variant needs DPAD/4 >= one 16-byte piece")
     labels, mind = ops.assign(X.to(DEV), C.to(DEV), with_dist=True, layout=layout)
     _check_assign(X, C, labels, mind, rel=2e-5 if dtype == torch.float32 else 3e-5)
@@ -66,13 +66,15 @@ def test_assign16_tile_groups(native, gt):
     _check_assign(X, C, labels, mind, rel=3e-5)
 
 
-def test_assign_exact_f32_small_ints(native):
+@pytest.mark.parametrize("layout", [16, 116, 32])
+def test_assign_exact_f32_small_ints(native, layout):
     # integer data: scores are exact in f32, so labels must equal argmin exactly (lowest index on ties)
     g = torch.Generator().manual_seed(3)
     X = torch.randint(-8, 8, (5000, 64), generator=g).float()
-    C = torch.randint(-8, 8, (300, 64), generator=g).float()
-    C[17] = C[5]  # exact duplicate centre: index 5 must win
-    labels, _ = ops.assign(X.to(DEV), C.to(DEV), with_dist=False)
+    C = torch.randint(-8, 8, (1300, 64), generator=g).float()
+    C[17] = C[5]      # exact duplicate centre: index 5 must win
+    C[1200] = C[40]   # ... also across resident-kernel passes (116: 3 passes here)
+    labels, _ = ops.assign(X.to(DEV), C.to(DEV), with_dist=False, layout=layout)
     exp, _ = ref.assign(X, C)
     sc = ref.scores(X, C)
     tie = (sc == sc.min(1, keepdim=True).values).sum(1) > 1
