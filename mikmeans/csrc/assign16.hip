@@ -345,6 +345,9 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
       case 32: return launch16_t<T, DPAD, P, 1, 4, 2, 16, 8>(a, s);  // 8 waves share the ring
       case 33: return launch16_t<T, DPAD, P, 1, 4, 3, 16, 8>(a, s);
       case 34: return launch16_t<T, DPAD, P, 1, 2, 3, 16, 8>(a, s);
+      case 35: return launch16_t<T, DPAD, P, 1, 2, 2, 16, 2>(a, s);  // 2 waves per ring
+      case 36: return launch16_t<T, DPAD, P, 1, 2, 3, 16, 2>(a, s);
+      case 37: return launch16_t<T, DPAD, P, 1, 1, 3, 16, 4>(a, s);  // 4 KiB chunks
       case 21: return launch16_t<T, DPAD, 2, 1, 4, 2>(a, s);
       case 22: return launch16_t<T, DPAD, 8, 1, 4, 2>(a, s);
       default: break;

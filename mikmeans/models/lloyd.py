@@ -84,6 +84,11 @@ class LloydEngine:
         self.gpu = X.device.type == "cuda"
         self.X = pad_columns(X) if self.gpu else X
         self.Dp = int(self.X.shape[1])
+        if self.gpu and native.dpad_for(self.Dp, self.X.dtype) == 0:
+            # D > 256: beyond the MFMA kernels' register-resident rows; run the PyTorch
+            # path on the device instead (hipBLASLt GEMM scores + index_add sums).
+            native.warn_once(f"D={self.D} > 256: Lloyd steps use the PyTorch GEMM path on {X.device}")
+            self.gpu = False
         self.n = int(self.X.shape[0])
         self.dtype = self.X.dtype
         self.empty_policy = empty_policy
@@ -116,8 +121,6 @@ class LloydEngine:
         C = native.require()
         self._C = C
         self.dt = native.dtype_code(self.dtype)
-        if native.dpad_for(self.Dp, self.dtype) == 0:
-            raise NotImplementedError(f"mikmeans: the GPU engine supports D <= 256 (got {self.D})")
         dev = self.device
         self.pk = CentroidPack(self.K, self.Dp, self.dtype, dev)
         self.slots = torch.zeros(C.NSLOT * C.SLOT_STRIDE, dtype=torch.float64, device=dev)

@@ -42,12 +42,13 @@ class MiniBatchEngine:
             self.frozen = torch.as_tensor(frozen, dtype=torch.uint8).reshape(-1).to(self.device)
         self.steps = 0
         self.batch_inertia = 0.0
+        if self.gpu and native.dpad_for(self.Dp, dtype) == 0:
+            native.warn_once(f"D={self.D} > 256: mini-batch steps use the PyTorch GEMM path")
+            self.gpu = False
         if self.gpu:
             C = native.require()
             self._C = C
             self.dt = native.dtype_code(dtype)
-            if native.dpad_for(self.Dp, dtype) == 0:
-                raise NotImplementedError("mikmeans: GPU mini-batch supports D <= 256")
             from ..ops import CentroidPack
 
             dev = self.device

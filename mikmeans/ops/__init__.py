@@ -111,8 +111,8 @@ def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True, la
     bf16 points are compared against bf16-quantised centroids (scores
     accumulated in fp32 on the matrix cores); f32 points use the exact-f32 MFMA.
     """
-    if not X.is_cuda:
-        return cpu.assign(X, centers, with_dist=with_dist)
+    if not X.is_cuda or dpad_for(pad_columns(X[:1]).shape[1], X.dtype) == 0:
+        return cpu.assign(X, centers.to(X.device), with_dist=with_dist)  # CPU, or D > 256 on the GPU
     C = require()
     Xp = pad_columns(X)
     D = Xp.shape[1]

@@ -92,6 +92,17 @@ def preferred_layout(dtype: torch.dtype, dpad: int, K: int | None = None) -> int
 DEFAULT_LAYOUT = 16
 
 
+_warned: set = set()
+
+
+def warn_once(msg: str) -> None:
+    if msg not in _warned:
+        _warned.add(msg)
+        import warnings
+
+        warnings.warn("mikmeans: " + msg, stacklevel=3)
+
+
 def loaded_path() -> str | None:
     m = _load()
     return getattr(m, "__file__", None) if m is not None else None

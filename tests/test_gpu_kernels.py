@@ -286,3 +286,25 @@ def test_lloyd_graph_replay_matches_eager(native, weighted):
     ea.step()
     eb.step()
     assert torch.equal(ea.centers, eb.centers)
+
+
+def test_wide_features_use_gemm_path(native):
+    """D > 256: the MFMA kernels do not apply; fit/predict/mini-batch run the PyTorch
+    GEMM path on the device and agree with the CPU engine."""
+    import warnings
+
+    from mikmeans import KMeans, MiniBatchKMeans
+
+    X = B.make_blobs(6000, 300, 8, seed=4)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        kg = KMeans(8, init="random", seed=1, max_iter=10, tol=-1.0, device=DEV).fit(X.to(DEV))
+        kc = KMeans(8, init="random", seed=1, max_iter=10, tol=-1.0, device="cpu").fit(X)
+        lab = kg.predict(X.to(DEV))
+        mb = MiniBatchKMeans(8, batch_size=1000, max_iter=5, device=DEV, seed=0).fit(X.to(DEV))
+    assert lab.is_cuda and torch.equal(lab.cpu(), kg.labels_.cpu())
+    # GPU vs CPU GEMM rounding may flip near-tie points (a split blob): compare the fits
+    agree = (kg.labels_.cpu() == kc.labels_).float().mean().item()
+    assert agree > 0.99
+    assert abs(kg.inertia_ - kc.inertia_) <= 1e-3 * kc.inertia_
+    assert mb.cluster_centers_.shape == (8, 300)
