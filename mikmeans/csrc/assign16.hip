@@ -131,6 +131,9 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : 1) void assign16_kernel(
       if (c + C::NBUF - 1 < nch) issue_chunk(c + C::NBUF - 1);
     }
     const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
+    // DBG & 64 / 128: LLVM's MFMA/DS interleaving strategies for the chunk body (A/B)
+    if constexpr ((DBG & 64) != 0) __builtin_amdgcn_iglp_opt(0);
+    if constexpr ((DBG & 128) != 0) __builtin_amdgcn_iglp_opt(1);
     // A fragments + |c|^2 of one tile from the LDS ring
     auto load_tile = [&](int tl_i, u32x4* aw_, f32x4& ci_) {
       const int tile = c * C::CT + tl_i;
@@ -348,6 +351,8 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
       case 35: return launch16_t<T, DPAD, P, 1, 2, 2, 16, 2>(a, s);  // 2 waves per ring
       case 36: return launch16_t<T, DPAD, P, 1, 2, 3, 16, 2>(a, s);
       case 37: return launch16_t<T, DPAD, P, 1, 1, 3, 16, 4>(a, s);  // 4 KiB chunks
+      case 38: return launch16_t<T, DPAD, P, 1, 4, 2, 16 | 64>(a, s);   // iglp_opt(0)
+      case 39: return launch16_t<T, DPAD, P, 1, 4, 2, 16 | 128>(a, s);  // iglp_opt(1)
       case 21: return launch16_t<T, DPAD, 2, 1, 4, 2>(a, s);
       case 22: return launch16_t<T, DPAD, 8, 1, 4, 2>(a, s);
       default: break;
