@@ -198,7 +198,7 @@ __host__ __device__ static inline size_t upd_lds_bytes(int K, int ldc, bool weig
   return b + ((size_t)(K + 1) * 2 + 7) / 8 * 8;                     // hot-label list (u16)
 }
 
-template <typename T, int SW, int MODE, int NT = UPD_NT>
+template <typename T, int SW, int MODE, int NT = UPD_NT, int NBF = UPD_NBUF, int PER = UPD_MAX_PERIOD>
 __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
                                                         int64_t rows_per_chunk) {
   constexpr bool CLAMP = MODE & UPD_CLAMP;
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   constexpr int V = PB / ES;                           // elements per lane load (even)
   constexpr int LPR = SW / V;                          // lanes per row
   constexpr int RPP = NT / LPR;                        // rows per pass
-  constexpr int UNR = (UPD_MAX_PERIOD / RPP) < 8 ? (UPD_MAX_PERIOD / RPP) : 8;
+  constexpr int UNR = (PER / RPP) < 8 ? (PER / RPP) : 8;
   constexpr int PERIOD = RPP * UNR;
   constexpr unsigned THRESH = FX_LIM - PERIOD + 1;     // flush before any label passes FX_LIM
   constexpr int NP = SW / 2;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   };
 
   // NB-deep ring of period buffers: NB-1 periods of loads in flight while one accumulates
-  constexpr int NB = UPD_NBUF;
+  constexpr int NB = NBF;
   LT wb[NB][UNR];
   int lb[NB][UNR];
   float tb[NB][UNR];
@@ -455,17 +455,17 @@ int fixed_exp(double maxabs) {
 static int g_update_nt = 0;
 void set_update_nt(int nt) { g_update_nt = nt; }
 
-template <typename T, int SW, int MODE, int NT>
+template <typename T, int SW, int MODE, int NT, int NBF = UPD_NBUF, int PER = UPD_MAX_PERIOD>
 static hipError_t launch_nt(const UpdateArgs& a, int ldc, hipStream_t s) {
   const int n_slices = (a.D + SW - 1) / SW;
   const int64_t rows_per_chunk = (a.N + a.n_chunks - 1) / a.n_chunks;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)update_kernel<T, SW, MODE, NT>,
+    hipFuncSetAttribute((const void*)update_kernel<T, SW, MODE, NT, NBF, PER>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)UPD_LDS_MAX);
     attr = true;
   }
-  hipLaunchKernelGGL((update_kernel<T, SW, MODE, NT>), dim3(a.n_chunks * n_slices), dim3(NT),
+  hipLaunchKernelGGL((update_kernel<T, SW, MODE, NT, NBF, PER>), dim3(a.n_chunks * n_slices), dim3(NT),
                      upd_lds_bytes(a.K, ldc, (MODE & UPD_WEIGHTED) != 0), s, a, n_slices, rows_per_chunk);
   return hipGetLastError();
 }
@@ -479,11 +479,32 @@ constexpr int upd_default_nt() {
 
 template <typename T, int SW, int MODE>
 static hipError_t launch_sw(const UpdateArgs& a, int ldc, hipStream_t s) {
-  if (sizeof(T) == 2 && SW == 32 && MODE == 0 && g_update_nt == 512)
-    return launch_nt<T, SW, MODE, 512>(a, ldc, s);
-  if (sizeof(T) == 2 && SW == 32 && MODE == 0 && g_update_nt == 256)
-    return launch_nt<T, SW, MODE, 256>(a, ldc, s);
-  return launch_nt<T, SW, MODE, upd_default_nt<T, SW, MODE>()>(a, ldc, s);
+  if constexpr (sizeof(T) == 2 && SW == 32 && MODE == 0) {
+    // A/B knobs (values are codes, not thread counts beyond 256 / 512)
+    switch (g_update_nt) {
+      case 512: return launch_nt<T, SW, MODE, 512>(a, ldc, s);
+      case 256: return launch_nt<T, SW, MODE, 256>(a, ldc, s);
+      case 1024: return launch_nt<T, SW, MODE, 1024, 3, 1024>(a, ldc, s);  // previous default
+      case 1022: return launch_nt<T, SW, MODE, 1024, 2>(a, ldc, s);        // 2-deep ring
+      case 1028: return launch_nt<T, SW, MODE, 1024, 4>(a, ldc, s);        // 4-deep ring
+      case 1029: return launch_nt<T, SW, MODE, 1024, 4, 512>(a, ldc, s);   // 4 x half periods
+      case 1030: return launch_nt<T, SW, MODE, 1024, 6, 512>(a, ldc, s);   // 6 x half periods
+      case 1031: return launch_nt<T, SW, MODE, 1024, 8, 512>(a, ldc, s);
+      case 1032: return launch_nt<T, SW, MODE, 1024, 8, 256>(a, ldc, s);   // 1 row per lane
+      case 1033: return launch_nt<T, SW, MODE, 1024, 12, 256>(a, ldc, s);
+      case 1034: return launch_nt<T, SW, MODE, 1024, 6, 256>(a, ldc, s);
+      default: break;
+    }
+  }
+  constexpr int NT = upd_default_nt<T, SW, MODE>();
+  // 1024 threads: 512-row periods, 6-deep ring (5 periods of loads in flight).  N=1e8
+  // D=128 K=1024 bf16: 5.33-5.76 ms vs 5.96-6.34 for 3 x 1024-row periods (same boxes).
+  constexpr int ES = sizeof(T);
+  constexpr int V = ((SW * ES >= 16) ? 16 : SW * ES) / ES;
+  constexpr int RPP = NT / (SW / V);
+  constexpr int PER = RPP > 512 ? RPP : 512;
+  if constexpr (NT == 1024) return launch_nt<T, SW, MODE, 1024, 6, PER>(a, ldc, s);
+  else return launch_nt<T, SW, MODE, NT>(a, ldc, s);
 }
 
 template <typename T, int SW>
