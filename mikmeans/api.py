@@ -68,7 +68,7 @@ class KMeans:
                  empty_cluster: str = "keep", check_every: int = 1, n_local_trials=None,
                  verbose: int = 0, mode: str = "learn", run_id: str | None = None,
                  checkpoint_every: int = 0, checkpoint_dir: str | None = None, metrics_path: str | None = None,
-                 graph: bool = False):
+                 graph: bool = False, incremental: bool = True):
         self.n_clusters = int(n_clusters)
         self.init = init
         self.n_init = int(n_init)
@@ -89,6 +89,7 @@ class KMeans:
         self.checkpoint_dir = checkpoint_dir
         self.metrics_path = metrics_path
         self.graph = bool(graph)
+        self.incremental = bool(incremental)
         self.history_: list[dict] = []
 
     # ---------------------------------------------------------------- config
@@ -99,7 +100,8 @@ class KMeans:
                    empty_cluster=cfg.empty_cluster, check_every=cfg.check_every,
                    n_local_trials=cfg.n_local_trials, verbose=cfg.verbose, mode=cfg.mode,
                    run_id=cfg.run_id, checkpoint_every=cfg.checkpoint_every,
-                   checkpoint_dir=cfg.checkpoint_dir, metrics_path=cfg.metrics_path, graph=cfg.graph, **kw)
+                   checkpoint_dir=cfg.checkpoint_dir, metrics_path=cfg.metrics_path, graph=cfg.graph,
+                   incremental=cfg.incremental, **kw)
 
     def get_config(self) -> KMeansConfig:
         return KMeansConfig(n_clusters=self.n_clusters, init=self.init if isinstance(self.init, str) else "array",
@@ -110,7 +112,7 @@ class KMeans:
                             n_local_trials=self.n_local_trials, mode=self.mode, run_id=self.run_id,
                             verbose=self.verbose, checkpoint_every=self.checkpoint_every,
                             checkpoint_dir=self.checkpoint_dir, metrics_path=self.metrics_path,
-                            graph=self.graph)
+                            graph=self.graph, incremental=self.incremental)
 
     # ------------------------------------------------------------------- fit
     def fit(self, X, y=None, sample_weight=None, *, resume_from=None):
@@ -134,7 +136,7 @@ class KMeans:
         start_iter = 0
         for trial in range(max(1, self.n_init)):
             eng = LloydEngine(Xt, self.n_clusters, comm=comm, sample_weight=w, frozen=self.frozen,
-                              empty_policy=self.empty_cluster, n_features=D)
+                              empty_policy=self.empty_cluster, n_features=D, incremental=self.incremental)
             if resume_from is not None and trial == 0:
                 from .utils.checkpoint import load_checkpoint
 

@@ -57,6 +57,7 @@ class KMeansConfig:
     verbose: int = 0
     metrics_path: str | None = None  # per-iteration JSONL (rank 0)
     graph: bool = False              # replay each Lloyd iteration as one captured hipGraph
+    incremental: bool = True         # M-step re-scatters only rows whose label changed (exact)
 
     def to_dict(self):
         return asdict(self)
@@ -72,7 +73,8 @@ class KMeansConfig:
             flag = "--" + f.name.replace("_", "-")
             default = f.default
             if isinstance(default, bool):
-                ap.add_argument(flag, action="store_true", default=default)
+                # --flag / --no-flag (a default-on switch must be switchable off)
+                ap.add_argument(flag, action=argparse.BooleanOptionalAction, default=default)
             elif default is None:
                 typ = int if f.name == "n_local_trials" else str
                 ap.add_argument(flag, type=typ, default=None)

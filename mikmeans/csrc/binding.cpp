@@ -158,6 +158,72 @@ void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab
   hip_check(mk::launch_update(dt, a, stream()), "update");
 }
 
+// Incremental M-step (LloydEngine(incremental=True)): the changed-row list ...
+void label_delta(const Tensor& labels, const Tensor& prev, const Tensor& list, const Tensor& count) {
+  const int64_t N = labels.numel();
+  check_i32(labels, "labels", N);
+  check_i32(prev, "prev", N);
+  check_i32(count, "count", 1);
+  check_cuda(list, "list");
+  TORCH_CHECK(list.scalar_type() == at::kInt && list.dim() == 2 && list.size(1) == 2 && list.is_contiguous(),
+              "mikmeans: list must be contiguous int32 [cap, 2]");
+  TORCH_CHECK(N < ((int64_t)1 << 31) && list.size(0) < ((int64_t)1 << 31), "mikmeans: shard too large");
+  hip_check(mk::launch_label_delta(labels.data_ptr<int32_t>(), prev.data_ptr<int32_t>(), N,
+                                   (int2*)list.data_ptr<int32_t>(), (int)list.size(0),
+                                   count.data_ptr<int32_t>(), stream()),
+            "label_delta");
+}
+
+// ... its scatter-add: +x to the new label, -x to the old one (all rows on overflow)
+void update_delta(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab,
+                  const Tensor& cnt_slab, int64_t n_chunks, const c10::optional<Tensor>& weights,
+                  const Tensor& col_exp, int64_t cnt_exp, const Tensor& list, const Tensor& count) {
+  const int dt = dtype_of(X);
+  const int64_t ldx = check_points(X, dt);
+  const int64_t N = X.size(0);
+  const int D = (int)X.size(1);
+  check_i32(labels, "labels", N);
+  check_i32(count, "count", 1);
+  check_cuda(list, "list");
+  TORCH_CHECK(list.scalar_type() == at::kInt && list.dim() == 2 && list.size(1) == 2 && list.is_contiguous(),
+              "mikmeans: list must be contiguous int32 [cap, 2]");
+  const int sw = mk::update_slice_width(dt, (int)K, D, true);
+  TORCH_CHECK(sw > 0, "mikmeans: incremental M-step needs an LDS slice (K too large)");
+  TORCH_CHECK(n_chunks % 8 == 0, "mikmeans: bad n_chunks");
+  check_i64(slab, "slab", n_chunks * K * D);
+  check_i64(cnt_slab, "cnt_slab", n_chunks * K);
+  if (weights.has_value()) check_f32(*weights, "weights", N);
+  check_i32(col_exp, "col_exp", D);
+  mk::UpdateArgs a;
+  a.X = X.data_ptr(); a.N = N; a.D = D; a.ldx = ldx;
+  a.labels = labels.data_ptr<int32_t>(); a.K = (int)K; a.n_chunks = (int)n_chunks;
+  a.slab = (long long*)slab.data_ptr<int64_t>(); a.cnt_slab = (long long*)cnt_slab.data_ptr<int64_t>();
+  a.weights = opt_ptr<const float>(weights);
+  a.col_exp = col_exp.data_ptr<int32_t>(); a.cnt_exp = (int)cnt_exp; a.clamp = 0;
+  a.dlist = (const int2*)list.data_ptr<int32_t>(); a.dcount = count.data_ptr<int32_t>();
+  a.dcap = (int)list.size(0);
+  hip_check(mk::launch_update(dt, a, stream()), "update_delta");
+}
+
+// ... and the running totals it feeds (tot = [K*D sums | K counts] int64)
+void reduce_delta(const Tensor& slab, const Tensor& cnt_slab, int64_t n_chunks, int64_t K, int64_t D,
+                  const c10::optional<Tensor>& slots, const Tensor& packed, const Tensor& col_exp,
+                  int64_t cnt_exp, const Tensor& tot, const Tensor& count, int64_t cap) {
+  check_i64(slab, "slab", n_chunks * K * D);
+  check_i64(cnt_slab, "cnt_slab", n_chunks * K);
+  check_f64(packed, "packed", K * D + K + 2);
+  if (slots.has_value()) check_f64(*slots, "slots", mk::NSLOT * mk::SLOT_STRIDE);
+  check_i32(col_exp, "col_exp", D);
+  check_i64(tot, "tot", K * D + K);
+  check_i32(count, "count", 1);
+  hip_check(mk::launch_reduce((const long long*)slab.data_ptr<int64_t>(),
+                              (const long long*)cnt_slab.data_ptr<int64_t>(), (int)n_chunks, (int)K,
+                              (int)D, col_exp.data_ptr<int32_t>(), (int)cnt_exp, opt_ptr<double>(slots),
+                              packed.data_ptr<double>(), stream(), (long long*)tot.data_ptr<int64_t>(),
+                              count.data_ptr<int32_t>(), (int)cap),
+            "reduce_delta");
+}
+
 void reduce(const Tensor& slab, const Tensor& cnt_slab, int64_t n_chunks, int64_t K, int64_t D,
             const c10::optional<Tensor>& slots, const Tensor& packed, const Tensor& col_exp,
             int64_t cnt_exp) {
@@ -330,6 +396,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("assign", &assign, "fused MFMA distance + argmin (K2)");
   m.def("update", &update, "LDS-privatised per-cluster sums/counts (K3)");
   m.def("reduce", &reduce, "slab reduction into the packed f64 all-reduce message");
+  m.def("label_delta", &label_delta, "changed-row list for the incremental M-step");
+  m.def("update_delta", &update_delta, "incremental M-step scatter-add (+new / -old label)");
+  m.def("reduce_delta", &reduce_delta, "slab reduction into running totals + packed message");
   m.def("finalize", &finalize, "new centroids, shift, fragment re-pack (K4)");
   m.def("row_sqnorm", &row_sqnorm, "row squared norms (K1)");
   m.def("kpp_d2", &kpp_d2, "k-means++ D^2 update (K5)");

@@ -72,6 +72,13 @@ struct UpdateArgs {
   const int* col_exp;    // [D] column d's contributions are rne(x * w * 2^col_exp[d]), |.| <= 2^20
   int cnt_exp;           // counts scale 2^cnt_exp (0 when unweighted)
   int clamp;             // saturate contributions outside +-2^21 (streamed data)
+  // Incremental M-step (optional): rows whose label changed since the last M-step, as
+  // (row, previous label) pairs from launch_label_delta.  Each is added to its new
+  // label and subtracted from its old one; when *dcount > dcap the list overflowed
+  // and the kernel accumulates all N rows instead (the reduce then restarts totals).
+  const int2* dlist = nullptr;
+  const int* dcount = nullptr;
+  int dcap = 0;
 };
 int update_slice_width(int dtype, int K, int D, bool weighted = false);  // 0 = global fallback
 int update_n_chunks(int dtype, int K, int D, int64_t N, bool weighted = false);
@@ -79,12 +86,20 @@ int fixed_exp(double maxabs);                     // largest e with maxabs * 2^e
 void set_update_max_sw(int sw);                   // cap the slice width (0 = none)
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s);
 void set_update_nt(int nt);                       // A/B knob: threads per workgroup
+// Changed rows: for every i with labels[i] != prev[i], append (i, prev[i]) to list
+// (first `cap` entries kept, *count counts all) and set prev[i] = labels[i].
+// Zeroes *count first (stream-ordered).
+hipError_t launch_label_delta(const int32_t* labels, int32_t* prev, int64_t N, int2* list, int cap,
+                              int* count, hipStream_t s);
 
 // Reduce slabs (+ assign slots) into the packed f64 message
 // [K*D sums | K counts | inertia | n_changed] (length K*D + K + 2).
 hipError_t launch_reduce(const long long* slab, const long long* cnt_slab, int n_chunks, int K,
                          int D, const int* col_exp, int cnt_exp, double* slots, double* packed,
-                         hipStream_t s);
+                         hipStream_t s, long long* tot = nullptr, const int* dcount = nullptr,
+                         int dcap = 0);
+// With `tot` ([K*D + K] int64, persistent across iterations): tot += slab sums (or
+// tot = slab sums when *dcount > dcap), and the message is built from tot.
 
 // ---- finalize (new centroids + shift + re-pack) -------------------------------
 enum FinalizeMode : int { FIN_PACK_ONLY = 0, FIN_LLOYD = 1, FIN_MINIBATCH = 2 };

@@ -112,11 +112,15 @@ constexpr unsigned NADD_MASK = 0x7fffffffu, NADD_WRITTEN = 0x80000000u;
 // Mid-chunk flush of every label whose add count reached `thresh`: list them, then
 // decode their cells with one (label, pair) per thread so the slab read-modify-writes
 // of a label are contiguous across lanes.  Called by all threads after an LDS barrier.
+// counts come from the signed 64-bit per-label counters (weighted or incremental
+// M-step) instead of the add counts
+__device__ __forceinline__ bool upd_wcounts(const UpdateArgs& a) { return a.weights || a.dlist; }
+
 template <int SW>
 __device__ void upd_flush_hot(const UpdateArgs& a, const UpdLayout& L, char* m, int slice, int chunk,
                               unsigned thresh) {
   constexpr int NP = SW / 2;
-  const bool W = a.weights != nullptr;
+  const bool W = upd_wcounts(a);
   unsigned* nadd = L.nadd(m);
   unsigned short* hot = L.hot(m, W);
   if (threadIdx.x == 0) *L.nhot(m) = 0;
@@ -181,14 +185,14 @@ __device__ void upd_flush_all(const UpdateArgs& a, const UpdLayout& L, char* m, 
   if (slice == 0) {
     for (int k = threadIdx.x; k < a.K; k += blockDim.x) {
       const unsigned na = nadd[k];
-      const long long c = a.weights ? L.wcnt(m)[k] : (long long)(na & NADD_MASK);
+      const long long c = upd_wcounts(a) ? L.wcnt(m)[k] : (long long)(na & NADD_MASK);
       long long* dst = a.cnt_slab + (int64_t)chunk * a.K + k;
       if (na & NADD_WRITTEN) *dst += c; else *dst = c;
     }
   }
 }
 
-enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4 };
+enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8 };
 
 constexpr int upd_ksh(int np) { return np >= 32 ? 0 : np == 16 ? 1 : np == 8 ? 2 : np == 4 ? 3 : np == 2 ? 4 : 5; }
 __host__ __device__ static inline size_t upd_lds_bytes(int K, int ldc, bool weighted) {
@@ -201,8 +205,10 @@ __host__ __device__ static inline size_t upd_lds_bytes(int K, int ldc, bool weig
 template <typename T, int SW, int MODE, int NT = UPD_NT, int NBF = UPD_NBUF, int PER = UPD_MAX_PERIOD>
 __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
                                                         int64_t rows_per_chunk) {
+  // (rows_per_chunk is recomputed from the list length in incremental mode)
   constexpr bool CLAMP = MODE & UPD_CLAMP;
-  constexpr bool W = MODE & UPD_WEIGHTED;
+  constexpr bool DELTA = MODE & UPD_DELTA;
+  constexpr bool W = MODE & (UPD_WEIGHTED | UPD_DELTA);  // per-row signed weights
   constexpr bool SWZ = MODE & UPD_SWZ;
   constexpr int ES = sizeof(T);
   constexpr int PB = (SW * ES >= 16) ? 16 : SW * ES;  // bytes per lane load
@@ -234,9 +240,22 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
     for (int e = threadIdx.x; e < nz; e += NT) z[e] = 0;
   }
 
+  // Incremental mode: the rows are the 2*c entries of the changed-row list (c adds
+  // to the new labels, then c subtractions from the old ones) unless it overflowed.
+  int64_t nrows = a.N;
+  int dc = 0;
+  bool full = true;
+  if constexpr (DELTA) {
+    dc = *a.dcount;
+    full = dc > a.dcap;
+    if (!full) {
+      nrows = 2 * (int64_t)dc;
+      rows_per_chunk = (nrows + a.n_chunks - 1) / a.n_chunks;
+    }
+  }
   const int64_t row0 = (int64_t)chunk * rows_per_chunk;
   int64_t row1 = row0 + rows_per_chunk;
-  if (row1 > a.N) row1 = a.N;
+  if (row1 > nrows) row1 = nrows;
   const int lr = threadIdx.x / LPR, lp = threadIdx.x % LPR;
   const int col = slice * SW + lp * V;
   const bool colok = col < a.D;
@@ -255,16 +274,30 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   // of one lane are one address plus immediate offsets.
   const T* xrow = (const T*)a.X + (row0 + (int64_t)lr * UNR) * a.ldx + colc;
   const int* lrow = a.labels + row0 + lr * UNR;
-  const float* wrow = W ? a.weights + row0 + lr * UNR : nullptr;
+  const float* wrow = a.weights ? a.weights + row0 + lr * UNR : nullptr;
   auto load = [&](int64_t base, LT* w_, int* lab_, float* wt_) {
     const int64_t off = base - row0;
-    if (base + PERIOD <= row1) {                       // whole period (all but the last)
+    if (DELTA && !full) {                              // gather the listed rows
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int64_t j0 = base + (int64_t)lr * UNR + u;
+        const int64_t j = j0 < row1 ? j0 : row1 - 1;
+        const bool neg = j >= dc;
+        const int2 e = a.dlist[neg ? j - dc : j];
+        const int l = neg ? e.y : a.labels[e.x];
+        lab_[u] = (j0 < row1 && (unsigned)l < (unsigned)a.K) ? l : a.K;
+        const float wv = a.weights ? a.weights[e.x] : 1.f;
+        wt_[u] = neg ? -wv : wv;
+        w_[u] = *(const LT*)((const T*)a.X + (int64_t)e.x * a.ldx + colc);
+      }
+    } else if (base + PERIOD <= row1) {                // whole period (all but the last)
       const T* p = xrow + off * a.ldx;
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const int l = lrow[off + u];
         lab_[u] = ((unsigned)l < (unsigned)a.K) ? l : a.K;
-        if constexpr (W) wt_[u] = wrow[off + u];
+        if constexpr (DELTA) wt_[u] = wrow ? wrow[off + u] : 1.f;
+        else if constexpr (W) wt_[u] = wrow[off + u];
         w_[u] = *(const LT*)(p + u * a.ldx);
       }
     } else {                                           // clamp rows past the chunk -> sink row K
@@ -274,7 +307,8 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
         const int64_t i = i0 < row1 ? i0 : row1 - 1;
         const int l = a.labels[i];
         lab_[u] = (i0 < row1 && (unsigned)l < (unsigned)a.K) ? l : a.K;
-        if constexpr (W) wt_[u] = a.weights[i];
+        if constexpr (DELTA) wt_[u] = a.weights ? a.weights[i] : 1.f;
+        else if constexpr (W) wt_[u] = a.weights[i];
         w_[u] = *(const LT*)((const T*)a.X + i * a.ldx + colc);
       }
     }
@@ -466,7 +500,8 @@ static hipError_t launch_nt(const UpdateArgs& a, int ldc, hipStream_t s) {
     attr = true;
   }
   hipLaunchKernelGGL((update_kernel<T, SW, MODE, NT, NBF, PER>), dim3(a.n_chunks * n_slices), dim3(NT),
-                     upd_lds_bytes(a.K, ldc, (MODE & UPD_WEIGHTED) != 0), s, a, n_slices, rows_per_chunk);
+                     upd_lds_bytes(a.K, ldc, (MODE & (UPD_WEIGHTED | UPD_DELTA)) != 0), s, a, n_slices,
+                     rows_per_chunk);
   return hipGetLastError();
 }
 
@@ -474,7 +509,7 @@ static hipError_t launch_nt(const UpdateArgs& a, int ldc, hipStream_t s) {
 // spilling; measured at N=1e8 D=128 K=1024 bf16: 5.67 ms vs 5.89 (512) vs 6.74 (256).
 template <typename T, int SW, int MODE>
 constexpr int upd_default_nt() {
-  return (sizeof(T) == 2 && SW <= 32 && !(MODE & UPD_WEIGHTED)) ? 1024 : UPD_NT;
+  return (sizeof(T) == 2 && SW <= 32 && !(MODE & (UPD_WEIGHTED | UPD_DELTA))) ? 1024 : UPD_NT;
 }
 
 template <typename T, int SW, int MODE>
@@ -511,6 +546,11 @@ template <typename T, int SW>
 static hipError_t launch_clamp(const UpdateArgs& a, int ldc, hipStream_t s) {
   const int mode = (a.clamp ? UPD_CLAMP : 0) | (a.weights ? UPD_WEIGHTED : 0) |
                    (ldc == SW / 2 ? UPD_SWZ : 0);
+  if (a.dlist) {  // incremental M-step (Lloyd: never clamped; weights read at run time)
+    if (a.clamp) return hipErrorInvalidValue;
+    return (mode & UPD_SWZ) ? launch_sw<T, SW, UPD_DELTA | UPD_SWZ>(a, ldc, s)
+                            : launch_sw<T, SW, UPD_DELTA>(a, ldc, s);
+  }
   switch (mode) {
     case 0: return launch_sw<T, SW, 0>(a, ldc, s);
     case 1: return launch_sw<T, SW, 1>(a, ldc, s);
@@ -544,8 +584,9 @@ static hipError_t launch_update_t(const UpdateArgs& a, hipStream_t s, int sw, in
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s) {
   if (a.N <= 0) return hipSuccess;
   int ldc = 0;
-  const int sw = choose_sw(dtype, a.K, a.D, a.weights != nullptr, &ldc);
+  const int sw = choose_sw(dtype, a.K, a.D, a.weights != nullptr || a.dlist != nullptr, &ldc);
   if (sw > 0 && a.n_chunks % 8) return hipErrorInvalidValue;
+  if (a.dlist && sw == 0) return hipErrorInvalidValue;  // no incremental global fallback
   return dtype == DT_BF16 ? launch_update_t<uint16_t>(a, s, sw, ldc)
                           : launch_update_t<float>(a, s, sw, ldc);
 }
@@ -558,11 +599,20 @@ __global__ __launch_bounds__(256) void reduce_kernel(const long long* __restrict
                                                      const long long* __restrict__ cnt_slab,
                                                      int n_chunks, int K, int D,
                                                      const int* __restrict__ col_exp,
-                                                     double inv_c, double* slots, double* packed) {
+                                                     double inv_c, double* slots, double* packed,
+                                                     long long* tot, const int* dcount, int dcap) {
   const int64_t KD = (int64_t)K * D;
   const int64_t total = KD + K;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e < total) {
+  if (e < total && tot) {  // incremental: running integer totals (exact, order-free)
+    const long long* src = e < KD ? slab + e : cnt_slab + (e - KD);
+    const int64_t stride = e < KD ? KD : K;
+    long long acc = 0;
+    for (int c = 0; c < n_chunks; ++c) acc += src[(int64_t)c * stride];
+    const long long t = (*dcount > dcap) ? acc : tot[e] + acc;
+    tot[e] = t;
+    packed[e] = e < KD ? ldexp((double)t, -col_exp[e % D]) : (double)t * inv_c;
+  } else if (e < total) {
     double acc = 0.0;
     if (e < KD) {
       for (int c = 0; c < n_chunks; ++c) acc += (double)slab[(int64_t)c * KD + e];
@@ -598,11 +648,66 @@ __global__ __launch_bounds__(256) void reduce_kernel(const long long* __restrict
 
 hipError_t launch_reduce(const long long* slab, const long long* cnt_slab, int n_chunks, int K,
                          int D, const int* col_exp, int cnt_exp, double* slots, double* packed,
-                         hipStream_t s) {
+                         hipStream_t s, long long* tot, const int* dcount, int dcap) {
+  if (tot && !dcount) return hipErrorInvalidValue;
   const int64_t total = (int64_t)K * D + K;
   const unsigned nb = (unsigned)((total + 255) / 256);
   hipLaunchKernelGGL(reduce_kernel, dim3(nb), dim3(256), 0, s, slab, cnt_slab, n_chunks, K, D,
-                     col_exp, ldexp(1.0, -cnt_exp), slots, packed);
+                     col_exp, ldexp(1.0, -cnt_exp), slots, packed, tot, dcount, dcap);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// launch_label_delta: the changed-row list of the incremental M-step.  Each thread
+// checks LD_R rows (coalesced, stride 256); a workgroup reserves its list range with
+// one global atomic.  List order is not deterministic, but the M-step sums are
+// integers, so the result is.
+constexpr int LD_R = 16;
+
+__global__ __launch_bounds__(256) void label_delta_kernel(const int32_t* __restrict__ labels,
+                                                          int32_t* __restrict__ prev, int64_t N,
+                                                          int2* __restrict__ list, int cap,
+                                                          int* count) {
+  __shared__ int wg_n, wg_base;
+  if (threadIdx.x == 0) wg_n = 0;
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * 256 * LD_R + threadIdx.x;
+  int lab[LD_R], old[LD_R];
+  unsigned m = 0;
+#pragma unroll
+  for (int t = 0; t < LD_R; ++t) {
+    const int64_t i = b0 + t * 256;
+    if (i < N) {
+      lab[t] = labels[i];
+      old[t] = prev[i];
+      if (lab[t] != old[t]) m |= 1u << t;
+    }
+  }
+  const int n = __popc(m);
+  const int off = n ? atomicAdd(&wg_n, n) : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) wg_base = wg_n ? atomicAdd(count, wg_n) : 0;
+  __syncthreads();
+  int pos = wg_base + off;
+#pragma unroll
+  for (int t = 0; t < LD_R; ++t) {
+    if (m >> t & 1u) {
+      const int64_t i = b0 + t * 256;
+      prev[i] = lab[t];
+      if (pos < cap) list[pos] = make_int2((int)i, old[t]);
+      ++pos;
+    }
+  }
+}
+
+hipError_t launch_label_delta(const int32_t* labels, int32_t* prev, int64_t N, int2* list, int cap,
+                              int* count, hipStream_t s) {
+  if (N >= (int64_t)1 << 31) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(count, 0, sizeof(int), s);
+  if (e != hipSuccess || N <= 0) return e;
+  const int64_t per = 256 * LD_R;
+  hipLaunchKernelGGL(label_delta_kernel, dim3((unsigned)((N + per - 1) / per)), dim3(256), 0, s,
+                     labels, prev, N, list, cap, count);
   return hipGetLastError();
 }
 

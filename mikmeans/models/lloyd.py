@@ -72,9 +72,15 @@ class LloydEngine:
     def __init__(self, X: torch.Tensor, n_clusters: int, *, comm: Comm | None = None,
                  sample_weight: torch.Tensor | None = None, frozen=None,
                  empty_policy: str = "keep", n_features: int | None = None, segments: int = 1,
-                 overlap_sw: int = 8):
+                 overlap_sw: int = 8, incremental: bool = False, delta_cap: float = 0.125):
         from ..ops import pad_columns
 
+        # Incremental M-step: keep per-rank integer running totals of the cluster sums and
+        # re-scatter only the rows whose label changed (+ to the new label, - from the old).
+        # Bitwise identical to the full M-step (integer fixed point); the full pass runs
+        # automatically while more than ``delta_cap * n`` rows change.
+        self.incremental = bool(incremental)
+        self.delta_cap = float(delta_cap)
         self.segments = max(1, int(segments))
         self.overlap_sw = overlap_sw
         self.comm = comm or Comm.local(X.device)
@@ -141,7 +147,8 @@ class LloydEngine:
             self.side_done = torch.cuda.Event()
         else:
             self.segments = 1
-            self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, max(self.n, 1), self.weights is not None)
+            self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, max(self.n, 1),
+                                              self.weights is not None or self.incremental)
         self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.int64, device=dev)
         self.cnt_slab = torch.empty(self.n_chunks * self.K, dtype=torch.int64, device=dev)
         self.xn = torch.empty(self.n, dtype=torch.float32, device=dev)
@@ -154,6 +161,21 @@ class LloydEngine:
         self.col_exp, self.cnt_exp = fixed_exps(self.X, self.weights, comm=self.comm)
         if self.weights is not None:
             self.mind = torch.empty(self.n, dtype=torch.float32, device=dev)
+        self.delta = None
+        if self.incremental:
+            if self.segments > 1 or self.n >= 2**31 or C.update_slice_width(self.dt, self.K, self.Dp, True) == 0:
+                native.warn_once("incremental M-step unavailable for this shape/overlap mode; using full passes")
+            else:
+                cap = max(1, min(self.n, int(self.n * self.delta_cap)))
+                self.delta = {
+                    # labels the running totals correspond to (-1: none yet -> first pass is full)
+                    "prev": torch.full((self.n,), -1, dtype=torch.int32, device=dev),
+                    "list": torch.empty((cap, 2), dtype=torch.int32, device=dev),
+                    "count": torch.zeros(1, dtype=torch.int32, device=dev),
+                    "tot": torch.zeros(self.K * self.Dp + self.K, dtype=torch.int64, device=dev),
+                }
+                if self.n == 0:
+                    self.delta = None
 
     def reset_labels(self):
         """Unassign every point (the reference's Restart, app.mjs:167-178); the next
@@ -236,10 +258,19 @@ class LloydEngine:
             with _phase("mikmeans.assign"):
                 self.pk.assign(self.X, self.xn, self.labels, self.mind, self.slots, True)
             with _phase("mikmeans.update"):
-                C.update(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks, self.weights,
-                         self.col_exp, self.cnt_exp, False)
-                C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
-                         self.col_exp, self.cnt_exp)
+                d = self.delta
+                if d is not None:
+                    C.label_delta(self.labels, d["prev"], d["list"], d["count"])
+                    C.update_delta(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks,
+                                   self.weights, self.col_exp, self.cnt_exp, d["list"], d["count"])
+                    C.reduce_delta(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots,
+                                   self.packed, self.col_exp, self.cnt_exp, d["tot"], d["count"],
+                                   d["list"].shape[0])
+                else:
+                    C.update(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks,
+                             self.weights, self.col_exp, self.cnt_exp, False)
+                    C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots,
+                             self.packed, self.col_exp, self.cnt_exp)
             if self.weights is not None:
                 self.packed[KD + self.K] = (self.mind.double() * self.weights.double()).sum()
         else:

@@ -288,6 +288,83 @@ def test_lloyd_graph_replay_matches_eager(native, weighted):
     assert torch.equal(ea.centers, eb.centers)
 
 
+@pytest.mark.parametrize("cap", [0, 7, 5000, 200_000])
+def test_label_delta_list(native, cap):
+    """Changed-row list of the incremental M-step: every changed row once, with its old label."""
+    n = 100_003
+    g = torch.Generator().manual_seed(cap)
+    prev0 = torch.randint(-1, 50, (n,), generator=g, dtype=torch.int32)
+    lab = prev0.clone()
+    flip = torch.rand(n, generator=g) < 0.03
+    lab[flip] = torch.randint(0, 50, (int(flip.sum()),), generator=g, dtype=torch.int32)
+    changed = (lab != prev0).nonzero().flatten()
+    prev = prev0.to(DEV)
+    lst = torch.full((max(cap, 1), 2), -7, dtype=torch.int32, device=DEV)[: cap] if cap else \
+        torch.empty((0, 2), dtype=torch.int32, device=DEV)
+    cnt = torch.full((1,), 123, dtype=torch.int32, device=DEV)
+    native.label_delta(lab.to(DEV), prev, lst, cnt)
+    assert int(cnt) == changed.numel()
+    assert torch.equal(prev.cpu(), lab)
+    m = min(cap, changed.numel())
+    got = lst[:m].cpu()
+    rows = got[:, 0].long()
+    assert rows.unique().numel() == m
+    assert torch.equal(got[:, 1], prev0[rows])
+    assert bool((lab[rows] != prev0[rows]).all())
+    if cap >= changed.numel():
+        assert torch.equal(rows.sort().values, changed)
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("delta_cap", [0.0001, 0.125, 1.0])
+def test_incremental_mstep_bitwise(native, weighted, dtype, delta_cap):
+    """LloydEngine(incremental=True) re-scatters only changed rows into running integer
+    totals; centres, counts and the message must equal the full M-step bit for bit,
+    through list overflow (tiny cap), label resets and re-seeding."""
+    from mikmeans.models.lloyd import LloydEngine
+
+    n, D, K = 120_000, 64, 48
+    X = B.make_blobs(n, D, K, seed=3, dtype=dtype, device=DEV)
+    w = torch.rand(n, device=DEV) + 0.5 if weighted else None
+    C0 = X[:K].float()
+    ea = LloydEngine(X, K, sample_weight=w).set_centers(C0)
+    eb = LloydEngine(X, K, sample_weight=w, incremental=True, delta_cap=delta_cap).set_centers(C0)
+    assert eb.delta is not None
+    KD = K * ea.Dp
+    for it in range(10):
+        if it == 6:  # re-seed: most labels change -> overflow / full pass
+            C1 = X[K: 2 * K].float()
+            ea.set_centers(C1)
+            eb.set_centers(C1)
+        if it == 8:
+            ea.reset_labels()
+            eb.reset_labels()
+        ea.step()
+        eb.step()
+        torch.cuda.synchronize()
+        assert torch.equal(ea.packed[: KD + K], eb.packed[: KD + K]), it
+        assert torch.equal(ea.centers, eb.centers), it
+        sa, sb = ea.last_stats(), eb.last_stats()
+        assert sa.n_changed == sb.n_changed and sa.inertia == sb.inertia
+
+
+def test_incremental_mstep_graph(native):
+    """The incremental step is sync-free, so it captures into the Lloyd hipGraph too."""
+    from mikmeans.models.lloyd import LloydEngine
+
+    X = B.make_blobs(80_000, 128, 64, seed=5, dtype=torch.bfloat16, device=DEV)
+    C0 = X[:64].float()
+    ea = LloydEngine(X, 64).set_centers(C0)
+    eb = LloydEngine(X, 64, incremental=True).set_centers(C0).capture()
+    assert eb._graphs is not None
+    for _ in range(8):
+        ea.step()
+        eb.step()
+        torch.cuda.synchronize()
+        assert torch.equal(ea.centers, eb.centers)
+
+
 def test_wide_features_use_gemm_path(native):
     """D > 256: the MFMA kernels do not apply; fit/predict/mini-batch run the PyTorch
     GEMM path on the device and agree with the CPU engine."""
