@@ -43,11 +43,16 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
-    ap.add_argument("--n", type=int, default=None, help="override total points")
+    ap.add_argument("--points", "--n", dest="n", type=int, default=None, help="override total points")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--batch", type=int, default=1 << 24, help="cfg5 rows per rank per step")
     ap.add_argument("--incremental", action="store_true",
                     help="incremental M-step (re-scatter changed rows only; not the headline mode)")
+    ap.add_argument("--also-incremental", action=argparse.BooleanOptionalAction, default=True,
+                    help="cfg3: after the timed full-M-step run, time the library default "
+                         "(incremental M-step) from the same start and report it as an extra field")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: gloo rehearsal of the multi-rank path (tests; tiny --n)")
     args = ap.parse_args(argv)
 
     import mikmeans
@@ -59,11 +64,12 @@ def main(argv=None):
     cfg = dict(CONFIGS[args.config])
     if args.n:
         cfg["n"] = args.n
-    comm = Comm.from_env("cuda")
+    comm = Comm.from_env(args.device)
     world = comm.world
     if args.gpus != world and comm.rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     dev = comm.device
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     dtype = torch.bfloat16 if cfg["dtype"] == "bfloat16" else torch.float32
     N, D, K = cfg["n"], cfg["d"], cfg["k"]
     extra = {}
@@ -76,28 +82,17 @@ def main(argv=None):
         t0 = time.perf_counter()
         centers = blob_centers(K, D, 10.0, args.seed, device=dev)
         X = make_blobs(e - s, D, K, seed=args.seed, i0=s, dtype=dtype, device=dev, centers=centers)
-        torch.cuda.synchronize()
+        sync()
         extra["datagen_s"] = round(time.perf_counter() - t0, 3)
         t0 = time.perf_counter()
         if args.config == "cfg4":
             C0 = init_kmeanspp(X, D, K, N, s, comm, args.seed)
         else:
             C0 = init_random(X, D, K, N, s, comm, args.seed)
-        torch.cuda.synchronize()
+        sync()
         extra["init_s"] = round(time.perf_counter() - t0, 3)
         eng = LloydEngine(X, K, comm=comm, incremental=args.incremental).set_centers(C0)
-        for _ in range(args.warmup):
-            eng.step()
-        comm.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            eng.step()
-        torch.cuda.synchronize()
-        comm.barrier()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        comm.allreduce_max_(el)
-        elapsed = float(el.item())
+        elapsed = _timed_steps(eng, comm, args.warmup, args.steps, sync)
         ms = elapsed * 1e3 / args.steps
         value = args.steps / elapsed
         unit = "iter/s"
@@ -107,9 +102,24 @@ def main(argv=None):
             mfma_tflops=2.0 * N * K * D * value / 1e12,
             inertia=st.inertia,
             n_changed=st.n_changed,
-            phase_ms=None if args.incremental else _phase_breakdown(eng),  # extra untimed iteration
-            assign_layout=eng.pk.layout,
+            # one extra, untimed, event-instrumented iteration
+            phase_ms=_phase_breakdown(eng) if (eng.gpu and not args.incremental) else None,
+            assign_layout=eng.pk.layout if eng.gpu else None,
         )
+        if args.config == "cfg3" and args.also_incremental and not args.incremental and eng.gpu:
+            # The library default (KMeans(incremental=True)) from the same start: identical
+            # E-step, the M-step re-scatters only rows whose label changed into exact int64
+            # running totals.  Reported beside the headline, which stays the full M-step.
+            C_full = eng.centers.clone()
+            del eng
+            inc = LloydEngine(X, K, comm=comm, incremental=True).set_centers(C0)
+            el_inc = _timed_steps(inc, comm, args.warmup, args.steps, sync)
+            extra["incremental_mstep"] = {
+                "value": args.steps / el_inc,
+                "ms_per_step": el_inc * 1e3 / args.steps,
+                "assignments_per_s": args.steps / el_inc * N,
+                "centres_bitwise_equal_to_full": bool(torch.equal(inc.centers, C_full)),
+            }
     if comm.rank == 0:
         out = {
             "metric": METRIC if args.config == "cfg3" else f"{cfg['model']} ({unit})",
@@ -138,6 +148,23 @@ def main(argv=None):
         }
         print(json.dumps(out), flush=True)
     comm.close()
+
+
+def _timed_steps(eng, comm, warmup: int, steps: int, sync) -> float:
+    """W untimed iterations, then exactly ``steps`` bracketed by barrier + device sync on
+    both sides; returns the max elapsed seconds over ranks."""
+    for _ in range(warmup):
+        eng.step()
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.step()
+    sync()
+    comm.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=comm.device)
+    comm.allreduce_max_(el)
+    return float(el.item())
 
 
 def _phase_breakdown(eng) -> dict:

@@ -291,7 +291,8 @@ void row_sqnorm(const Tensor& X, const Tensor& out) {
 }
 
 void kpp_d2(const Tensor& X, const Tensor& c, bool first, const Tensor& d2, const Tensor& block_sums,
-            int64_t rows_per_block) {
+            int64_t rows_per_block, const c10::optional<Tensor>& owner, const c10::optional<Tensor>& cc,
+            int64_t kcc, int64_t knew) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   const int64_t N = X.size(0);
@@ -299,10 +300,32 @@ void kpp_d2(const Tensor& X, const Tensor& c, bool first, const Tensor& d2, cons
   check_f32(d2, "d2", N);
   const int64_t nb = (N + rows_per_block - 1) / rows_per_block;
   check_f64(block_sums, "block_sums", nb);
+  int32_t* own = nullptr;
+  const float* ccp = nullptr;
+  if (owner.has_value() && owner->defined()) {
+    // pruned pass: owner values are centre indices < cc.numel() (the kernel gathers cc[owner[i]])
+    TORCH_CHECK(!first, "mikmeans: the first k-means++ pass cannot be pruned");
+    check_i32(*owner, "owner", N);
+    TORCH_CHECK(cc.has_value() && cc->defined(), "mikmeans: a pruned kpp_d2 needs cc");
+    check_f32(*cc, "cc", 1);
+    TORCH_CHECK(knew < cc->numel() && kcc >= 1 && kcc <= cc->numel(), "mikmeans: bad k for cc");
+    own = owner->data_ptr<int32_t>();
+    ccp = cc->data_ptr<float>();
+  }
   hip_check(mk::launch_kpp_d2(dt, X.data_ptr(), N, (int)X.size(1), ldx, c.data_ptr<float>(),
                               first ? 1 : 0, d2.data_ptr<float>(), block_sums.data_ptr<double>(),
-                              rows_per_block, (int)nb, stream()),
+                              rows_per_block, (int)nb, stream(), own, ccp, (int)kcc, (int)knew),
             "kpp_d2");
+}
+
+void kpp_cc(const Tensor& centers, int64_t k, const Tensor& cnew, const Tensor& cc) {
+  check_f32(centers, "centers");
+  TORCH_CHECK(centers.dim() == 2 && k >= 0 && k <= centers.size(0), "mikmeans: kpp_cc needs k <= K");
+  check_f32(cnew, "cnew", centers.size(1));
+  check_f32(cc, "cc", k);
+  hip_check(mk::launch_kpp_cc(centers.data_ptr<float>(), centers.size(1), (int)k, (int)centers.size(1),
+                              cnew.data_ptr<float>(), cc.data_ptr<float>(), stream()),
+            "kpp_cc");
 }
 
 void kpp_sample(const Tensor& block_sums, const Tensor& d2, int64_t rows_per_block,
@@ -401,7 +424,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("reduce_delta", &reduce_delta, "slab reduction into running totals + packed message");
   m.def("finalize", &finalize, "new centroids, shift, fragment re-pack (K4)");
   m.def("row_sqnorm", &row_sqnorm, "row squared norms (K1)");
-  m.def("kpp_d2", &kpp_d2, "k-means++ D^2 update (K5)");
+  m.def("kpp_d2", &kpp_d2, "k-means++ D^2 update (K5; triangle-inequality pruned with owner/cc)",
+        py::arg("X"), py::arg("c"), py::arg("first"), py::arg("d2"), py::arg("block_sums"),
+        py::arg("rows_per_block"), py::arg("owner") = py::none(), py::arg("cc") = py::none(),
+        py::arg("kcc") = 0, py::arg("knew") = -1);
+  m.def("kpp_cc", &kpp_cc, "centre-centre squared distances for the pruned K5 pass");
   m.def("kpp_sample", &kpp_sample, "k-means++ D^2 sampling (K6)");
   m.def("blob_centers", &blob_centers, "Philox blob centres");
   m.def("blobs", &blobs, "Philox Gaussian blobs (K8)");

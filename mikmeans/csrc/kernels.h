@@ -122,9 +122,15 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
                              hipStream_t s);
 
 // ---- k-means++ ---------------------------------------------------------------
+// With owner[N] (int32: centre each d2 was measured against) and cc[k] (|c - c_j|^2, from
+// launch_kpp_cc) rows the triangle inequality rules out are not read (bit-identical
+// result); knew >= 0 records the new centre as the owner of rows whose d2 drops.
 hipError_t launch_kpp_d2(int dtype, const void* X, int64_t N, int D, int64_t ldx, const float* c,
                          int first, float* d2, double* block_sums, int64_t rows_per_block,
-                         int nblocks, hipStream_t s);
+                         int nblocks, hipStream_t s, int32_t* owner = nullptr,
+                         const float* cc = nullptr, int kcc = 0, int knew = -1);
+hipError_t launch_kpp_cc(const float* C, int64_t ldc, int k, int D, const float* cnew, float* cc,
+                         hipStream_t s);
 // mode 0: target = device double (rank-local; < 0 writes zeros to crow); mode 1: target
 // holds u, scaled by this rank's total; mode 2: target holds u, totals_all[world] decide
 // the owner rank and its local target on device.

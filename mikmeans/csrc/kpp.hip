@@ -21,42 +21,89 @@ namespace mk {
 
 constexpr int KPP_NT = 256;
 
+// Pruned K5 (PRUNE): Elkan's triangle-inequality bound applied to D^2 seeding.
+// owner[i] is the centre d2[i] was measured against and cc[j] = |c_new - c_j|^2.
+// When cc[owner] >= KPP_PRUNE * d2[i], |x - c_new| >= |c_new - c_own| - |x - c_own|
+// >= 1.0009 |x - c_own|: the new centre cannot lower d2[i], so row i is not read.
+// The margin exceeds the f32 rounding of all three distances (relative <= D*2^-24
+// for sums of squares), so d2, owner and the block sums are bit-identical to the
+// unpruned pass; only the bytes read change.
+constexpr float KPP_PRUNE = 4.004f;
+constexpr int KPP_CC_LDS = 16384;  // centre-centre distances staged in LDS up to this k
+
 // LPR lanes per row (each 16 B per pass over the row), UNR rows in flight per lane group.
-template <typename T, int LPR>
+// knew >= 0: the owner of every row whose d2 drops becomes knew (< 0: owner is read only,
+// e.g. a greedy candidate evaluated into a scratch copy of d2).
+template <typename T, int LPR, bool PRUNE>
 __global__ __launch_bounds__(KPP_NT) void kpp_d2_kernel(const T* __restrict__ X, int64_t N, int D,
                                                         int64_t ldx, const float* __restrict__ c,
                                                         int first, float* __restrict__ d2,
                                                         double* __restrict__ block_sums,
-                                                        int64_t rows_per_block) {
+                                                        int64_t rows_per_block, int32_t* __restrict__ owner,
+                                                        const float* __restrict__ cc, int kcc, int knew) {
   constexpr int V = Elem<T>::V;
-  constexpr int UNR = 4;
+  constexpr int UNR = PRUNE ? 8 : 4;
   constexpr int RPW = KPP_NT / LPR;  // rows per pass of the workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* cs = (float*)smem;
   for (int d = threadIdx.x; d < D; d += KPP_NT) cs[d] = c[d];
+  // pruned pass: the k centre-centre distances live in LDS (one gather per row instead of a
+  // dependent global load), unless there are too many of them
+  const float* ccp = cc;
+  if constexpr (PRUNE) {
+    if (kcc <= KPP_CC_LDS) {
+      float* ccs = cs + ((D + 3) & ~3);
+      for (int j = threadIdx.x; j < kcc; j += KPP_NT) ccs[j] = cc[j];
+      ccp = ccs;
+    }
+  }
   __syncthreads();
   const int sub = threadIdx.x % LPR;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   int64_t r1 = r0 + rows_per_block;
   if (r1 > N) r1 = N;
   double part = 0.0;
-  for (int64_t base = r0 + threadIdx.x / LPR; base < r1; base += (int64_t)RPW * UNR) {
-    float acc[UNR];
+  // pruned pass: (d2, owner) of the next period are loaded while this one computes, so the
+  // prune test costs no exposed global latency
+  float old_n[UNR];
+  int own_n[UNR];
+  auto meta = [&](int64_t b) {
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) acc[u] = 0.f;
-    for (int cc = sub * V; cc < D; cc += LPR * V) {
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t i = b + (int64_t)u * RPW;
+      old_n[u] = i < r1 ? d2[i] : 0.f;
+      own_n[u] = i < r1 ? owner[i] : -1;
+    }
+  };
+  if constexpr (PRUNE) meta(r0 + threadIdx.x / LPR);
+  for (int64_t base = r0 + threadIdx.x / LPR; base < r1; base += (int64_t)RPW * UNR) {
+    float acc[UNR], old[UNR];
+    bool need[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      acc[u] = 0.f;
+      if constexpr (PRUNE) {
+        old[u] = old_n[u];
+        need[u] = own_n[u] >= 0 && !(ccp[own_n[u]] >= KPP_PRUNE * old[u]);
+      } else {
+        old[u] = 0.f;
+        need[u] = base + (int64_t)u * RPW < r1;
+      }
+    }
+    if constexpr (PRUNE) meta(base + (int64_t)RPW * UNR);
+    for (int col = sub * V; col < D; col += LPR * V) {
       u32x4 w[UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const int64_t i = base + (int64_t)u * RPW;
-        w[u] = i < r1 ? *(const u32x4*)(X + i * ldx + cc) : u32x4{0u, 0u, 0u, 0u};
+        w[u] = need[u] ? *(const u32x4*)(X + i * ldx + col) : u32x4{0u, 0u, 0u, 0u};
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         float f[V];
         unpack16(w[u], f, (T*)nullptr);
 #pragma unroll
-        for (int e = 0; e < V; ++e) { const float df = f[e] - cs[cc + e]; acc[u] += df * df; }
+        for (int e = 0; e < V; ++e) { const float df = f[e] - cs[col + e]; acc[u] += df * df; }
       }
     }
 #pragma unroll
@@ -65,8 +112,20 @@ __global__ __launch_bounds__(KPP_NT) void kpp_d2_kernel(const T* __restrict__ X,
       for (int o = 1; o < LPR; o <<= 1) acc[u] += __shfl_xor(acc[u], o, 64);
       const int64_t i = base + (int64_t)u * RPW;
       if (sub == 0 && i < r1) {
-        const float v = first ? acc[u] : fminf(acc[u], d2[i]);
-        d2[i] = v;
+        float v;
+        if constexpr (PRUNE) {
+          // == fminf(acc, old) of the unpruned pass (a NaN acc keeps old); stored on change only.
+          // Rows are visited in the same order, so `part` sums the same values in the same order.
+          v = old[u];
+          if (need[u] && acc[u] < old[u]) {
+            v = acc[u];
+            d2[i] = v;
+            if (knew >= 0) owner[i] = knew;
+          }
+        } else {
+          v = first ? acc[u] : fminf(acc[u], d2[i]);
+          d2[i] = v;
+        }
         part += v;
       }
     }
@@ -82,15 +141,16 @@ __global__ __launch_bounds__(KPP_NT) void kpp_d2_kernel(const T* __restrict__ X,
   }
 }
 
-template <typename T>
+template <typename T, bool PRUNE>
 static void launch_kpp_d2_t(const void* X, int64_t N, int D, int64_t ldx, const float* c, int first,
                             float* d2, double* block_sums, int64_t rows_per_block, int nblocks,
-                            size_t lds, hipStream_t s) {
+                            size_t lds, int32_t* owner, const float* cc, int kcc, int knew,
+                            hipStream_t s) {
   const int pieces = (D * (int)sizeof(T) + 15) / 16;  // 16-byte pieces per row
   const T* Xt = (const T*)X;
-#define MK_KPP_LAUNCH(L)                                                                        \
-  hipLaunchKernelGGL((kpp_d2_kernel<T, L>), dim3(nblocks), dim3(KPP_NT), lds, s, Xt, N, D, ldx, c, \
-                     first, d2, block_sums, rows_per_block)
+#define MK_KPP_LAUNCH(L)                                                                         \
+  hipLaunchKernelGGL((kpp_d2_kernel<T, L, PRUNE>), dim3(nblocks), dim3(KPP_NT), lds, s, Xt, N, D, \
+                     ldx, c, first, d2, block_sums, rows_per_block, owner, cc, kcc, knew)
   if (pieces >= 16) MK_KPP_LAUNCH(16);
   else if (pieces >= 8) MK_KPP_LAUNCH(8);
   else if (pieces >= 4) MK_KPP_LAUNCH(4);
@@ -101,12 +161,51 @@ static void launch_kpp_d2_t(const void* X, int64_t N, int D, int64_t ldx, const 
 
 hipError_t launch_kpp_d2(int dtype, const void* X, int64_t N, int D, int64_t ldx, const float* c,
                          int first, float* d2, double* block_sums, int64_t rows_per_block,
-                         int nblocks, hipStream_t s) {
-  const size_t lds = ((size_t)D * 4 + 15) / 16 * 16;
-  if (dtype == DT_BF16)
-    launch_kpp_d2_t<uint16_t>(X, N, D, ldx, c, first, d2, block_sums, rows_per_block, nblocks, lds, s);
-  else
-    launch_kpp_d2_t<float>(X, N, D, ldx, c, first, d2, block_sums, rows_per_block, nblocks, lds, s);
+                         int nblocks, hipStream_t s, int32_t* owner, const float* cc, int kcc,
+                         int knew) {
+  const bool prune = owner != nullptr && cc != nullptr && !first;
+  size_t lds = ((size_t)D * 4 + 15) / 16 * 16;
+  if (prune && kcc <= KPP_CC_LDS) lds += (size_t)kcc * 4;
+  if (dtype == DT_BF16) {
+    if (prune)
+      launch_kpp_d2_t<uint16_t, true>(X, N, D, ldx, c, 0, d2, block_sums, rows_per_block, nblocks, lds,
+                                      owner, cc, kcc, knew, s);
+    else
+      launch_kpp_d2_t<uint16_t, false>(X, N, D, ldx, c, first, d2, block_sums, rows_per_block, nblocks,
+                                       lds, nullptr, nullptr, 0, -1, s);
+  } else {
+    if (prune)
+      launch_kpp_d2_t<float, true>(X, N, D, ldx, c, 0, d2, block_sums, rows_per_block, nblocks, lds,
+                                   owner, cc, kcc, knew, s);
+    else
+      launch_kpp_d2_t<float, false>(X, N, D, ldx, c, first, d2, block_sums, rows_per_block, nblocks,
+                                    lds, nullptr, nullptr, 0, -1, s);
+  }
+  return hipGetLastError();
+}
+
+// cc[j] = |cnew - C[j]|^2 for the k centres already chosen (one wave per centre): the
+// centre-centre distances of the pruned K5 pass.
+__global__ __launch_bounds__(256) void kpp_cc_kernel(const float* __restrict__ C, int64_t ldc, int k,
+                                                     int D, const float* __restrict__ cnew,
+                                                     float* __restrict__ cc) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);  // wave-uniform
+  if (j >= k) return;
+  const int lane = threadIdx.x & 63;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float df = cnew[d] - C[(int64_t)j * ldc + d];
+    s += df * df;
+  }
+  s = wave_sum(s);
+  if (lane == 0) cc[j] = s;
+}
+
+hipError_t launch_kpp_cc(const float* C, int64_t ldc, int k, int D, const float* cnew, float* cc,
+                         hipStream_t s) {
+  if (k <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kpp_cc_kernel, dim3((unsigned)((k + 3) / 4)), dim3(256), 0, s, C, ldc, k, D, cnew,
+                     cc);
   return hipGetLastError();
 }
 

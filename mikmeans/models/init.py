@@ -21,6 +21,7 @@ app.mjs:126-129); here seeding is algorithmic and reproducible by seed.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -63,11 +64,16 @@ def init_random(X, D, K, n_global, start, comm: Comm, seed: int) -> torch.Tensor
 
 
 def init_kmeanspp(X: torch.Tensor, D: int, K: int, n_global: int, start: int, comm: Comm, seed: int,
-                  n_local_trials: int = 1, xn: torch.Tensor | None = None) -> torch.Tensor:
+                  n_local_trials: int = 1, xn: torch.Tensor | None = None,
+                  prune: bool | None = None) -> torch.Tensor:
     """k-means++ seeding; returns replicated f32 centres [K, D].
 
-    ``X`` may be column-padded (only the first ``D`` columns are real).
+    ``X`` may be column-padded (only the first ``D`` columns are real).  ``prune``
+    (GPU; default on, ``MIKMEANS_KPP_PRUNE=0`` turns it off) skips the rows the
+    triangle inequality rules out of each D^2 pass; the centres are bit-identical.
     """
+    if prune is None:
+        prune = os.environ.get("MIKMEANS_KPP_PRUNE", "1") not in ("0", "")
     rng = np.random.default_rng(seed)
     first = int(rng.integers(0, n_global))
     centers = torch.zeros((K, X.shape[1]), dtype=torch.float32, device=X.device)
@@ -78,7 +84,7 @@ def init_kmeanspp(X: torch.Tensor, D: int, K: int, n_global: int, start: int, co
     # every random number up front: the GPU loop then never waits for the host
     u = torch.as_tensor(rng.random((K - 1) * L), dtype=torch.float64)
     if X.is_cuda:
-        _kpp_gpu(X, centers, K, comm, u.to(X.device), L)
+        _kpp_gpu(X, centers, K, comm, u.to(X.device), L, prune)
     else:
         _kpp_cpu(X, centers, K, comm, u, L)
     return centers[:, :D].contiguous()
@@ -101,7 +107,7 @@ def _local_target(totals_all: torch.Tensor, u: torch.Tensor, rank: int) -> tuple
     return torch.where(owner, local, torch.full_like(local, -1.0)), total
 
 
-def _kpp_gpu(X, centers, K, comm: Comm, u, L):
+def _kpp_gpu(X, centers, K, comm: Comm, u, L, prune: bool = True):
     C = native.require()
     n = X.shape[0]
     dev = X.device
@@ -114,6 +120,19 @@ def _kpp_gpu(X, centers, K, comm: Comm, u, L):
     bsc = torch.zeros_like(bs) if L > 1 else None
     crow = torch.empty(D, dtype=torch.float32, device=dev)
     cand = torch.empty((L, D), dtype=torch.float32, device=dev)
+    # Triangle-inequality pruning of the D^2 passes (csrc/kpp.hip, KPP_PRUNE): owner[i] is
+    # the centre d2[i] belongs to, cc the new centre's squared distances to the previous
+    # ones.  Same d2 bits and block sums as the unpruned pass, far fewer rows read.
+    owner = torch.zeros(max(n, 1), dtype=torch.int32, device=dev) if prune else None
+    cc = torch.empty(K, dtype=torch.float32, device=dev) if prune else None
+
+    def d2_pass(c, k, d2_, bs_, record):
+        if owner is None:
+            C.kpp_d2(X, c, False, d2_, bs_, rpb)
+        else:
+            C.kpp_cc(centers, k, c, cc)
+            C.kpp_d2(X, c, False, d2_, bs_, rpb, owner, cc, k, k if record else -1)
+
     if n:
         C.kpp_d2(X, centers[0], True, d2, bs, rpb)
     W = comm.world
@@ -138,20 +157,20 @@ def _kpp_gpu(X, centers, K, comm: Comm, u, L):
                 centers[k] = row
         if L == 1:
             if n:
-                C.kpp_d2(X, centers[k], False, d2, bs, rpb)
+                d2_pass(centers[k], k, d2, bs, True)
             continue
         # greedy: potential of each candidate, keep the best (ties -> first)
         pots = torch.zeros(L, dtype=torch.float64, device=dev)
         for t in range(L):
             if n:
                 d2c.copy_(d2)
-                C.kpp_d2(X, cand[t], False, d2c, bsc, rpb)
+                d2_pass(cand[t], k, d2c, bsc, False)
                 pots[t] = bsc.sum()
         comm.allreduce_(pots)
         best = torch.argmin(pots)
         centers[k] = cand[best]
         if n:
-            C.kpp_d2(X, centers[k], False, d2, bs, rpb)
+            d2_pass(centers[k], k, d2, bs, True)
 
 
 def _kpp_cpu(X, centers, K, comm: Comm, u, L):

@@ -222,6 +222,21 @@ def test_kmeanspp_gpu_picks_data_rows(native):
     assert len(set(lab.cpu().tolist())) >= 17
 
 
+@pytest.mark.parametrize("dtype,d,trials", [(torch.bfloat16, 64, 1), (torch.float32, 32, 1),
+                                            (torch.bfloat16, 128, 3)])
+def test_kmeanspp_pruned_is_bitwise_unpruned(native, dtype, d, trials):
+    """The triangle-inequality pruned D^2 passes must reproduce the unpruned seeding bit for bit."""
+    from mikmeans.models.init import init_kmeanspp
+    from mikmeans.parallel import Comm
+
+    n, k = 60000, 96
+    X = B.make_blobs(n, d, 40, seed=11, dtype=dtype, device=DEV)
+    comm = Comm.local(DEV)
+    a = init_kmeanspp(X, d, k, n, 0, comm, seed=2, n_local_trials=trials, prune=True)
+    b = init_kmeanspp(X, d, k, n, 0, comm, seed=2, n_local_trials=trials, prune=False)
+    assert torch.equal(a, b)
+
+
 def test_kmeanspp_gpu_cpu_same_seed_same_first_center(native):
     X = B.make_blobs(5000, 16, 8, seed=1)
     Cg = mikmeans.kmeans_plusplus(X.to(DEV), 8, seed=7).cpu()
