@@ -370,8 +370,12 @@ struct U4 { uint32_t x, y, z, w; };
 __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    // one 32x32->64 product per word: a single v_mad_u64_u32 (quarter rate) instead of a
+    // v_mul_lo_u32 + v_mul_hi_u32 pair
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -430,11 +434,15 @@ __global__ __launch_bounds__(256) void blobs_kernel(T* X, int64_t i0, int64_t n,
     T* out = X + il * ldx;
     for (int g = t; g < G; g += TPR) {
       const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
-      const float rad0 = sqrtf(-2.f * logf(u01_open0(r.x)));
-      const float rad1 = sqrtf(-2.f * logf(u01_open0(r.z)));
-      float s0, c0, s1, c1;
-      sincospif(2.f * u01(r.y), &s0, &c0);
-      sincospif(2.f * u01(r.w), &s1, &c1);
+      // Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32, and
+      // v_sin_f32 / v_cos_f32, whose argument is in revolutions, so sin(2*pi*u) is one
+      // instruction.  A few ulp from the libm forms, a third of the instructions.
+      constexpr float M2LN2 = -1.38629436111989f;  // -2 ln 2
+      const float rad0 = __builtin_amdgcn_sqrtf(M2LN2 * __builtin_amdgcn_logf(u01_open0(r.x)));
+      const float rad1 = __builtin_amdgcn_sqrtf(M2LN2 * __builtin_amdgcn_logf(u01_open0(r.z)));
+      const float a0 = u01(r.y), a1 = u01(r.w);
+      const float s0 = __builtin_amdgcn_sinf(a0), c0 = __builtin_amdgcn_cosf(a0);
+      const float s1 = __builtin_amdgcn_sinf(a1), c1 = __builtin_amdgcn_cosf(a1);
       const float z[4] = {rad0 * c0, rad0 * s0, rad1 * c1, rad1 * s1};
       T v[4];
 #pragma unroll

@@ -5,7 +5,8 @@ Philox4x32-10), so every rank of a data-parallel job generates exactly its own
 row range, on device, with no host traffic (BASELINE config 5 streams 1e9 rows:
 PCIe at 63 GB/s would be ~100x too slow).  The GPU path is the HIP kernel K8
 (csrc/kpp.hip); the CPU path below is a NumPy mirror of the same generator
-(bit-identical integers; the float transforms agree to ~1 ulp before rounding).
+(bit-identical integers; the device uses the hardware log2/sqrt/sin/cos, so the floats
+agree to a few ulp before rounding).
 
 Blob centres are uniform in ``[-box, box]^D`` (like sklearn's ``make_blobs``
 ``center_box=(-10, 10)``); the cluster of row i is ``mulhi(philox(i), n_centers)``.
