@@ -243,7 +243,10 @@ int get_assign_p() { return g_assign_p; }
 
 template <typename T, int DPAD>
 static hipError_t launch_p(const AssignArgs& a, hipStream_t s) {
-  const int p = g_assign_p ? g_assign_p : 2;
+  // default: 4 point blocks per wave where the rows are short (bf16 D <= 64, f32 D <= 32),
+  // which halves the centroid LDS traffic per FLOP (cfg4 data, N=1e7 D=64 K=4096: 4.29 vs
+  // 4.65 ms for P=2; profiles/r1_16_assign_shapes.md)
+  const int p = g_assign_p ? g_assign_p : (DPAD * sizeof(T) <= 128 ? 4 : 2);
   if (p == 1) return launch_t<T, DPAD, 1>(a, s);
   if (p == 4 && DPAD * sizeof(T) <= 256) return launch_t<T, DPAD, 4>(a, s);
   return launch_t<T, DPAD, 2>(a, s);

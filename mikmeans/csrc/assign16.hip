@@ -358,7 +358,10 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
       default: break;
     }
   }
-  if (g_assign16_gt == 0) {
+  // gt knob: 0/1 = the GT1 default below, 2/4 = GT2/GT4.  GT1 is the fastest on every
+  // BASELINE shape when timed on the bench's own data and centres (scripts/ab_shapes.py,
+  // profiles/r1_16_assign_shapes.md); on random centres GT2 can look faster.
+  if (g_assign16_gt <= 1) {
     // Default: 1-tile epilogue with segmented 6-bit keys (1.5 VALU per score), 16 KiB
     // chunks in a 2-slot ring.  A/B on MI355X at N=2e7 D=128 K=1024 bf16 (scripts/
     // ab_kernels.py, one process, interleaved rounds): 1279-1317 TF/s vs 1218-1265 for
@@ -368,7 +371,7 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
     constexpr int WB = sizeof(T) == 2 ? 16 : 0;
     return launch16_t<T, DPAD, P, 1, CT, 2, WB>(a, s);
   }
-  const int want = g_assign16_gt;
+  const int want = g_assign16_gt;  // >= 2
   if (want >= 4 && CT % 4 == 0) return launch16_t<T, DPAD, P, (CT % 4 == 0 ? 4 : 1)>(a, s);
   if (want >= 2 && CT % 2 == 0) return launch16_t<T, DPAD, P, (CT % 2 == 0 ? 2 : 1)>(a, s);
   return launch16_t<T, DPAD, P, 1>(a, s);

@@ -41,7 +41,9 @@ class Comm:
         """Join (or create) the default process group described by torchrun's env vars.
 
         ``device`` "cuda" binds LOCAL_RANK's GPU and uses RCCL; "cpu" uses gloo.
-        Without WORLD_SIZE>1 in the environment this returns a single-rank Comm.
+        Without WORLD_SIZE>1 in the environment this returns a single-rank Comm without a
+        process group, unless ``MIKMEANS_FORCE_PG=1``: then even one rank joins a real group
+        and every collective below is issued (a one-GPU rehearsal of the RCCL path).
         """
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
@@ -55,7 +57,8 @@ class Comm:
         else:
             dev = torch.device("cpu")
             backend = "gloo"
-        if world <= 1 and not dist.is_initialized():
+        force = os.environ.get("MIKMEANS_FORCE_PG", "0") not in ("", "0")
+        if world <= 1 and not dist.is_initialized() and not force:
             return Comm(device=dev, backend=None)
         owns = False
         if not dist.is_initialized():
@@ -92,26 +95,31 @@ class Comm:
     def distributed(self) -> bool:
         return self.world > 1
 
+    @property
+    def grouped(self) -> bool:
+        """A process group exists: collectives are issued (also on a forced 1-rank group)."""
+        return self.backend is not None and dist.is_initialized()
+
     # ---------------------------------------------------------- collectives
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place SUM across ranks (no-op on one rank)."""
-        if self.world > 1:
+        """In-place SUM across ranks (no-op on one rank without a group)."""
+        if self.grouped:
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t
 
     def allreduce_max_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world > 1:
+        if self.grouped:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        if self.world > 1:
+        if self.grouped:
             dist.broadcast(t, src=src)
         return t
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """Stack ``t`` from every rank: shape ``[world, *t.shape]``."""
-        if self.world == 1:
+        if not self.grouped:
             return t.unsqueeze(0).clone()
         flat = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(flat, t.contiguous().reshape(-1))  # gloo wants flat buffers
@@ -157,7 +165,7 @@ class Comm:
         return buf.cpu()[: int(n.item())].numpy().tobytes()
 
     def barrier(self):
-        if self.world > 1:
+        if self.grouped:
             if self.backend == "nccl":
                 dist.barrier(device_ids=[self.device.index])
             else:
