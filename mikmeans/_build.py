@@ -38,6 +38,9 @@ DEVICE_FLAGS = [
     "-amdgpu-mfma-vgpr-form=1",
     "-Wno-unused-result",
 ]
+if os.environ.get("MIKMEANS_AB") == "1":
+    # diagnostic kernel variants for scripts/ab_kernels.py (not in the default build)
+    DEVICE_FLAGS.append("-DMK_AB_VARIANTS")
 
 
 def ext_path() -> Path:

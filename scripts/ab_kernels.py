@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of kernel variants in ONE process (cdna guide §5.4 rule 24).
 
+    MIKMEANS_AB=1 python -m mikmeans._build   # the variant knobs need the A/B build
     python scripts/ab_kernels.py --n 20000000 --d 128 --k 1024 --dtype bf16 --rounds 5
 
 Times the assign kernel for every points-per-wave variant and the update kernel,
