@@ -66,20 +66,11 @@ template <> struct Mfma16<float> {
   }
 };
 
-// DBG bit flags (diagnostic builds for A/B; 4 and 16 are pipeline options; 16 = at
-// least 4 waves per SIMD, i.e. <= 128 VGPRs): 1 = epilogue replaced by
+// DBG bit flags (diagnostic builds for A/B; 4, 16 and 32 are pipeline options; 16 = at
+// least 4 waves per SIMD, i.e. <= 128 VGPRs; 32 = at least 3, <= 168): 1 = epilogue replaced by
 // one add per tile (MFMA + LDS pipeline alone), 2 = no ring refills / waits (MFMA +
 // epilogue alone on whatever the LDS holds).
-// HINT (GT == 1 only): the labels on entry are the previous assignment.  A prologue
-// scores every point against its previous centre on the same MFMA (the centre's
-// fragments gathered per row: the diagonal of one 16x16 product per point block) and
-// seeds the running best with that exact score; the main loop then only asks, per
-// tile, whether ANY lane holds a strictly smaller score (2 v_min3 + 1 v_cmp per block
-// instead of 4 key packs + 2 v_min3) and runs the exact per-score update only for the
-// rare tiles where one does.  Every score is still computed; the result is the argmin
-// of the raw fp32 scores, ties kept by the previous label, else the lowest index.
-template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0, int NW_ = 4,
-          bool HINT = false>
+template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0, int NW_ = 4>
 __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_, NW_>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -119,45 +110,6 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
       else xr[p][q] = u32x4{0u, 0u, 0u, 0u};
     }
   }
-  // HINT prologue: hb[p] / hk[p] = exact score / index of the previous centre
-  float hb[C::P];
-  int hk[C::P];
-  if constexpr (HINT && (DBG & 1024) == 0) {
-    static_assert(GT == 1, "hinted assign uses the 1-tile epilogue");
-#pragma unroll
-    for (int p = 0; p < C::P; ++p) {
-      const int64_t p0 = pbase + p * 16;
-      const int64_t row = p0 + r;
-      const int prev = row < a.N ? a.labels[row] : -1;
-      const bool ok = prev >= 0 && prev < a.Kpad;
-      const int kc = ok ? prev : 0;
-      // A fragment of row r = centre kc (tile kc/16, slot kc%16), feature quarter g
-      const char* src = gC + ((int64_t)(kc >> 4) * C::NQ * 64 + (kc & 15) + 16 * g) * 16;
-      u32x4 af[C::NQ];
-#pragma unroll
-      for (int q = 0; q < C::NQ; ++q) af[q] = *(const u32x4*)(src + q * 1024);
-      // seed of output row 4g+e: |c|^2 of the previous centre of point p0+4g+e
-      f32x4 acc;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int64_t rj = p0 + 4 * g + e;
-        const int pj = rj < a.N ? a.labels[rj] : -1;
-        acc[e] = (pj >= 0 && pj < a.Kpad) ? a.cn[pj] : 0.f;
-      }
-#pragma unroll
-      for (int q = 0; q < C::NQ; ++q) acc = Mfma16<T>::run(af[q], xr[p][q], acc);
-      // D[r][r] lives in lane (r, r/4), register r%4
-      const int e = r & 3;
-      const float mine = e == 0 ? acc[0] : e == 1 ? acc[1] : e == 2 ? acc[2] : acc[3];
-      const float sp = __shfl(mine, r + 16 * (r >> 2), 64);
-      hb[p] = ok ? sp : 3.0e38f;
-      hk[p] = ok ? prev : 0x7fffffff;
-    }
-  }
-  if constexpr (HINT && (DBG & 1024) != 0) {  // diagnostics: no prologue, nothing triggers
-#pragma unroll
-    for (int p = 0; p < C::P; ++p) { hb[p] = -3.0e38f; hk[p] = 0; }
-  }
   wait_vmcnt<0>();  // see assign.hip: retire the fragments before the LDS-DMA loop
   if (C::NBUF == 3 && nch > 1) issue_chunk(1);
 
@@ -167,12 +119,6 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
   for (int p = 0; p < C::P; ++p) { best[p] = 3.0e38f; seg_best[p] = 3.0e38f; bg[p] = 0; }
   const int last_grp = nch * (C::CT / GT) - 1;
   const unsigned kmask = key6_mask();
-
-  // HINT: tmask bit (tile & 63) = some lane of this wave saw a score below its seed in
-  // that tile (SALU only, no branch in the tile loop); every 64 tiles the mask moves into
-  // lanes 2w / 2w+1 of hwords.  The marked tiles are re-scored exactly after the loop.
-  unsigned long long tmask = 0;
-  int hwords = 0;
 
   float dbg_sink = 0.f;
   if constexpr ((DBG & 2) != 0) { wait_vmcnt<0>(); raw_barrier(); }
@@ -227,21 +173,6 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
       if constexpr ((DBG & 1) != 0) {
 #pragma unroll
         for (int p = 0; p < C::P; ++p) dbg_sink += acc[p][0][0];
-        continue;
-      }
-      if constexpr (HINT) {
-        // does any lane of the wave see a strictly smaller score in this tile?  (the
-        // compiler-visible v_cmp is the first reader of each MFMA result: see min3f_after)
-        unsigned long long hit = 0;
-#pragma unroll
-        for (int p = 0; p < C::P; ++p) {
-          const f32x4& sv = acc[p][0];
-          const unsigned long long h0 = __ballot(sv[0] < hb[p]);
-          const float m = min3f_after(sv[1], sv[2], sv[3], h0);
-          hit |= h0 | __ballot(m < hb[p]);
-        }
-        if constexpr ((DBG & 256) != 0) hit = 0;  // diagnostics: fast path only
-        tmask |= hit ? (1ull << (grp & 63)) : 0ull;
         continue;
       }
       if constexpr (GT == 1) {
@@ -300,52 +231,6 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
         if (m < best[p]) { best[p] = m; bg[p] = grp; }
       }
     }
-    if constexpr (HINT) {
-      const int done = (c + 1) * C::CT;  // tiles scored so far (CT divides 64)
-      if ((done & 63) == 0 || c + 1 == nch) {
-        const int w = (done - 1) >> 6;
-        hwords = lane == 2 * w ? (int)(unsigned)tmask : hwords;
-        hwords = lane == 2 * w + 1 ? (int)(unsigned)(tmask >> 32) : hwords;
-        tmask = 0;
-      }
-    }
-  }
-
-  if constexpr (HINT) {
-    // exact pass over the marked tiles, in increasing order (strict '<': the seed keeps
-    // ties, then the lowest index).  Fragments come straight from the packed centres in
-    // global memory (L2): the same bytes the LDS ring held, so the same scores.
-    const int nwords = (nch * C::CT + 63) >> 6;
-    for (int w = 0; w < nwords; ++w) {
-      unsigned long long bits =
-          ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(hwords, 2 * w + 1) << 32) |
-          (unsigned)__builtin_amdgcn_readlane(hwords, 2 * w);
-      if constexpr ((DBG & 512) != 0) {  // diagnostics: count re-scored tiles
-        if (lane == 0 && a.slots) atomicAdd(a.slots + 2, (double)__builtin_popcountll(bits));
-        bits = 0;
-      }
-      while (bits) {
-        const int t = w * 64 + __builtin_ctzll(bits);
-        bits &= bits - 1;
-        const char* src = gC + ((int64_t)t * C::NQ * 64 + lane) * 16;
-        u32x4 aw[C::NQ];
-#pragma unroll
-        for (int q = 0; q < C::NQ; ++q) aw[q] = *(const u32x4*)(src + q * 1024);
-        const f32x4 ci = *(const f32x4*)(a.cn + t * 16 + 4 * g);
-        const int kb = t * 16 + 4 * g;
-#pragma unroll
-        for (int p = 0; p < C::P; ++p) {
-          f32x4 acc = ci;
-#pragma unroll
-          for (int q = 0; q < C::NQ; ++q) acc = Mfma16<T>::run(aw[q], xr[p][q], acc);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float sc = acc[e];
-            if (sc < hb[p]) { hb[p] = sc; hk[p] = kb + e; }
-          }
-        }
-      }
-    }
   }
 
   if constexpr ((DBG & 1) != 0) best[0] = fminf(best[0], dbg_sink);
@@ -356,10 +241,7 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
     const unsigned bits = __float_as_uint(best[p]);
     int k;
     float v;
-    if constexpr (HINT) {
-      k = hk[p];
-      v = hb[p];
-    } else if constexpr (GT == 1) {  // bg = segment of 16 tiles, 6-bit key
+    if constexpr (GT == 1) {  // bg = segment of 16 tiles, 6-bit key
       const int idx = (int)(bits & 63u);
       k = (bg[p] * 16 + (idx >> 2)) * 16 + 4 * g + (idx & 3);
       v = __uint_as_float(bits & ~63u);
@@ -404,8 +286,7 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
   }
 }
 
-template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0, int NW_ = 4,
-          bool HINT = false>
+template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0, int NW_ = 4>
 static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_, NW_>;
   if (a.Kpad % (16 * C::CT) != 0) return hipErrorInvalidValue;
@@ -414,13 +295,13 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_, HINT>,
+    hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
   if (nblk <= 0) return hipSuccess;
-  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_, HINT>), dim3((unsigned)nblk),
+  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_>), dim3((unsigned)nblk),
                      dim3(C::NW * 64), lds, s, a);
   return hipGetLastError();
 }
@@ -483,9 +364,6 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
       case 39: return launch16_t<T, DPAD, P, 1, 4, 2, 16 | 128>(a, s);  // iglp_opt(1)
       case 21: return launch16_t<T, DPAD, 2, 1, 4, 2>(a, s);
       case 22: return launch16_t<T, DPAD, 8, 1, 4, 2>(a, s);
-      case 60: return launch16_t<T, DPAD, P, 1, 4, 2, 16 | 256, 4, true>(a, s);  // hinted, no exact path
-      case 61: return launch16_t<T, DPAD, P, 1, 4, 2, 16 | 512, 4, true>(a, s);  // hinted, count exact tiles
-      case 62: return launch16_t<T, DPAD, P, 1, 4, 2, 16 | 1024, 4, true>(a, s); // hinted, no prologue
       case 63: return launch16_t<T, DPAD, P, 1, 4, 2, 4 | 32>(a, s);  // A prefetch at 3 waves/SIMD
       case 64: return launch16_t<T, DPAD, P, 1, 4, 3, 4 | 32>(a, s);
       case 65: return launch16_t<T, DPAD, 5, 1, 4, 2, 4 | 32>(a, s);
@@ -508,7 +386,6 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
     // bf16: at most 128 VGPRs (4 waves per SIMD; <= 5 spilled registers): +2.5 % at the
     // headline shape (1339 vs 1306 TF/s).  f32 would spill heavily under that bound.
     constexpr int WB = sizeof(T) == 2 ? 16 : 0;
-    if (a.hint) return launch16_t<T, DPAD, P, 1, CT, 2, WB, 4, true>(a, s);
     return launch16_t<T, DPAD, P, 1, CT, 2, WB>(a, s);
   }
   const int want = g_assign16_gt;  // >= 2

@@ -73,7 +73,7 @@ void check_i64(const Tensor& t, const char* name, int64_t numel_min);
 void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::optional<Tensor>& xn,
             const Tensor& labels, const c10::optional<Tensor>& mind,
             const c10::optional<Tensor>& slots, int64_t Kpad, int64_t dpad, bool track_changed,
-            int64_t layout, const c10::optional<Tensor>& keys, bool hint) {
+            int64_t layout, const c10::optional<Tensor>& keys) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   const int64_t N = X.size(0);
@@ -104,7 +104,6 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
   a.mind = opt_ptr<float>(mind);
   a.slots = opt_ptr<double>(slots);
   a.track_changed = track_changed ? 1 : 0;
-  a.hint = hint ? 1 : 0;  // read by the 16x16 default path only; never changes correctness
   if (layout == 116) {
     const int passes = mk::assign_res_passes(dt, (int)dpad, (int)Kpad);
     TORCH_CHECK(passes >= 1, "mikmeans: resident assign does not support this shape");

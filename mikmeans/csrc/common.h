@@ -99,16 +99,6 @@ __device__ __forceinline__ float min3f(float a, float b, float c) {
   return d;
 }
 
-// min3 that may read an MFMA result only after `dep` exists: make `dep` come from a
-// compiler-visible reader of the same accumulator (e.g. a v_cmp), so the hazard
-// recognizer has already padded the MFMA latency (all four result registers of one
-// MFMA land together) and the asm cannot be scheduled above it.
-__device__ __forceinline__ float min3f_after(float a, float b, float c, unsigned long long dep) {
-  float d;
-  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c), "s"(dep));
-  return d;
-}
-
 // ---------------------------------------------------------------------------
 // 64-lane reductions
 __device__ __forceinline__ float wave_sum(float v) {

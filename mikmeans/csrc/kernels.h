@@ -42,7 +42,6 @@ struct AssignArgs {
   float* mind;          // optional: squared distance to the chosen centroid
   double* slots;        // optional: [NSLOT][SLOT_STRIDE] (+inertia, +changed)
   int track_changed;
-  int hint;             // labels on entry are the previous assignment (assign16 default path)
 };
 hipError_t launch_assign(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);

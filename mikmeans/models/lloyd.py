@@ -79,12 +79,6 @@ class LloydEngine:
         # re-scatter only the rows whose label changed (+ to the new label, - from the old).
         # Bitwise identical to the full M-step (integer fixed point); the full pass runs
         # automatically while more than ``delta_cap * n`` rows change.
-        # Previous-label hint for the E-step (csrc/assign16.hip, HINT): labels that already
-        # hold an assignment seed each point with its old centre's exact score, so the
-        # argmin bookkeeping runs only on tiles where some point finds a closer centre.
-        # MIKMEANS_ASSIGN_HINT=0 turns it off (A/B); results never depend on its validity.
-        self.hint = os.environ.get("MIKMEANS_ASSIGN_HINT", "1") != "0"
-        self._labels_set = False
         self.incremental = bool(incremental)
         self.delta_cap = float(delta_cap)
         self.segments = max(1, int(segments))
@@ -187,7 +181,6 @@ class LloydEngine:
         """Unassign every point (the reference's Restart, app.mjs:167-178); the next
         step re-assigns from the current centres and counts every point as changed."""
         self.labels.fill_(-1)
-        self._labels_set = False
         return self
 
     def set_centers(self, centers: torch.Tensor):
@@ -208,14 +201,11 @@ class LloydEngine:
     def step(self):
         """One Lloyd iteration (E-step on the current centres, M-step, all-reduce, finalize)."""
         graphs = getattr(self, "_graphs", None)
-        if graphs is not None and (self._labels_set or not self.hint):
-            # (the graphs bake the hinted E-step in: a step on unassigned labels runs eagerly)
+        if graphs is not None:
             graphs[self._gphase].replay()   # one hipGraph launch for the whole iteration
             self._gphase ^= 1
         elif self.gpu:
             self._step_gpu()
-            if graphs is not None:
-                self._gphase ^= 1           # keep the graphs' centre-buffer parity in step
         else:
             self._step_cpu()
         self.C, self.Cnew = self.Cnew, self.C
@@ -235,7 +225,6 @@ class LloydEngine:
         side.wait_stream(torch.cuda.current_stream(self.device))
         C0 = self.C.clone()
         lab0 = self.labels.clone()
-        set0 = self._labels_set
         with torch.cuda.stream(side):
             self._step_gpu()
         torch.cuda.current_stream(self.device).wait_stream(side)
@@ -249,7 +238,6 @@ class LloydEngine:
         # the warm-up changed labels / slots: restore the pre-capture state
         self.C.copy_(C0)
         self.labels.copy_(lab0)
-        self._labels_set = set0
         self.pk.finalize(0, None, self.C)
         if self.slots is not None:
             self.slots.zero_()
@@ -268,9 +256,7 @@ class LloydEngine:
                 self.packed[KD + self.K] = (self.mind.double() * self.weights.double()).sum()
         elif self.n:
             with _phase("mikmeans.assign"):
-                self.pk.assign(self.X, self.xn, self.labels, self.mind, self.slots, True,
-                               hint=self.hint and self._labels_set)
-                self._labels_set = True
+                self.pk.assign(self.X, self.xn, self.labels, self.mind, self.slots, True)
             with _phase("mikmeans.update"):
                 d = self.delta
                 if d is not None:
@@ -302,10 +288,8 @@ class LloydEngine:
         kd, nc = self.K * self.Dp, self.seg_chunks
         for s, (r0, r1) in enumerate(self.seg_ranges):
             mind = self.mind[r0:r1] if self.mind is not None else None
-            self.pk.assign(self.X[r0:r1], self.xn[r0:r1], self.labels[r0:r1], mind, self.slots, True,
-                           hint=self.hint and self._labels_set)
+            self.pk.assign(self.X[r0:r1], self.xn[r0:r1], self.labels[r0:r1], mind, self.slots, True)
             self.seg_events[s].record(main)
-        self._labels_set = True
         C.set_update_max_sw(self.overlap_sw)
         try:
             with torch.cuda.stream(self.side):

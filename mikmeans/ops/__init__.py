@@ -94,21 +94,15 @@ class CentroidPack:
         self._C.finalize(mode, packed, Cold, Cnew, frozen, mb_counts, self.pack, self.cn, shift, counts,
                          self.dpad, self.Kpad, self.pack_layout)
 
-    def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False,
-               hint: bool = False):
-        """K2 on these centres (``X`` column-padded, 16-B rows).
-
-        ``hint``: ``labels`` holds the previous assignment; the 16x16 kernel then seeds
-        each point with its previous centre's exact score and keeps it on ties (see
-        ``csrc/assign16.hip``).  Rows whose label is out of range are simply unseeded.
-        """
+    def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False):
+        """K2 on these centres (``X`` column-padded, 16-B rows)."""
         keys = None
         if self.layout == 116 and self._C.assign_res_passes(self.dt, self.dpad, self.Kpad) > 1:
             if self._keys is None or self._keys.numel() < X.shape[0]:
                 self._keys = torch.empty(max(X.shape[0], 1), dtype=torch.int64, device=X.device)
             keys = self._keys
         self._C.assign(X, self.pack, self.cn, xn, labels, mind, slots, self.Kpad, self.dpad,
-                       track_changed, self.layout, keys, bool(hint))
+                       track_changed, self.layout, keys)
 
 
 def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True, layout: int | None = None):

@@ -400,93 +400,3 @@ def test_wide_features_use_gemm_path(native):
     assert agree > 0.99
     assert abs(kg.inertia_ - kc.inertia_) <= 1e-3 * kc.inertia_
     assert mb.cluster_centers_.shape == (8, 300)
-
-
-def _hinted_assign(X, C, prev):
-    """The 16x16 kernel with the previous-label hint (labels in/out)."""
-    Xp = ops.pad_columns(X.to(DEV))
-    D = Xp.shape[1]
-    cen = torch.zeros((C.shape[0], D), dtype=torch.float32, device=DEV)
-    cen[:, : C.shape[1]] = C.to(DEV)
-    pk = ops.CentroidPack(C.shape[0], D, Xp.dtype, DEV, layout=16).load(cen)
-    xn = ops.row_sqnorm(Xp)
-    mind = torch.empty(Xp.shape[0], dtype=torch.float32, device=DEV)
-    labels = prev.to(device=DEV, dtype=torch.int32).clone()
-    pk.assign(Xp, xn, labels, mind, hint=True)
-    return labels, mind
-
-
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("n,d,k", [(20000, 128, 256), (9000, 128, 1024), (4096, 64, 4096), (3000, 256, 512),
-                                   (255, 100, 70), (70000, 32, 9), (1000, 2, 3)])
-@pytest.mark.parametrize("hint", ["exact", "random", "invalid"])
-def test_assign_hinted_is_argmin(native, dtype, n, d, k, hint):
-    """Seeding with the previous label (right, wrong or out of range) never changes optimality."""
-    X = _points(n, d, dtype, seed=k + 3)
-    C = _points(k, d, torch.float32, seed=k + 4)
-    dp = ops.dpad_for(ops.pad_columns(X[:1]).shape[1], dtype)
-    if not native.assign16_supported(ops.dtype_code(dtype), dp):
-        pytest.skip("16x16 variant needs DPAD/4 >= one 16-byte piece")
-    g = torch.Generator().manual_seed(n)
-    if hint == "exact":
-        prev, _ = ops.assign(X.to(DEV), C.to(DEV), with_dist=False, layout=16)
-    elif hint == "random":
-        prev = torch.randint(0, k, (n,), generator=g)
-    else:
-        prev = torch.randint(-3, k + 40, (n,), generator=g)
-        prev[::7] = -1
-    labels, mind = _hinted_assign(X, C, prev)
-    _check_assign(X, C, labels, mind, rel=2e-5 if dtype == torch.float32 else 3e-5)
-
-
-def test_assign_hinted_keeps_previous_on_ties(native):
-    # integer data: exact scores.  A point tied between centres keeps its previous label
-    # when that label is among the tied ones, else takes the lowest tied index.
-    g = torch.Generator().manual_seed(5)
-    X = torch.randint(-8, 8, (6000, 64), generator=g).float()
-    C = torch.randint(-8, 8, (700, 64), generator=g).float()
-    C[400] = C[30]
-    C[650] = C[31]
-    sc = ref.scores(X, C)
-    best = sc.min(1, keepdim=True).values
-    tied = sc == best
-    exp, _ = ref.assign(X, C)                       # lowest index among ties
-    prev = exp.clone()
-    prev[tied[:, 400]] = 400                        # previous label = the higher duplicate
-    prev[tied[:, 650]] = 650
-    labels, _ = _hinted_assign(X, C, prev)
-    lab = labels.cpu()
-    assert torch.equal(lab, prev)                   # exact previous labels are all optimal
-    assert int(tied[:, 400].sum()) > 0 and int(tied[:, 650].sum()) > 0
-    # wrong hint: ties resolve to the lowest index, everything else to the argmin
-    labels, _ = _hinted_assign(X, C, (exp + 1) % 700)
-    lab = labels.cpu()
-    multi = tied.sum(1) > 1
-    assert torch.equal(lab[~multi], exp[~multi])
-    assert bool(tied.gather(1, lab.long()[:, None]).all())
-
-
-def test_lloyd_hint_matches_unhinted(native, monkeypatch):
-    """The hinted E-step (default) and the plain one reach the same fit up to near-ties."""
-    from mikmeans.models.lloyd import LloydEngine
-
-    X = B.make_blobs(200_000, 128, 256, seed=4, dtype=torch.bfloat16, device=DEV)
-    C0 = X[:256].float()
-    monkeypatch.setenv("MIKMEANS_ASSIGN_HINT", "0")
-    ea = LloydEngine(X, 256).set_centers(C0)
-    monkeypatch.setenv("MIKMEANS_ASSIGN_HINT", "1")
-    eb = LloydEngine(X, 256).set_centers(C0)
-    assert not ea.hint and eb.hint
-    for it in range(8):
-        ea.step()
-        eb.step()
-        if it == 0:      # first step unhinted on both: identical
-            assert torch.equal(ea.labels, eb.labels)
-            C1 = ea.centers.clone()
-        if it == 1:      # same centres, hinted vs plain E-step: both optimal, near-ties may differ
-            agree = float((ea.labels == eb.labels).float().mean())
-            assert agree > 0.999, agree
-            _check_assign(X.cpu(), C1.cpu(), eb.labels, None, rel=3e-5)
-    # afterwards the trajectories may separate at near-ties; the objective must agree closely
-    sa, sb = ea.last_stats(), eb.last_stats()
-    assert abs(sa.inertia - sb.inertia) <= 1e-4 * abs(sa.inertia)
