@@ -122,6 +122,14 @@ def cmd_room(a) -> int:
         r.set_iteration(a.iteration)
     if a.export:
         Path(a.export).write_text(r.export_json())
+    if a.link is not None:
+        print(r.share_link(a.link))
+    if a.coin:
+        print(r.coin())
+    if a.d12:
+        print(f"d12 \u2192 {r.d12()}")
+    if a.shuffle_names:
+        print("Suggested order:\n\n" + "\n".join(r.shuffled_titles()))
     d = r.dashboard()
     print("\n".join(d["chips"] + [" ".join(x for x in (row["name"], f"{row['bar_pct']}%", row["cohesion"],
                                                              row["top"], row["suggested"])) for row in d["rows"]]))
@@ -239,6 +247,11 @@ def build_parser():
     r.add_argument("--iteration", type=int)
     r.add_argument("--export", help="write kmeans-room JSON here")
     r.add_argument("--seed", type=int, default=0)
+    r.add_argument("--link", nargs="?", const="", default=None, metavar="BASE_URL",
+                   help="print the share link (?room=<code>)")
+    r.add_argument("--coin", action="store_true", help="flip a coin (Heads/Tails)")
+    r.add_argument("--d12", action="store_true", help="roll a twelve-sided die")
+    r.add_argument("--shuffle-names", action="store_true", help="print a shuffled order of the card titles")
     e = sub.add_parser("export", help="checkpoint -> flat centroid JSON or room-export JSON")
     e.add_argument("--model", required=True)
     e.add_argument("--format", choices=["flat", "room"], default="flat")

@@ -231,6 +231,30 @@ class Room:
         self.cards = A + U
         self.log.append(("shuffle_unassigned",))
 
+    # ------------------------------------------------- top-control utilities
+    def share_link(self, base_url: str = "") -> str:
+        """The reference's "Copy link" (app.mjs:239-242) copies ``location.href``, i.e.
+        the page URL carrying ``?room=<code>`` (written by app.mjs:17)."""
+        sep = "&" if "?" in base_url else "?"
+        return f"{base_url}{sep}room={self.room}"
+
+    def coin(self) -> str:
+        """``Math.random() < 0.5 ? "Heads" : "Tails"`` (app.mjs:254)."""
+        return "Heads" if self.rng.random() < 0.5 else "Tails"
+
+    def d12(self) -> int:
+        """``1 + floor(Math.random() * 12)`` (app.mjs:255)."""
+        return 1 + int(self.rng.random() * 12)
+
+    def shuffled_titles(self) -> list[str]:
+        """The "Shuffle names" suggestion (app.mjs:256-260): a Fisher-Yates permutation of
+        every card title, from the last index down; the board itself is not changed."""
+        n = [c["title"] for c in self.cards]
+        for i in range(len(n) - 1, 0, -1):
+            j = int(self.rng.random() * (i + 1))
+            n[i], n[j] = n[j], n[i]
+        return n
+
     def restart_all(self):
         self.cards = [{**c, "assignedTo": None} if c.get("assignedTo") else c for c in self.cards]
         for k in self.meta.keys():

@@ -178,3 +178,46 @@ def test_auto_assign_clusters_traits():
     r.auto_assign(seed=1)
     assert sorted(x["id"] for x in r.cards if x["assignedTo"] == a["id"]) == sorted(members)
     assert jsjson.parse(r.export_json())["centroids"][0]["locked"] is True
+
+
+class _Scripted:
+    """Stands in for Math.random(): returns the scripted values in order."""
+
+    def __init__(self, vals):
+        self.vals = list(vals)
+
+    def random(self):
+        return self.vals.pop(0)
+
+
+def test_top_control_utilities():
+    # app.mjs:239-260: copy link, coin, d12, shuffled title order (board unchanged)
+    r = make_room()
+    assert r.share_link("https://x.test/k/") == "https://x.test/k/?room=ABCD"
+    assert r.share_link("https://x.test/k/?v=2") == "https://x.test/k/?v=2&room=ABCD"
+    r.populate_test_data()
+    before = [c["id"] for c in r.cards]
+    r.rng = _Scripted([0.49999, 0.5, 0.0, 0.999999])
+    assert (r.coin(), r.coin()) == ("Heads", "Tails")
+    assert (r.d12(), r.d12()) == (1, 12)
+    titles = [c["title"] for c in r.cards]
+    n = len(titles)
+    # j = floor(u * (i + 1)) with u = 0 for every i: each position swaps with index 0
+    r.rng = _Scripted([0.0] * (n - 1))
+    exp = list(titles)
+    for i in range(n - 1, 0, -1):
+        exp[i], exp[0] = exp[0], exp[i]
+    assert r.shuffled_titles() == exp
+    assert sorted(exp) == sorted(titles) and [c["id"] for c in r.cards] == before
+
+
+def test_cli_room_utilities(tmp_path, capsys):
+    from mikmeans import cli
+
+    assert cli.main(["room", "--room", "WXYZ", "--populate", "--link", "https://h/p", "--coin", "--d12",
+                     "--shuffle-names"]) == 0
+    out = capsys.readouterr().out.splitlines()
+    assert out[0] == "https://h/p?room=WXYZ"
+    assert out[1] in ("Heads", "Tails")
+    assert re.fullmatch(r"d12 → ([1-9]|1[0-2])", out[2])
+    assert out[3] == "Suggested order:"
