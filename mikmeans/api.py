@@ -214,6 +214,25 @@ class KMeans:
         if not hasattr(self, "cluster_centers_"):
             raise RuntimeError("KMeans instance is not fitted yet; call fit() first")
 
+    def _serving_pack(self, Xt):
+        """The fitted centres packed for the assign kernel, built once and reused by every
+        predict/score call until the centres change (serving: one kernel launch per batch)."""
+        from . import ops
+
+        c = self.cluster_centers_
+        if not Xt.is_cuda or not c.is_cuda:
+            return None
+        D = ops.pad_columns(Xt[:1]).shape[1]
+        if ops.dpad_for(D, Xt.dtype) == 0:
+            return None
+        key = (c._version, Xt.dtype, D, Xt.device)
+        cached = getattr(self, "_pack_cache", None)
+        # (the cache holds the centres tensor itself: identity + version detect any change)
+        if cached is None or cached[0] is not c or cached[1] != key:
+            cached = (c, key, ops.pack_centers(c, D, Xt.dtype, Xt.device))
+            self._pack_cache = cached
+        return cached[2]
+
     def _out(self, t):
         if getattr(self, "_numpy_io", False):
             return t.cpu().numpy()
@@ -228,7 +247,7 @@ class KMeans:
 
         device = self.cluster_centers_.device
         Xt, was_numpy = _to_tensor(X, device, self.dtype)
-        labels, _ = ops.assign(Xt, self.cluster_centers_, with_dist=False)
+        labels, _ = ops.assign(Xt, self.cluster_centers_, with_dist=False, pack=self._serving_pack(Xt))
         if unassign_nonfinite:
             bad = ~torch.isfinite(Xt).all(dim=1)
             labels = labels.masked_fill(bad, -1)
@@ -250,7 +269,7 @@ class KMeans:
 
         device = self.cluster_centers_.device
         Xt, _ = _to_tensor(X, device, self.dtype)
-        _, mind = ops.assign(Xt, self.cluster_centers_, with_dist=True)
+        _, mind = ops.assign(Xt, self.cluster_centers_, with_dist=True, pack=self._serving_pack(Xt))
         if sample_weight is not None:
             mind = mind * torch.as_tensor(np.asarray(sample_weight), dtype=torch.float32, device=device)
         return -float(mind.double().sum())

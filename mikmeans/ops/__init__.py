@@ -23,6 +23,7 @@ __all__ = [
     "dpad_for",
     "vec_elems",
     "pad_columns",
+    "pack_centers",
     "row_sqnorm",
     "assign",
     "cluster_sums",
@@ -105,20 +106,31 @@ class CentroidPack:
                        track_changed, self.layout, keys)
 
 
-def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True, layout: int | None = None):
+def pack_centers(centers: torch.Tensor, D: int, dtype: torch.dtype, device, layout: int | None = None):
+    """A CentroidPack of ``centers`` for points with ``D`` (column-padded) features."""
+    cen = torch.zeros((centers.shape[0], D), dtype=torch.float32, device=device)
+    cen[:, : centers.shape[1]] = centers.to(device=device, dtype=torch.float32)
+    return CentroidPack(cen.shape[0], D, dtype, device, layout=layout).load(cen)
+
+
+def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True, layout: int | None = None,
+           pack: "CentroidPack | None" = None):
     """Nearest centroid of every row: returns ``(labels int32, sqdist float32 or None)``.
 
     bf16 points are compared against bf16-quantised centroids (scores
     accumulated in fp32 on the matrix cores); f32 points use the exact-f32 MFMA.
+    ``pack``: a CentroidPack of ``centers`` made earlier by :func:`pack_centers` for the
+    same (padded) width, dtype and device (serving: pack once, assign many batches).
     """
     if not X.is_cuda or dpad_for(pad_columns(X[:1]).shape[1], X.dtype) == 0:
         return cpu.assign(X, centers.to(X.device), with_dist=with_dist)  # CPU, or D > 256 on the GPU
     C = require()
     Xp = pad_columns(X)
     D = Xp.shape[1]
-    cen = torch.zeros((centers.shape[0], D), dtype=torch.float32, device=X.device)
-    cen[:, : centers.shape[1]] = centers.to(device=X.device, dtype=torch.float32)
-    pk = CentroidPack(cen.shape[0], D, Xp.dtype, X.device, layout=layout).load(cen)
+    if pack is not None and (pack.D, pack.dtype, pack.pack.device) == (D, Xp.dtype, Xp.device):
+        pk = pack
+    else:
+        pk = pack_centers(centers, D, Xp.dtype, X.device, layout)
     n = Xp.shape[0]
     labels = torch.empty(n, dtype=torch.int32, device=X.device)
     xn = mind = None

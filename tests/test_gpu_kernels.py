@@ -400,3 +400,21 @@ def test_wide_features_use_gemm_path(native):
     assert agree > 0.99
     assert abs(kg.inertia_ - kc.inertia_) <= 1e-3 * kc.inertia_
     assert mb.cluster_centers_.shape == (8, 300)
+
+
+def test_predict_reuses_pack_until_centres_change(native):
+    km = mikmeans.KMeans(64, dtype="bfloat16", max_iter=3).fit(
+        B.make_blobs(20000, 32, 64, seed=2, dtype=torch.bfloat16, device=DEV))
+    X = B.make_blobs(5000, 32, 64, seed=3, dtype=torch.bfloat16, device=DEV)
+    l0 = km.predict(X)
+    pk = km._pack_cache[2]
+    assert torch.equal(km.predict(X), l0) and km._pack_cache[2] is pk      # reused
+    with torch.no_grad():                                                  # in-place edit
+        km.cluster_centers_[[0, 1]] = km.cluster_centers_[[1, 0]]
+    l1 = km.predict(X)
+    assert km._pack_cache[2] is not pk
+    sw = l0.clone()
+    sw[l0 == 0], sw[l0 == 1] = 1, 0
+    assert torch.equal(l1, sw)
+    km.cluster_centers_ = km.cluster_centers_.clone()                      # new tensor
+    assert torch.equal(km.predict(X), l1) and km._pack_cache[0] is km.cluster_centers_
