@@ -80,7 +80,12 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
   const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
   char* cn_lds = smem;
   char* bufs = smem + cn_bytes;
-  const int nch = a.Kpad / (16 * C::CT);
+  // Centre split (small N): grid.y splits the chunk range; each split leaves its
+  // (value, index) in a.split_keys and split_finish_kernel writes the labels.
+  const int nch_all = a.Kpad / (16 * C::CT);
+  const int cps = (nch_all + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int c0 = (int)blockIdx.y * cps;
+  const int nch = c0 + cps < nch_all ? c0 + cps : nch_all;  // one past this split's last chunk
   const char* gC = (const char*)a.Cpack;
 
   for (int p = wid; p < cn_bytes / 1024; p += C::NW)
@@ -94,7 +99,7 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
       glds16(src + pc * 1024, (MK_LDS void*)(dst + pc * 1024));
     }
   };
-  issue_chunk(0);
+  issue_chunk(c0);
 
   const int64_t pbase = (int64_t)blockIdx.x * C::PTS + (int64_t)wid * (C::P * 16);
   u32x4 xr[C::P][C::NQ];
@@ -111,7 +116,7 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
     }
   }
   wait_vmcnt<0>();  // see assign.hip: retire the fragments before the LDS-DMA loop
-  if (C::NBUF == 3 && nch > 1) issue_chunk(1);
+  if (C::NBUF == 3 && nch > c0 + 1) issue_chunk(c0 + 1);
 
   float best[C::P], seg_best[C::P];
   int bg[C::P];
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
 
   float dbg_sink = 0.f;
   if constexpr ((DBG & 2) != 0) { wait_vmcnt<0>(); raw_barrier(); }
-  for (int c = 0; c < nch; ++c) {
+  for (int c = c0; c < nch; ++c) {
     if constexpr ((DBG & 2) == 0) {
       // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
       if (C::NBUF == 3 && c + 1 < nch) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
@@ -258,7 +263,9 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
     }
     if ((p & 3) == g) {
       const int64_t i = pbase + p * 16 + r;
-      if (i < a.N) {
+      if (a.split_keys) {
+        if (i < a.N) atomicMin(a.split_keys + i, split_key(v, k));
+      } else if (i < a.N) {
         if (a.track_changed) changed += (a.labels[i] != k);
         a.labels[i] = k;
         if (a.xn) {
@@ -269,7 +276,7 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
       }
     }
   }
-  if (a.slots) {
+  if (a.slots && !a.split_keys) {
     double di = wave_sum((double)inert);
     int dc = wave_sum(changed);
     double* red = (double*)(bufs + C::NBUF * C::CHUNK_BYTES);
@@ -284,6 +291,50 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
       atomicAdd(slot + 1, sc);
     }
   }
+}
+
+// Centre-split epilogue: labels, squared distances, inertia and changed count from the
+// per-point minimum key the splits left; resets every key for the next call.
+__global__ __launch_bounds__(256) void split_finish_kernel(AssignArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  float inert = 0.f;
+  int changed = 0;
+  if (i < a.N) {
+    const unsigned long long key = a.split_keys[i];
+    a.split_keys[i] = ~0ull;
+    const int k = (int)(unsigned)key;
+    const float v = split_value(key);
+    if (a.track_changed) changed = a.labels[i] != k;
+    a.labels[i] = k;
+    if (a.xn) {
+      const float d = fmaxf(a.xn[i] + v, 0.f);
+      inert = d;
+      if (a.mind) a.mind[i] = d;
+    }
+  }
+  if (a.slots) {
+    __shared__ double red[8];
+    const double di = wave_sum((double)inert);
+    const int dc = wave_sum(changed);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) { red[2 * w] = di; red[2 * w + 1] = (double)dc; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double* slot = a.slots + (blockIdx.x % NSLOT) * SLOT_STRIDE;
+      atomicAdd(slot + 0, red[0] + red[2] + red[4] + red[6]);
+      atomicAdd(slot + 1, red[1] + red[3] + red[5] + red[7]);
+    }
+  }
+}
+
+// Splits of the centre range for N points: enough workgroups to fill the chip when the
+// point blocks alone do not (a 1k-point batch is 4 workgroups streaming all of C).
+static int assign16_splits(int64_t nblk, int nch) {
+  if (nblk >= 1024 || nch <= 1) return 1;
+  const int64_t want = (2048 + nblk - 1) / nblk;
+  const int sp = (int)(want < nch ? want : nch);
+  const int cps = (nch + sp - 1) / sp;
+  return (nch + cps - 1) / cps;  // no empty split (the kernel's chunk range must be non-empty)
 }
 
 template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0, int NW_ = 4>
@@ -301,8 +352,13 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   }
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
   if (nblk <= 0) return hipSuccess;
-  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_>), dim3((unsigned)nblk),
-                     dim3(C::NW * 64), lds, s, a);
+  const int splits = a.split_keys ? assign16_splits(nblk, a.Kpad / (16 * C::CT)) : 1;
+  AssignArgs b = a;
+  if (splits == 1) b.split_keys = nullptr;
+  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_>),
+                     dim3((unsigned)nblk, (unsigned)splits), dim3(C::NW * 64), lds, s, b);
+  if (splits > 1)
+    hipLaunchKernelGGL(split_finish_kernel, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 

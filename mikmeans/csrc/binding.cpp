@@ -117,6 +117,10 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
                                     stream()),
               "assign_res");
   } else if (layout == 16) {
+    if (keys.has_value()) {  // all-ones u64 scratch: lets small N split the centre range
+      check_i64(*keys, "keys", N);
+      a.split_keys = (unsigned long long*)keys->data_ptr<int64_t>();
+    }
     hip_check(mk::launch_assign16(dt, (int)dpad, a, stream()), "assign16");
   } else {
     hip_check(mk::launch_assign(dt, (int)dpad, a, stream()), "assign");

@@ -99,6 +99,18 @@ __device__ __forceinline__ float min3f(float a, float b, float c) {
   return d;
 }
 
+// (score, centre) as one u64 whose unsigned order is (score, then lower index): the
+// float's bits mapped to an order-preserving u32 in the high word.
+__device__ __forceinline__ unsigned long long split_key(float v, int k) {
+  const unsigned b = __float_as_uint(v);
+  const unsigned o = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  return ((unsigned long long)o << 32) | (unsigned)k;
+}
+__device__ __forceinline__ float split_value(unsigned long long key) {
+  const unsigned o = (unsigned)(key >> 32);
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+
 // ---------------------------------------------------------------------------
 // 64-lane reductions
 __device__ __forceinline__ float wave_sum(float v) {

@@ -42,6 +42,9 @@ struct AssignArgs {
   float* mind;          // optional: squared distance to the chosen centroid
   double* slots;        // optional: [NSLOT][SLOT_STRIDE] (+inertia, +changed)
   int track_changed;
+  // assign16 only: optional u64 [N] all-ones scratch; small N then splits the centre
+  // range over grid.y (split_finish_kernel writes labels and restores the all-ones)
+  unsigned long long* split_keys = nullptr;
 };
 hipError_t launch_assign(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);

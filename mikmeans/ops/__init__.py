@@ -59,6 +59,9 @@ def row_sqnorm(X: torch.Tensor) -> torch.Tensor:
     return out
 
 
+SPLIT_MAX_ROWS = 1 << 18   # assign16 splits the centre range only below ~1024 point blocks
+
+
 class CentroidPack:
     """Centroids in the assign kernel's fragment-packed layout (see csrc/kernels.h).
 
@@ -101,6 +104,12 @@ class CentroidPack:
         if self.layout == 116 and self._C.assign_res_passes(self.dt, self.dpad, self.Kpad) > 1:
             if self._keys is None or self._keys.numel() < X.shape[0]:
                 self._keys = torch.empty(max(X.shape[0], 1), dtype=torch.int64, device=X.device)
+            keys = self._keys
+        elif self.layout == 16 and 0 < X.shape[0] <= SPLIT_MAX_ROWS:
+            # small batches split the centre range across workgroups (assign16 grid.y);
+            # the kernels leave the scratch all-ones again, so it is filled only once
+            if self._keys is None or self._keys.numel() < X.shape[0]:
+                self._keys = torch.full((X.shape[0],), -1, dtype=torch.int64, device=X.device)
             keys = self._keys
         self._C.assign(X, self.pack, self.cn, xn, labels, mind, slots, self.Kpad, self.dpad,
                        track_changed, self.layout, keys)

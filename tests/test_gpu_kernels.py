@@ -418,3 +418,35 @@ def test_predict_reuses_pack_until_centres_change(native):
     assert torch.equal(l1, sw)
     km.cluster_centers_ = km.cluster_centers_.clone()                      # new tensor
     assert torch.equal(km.predict(X), l1) and km._pack_cache[0] is km.cluster_centers_
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("n,d,k", [(1, 128, 1024), (1000, 128, 1024), (16384, 64, 4096), (3000, 256, 512),
+                                   (70000, 32, 300), (5000, 128, 70)])
+def test_assign_centre_split_small_batches(native, dtype, n, d, k):
+    """Small batches split the centre range over workgroups; labels, distances and the
+    inertia / changed counters equal the one-pass kernel's, calls reuse the scratch."""
+    X = _points(n, d, dtype, seed=n + k)
+    C = _points(k, d, torch.float32, seed=k + 11)
+    Xp = ops.pad_columns(X.to(DEV))
+    pk = ops.pack_centers(C.to(DEV), Xp.shape[1], Xp.dtype, DEV, layout=16)
+    assert n <= ops.SPLIT_MAX_ROWS
+    xn = ops.row_sqnorm(Xp)
+    res = []
+    for split in (False, True, True):
+        lab = torch.full((n,), 7, dtype=torch.int32, device=DEV)
+        mind = torch.empty(n, dtype=torch.float32, device=DEV)
+        slots = torch.zeros(native.NSLOT * native.SLOT_STRIDE, dtype=torch.float64, device=DEV)
+        if split:
+            pk.assign(Xp, xn, lab, mind, slots, True)
+        else:
+            native.assign(Xp, pk.pack, pk.cn, xn, lab, mind, slots, pk.Kpad, pk.dpad, True, 16, None)
+        s = slots.view(native.NSLOT, native.SLOT_STRIDE).sum(0)
+        res.append((lab.cpu(), mind.cpu(), float(s[0]), float(s[1])))
+    assert int((pk._keys[:n] != -1).sum()) == 0          # scratch restored to all-ones
+    for lab, mind, inert, changed in res[1:]:
+        assert torch.equal(lab, res[0][0])
+        assert torch.equal(mind, res[0][1])
+        assert changed == res[0][3] == float((res[0][0] != 7).sum())
+        assert inert == pytest.approx(res[0][2], rel=1e-6)
+    _check_assign(X, C, res[1][0], res[1][1], rel=2e-5 if dtype == torch.float32 else 3e-5)
