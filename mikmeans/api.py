@@ -59,7 +59,47 @@ def _shard_info(n_local: int, comm: Comm, device):
     return int(sizes.sum()), start
 
 
-class KMeans:
+class _Serving:
+    """Inference surface shared by KMeans and MiniBatchKMeans (fitted ``cluster_centers_``)."""
+
+    def _serving_pack(self, Xt):
+        """The fitted centres packed for the assign kernel, built once and reused by every
+        predict/score call until the centres change (serving: one kernel launch per batch)."""
+        from . import ops
+
+        c = self.cluster_centers_
+        if not Xt.is_cuda or not c.is_cuda:
+            return None
+        D = ops.pad_columns(Xt[:1]).shape[1]
+        if ops.dpad_for(D, Xt.dtype) == 0:
+            return None
+        key = (c._version, Xt.dtype, D, Xt.device)
+        cached = getattr(self, "_pack_cache", None)
+        # (the cache holds the centres tensor itself: identity + version detect any change)
+        if cached is None or cached[0] is not c or cached[1] != key:
+            cached = (c, key, ops.pack_centers(c, D, Xt.dtype, Xt.device))
+            self._pack_cache = cached
+        return cached[2]
+
+    def transform(self, X):
+        """Euclidean distances to every centre, ``[n, K]`` (float32)."""
+        self._check_fitted()
+        device = self.cluster_centers_.device
+        Xt, was_numpy = _to_tensor(X, device, self.dtype)
+        c = cpu_ops.quantize_centers(self.cluster_centers_, self.dtype)
+        d = torch.cdist(Xt.to(torch.float32), c)
+        return d.cpu().numpy() if was_numpy else d
+
+    def fit_transform(self, X, *args, **kw):
+        """``fit(X)`` then the distances of ``X`` to the fitted centres."""
+        return self.fit(X, *args, **kw).transform(X)
+
+    def _check_fitted(self):
+        if not hasattr(self, "cluster_centers_"):
+            raise RuntimeError(f"{type(self).__name__} instance is not fitted yet; call fit() first")
+
+
+class KMeans(_Serving):
     """Lloyd k-means on MI355X (full batch, data-parallel over ranks)."""
 
     def __init__(self, n_clusters: int = 8, *, init="k-means++", n_init: int = 1, max_iter: int = 300,
@@ -210,29 +250,6 @@ class KMeans:
         self.history_ = []
         return self
 
-    def _check_fitted(self):
-        if not hasattr(self, "cluster_centers_"):
-            raise RuntimeError("KMeans instance is not fitted yet; call fit() first")
-
-    def _serving_pack(self, Xt):
-        """The fitted centres packed for the assign kernel, built once and reused by every
-        predict/score call until the centres change (serving: one kernel launch per batch)."""
-        from . import ops
-
-        c = self.cluster_centers_
-        if not Xt.is_cuda or not c.is_cuda:
-            return None
-        D = ops.pad_columns(Xt[:1]).shape[1]
-        if ops.dpad_for(D, Xt.dtype) == 0:
-            return None
-        key = (c._version, Xt.dtype, D, Xt.device)
-        cached = getattr(self, "_pack_cache", None)
-        # (the cache holds the centres tensor itself: identity + version detect any change)
-        if cached is None or cached[0] is not c or cached[1] != key:
-            cached = (c, key, ops.pack_centers(c, D, Xt.dtype, Xt.device))
-            self._pack_cache = cached
-        return cached[2]
-
     def _out(self, t):
         if getattr(self, "_numpy_io", False):
             return t.cpu().numpy()
@@ -252,15 +269,6 @@ class KMeans:
             bad = ~torch.isfinite(Xt).all(dim=1)
             labels = labels.masked_fill(bad, -1)
         return labels.cpu().numpy() if was_numpy else labels
-
-    def transform(self, X):
-        """Euclidean distances to every centre, ``[n, K]`` (float32)."""
-        self._check_fitted()
-        device = self.cluster_centers_.device
-        Xt, was_numpy = _to_tensor(X, device, self.dtype)
-        c = cpu_ops.quantize_centers(self.cluster_centers_, self.dtype)
-        d = torch.cdist(Xt.to(torch.float32), c)
-        return d.cpu().numpy() if was_numpy else d
 
     def score(self, X, sample_weight=None):
         """Negative inertia of ``X`` under the fitted centres."""
@@ -310,7 +318,7 @@ class KMeans:
         return km
 
 
-class MiniBatchKMeans:
+class MiniBatchKMeans(_Serving):
     """Mini-batch k-means (Sculley 2010) over tensors or device-generated streams."""
 
     def __init__(self, n_clusters: int = 8, *, batch_size: int = 1024, max_iter: int = 100,
@@ -400,15 +408,20 @@ class MiniBatchKMeans:
     def predict(self, X):
         from . import ops
 
+        self._check_fitted()
         Xt, was_numpy = _to_tensor(X, self.cluster_centers_.device, self.dtype)
-        labels, _ = ops.assign(Xt, self.cluster_centers_, with_dist=False)
+        labels, _ = ops.assign(Xt, self.cluster_centers_, with_dist=False, pack=self._serving_pack(Xt))
         return labels.cpu().numpy() if was_numpy else labels
+
+    def fit_predict(self, X):
+        return self.fit(X).predict(X)
 
     def score(self, X):
         from . import ops
 
+        self._check_fitted()
         Xt, _ = _to_tensor(X, self.cluster_centers_.device, self.dtype)
-        _, mind = ops.assign(Xt, self.cluster_centers_, with_dist=True)
+        _, mind = ops.assign(Xt, self.cluster_centers_, with_dist=True, pack=self._serving_pack(Xt))
         return -float(mind.double().sum())
 
 

@@ -59,6 +59,11 @@ def test_kmeans_methods_and_metrics():
     m = km.metrics()
     assert m["k"] == 5 and sum(m["counts"]) == 3000 and m["balance"]["gap"] == max(m["counts"]) - min(m["counts"])
     assert km.n_iter_ >= 1 and km.converged_
+    ft = mikmeans.KMeans(5, device="cpu", seed=0).fit_transform(X)
+    assert ft.shape == (3000, 5)
+    torch.testing.assert_close(ft.argmin(1).to(torch.int32), km.predict(X))
+    with pytest.raises(RuntimeError, match="not fitted"):
+        mikmeans.MiniBatchKMeans(3).predict(X)
 
 
 def test_sample_weight_matches_sklearn():
@@ -125,6 +130,10 @@ def test_minibatch_cpu_converges():
     full = mikmeans.KMeans(6, device="cpu", seed=0).fit(X)
     assert mb.score(X) >= 1.05 * full.score(X)   # scores are negative inertias
     assert mb.n_steps_ > 0 and float(mb.counts_.sum()) == pytest.approx(mb.n_steps_ * 1024)
+    lab = mb.predict(X)
+    torch.testing.assert_close(mb.transform(X).argmin(1).to(torch.int32), lab)
+    mb2 = mikmeans.MiniBatchKMeans(6, batch_size=1024, max_iter=5, device="cpu", seed=0)
+    assert torch.equal(mb2.fit_predict(X), lab)
 
 
 def test_minibatch_partial_fit_stream():
