@@ -428,6 +428,16 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
       default: break;
     }
   }
+  if constexpr (sizeof(T) == 2 && DPAD == 256) {  // cfg5 shape (P=2 default, 8 KiB tiles)
+    switch (g_assign16_cfg) {
+      case 70: return launch16_t<T, DPAD, 3, 1, 2, 2, 32>(a, s);  // 3 point blocks, 3 waves/SIMD
+      case 71: return launch16_t<T, DPAD, 4, 1, 2, 2>(a, s);      // 4 point blocks, 2 waves/SIMD
+      case 72: return launch16_t<T, DPAD, 3, 1, 1, 3, 32>(a, s);
+      case 73: return launch16_t<T, DPAD, 2, 1, 1, 3, 16>(a, s);
+      case 74: return launch16_t<T, DPAD, 4, 1, 1, 3>(a, s);
+      default: break;
+    }
+  }
 #else
   if (g_assign16_cfg != 0) return hipErrorNotSupported;  // variant knob needs an A/B build
 #endif
