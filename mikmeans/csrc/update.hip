@@ -192,7 +192,7 @@ __device__ void upd_flush_all(const UpdateArgs& a, const UpdLayout& L, char* m, 
   }
 }
 
-enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8 };
+enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8, UPD_NTLOAD = 16 };
 
 constexpr int upd_ksh(int np) { return np >= 32 ? 0 : np == 16 ? 1 : np == 8 ? 2 : np == 4 ? 3 : np == 2 ? 4 : 5; }
 __host__ __device__ static inline size_t upd_lds_bytes(int K, int ldc, bool weighted) {
@@ -210,6 +210,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   constexpr bool DELTA = MODE & UPD_DELTA;
   constexpr bool W = MODE & (UPD_WEIGHTED | UPD_DELTA);  // per-row signed weights
   constexpr bool SWZ = MODE & UPD_SWZ;
+  constexpr bool NTL = MODE & UPD_NTLOAD;                // non-temporal X stream (A/B)
   constexpr int ES = sizeof(T);
   constexpr int PB = (SW * ES >= 16) ? 16 : SW * ES;  // bytes per lane load
   constexpr int V = PB / ES;                           // elements per lane load (even)
@@ -298,7 +299,8 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
         lab_[u] = ((unsigned)l < (unsigned)a.K) ? l : a.K;
         if constexpr (DELTA) wt_[u] = wrow ? wrow[off + u] : 1.f;
         else if constexpr (W) wt_[u] = wrow[off + u];
-        w_[u] = *(const LT*)(p + u * a.ldx);
+        if constexpr (NTL) w_[u] = __builtin_nontemporal_load((const LT*)(p + u * a.ldx));
+        else w_[u] = *(const LT*)(p + u * a.ldx);
       }
     } else {                                           // clamp rows past the chunk -> sink row K
 #pragma unroll
@@ -528,6 +530,8 @@ static hipError_t launch_sw(const UpdateArgs& a, int ldc, hipStream_t s) {
       case 1032: return launch_nt<T, SW, MODE, 1024, 8, 256>(a, ldc, s);   // 1 row per lane
       case 1033: return launch_nt<T, SW, MODE, 1024, 12, 256>(a, ldc, s);
       case 1034: return launch_nt<T, SW, MODE, 1024, 6, 256>(a, ldc, s);
+      case 2030: return launch_nt<T, SW, UPD_NTLOAD, 1024, 6, 512>(a, ldc, s);  // default + nt loads
+      case 2031: return launch_nt<T, SW, UPD_NTLOAD, 1024, 8, 512>(a, ldc, s);
       default: break;
     }
   }
