@@ -108,7 +108,8 @@ class KMeans(_Serving):
                  empty_cluster: str = "keep", check_every: int = 1, n_local_trials=None,
                  verbose: int = 0, mode: str = "learn", run_id: str | None = None,
                  checkpoint_every: int = 0, checkpoint_dir: str | None = None, metrics_path: str | None = None,
-                 graph: bool = False, incremental: bool = True):
+                 graph: bool = False, incremental: bool = True, chunk_rows: int | None = None,
+                 init_size: int | None = None):
         self.n_clusters = int(n_clusters)
         self.init = init
         self.n_init = int(n_init)
@@ -130,6 +131,10 @@ class KMeans(_Serving):
         self.metrics_path = metrics_path
         self.graph = bool(graph)
         self.incremental = bool(incremental)
+        # out-of-core fits (models/streaming.py): X stays in host memory and streams through
+        # the GPU in chunks of `chunk_rows`; the init (and tol scale) use `init_size` rows
+        self.chunk_rows = int(chunk_rows) if chunk_rows else None
+        self.init_size = init_size
         self.history_: list[dict] = []
 
     # ---------------------------------------------------------------- config
@@ -141,7 +146,7 @@ class KMeans(_Serving):
                    n_local_trials=cfg.n_local_trials, verbose=cfg.verbose, mode=cfg.mode,
                    run_id=cfg.run_id, checkpoint_every=cfg.checkpoint_every,
                    checkpoint_dir=cfg.checkpoint_dir, metrics_path=cfg.metrics_path, graph=cfg.graph,
-                   incremental=cfg.incremental, **kw)
+                   incremental=cfg.incremental, chunk_rows=cfg.chunk_rows, **kw)
 
     def get_config(self) -> KMeansConfig:
         return KMeansConfig(n_clusters=self.n_clusters, init=self.init if isinstance(self.init, str) else "array",
@@ -152,13 +157,14 @@ class KMeans(_Serving):
                             n_local_trials=self.n_local_trials, mode=self.mode, run_id=self.run_id,
                             verbose=self.verbose, checkpoint_every=self.checkpoint_every,
                             checkpoint_dir=self.checkpoint_dir, metrics_path=self.metrics_path,
-                            graph=self.graph, incremental=self.incremental)
+                            graph=self.graph, incremental=self.incremental, chunk_rows=self.chunk_rows)
 
     # ------------------------------------------------------------------- fit
     def fit(self, X, y=None, sample_weight=None, *, resume_from=None):
         comm = self.comm or get_comm()
         device = _default_device(self.device, X) if self.device is not None or comm.world == 1 else comm.device
-        Xt, was_numpy = _to_tensor(X, device, self.dtype)
+        streaming = self.chunk_rows is not None and device.type == "cuda"
+        Xt, was_numpy = _to_tensor(X, torch.device("cpu") if streaming else device, self.dtype)
         self._numpy_io = was_numpy
         D = Xt.shape[1]
         if Xt.is_cuda:
@@ -168,21 +174,44 @@ class KMeans(_Serving):
             raise ValueError(f"n_samples={n_global} should be >= n_clusters={self.n_clusters}")
         w = None
         if sample_weight is not None:
+            if streaming:
+                raise NotImplementedError("sample_weight with chunk_rows (out-of-core) is not supported")
             w = torch.as_tensor(np.asarray(sample_weight) if not torch.is_tensor(sample_weight)
                                 else sample_weight, dtype=torch.float32).to(device)
-        tol_abs = tol_to_abs(self.tol, Xt[:, :D] if Xt.shape[1] != D else Xt, comm, n_global)
+        Xs = None
+        if streaming:
+            from .models.streaming import StreamingLloydEngine
+
+            if self.empty_cluster != "keep":
+                raise NotImplementedError("chunk_rows (out-of-core) supports empty_cluster='keep' only")
+            sengine = StreamingLloydEngine(Xt, self.n_clusters, chunk_rows=self.chunk_rows, comm=comm,
+                                           device=device, frozen=self.frozen, n_features=D)
+            # init + tol scale on a device-resident sample of every rank's rows
+            m = self.init_size or max(20 * self.n_clusters, 1 << 16)
+            Xs = sengine.sample_rows(m, self.seed)
+            s_global, s_start = _shard_info(Xs.shape[0], comm, device)
+        tol_src = Xs if streaming else Xt
+        tol_abs = tol_to_abs(self.tol, tol_src[:, :D] if tol_src.shape[1] != D else tol_src, comm,
+                             s_global if streaming else n_global)
         best = None
         t0 = time.perf_counter()
         start_iter = 0
         for trial in range(max(1, self.n_init)):
-            eng = LloydEngine(Xt, self.n_clusters, comm=comm, sample_weight=w, frozen=self.frozen,
-                              empty_policy=self.empty_cluster, n_features=D, incremental=self.incremental)
+            if streaming:
+                eng = sengine
+                eng.reset_labels()
+            else:
+                eng = LloydEngine(Xt, self.n_clusters, comm=comm, sample_weight=w, frozen=self.frozen,
+                                  empty_policy=self.empty_cluster, n_features=D, incremental=self.incremental)
             if resume_from is not None and trial == 0:
                 from .utils.checkpoint import load_checkpoint
 
                 ck = load_checkpoint(resume_from, comm=comm)
                 centers = ck["centers"].to(device)
                 start_iter = int(ck["iteration"])
+            elif streaming:
+                centers = resolve_init(self.init, Xs, D, self.n_clusters, s_global, s_start, comm,
+                                       self.seed + trial, self.n_local_trials)
             else:
                 centers = resolve_init(self.init, Xt, D, self.n_clusters, n_global, start, comm,
                                        self.seed + trial, self.n_local_trials)
@@ -223,9 +252,11 @@ class KMeans(_Serving):
             inertia = float(inert.item())
             if best is None or inertia < best[0]:
                 best = (inertia, eng, labels, n_iter, converged, hist)
-        inertia, eng, labels, n_iter, converged, hist = best
+                if streaming:   # the engine is reused by the next trial: keep this one's centres
+                    best = best + (eng.centers.clone(),)
+        inertia, eng, labels, n_iter, converged, hist = best[:6]
         self._engine = eng
-        self.cluster_centers_ = eng.centers.clone()
+        self.cluster_centers_ = best[6] if streaming else eng.centers.clone()
         self.labels_ = labels
         self.inertia_ = inertia
         self.n_iter_ = n_iter

@@ -58,6 +58,7 @@ class KMeansConfig:
     metrics_path: str | None = None  # per-iteration JSONL (rank 0)
     graph: bool = False              # replay each Lloyd iteration as one captured hipGraph
     incremental: bool = True         # M-step re-scatters only rows whose label changed (exact)
+    chunk_rows: int | None = None    # out-of-core: keep X on the host, stream it in chunks of rows
 
     def to_dict(self):
         return asdict(self)
@@ -76,7 +77,7 @@ class KMeansConfig:
                 # --flag / --no-flag (a default-on switch must be switchable off)
                 ap.add_argument(flag, action=argparse.BooleanOptionalAction, default=default)
             elif default is None:
-                typ = int if f.name == "n_local_trials" else str
+                typ = int if f.name in ("n_local_trials", "chunk_rows") else str
                 ap.add_argument(flag, type=typ, default=None)
             else:
                 ap.add_argument(flag, type=type(default), default=default)

@@ -186,3 +186,12 @@ def test_bf16_cpu_path_quantises_like_kernel():
     km = mikmeans.KMeans(4, dtype="bfloat16", device="cpu", seed=0).fit(X)
     assert km.cluster_centers_.dtype == torch.float32
     assert np.isfinite(km.inertia_)
+
+
+def test_chunk_rows_on_cpu_is_the_resident_fit():
+    # out-of-core streaming needs a GPU; on the CPU the option leaves the fit unchanged
+    X, _ = blobs(4000, 6, 5, seed=3)
+    a = mikmeans.KMeans(5, device="cpu", seed=0).fit(X)
+    b = mikmeans.KMeans(5, device="cpu", seed=0, chunk_rows=512).fit(X)
+    assert torch.equal(a.cluster_centers_, b.cluster_centers_)
+    assert b.get_config().chunk_rows == 512

@@ -450,3 +450,38 @@ def test_assign_centre_split_small_batches(native, dtype, n, d, k):
         assert changed == res[0][3] == float((res[0][0] != 7).sum())
         assert inert == pytest.approx(res[0][2], rel=1e-6)
     _check_assign(X, C, res[1][0], res[1][1], rel=2e-5 if dtype == torch.float32 else 3e-5)
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_streaming_fit_matches_resident(native, dtype):
+    """Out-of-core Lloyd (host rows streamed in chunks, copy/compute overlap) gives the
+    device-resident fit's centres and labels bit for bit (integer M-step, same scales)."""
+    X = B.make_blobs(50_000, 60, 32, seed=21, dtype=torch.float32, device=DEV)
+    C0 = X[:32].cpu()
+    ref = mikmeans.KMeans(32, init=C0, dtype=dtype, max_iter=6, tol=0, device=DEV).fit(X)
+    st = mikmeans.KMeans(32, init=C0, dtype=dtype, max_iter=6, tol=0, device=DEV, chunk_rows=7_000).fit(X.cpu())
+    from mikmeans.models.streaming import StreamingLloydEngine
+
+    assert isinstance(st._engine, StreamingLloydEngine) and len(st._engine.ranges) == 8
+    assert st.n_iter_ == ref.n_iter_
+    assert torch.equal(st.cluster_centers_, ref.cluster_centers_)
+    assert torch.equal(st.labels_, ref.labels_)
+    assert st.inertia_ == pytest.approx(ref.inertia_, rel=1e-9)
+    torch.testing.assert_close(st.predict(X), ref.predict(X))
+
+
+def test_streaming_fit_kmeanspp_sample_init(native):
+    # k-means++ runs on a device-resident sample of init_size rows (seeded, sorted draw);
+    # the resident fit started from the same seeding must give the same model
+    from mikmeans.models.init import resolve_init
+    from mikmeans.parallel import Comm
+
+    X = B.make_blobs(40_000, 32, 16, seed=5, dtype=torch.bfloat16, device="cpu")
+    km = mikmeans.KMeans(16, dtype="bfloat16", max_iter=20, device=DEV, chunk_rows=1 << 13,
+                         init_size=4096).fit(X)
+    idx = torch.randperm(40_000, generator=torch.Generator().manual_seed(0))[:4096].sort().values
+    C0 = resolve_init("k-means++", X[idx].to(DEV), 32, 16, 4096, 0, Comm.local(torch.device(DEV)), 0)
+    ref = mikmeans.KMeans(16, init=C0.cpu(), dtype="bfloat16", max_iter=20, device=DEV).fit(X.to(DEV))
+    assert km.labels_.is_cuda and km.labels_.shape == (40_000,)
+    assert torch.equal(km.cluster_centers_, ref.cluster_centers_)
+    assert km.n_iter_ == ref.n_iter_
