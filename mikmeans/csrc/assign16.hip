@@ -86,11 +86,12 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
   const int cps = (nch_all + (int)gridDim.y - 1) / (int)gridDim.y;
   const int c0 = (int)blockIdx.y * cps;
   const int nch = c0 + cps < nch_all ? c0 + cps : nch_all;  // one past this split's last chunk
-  const char* gC = (const char*)a.Cpack;
+  const int ncl = nch - c0;                                    // chunks of this split
+  const char* gC = (const char*)a.Cpack + (int64_t)c0 * C::CHUNK_BYTES;
 
   for (int p = wid; p < cn_bytes / 1024; p += C::NW)
     glds16((const char*)a.cn + p * 1024 + lane * 16, (MK_LDS void*)(cn_lds + p * 1024));
-  auto issue_chunk = [&](int c) {
+  auto issue_chunk = [&](int c) {  // c: chunk index within this split (ring slot c % NBUF)
     const char* src = gC + (int64_t)c * C::CHUNK_BYTES + lane * 16;
     char* dst = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
 #pragma unroll
@@ -99,7 +100,7 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
       glds16(src + pc * 1024, (MK_LDS void*)(dst + pc * 1024));
     }
   };
-  issue_chunk(c0);
+  issue_chunk(0);
 
   const int64_t pbase = (int64_t)blockIdx.x * C::PTS + (int64_t)wid * (C::P * 16);
   u32x4 xr[C::P][C::NQ];
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
     }
   }
   wait_vmcnt<0>();  // see assign.hip: retire the fragments before the LDS-DMA loop
-  if (C::NBUF == 3 && nch > c0 + 1) issue_chunk(c0 + 1);
+  if (C::NBUF == 3 && ncl > 1) issue_chunk(1);
 
   float best[C::P], seg_best[C::P];
   int bg[C::P];
@@ -127,13 +128,13 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
 
   float dbg_sink = 0.f;
   if constexpr ((DBG & 2) != 0) { wait_vmcnt<0>(); raw_barrier(); }
-  for (int c = c0; c < nch; ++c) {
+  for (int c = 0; c < ncl; ++c) {
     if constexpr ((DBG & 2) == 0) {
       // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
-      if (C::NBUF == 3 && c + 1 < nch) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
+      if (C::NBUF == 3 && c + 1 < ncl) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
       wait_lgkm0();
       raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
-      if (c + C::NBUF - 1 < nch) issue_chunk(c + C::NBUF - 1);
+      if (c + C::NBUF - 1 < ncl) issue_chunk(c + C::NBUF - 1);
     }
     const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
     // DBG & 64 / 128: LLVM's MFMA/DS interleaving strategies for the chunk body (A/B)
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
     if constexpr ((DBG & 128) != 0) __builtin_amdgcn_iglp_opt(1);
     // A fragments + |c|^2 of one tile from the LDS ring
     auto load_tile = [&](int tl_i, u32x4* aw_, f32x4& ci_) {
-      const int tile = c * C::CT + tl_i;
+      const int tile = (c0 + c) * C::CT + tl_i;
       ci_ = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
       const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
 #pragma unroll
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
             acc[p][t] = Mfma16<T>::run(aw[q], xr[p][q], q == 0 ? ci : acc[p][t]);
         }
       }
-      const int grp = c * (C::CT / GT) + tg;
+      const int grp = (c0 + c) * (C::CT / GT) + tg;
       if constexpr ((DBG & 1) != 0) {
 #pragma unroll
         for (int p = 0; p < C::P; ++p) dbg_sink += acc[p][0][0];
