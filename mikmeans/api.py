@@ -53,6 +53,15 @@ def _to_tensor(X, device, dtype):
     return t, was_numpy
 
 
+def _unit_rows(X: torch.Tensor, block: int = 1 << 22) -> torch.Tensor:
+    """Rows scaled to unit L2 norm (f32 arithmetic, result in X's dtype; zero rows stay 0)."""
+    out = torch.empty_like(X)
+    for i in range(0, X.shape[0], block):
+        xb = X[i : i + block].to(torch.float32)
+        out[i : i + block] = (xb / xb.norm(dim=1, keepdim=True).clamp_min(1e-30)).to(X.dtype)
+    return out
+
+
 def _shard_info(n_local: int, comm: Comm, device):
     sizes = comm.all_gather(torch.tensor([n_local], dtype=torch.int64, device=device)).reshape(-1).cpu()
     start = int(sizes[: comm.rank].sum())
@@ -81,11 +90,18 @@ class _Serving:
             self._pack_cache = cached
         return cached[2]
 
+    def _inputs(self, X):
+        """X on the model's device and dtype; unit rows for the cosine metric."""
+        Xt, was_numpy = _to_tensor(X, self.cluster_centers_.device, self.dtype)
+        if getattr(self, "metric", "euclidean") == "cosine":
+            Xt = _unit_rows(Xt)
+        return Xt, was_numpy
+
     def transform(self, X):
-        """Euclidean distances to every centre, ``[n, K]`` (float32)."""
+        """Euclidean distances to every centre, ``[n, K]`` (float32; for the cosine
+        metric, between unit rows and unit centres: sqrt(2 - 2 cos))."""
         self._check_fitted()
-        device = self.cluster_centers_.device
-        Xt, was_numpy = _to_tensor(X, device, self.dtype)
+        Xt, was_numpy = self._inputs(X)
         c = cpu_ops.quantize_centers(self.cluster_centers_, self.dtype)
         d = torch.cdist(Xt.to(torch.float32), c)
         return d.cpu().numpy() if was_numpy else d
@@ -109,7 +125,7 @@ class KMeans(_Serving):
                  verbose: int = 0, mode: str = "learn", run_id: str | None = None,
                  checkpoint_every: int = 0, checkpoint_dir: str | None = None, metrics_path: str | None = None,
                  graph: bool = False, incremental: bool = True, chunk_rows: int | None = None,
-                 init_size: int | None = None):
+                 init_size: int | None = None, metric: str = "euclidean"):
         self.n_clusters = int(n_clusters)
         self.init = init
         self.n_init = int(n_init)
@@ -134,6 +150,10 @@ class KMeans(_Serving):
         # out-of-core fits (models/streaming.py): X stays in host memory and streams through
         # the GPU in chunks of `chunk_rows`; the init (and tol scale) use `init_size` rows
         self.chunk_rows = int(chunk_rows) if chunk_rows else None
+        if metric not in ("euclidean", "cosine"):
+            raise ValueError(f"metric must be 'euclidean' or 'cosine', got {metric!r}")
+        # cosine = spherical k-means: unit rows, centres re-normalised after every M-step
+        self.metric = metric
         self.init_size = init_size
         self.history_: list[dict] = []
 
@@ -146,7 +166,7 @@ class KMeans(_Serving):
                    n_local_trials=cfg.n_local_trials, verbose=cfg.verbose, mode=cfg.mode,
                    run_id=cfg.run_id, checkpoint_every=cfg.checkpoint_every,
                    checkpoint_dir=cfg.checkpoint_dir, metrics_path=cfg.metrics_path, graph=cfg.graph,
-                   incremental=cfg.incremental, chunk_rows=cfg.chunk_rows, **kw)
+                   incremental=cfg.incremental, chunk_rows=cfg.chunk_rows, metric=cfg.metric, **kw)
 
     def get_config(self) -> KMeansConfig:
         return KMeansConfig(n_clusters=self.n_clusters, init=self.init if isinstance(self.init, str) else "array",
@@ -157,7 +177,8 @@ class KMeans(_Serving):
                             n_local_trials=self.n_local_trials, mode=self.mode, run_id=self.run_id,
                             verbose=self.verbose, checkpoint_every=self.checkpoint_every,
                             checkpoint_dir=self.checkpoint_dir, metrics_path=self.metrics_path,
-                            graph=self.graph, incremental=self.incremental, chunk_rows=self.chunk_rows)
+                            graph=self.graph, incremental=self.incremental, chunk_rows=self.chunk_rows,
+                            metric=self.metric)
 
     # ------------------------------------------------------------------- fit
     def fit(self, X, y=None, sample_weight=None, *, resume_from=None):
@@ -166,6 +187,10 @@ class KMeans(_Serving):
         streaming = self.chunk_rows is not None and device.type == "cuda"
         Xt, was_numpy = _to_tensor(X, torch.device("cpu") if streaming else device, self.dtype)
         self._numpy_io = was_numpy
+        if self.metric == "cosine":
+            if streaming:
+                raise NotImplementedError("metric='cosine' with chunk_rows (out-of-core) is not supported")
+            Xt = _unit_rows(Xt)
         D = Xt.shape[1]
         if Xt.is_cuda:
             Xt = pad_columns(Xt)
@@ -202,7 +227,8 @@ class KMeans(_Serving):
                 eng.reset_labels()
             else:
                 eng = LloydEngine(Xt, self.n_clusters, comm=comm, sample_weight=w, frozen=self.frozen,
-                                  empty_policy=self.empty_cluster, n_features=D, incremental=self.incremental)
+                                  empty_policy=self.empty_cluster, n_features=D, incremental=self.incremental,
+                                  spherical=self.metric == "cosine")
             if resume_from is not None and trial == 0:
                 from .utils.checkpoint import load_checkpoint
 
@@ -293,8 +319,7 @@ class KMeans(_Serving):
         self._check_fitted()
         from . import ops
 
-        device = self.cluster_centers_.device
-        Xt, was_numpy = _to_tensor(X, device, self.dtype)
+        Xt, was_numpy = self._inputs(X)
         labels, _ = ops.assign(Xt, self.cluster_centers_, with_dist=False, pack=self._serving_pack(Xt))
         if unassign_nonfinite:
             bad = ~torch.isfinite(Xt).all(dim=1)
@@ -307,7 +332,7 @@ class KMeans(_Serving):
         from . import ops
 
         device = self.cluster_centers_.device
-        Xt, _ = _to_tensor(X, device, self.dtype)
+        Xt, _ = self._inputs(X)
         _, mind = ops.assign(Xt, self.cluster_centers_, with_dist=True, pack=self._serving_pack(Xt))
         if sample_weight is not None:
             mind = mind * torch.as_tensor(np.asarray(sample_weight), dtype=torch.float32, device=device)

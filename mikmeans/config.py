@@ -59,6 +59,7 @@ class KMeansConfig:
     graph: bool = False              # replay each Lloyd iteration as one captured hipGraph
     incremental: bool = True         # M-step re-scatters only rows whose label changed (exact)
     chunk_rows: int | None = None    # out-of-core: keep X on the host, stream it in chunks of rows
+    metric: str = "euclidean"        # euclidean | cosine (spherical k-means on unit rows)
 
     def to_dict(self):
         return asdict(self)

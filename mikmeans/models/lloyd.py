@@ -72,7 +72,8 @@ class LloydEngine:
     def __init__(self, X: torch.Tensor, n_clusters: int, *, comm: Comm | None = None,
                  sample_weight: torch.Tensor | None = None, frozen=None,
                  empty_policy: str = "keep", n_features: int | None = None, segments: int = 1,
-                 overlap_sw: int = 8, incremental: bool = False, delta_cap: float = 0.125):
+                 overlap_sw: int = 8, incremental: bool = False, delta_cap: float = 0.125,
+                 spherical: bool = False):
         from ..ops import pad_columns
 
         # Incremental M-step: keep per-rank integer running totals of the cluster sums and
@@ -81,6 +82,9 @@ class LloydEngine:
         # automatically while more than ``delta_cap * n`` rows change.
         self.incremental = bool(incremental)
         self.delta_cap = float(delta_cap)
+        # spherical k-means (cosine metric on unit-norm rows): every M-step's centres are
+        # projected back onto the unit sphere and re-packed for the next E-step
+        self.spherical = bool(spherical)
         self.segments = max(1, int(segments))
         self.overlap_sw = overlap_sw
         self.comm = comm or Comm.local(X.device)
@@ -187,6 +191,8 @@ class LloydEngine:
         c = centers.to(device=self.device, dtype=torch.float32)
         if c.shape != (self.K, self.D):
             raise ValueError(f"centers must be [{self.K}, {self.D}], got {tuple(c.shape)}")
+        if self.spherical:
+            c = c / c.norm(dim=1, keepdim=True).clamp_min(1e-30)
         self.C.zero_()
         self.C[:, : self.D] = c
         if self.gpu:
@@ -206,8 +212,12 @@ class LloydEngine:
             self._gphase ^= 1
         elif self.gpu:
             self._step_gpu()
+            if self.spherical:
+                self._project_sphere()
         else:
             self._step_cpu()
+            if self.spherical:
+                self._project_sphere()
         self.C, self.Cnew = self.Cnew, self.C
         self.iteration += 1
 
@@ -233,6 +243,8 @@ class LloydEngine:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=side):
                 self._step_gpu()
+                if self.spherical:
+                    self._project_sphere()
             graphs.append(g)
             self.C, self.Cnew = self.Cnew, self.C
         # the warm-up changed labels / slots: restore the pre-capture state
@@ -280,6 +292,15 @@ class LloydEngine:
         with _phase("mikmeans.finalize"):
             self._relocate_empty()
             self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts)
+
+    def _project_sphere(self):
+        """Cnew <- Cnew / |Cnew| (empty / frozen rows are already unit or kept), then the
+        shift against the previous centres and the packed copy for the next E-step."""
+        Cn = self.Cnew[:, : self.D]
+        Cn.div_(Cn.norm(dim=1, keepdim=True).clamp_min(1e-30))
+        torch.sum((self.Cnew - self.C) ** 2, dim=1, out=self.shift)
+        if self.gpu:
+            self.pk.finalize(0, None, self.Cnew)
 
     def _assign_update_overlapped(self):
         C = self._C

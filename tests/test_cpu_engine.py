@@ -195,3 +195,36 @@ def test_chunk_rows_on_cpu_is_the_resident_fit():
     b = mikmeans.KMeans(5, device="cpu", seed=0, chunk_rows=512).fit(X)
     assert torch.equal(a.cluster_centers_, b.cluster_centers_)
     assert b.get_config().chunk_rows == 512
+
+
+def _spherical_reference(X, C0, iters):
+    """Plain NumPy spherical k-means (Dhillon & Modha): unit rows, cosine argmax, mean, renormalise."""
+    Xn = X / np.linalg.norm(X, axis=1, keepdims=True)
+    C = C0 / np.linalg.norm(C0, axis=1, keepdims=True)
+    for _ in range(iters):
+        lab = (Xn @ C.T).argmax(1)
+        for k in range(C.shape[0]):
+            m = Xn[lab == k]
+            if len(m):
+                s = m.sum(0)
+                C[k] = s / np.linalg.norm(s)
+    return C, lab
+
+
+def test_cosine_metric_is_spherical_kmeans():
+    X, _ = blobs(3000, 8, 6, seed=8)
+    X = X.numpy().astype(np.float64)
+    X *= np.random.default_rng(0).uniform(0.2, 5.0, size=(len(X), 1))   # row scale must not matter
+    C0 = X[:6].copy()
+    km = mikmeans.KMeans(6, init=C0.astype(np.float32), metric="cosine", max_iter=10, tol=0, device="cpu").fit(X)
+    C = km.cluster_centers_.double().numpy()
+    np.testing.assert_allclose(np.linalg.norm(C, axis=1), 1.0, rtol=1e-5)
+    ref_C, _ = _spherical_reference(X, C0, km.n_iter_)
+    np.testing.assert_allclose(C, ref_C, atol=2e-5)
+    Xn = X / np.linalg.norm(X, axis=1, keepdims=True)
+    assert np.array_equal(np.asarray(km.predict(X)), (Xn @ C.T).argmax(1))
+    km2 = mikmeans.KMeans(6, init=C0.astype(np.float32), metric="cosine", max_iter=10, tol=0,
+                          device="cpu").fit(X * 7.0)
+    np.testing.assert_allclose(km2.cluster_centers_.numpy(), km.cluster_centers_.numpy(), atol=1e-6)
+    with pytest.raises(ValueError):
+        mikmeans.KMeans(3, metric="manhattan")
