@@ -41,6 +41,7 @@ class StreamingLloydEngine(LloydEngine):
         C = native.require()
         self._C = C
         self.incremental = False
+        self.spherical = False
         self.delta = None
         self.segments = 1
         self.hint = False
