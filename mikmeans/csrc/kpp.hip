@@ -432,6 +432,40 @@ __global__ __launch_bounds__(256) void blobs_kernel(T* X, int64_t i0, int64_t n,
     if (y && t == 0) y[il] = cid;
     const float* mu = centers + (int64_t)cid * D;
     T* out = X + il * ldx;
+    if (vec) {
+      // Branch-free path (D % 4 == 0, 16-byte aligned centres and rows): the group's
+      // four means are one dwordx4 load issued before the Philox rounds, so its L2
+      // latency hides under them (the general path below waits on four dependent
+      // dword loads per group).  Same arithmetic, same bits.
+      for (int g = t; g < G; g += TPR) {
+        const f32x4 m = *(const f32x4*)(mu + 4 * g);
+        const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
+        constexpr float M2LN2 = -1.38629436111989f;
+        const float rad0 = __builtin_amdgcn_sqrtf(M2LN2 * __builtin_amdgcn_logf(u01_open0(r.x)));
+        const float rad1 = __builtin_amdgcn_sqrtf(M2LN2 * __builtin_amdgcn_logf(u01_open0(r.z)));
+        const float a0 = u01(r.y), a1 = u01(r.w);
+        const float z[4] = {rad0 * __builtin_amdgcn_cosf(a0), rad0 * __builtin_amdgcn_sinf(a0),
+                            rad1 * __builtin_amdgcn_cosf(a1), rad1 * __builtin_amdgcn_sinf(a1)};
+        float f[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f[j] = __builtin_fmaf(stddev, z[j], m[j]);
+        if constexpr (sizeof(T) == 2) {
+          uint32_t h[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {  // RNE to bf16; values are finite by construction
+            const uint32_t u = __float_as_uint(f[j]);
+            h[j] = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+            const float q = __uint_as_float(h[j] << 16);
+            sq = __builtin_fmaf(q, q, sq);
+          }
+          *(uint2*)(out + 4 * g) = uint2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sq = __builtin_fmaf(f[j], f[j], sq);
+          *(f32x4*)(out + 4 * g) = f32x4{f[0], f[1], f[2], f[3]};
+        }
+      }
+    } else
     for (int g = t; g < G; g += TPR) {
       const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
       // Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32, and
@@ -481,7 +515,8 @@ hipError_t launch_blobs(int dtype, void* X, int64_t i0, int64_t n, int D, int64_
   if (n <= 0) return hipSuccess;
   const int G = (D + 3) / 4;
   const int es = dtype == DT_BF16 ? 2 : 4;
-  const int vec = ((uintptr_t)X % (4 * es) == 0 && (ldx * es) % (4 * es) == 0) ? 1 : 0;
+  const int vec = ((uintptr_t)X % (4 * es) == 0 && (ldx * es) % (4 * es) == 0 && D % 4 == 0 &&
+                   (uintptr_t)centers % 16 == 0) ? 1 : 0;
   int tpr = 1;
   while (tpr < G && tpr < 16) tpr *= 2;
   const int64_t tot = n * tpr;
