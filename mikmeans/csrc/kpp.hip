@@ -405,17 +405,49 @@ hipError_t launch_blob_centers(float* centers, int n_centers, int D, float box, 
   return hipGetLastError();
 }
 
-// TPR threads per row (power of two); thread t generates the 4-element groups
+// TPR threads per row (power of two); thread t generates the EL-element groups
 // g = t, t + TPR, ... so each store instruction of the row's threads is contiguous.
 // The row's blob id is drawn once (lane t == 0) and broadcast; the squared norm of
 // the stored (rounded) values is reduced across the row's lanes when xn is given, so
 // a streamed mini-batch needs no separate row-norm pass.
+//
+// Normals per Philox4x32-10 call: f32 rows take 4 (Box-Muller on 24-bit uniforms);
+// bf16 rows (8 mantissa bits) take 8 from 16-bit uniforms -- radius from each word's
+// low half, angle from its high half, tails truncated at sqrt(32 ln 2) = 4.7 sigma --
+// which halves the Philox multiplies per value.  Box-Muller runs on the hardware
+// transcendentals: v_log_f32 (log2), v_sqrt_f32, and v_sin_f32 / v_cos_f32, whose
+// argument is in revolutions, so sin(2*pi*u) is one instruction.
+template <typename T>
+__device__ __forceinline__ void box_muller(const U4& r, float* z) {
+  constexpr float M2LN2 = -1.38629436111989f;  // -2 ln 2
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float u = (float)((w[j] & 0xffffu) + 1u) * (1.0f / 65536.0f);
+      const float a = (float)(w[j] >> 16) * (1.0f / 65536.0f);
+      const float rad = __builtin_amdgcn_sqrtf(M2LN2 * __builtin_amdgcn_logf(u));
+      z[2 * j] = rad * __builtin_amdgcn_cosf(a);
+      z[2 * j + 1] = rad * __builtin_amdgcn_sinf(a);
+    }
+  } else {
+    const float rad0 = __builtin_amdgcn_sqrtf(M2LN2 * __builtin_amdgcn_logf(u01_open0(r.x)));
+    const float rad1 = __builtin_amdgcn_sqrtf(M2LN2 * __builtin_amdgcn_logf(u01_open0(r.z)));
+    const float a0 = u01(r.y), a1 = u01(r.w);
+    z[0] = rad0 * __builtin_amdgcn_cosf(a0);
+    z[1] = rad0 * __builtin_amdgcn_sinf(a0);
+    z[2] = rad1 * __builtin_amdgcn_cosf(a1);
+    z[3] = rad1 * __builtin_amdgcn_sinf(a1);
+  }
+}
+
 template <typename T, int TPR>
 __global__ __launch_bounds__(256) void blobs_kernel(T* X, int64_t i0, int64_t n, int D, int64_t ldx,
                                                     const float* __restrict__ centers,
                                                     int n_centers, float stddev, uint32_t k0,
                                                     uint32_t k1, int32_t* y, float* xn, int vec) {
-  const int G = (D + 3) / 4;
+  constexpr int EL = sizeof(T) == 2 ? 8 : 4;  // values per Philox call (= 16-byte store)
+  const int G = (D + EL - 1) / EL;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t il = e / TPR;
   const int t = (int)(e % TPR);
@@ -433,72 +465,52 @@ __global__ __launch_bounds__(256) void blobs_kernel(T* X, int64_t i0, int64_t n,
     const float* mu = centers + (int64_t)cid * D;
     T* out = X + il * ldx;
     if (vec) {
-      // Branch-free path (D % 4 == 0, 16-byte aligned centres and rows): the group's
-      // four means are one dwordx4 load issued before the Philox rounds, so its L2
-      // latency hides under them (the general path below waits on four dependent
-      // dword loads per group).  Same arithmetic, same bits.
+      // Branch-free path (D % EL == 0, 16-byte aligned centres and rows): the group's
+      // means are dwordx4 loads issued before the Philox rounds, so their L2 latency
+      // hides under them (the general path waits on dependent dword loads).  Same bits.
       for (int g = t; g < G; g += TPR) {
-        const f32x4 m = *(const f32x4*)(mu + 4 * g);
+        f32x4 m[EL / 4];
+#pragma unroll
+        for (int q = 0; q < EL / 4; ++q) m[q] = *(const f32x4*)(mu + EL * g + 4 * q);
         const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
-        constexpr float M2LN2 = -1.38629436111989f;
-        const float rad0 = __builtin_amdgcn_sqrtf(M2LN2 * __builtin_amdgcn_logf(u01_open0(r.x)));
-        const float rad1 = __builtin_amdgcn_sqrtf(M2LN2 * __builtin_amdgcn_logf(u01_open0(r.z)));
-        const float a0 = u01(r.y), a1 = u01(r.w);
-        const float z[4] = {rad0 * __builtin_amdgcn_cosf(a0), rad0 * __builtin_amdgcn_sinf(a0),
-                            rad1 * __builtin_amdgcn_cosf(a1), rad1 * __builtin_amdgcn_sinf(a1)};
-        float f[4];
+        float z[EL], f[EL];
+        box_muller<T>(r, z);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) f[j] = __builtin_fmaf(stddev, z[j], m[j]);
+        for (int j = 0; j < EL; ++j) f[j] = __builtin_fmaf(stddev, z[j], m[j / 4][j % 4]);
         if constexpr (sizeof(T) == 2) {
-          uint32_t h[4];
+          uint32_t h[EL];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {  // RNE to bf16; values are finite by construction
+          for (int j = 0; j < EL; ++j) {  // RNE to bf16; values are finite by construction
             const uint32_t u = __float_as_uint(f[j]);
             h[j] = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
             const float q = __uint_as_float(h[j] << 16);
             sq = __builtin_fmaf(q, q, sq);
           }
-          *(uint2*)(out + 4 * g) = uint2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+          u32x4 w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[j] = h[2 * j] | (h[2 * j + 1] << 16);
+          *(u32x4*)(out + EL * g) = w;
         } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) sq = __builtin_fmaf(f[j], f[j], sq);
-          *(f32x4*)(out + 4 * g) = f32x4{f[0], f[1], f[2], f[3]};
+          for (int j = 0; j < EL; ++j) sq = __builtin_fmaf(f[j], f[j], sq);
+          *(f32x4*)(out + EL * g) = f32x4{f[0], f[1], f[2], f[3]};
         }
       }
-    } else
-    for (int g = t; g < G; g += TPR) {
-      const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
-      // Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32, and
-      // v_sin_f32 / v_cos_f32, whose argument is in revolutions, so sin(2*pi*u) is one
-      // instruction.  A few ulp from the libm forms, a third of the instructions.
-      constexpr float M2LN2 = -1.38629436111989f;  // -2 ln 2
-      const float rad0 = __builtin_amdgcn_sqrtf(M2LN2 * __builtin_amdgcn_logf(u01_open0(r.x)));
-      const float rad1 = __builtin_amdgcn_sqrtf(M2LN2 * __builtin_amdgcn_logf(u01_open0(r.z)));
-      const float a0 = u01(r.y), a1 = u01(r.w);
-      const float s0 = __builtin_amdgcn_sinf(a0), c0 = __builtin_amdgcn_cosf(a0);
-      const float s1 = __builtin_amdgcn_sinf(a1), c1 = __builtin_amdgcn_cosf(a1);
-      const float z[4] = {rad0 * c0, rad0 * s0, rad1 * c1, rad1 * s1};
-      T v[4];
+    } else {
+      for (int g = t; g < G; g += TPR) {
+        const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
+        float z[EL];
+        box_muller<T>(r, z);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int d = 4 * g + j;
-        v[j] = Elem<T>::from_f32(d < D ? mu[d] + stddev * z[j] : 0.f);
-        const float f = Elem<T>::to_f32(v[j]);
-        if (d < D) sq += f * f;
-      }
-      if (vec && 4 * g + 3 < D) {  // one 8-byte (bf16) / 16-byte (f32) store
-        if constexpr (sizeof(T) == 2) {
-          uint2 w;
-          w.x = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
-          w.y = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
-          *(uint2*)(out + 4 * g) = w;
-        } else {
-          *(f32x4*)(out + 4 * g) = f32x4{v[0], v[1], v[2], v[3]};
+        for (int j = 0; j < EL; ++j) {
+          const int d = EL * g + j;
+          if (d < D) {
+            const T v = Elem<T>::from_f32(__builtin_fmaf(stddev, z[j], mu[d]));
+            const float f = Elem<T>::to_f32(v);
+            sq = __builtin_fmaf(f, f, sq);
+            out[d] = v;
+          }
         }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (4 * g + j < D) out[4 * g + j] = v[j];
       }
     }
   }
@@ -513,9 +525,10 @@ hipError_t launch_blobs(int dtype, void* X, int64_t i0, int64_t n, int D, int64_
                         const float* centers, int n_centers, float stddev, uint64_t seed,
                         int32_t* y, float* xn, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  const int G = (D + 3) / 4;
+  const int el = dtype == DT_BF16 ? 8 : 4;  // values per group (see blobs_kernel)
+  const int G = (D + el - 1) / el;
   const int es = dtype == DT_BF16 ? 2 : 4;
-  const int vec = ((uintptr_t)X % (4 * es) == 0 && (ldx * es) % (4 * es) == 0 && D % 4 == 0 &&
+  const int vec = ((uintptr_t)X % 16 == 0 && (ldx * es) % 16 == 0 && D % el == 0 &&
                    (uintptr_t)centers % 16 == 0) ? 1 : 0;
   int tpr = 1;
   while (tpr < G && tpr < 16) tpr *= 2;

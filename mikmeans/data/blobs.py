@@ -59,22 +59,35 @@ def blob_centers_np(n_centers: int, d: int, box: float = 10.0, seed: int = 0) ->
 
 
 def blobs_np(i0: int, n: int, centers: np.ndarray, std: float = 1.0, seed: int = 0,
-             return_labels: bool = False):
-    """Rows ``[i0, i0+n)`` of the blob dataset as float32 (NumPy mirror of K8)."""
+             return_labels: bool = False, bits16: bool = False):
+    """Rows ``[i0, i0+n)`` of the blob dataset as float32 (NumPy mirror of K8).
+
+    ``bits16``: the bf16 dataset's scheme -- 8 values per Philox call from 16-bit
+    uniforms (radius from each word's low half, angle from its high half)."""
     nc, d = centers.shape
     gi = np.arange(i0, i0 + n, dtype=np.uint64)
     lo, hi = gi & np.uint64(MASK), gi >> np.uint64(32)
     rc = philox4x32(lo, hi, TAG_CID, 0, seed)[0]
     cid = ((rc * np.uint64(nc)) >> np.uint64(32)).astype(np.int64)
-    G = (d + 3) // 4
+    el = 8 if bits16 else 4
+    G = (d + el - 1) // el
     g = np.arange(G, dtype=np.uint64)[None, :]
     r0, r1, r2, r3 = philox4x32(lo[:, None], hi[:, None], g, TAG_NRM, seed)
-    rad0 = np.sqrt(np.float32(-2.0) * np.log(_u01_open0(r0))).astype(np.float32)
-    rad1 = np.sqrt(np.float32(-2.0) * np.log(_u01_open0(r2))).astype(np.float32)
-    a0 = np.float32(np.pi) * (np.float32(2.0) * _u01(r1))
-    a1 = np.float32(np.pi) * (np.float32(2.0) * _u01(r3))
-    z = np.stack([rad0 * np.cos(a0), rad0 * np.sin(a0), rad1 * np.cos(a1), rad1 * np.sin(a1)], -1)
-    z = z.reshape(n, G * 4)[:, :d].astype(np.float32)
+    if bits16:
+        zs = []
+        for w in (r0, r1, r2, r3):
+            u = ((w & np.uint64(0xFFFF)) + np.uint64(1)).astype(np.float32) * np.float32(1.0 / 65536.0)
+            a = np.float32(2.0 * np.pi) * ((w >> np.uint64(16)).astype(np.float32) * np.float32(1.0 / 65536.0))
+            rad = np.sqrt(np.float32(-2.0) * np.log(u)).astype(np.float32)
+            zs += [rad * np.cos(a), rad * np.sin(a)]
+        z = np.stack(zs, -1)
+    else:
+        rad0 = np.sqrt(np.float32(-2.0) * np.log(_u01_open0(r0))).astype(np.float32)
+        rad1 = np.sqrt(np.float32(-2.0) * np.log(_u01_open0(r2))).astype(np.float32)
+        a0 = np.float32(np.pi) * (np.float32(2.0) * _u01(r1))
+        a1 = np.float32(np.pi) * (np.float32(2.0) * _u01(r3))
+        z = np.stack([rad0 * np.cos(a0), rad0 * np.sin(a0), rad1 * np.cos(a1), rad1 * np.sin(a1)], -1)
+    z = z.reshape(n, G * el)[:, :d].astype(np.float32)
     X = (centers[cid] + np.float32(std) * z).astype(np.float32)
     return (X, cid.astype(np.int32)) if return_labels else X
 
@@ -109,7 +122,8 @@ def make_blobs(n: int, d: int, n_centers: int, *, std: float = 1.0, box: float =
         C.blobs(X, int(i0), centers.to(device=device, dtype=torch.float32).contiguous(), float(std),
                 int(seed), y, norms)
         return (X, y) if return_labels else X
-    res = blobs_np(i0, n, centers.cpu().numpy().astype(np.float32), std, seed, return_labels)
+    res = blobs_np(i0, n, centers.cpu().numpy().astype(np.float32), std, seed, return_labels,
+                   bits16=dtype == torch.bfloat16)
     Xn, y = (res if return_labels else (res, None))
     X = torch.from_numpy(Xn).to(dtype)
     if out is not None:

@@ -153,9 +153,13 @@ def test_tol_scaling():
 
 def test_blobs_shard_invariance():
     C = B.blob_centers_np(7, 5, 10.0, 3)
-    whole = B.blobs_np(0, 1000, C, 1.0, 3)
-    parts = np.concatenate([B.blobs_np(s, e - s, C, 1.0, 3) for s, e in (shard_range(1000, r, 3) for r in range(3))])
-    assert np.array_equal(whole, parts)
+    for b16 in (False, True):
+        whole = B.blobs_np(0, 1000, C, 1.0, 3, bits16=b16)
+        parts = np.concatenate([B.blobs_np(s, e - s, C, 1.0, 3, bits16=b16)
+                                for s, e in (shard_range(1000, r, 3) for r in range(3))])
+        assert np.array_equal(whole, parts)
+        z = whole - C[B.blobs_np(0, 1000, C, 1.0, 3, True, bits16=b16)[1]]   # unit normals
+        assert abs(float(z.mean())) < 0.05 and abs(float(z.std()) - 1.0) < 0.05
 
 
 def test_shard_plan():

@@ -164,7 +164,7 @@ def test_blobs_match_numpy_mirror(native, dtype):
     np.testing.assert_allclose(Cg.cpu().numpy(), Cn, rtol=0, atol=0)
     Xg, yg = B.make_blobs(5000, 40, 16, seed=11, i0=123456789, dtype=dtype, device=DEV,
                           return_labels=True, centers=Cg)
-    Xn, yn = B.blobs_np(123456789, 5000, Cn, 1.0, 11, True)
+    Xn, yn = B.blobs_np(123456789, 5000, Cn, 1.0, 11, True, bits16=dtype == torch.bfloat16)
     assert np.array_equal(yg.cpu().numpy(), yn)
     tol = 1e-4 if dtype == torch.float32 else 8e-2
     np.testing.assert_allclose(Xg.float().cpu().numpy(), Xn, rtol=0, atol=tol)
