@@ -46,6 +46,9 @@ def main(argv=None):
     ap.add_argument("--points", "--n", dest="n", type=int, default=None, help="override total points")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--batch", type=int, default=1 << 24, help="cfg5 rows per rank per step")
+    ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=False,
+                    help="cfg5: generate the next batch on a side stream while the current one is fitted "
+                         "(measured no faster: profiles/r1_18_blobstream_prefetch_ab.json)")
     ap.add_argument("--incremental", action="store_true",
                     help="incremental M-step (re-scatter changed rows only; not the headline mode)")
     ap.add_argument("--also-incremental", action=argparse.BooleanOptionalAction, default=True,
@@ -197,7 +200,8 @@ def _bench_minibatch(args, cfg, comm, dtype):
     N, D, K = cfg["n"], cfg["d"], cfg["k"]
     b = args.batch
     stream = BlobStream(N, D, K, b, seed=args.seed, dtype=dtype, device=comm.device, rank=comm.rank,
-                        world=comm.world, with_norms=True)  # row norms fused into the generator
+                        world=comm.world, with_norms=True,  # row norms fused into the generator
+                        prefetch=args.prefetch)  # batch j+1 generated on a side stream during step j
     eng = MiniBatchEngine(K, D, b, dtype=dtype, device=comm.device, comm=comm)
     first = next(stream)
     eng.set_centers(init_random(first, D, K, b * comm.world, comm.rank * b, comm, args.seed))

@@ -143,7 +143,7 @@ class BlobStream:
 
     def __init__(self, n_total: int, d: int, n_centers: int, batch: int, *, std=1.0, box=10.0,
                  seed=0, dtype=torch.float32, device="cpu", rank=0, world=1, offset=0,
-                 with_norms: bool = False):
+                 with_norms: bool = False, prefetch: bool = False):
         self.n_total, self.d, self.batch = n_total, d, batch
         self.std, self.seed, self.dtype = std, seed, dtype
         self.device = torch.device(device)
@@ -154,6 +154,15 @@ class BlobStream:
         self._nbuf = None
         self.last_norms = None   # squared row norms of the last batch (with_norms=True)
         self.step = 0
+        # prefetch (CUDA only): batch j+1 is generated on a side stream into the other of
+        # two buffers while the caller's stream consumes batch j, so the VALU-bound
+        # generator can share CUs with the LDS-bound M-step instead of running between
+        # steps.  The side stream waits for the caller's stream to finish with a buffer
+        # (event recorded when the next batch is requested) before overwriting it.
+        self.prefetch = bool(prefetch) and self.device.type == "cuda"
+        self._pf = None          # (X, norms, ready event) of the batch generated ahead
+        self._pool = []
+        self._side = torch.cuda.Stream(device=self.device) if self.prefetch else None
 
     def __iter__(self):
         return self
@@ -164,7 +173,46 @@ class BlobStream:
         n = min(self.batch, self.n_total - start)
         return start, n
 
+    def _bufs(self, slot: int):
+        while len(self._pool) <= slot:
+            X = torch.empty((self.batch, self.d), dtype=self.dtype, device=self.device)
+            nb = torch.empty(self.batch, dtype=torch.float32, device=self.device) if self.with_norms else None
+            self._pool.append((X, nb))
+        return self._pool[slot]
+
+    def _gen(self, step: int, slot: int):
+        start, n = self.rows_for(step)
+        Xb, nb = self._bufs(slot)
+        nrm = nb[:n] if nb is not None else None
+        X = make_blobs(n, self.d, 0, std=self.std, seed=self.seed, i0=start, dtype=self.dtype,
+                       device=self.device, centers=self.centers, out=Xb[:n], norms=nrm)
+        return X, nrm
+
+    def _next_prefetch(self) -> torch.Tensor:
+        cur = torch.cuda.current_stream(self.device)
+        j = self.step
+        if self._pf is None:                      # first batch: generate in order
+            X, nrm = self._gen(j, j % 2)
+        else:
+            X, nrm, ev = self._pf
+            cur.wait_event(ev)
+        # the caller has enqueued all its work on batch j-1 (slot (j+1) % 2): the side
+        # stream may overwrite that slot once the caller's stream gets past this point
+        freed = torch.cuda.Event()
+        freed.record(cur)
+        self._side.wait_event(freed)
+        with torch.cuda.stream(self._side):
+            Xn, nn = self._gen(j + 1, (j + 1) % 2)
+            ready = torch.cuda.Event()
+            ready.record(self._side)
+        self._pf = (Xn, nn, ready)
+        self.step += 1
+        self.last_norms = nrm
+        return X
+
     def __next__(self) -> torch.Tensor:
+        if self.prefetch:
+            return self._next_prefetch()
         start, n = self.rows_for(self.step)
         self.step += 1
         if self._buf is None or self._buf.shape[0] < self.batch:

@@ -176,6 +176,29 @@ def test_blobs_match_numpy_mirror(native, dtype):
     torch.testing.assert_close(nrm, Xg.float().pow(2).sum(1), rtol=1e-5, atol=1e-3)
 
 
+def test_blob_stream_prefetch_is_identical(native):
+    """Side-stream prefetch (bench cfg5) yields the same batches and the same mini-batch fit."""
+    from mikmeans.models.minibatch import MiniBatchEngine
+
+    D, K, b = 64, 32, 4096
+    res = []
+    for pf in (False, True):
+        s = B.BlobStream(10**6, D, K, b, seed=5, dtype=torch.bfloat16, device=DEV, with_norms=True, prefetch=pf)
+        eng = MiniBatchEngine(K, D, b, dtype=torch.bfloat16, device=DEV)
+        X0 = next(s)
+        eng.set_centers(X0[:K].float())
+        batches = [X0.clone()]
+        for _ in range(6):
+            Xb = next(s)
+            batches.append(Xb.clone())
+            eng.partial_fit(Xb, s.last_norms)
+        torch.cuda.synchronize()
+        res.append((batches, eng.C.clone()))
+    for a, c in zip(res[0][0], res[1][0]):
+        assert torch.equal(a, c)
+    assert torch.equal(res[0][1], res[1][1])
+
+
 def test_lloyd_gpu_matches_cpu_engine(native):
     from mikmeans.models.lloyd import LloydEngine
 
