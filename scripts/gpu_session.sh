@@ -21,6 +21,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     tests) step pytest_gpu 1200 python -m pytest tests -x -q -m gpu ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
     bench2) step bench_cfg2 300 python bench.py --config cfg2 --steps 50 --warmup 5 ;;
+    bench4) step bench_cfg4 300 python bench.py --config cfg4 --steps 20 --warmup 3 ;;
+    bench5) step bench_cfg5 300 python bench.py --config cfg5 --steps 20 --warmup 3 ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$OLDPWD}"
           step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -- python3 bench.py --steps 5 --warmup 1 ;;
   esac
