@@ -294,6 +294,19 @@ void row_sqnorm(const Tensor& X, const Tensor& out) {
             "row_sqnorm");
 }
 
+// out: int32 [D] zero-filled by the caller; receives max |x[:, d]| as float bit patterns.
+void col_absmax(const Tensor& X, const Tensor& out) {
+  const int dt = dtype_of(X);
+  const int64_t ldx = check_points(X, dt);
+  check_cuda(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kInt && out.is_contiguous() && out.numel() == X.size(1),
+              "mikmeans: col_absmax out must be int32 [D]");
+  TORCH_CHECK(X.size(1) / vec_of(dt) <= 64, "mikmeans: col_absmax supports D <= 64 16-B pieces");
+  hip_check(mk::launch_col_absmax(dt, X.data_ptr(), X.size(0), (int)X.size(1), ldx,
+                                  reinterpret_cast<uint32_t*>(out.data_ptr<int32_t>()), stream()),
+            "col_absmax");
+}
+
 void kpp_d2(const Tensor& X, const Tensor& c, bool first, const Tensor& d2, const Tensor& block_sums,
             int64_t rows_per_block, const c10::optional<Tensor>& owner, const c10::optional<Tensor>& cc,
             int64_t kcc, int64_t knew) {
@@ -428,6 +441,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("reduce_delta", &reduce_delta, "slab reduction into running totals + packed message");
   m.def("finalize", &finalize, "new centroids, shift, fragment re-pack (K4)");
   m.def("row_sqnorm", &row_sqnorm, "row squared norms (K1)");
+  m.def("col_absmax", &col_absmax, "per-column max |x| as f32 bit patterns (fixed-point scales)");
   m.def("kpp_d2", &kpp_d2, "k-means++ D^2 update (K5; triangle-inequality pruned with owner/cc)",
         py::arg("X"), py::arg("c"), py::arg("first"), py::arg("d2"), py::arg("block_sums"),
         py::arg("rows_per_block"), py::arg("owner") = py::none(), py::arg("cc") = py::none(),

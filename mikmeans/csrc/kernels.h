@@ -121,6 +121,8 @@ struct FinalizeArgs {
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 
 // ---- row squared norms -------------------------------------------------------
+hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
+                             hipStream_t s);
 hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t ldx, float* out,
                              hipStream_t s);
 

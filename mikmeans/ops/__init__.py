@@ -163,6 +163,13 @@ def col_max_abs(X: torch.Tensor) -> torch.Tensor:
     """Per-column max |x| as float64 ``[D]`` (no |X| temporary)."""
     if X.shape[0] == 0:
         return torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
+    if X.is_cuda and X.dtype in (torch.float32, torch.bfloat16):
+        v = 16 // X.element_size()
+        if (X.dim() == 2 and X.stride(1) == 1 and X.shape[1] % v == 0 and X.shape[1] // v <= 64
+                and (X.shape[0] <= 1 or X.stride(0) % v == 0) and X.data_ptr() % 16 == 0):
+            out = torch.zeros(X.shape[1], dtype=torch.int32, device=X.device)
+            require().col_absmax(X, out)   # one streaming pass (csrc/finalize.hip)
+            return out.view(torch.float32).double()
     mn, mx = torch.aminmax(X, dim=0)
     return torch.maximum(mn.double().abs(), mx.double().abs())
 

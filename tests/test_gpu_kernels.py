@@ -534,3 +534,23 @@ def test_cosine_metric_gpu(native):
         eb.step()
     torch.cuda.synchronize()
     assert torch.equal(ea.centers, eb.centers) and torch.equal(ea.labels, eb.labels)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,d", [(1, 64), (1000, 8), (12345, 128), (70001, 256), (3000, 512)])
+def test_col_absmax_matches_torch(native, dtype, n, d):
+    """Native per-column max |x| (fixed-point M-step scales) vs torch.aminmax; strided rows too."""
+    from mikmeans.ops import col_max_abs
+
+    if d * torch.tensor([], dtype=dtype).element_size() > 1024:
+        d = 1024 // torch.tensor([], dtype=dtype).element_size()   # kernel bound: 64 16-B pieces
+    g = torch.Generator(device=DEV).manual_seed(n + d)
+    X = (torch.randn(n, d, device=DEV, generator=g) * torch.linspace(0.1, 50, d, device=DEV)).to(dtype)
+    ref = X.float().abs().amax(0).double()
+    assert torch.equal(col_max_abs(X), ref)
+    Xs = torch.zeros(n, d + 16, device=DEV, dtype=dtype)[:, 8:8 + d] if dtype == torch.bfloat16 \
+        else torch.zeros(n, d + 8, device=DEV, dtype=dtype)[:, 4:4 + d]
+    Xs.copy_(X)
+    assert torch.equal(col_max_abs(Xs), ref)
+    X[n // 2, d // 3] = float("nan")
+    assert torch.isnan(col_max_abs(X)[d // 3]) and not torch.isnan(col_max_abs(X)[d // 3 + 1])
