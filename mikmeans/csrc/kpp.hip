@@ -22,6 +22,11 @@
 namespace mk {
 
 constexpr int KPP_NT = 256;
+// rows in flight per lane in the pruned pass: 6 (124 VGPRs, 4 waves/SIMD) beat 8 (166 VGPRs,
+// 3 waves/SIMD) and 4 at cfg4: k-means++ seeding 0.95 -> 0.83 s (profiles/r1_18_kpp_unr_ab.json)
+#ifndef MK_KPP_UNR_PRUNE
+#define MK_KPP_UNR_PRUNE 6
+#endif
 
 // Pruned K5 (PRUNE): Elkan's triangle-inequality bound applied to D^2 seeding.
 // owner[i] is the centre d2[i] was measured against and cc[j] = |c_new - c_j|^2.
@@ -44,20 +49,20 @@ __global__ __launch_bounds__(KPP_NT) void kpp_d2_kernel(const T* __restrict__ X,
                                                         int64_t rows_per_block, int32_t* __restrict__ owner,
                                                         const float* __restrict__ cc, int kcc, int knew) {
   constexpr int V = Elem<T>::V;
-  constexpr int UNR = PRUNE ? 8 : 4;
+  constexpr int UNR = PRUNE ? MK_KPP_UNR_PRUNE : 4;
   constexpr int RPW = KPP_NT / LPR;  // rows per pass of the workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* cs = (float*)smem;
   for (int d = threadIdx.x; d < D; d += KPP_NT) cs[d] = c[d];
   // pruned pass: the k centre-centre distances live in LDS (one gather per row instead of a
   // dependent global load), unless there are too many of them
-  const float* ccp = cc;
+  // (ccs is addressed through the __shared__ array itself so the gathers below compile to
+  // ds_read, not flat loads whose waits would also drain the in-flight row loads)
+  const int cc_off = (D + 3) & ~3;
+  const bool cc_lds = PRUNE && kcc <= KPP_CC_LDS;
   if constexpr (PRUNE) {
-    if (kcc <= KPP_CC_LDS) {
-      float* ccs = cs + ((D + 3) & ~3);
-      for (int j = threadIdx.x; j < kcc; j += KPP_NT) ccs[j] = cc[j];
-      ccp = ccs;
-    }
+    if (cc_lds)
+      for (int j = threadIdx.x; j < kcc; j += KPP_NT) ((float*)smem)[cc_off + j] = cc[j];
   }
   __syncthreads();
   const int sub = threadIdx.x % LPR;
@@ -79,14 +84,25 @@ __global__ __launch_bounds__(KPP_NT) void kpp_d2_kernel(const T* __restrict__ X,
   };
   if constexpr (PRUNE) meta(r0 + threadIdx.x / LPR);
   for (int64_t base = r0 + threadIdx.x / LPR; base < r1; base += (int64_t)RPW * UNR) {
-    float acc[UNR], old[UNR];
+    float acc[UNR], old[UNR], ccv[UNR];
     bool need[UNR];
+    if constexpr (PRUNE) {
+      // unconditional gathers (index clamped), all issued before the first compare: the
+      // UNR reads share one wait instead of a branch + full wait each
+      if (cc_lds) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) ccv[u] = ((const float*)smem)[cc_off + (own_n[u] > 0 ? own_n[u] : 0)];
+      } else {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) ccv[u] = cc[own_n[u] > 0 ? own_n[u] : 0];
+      }
+    }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       acc[u] = 0.f;
       if constexpr (PRUNE) {
         old[u] = old_n[u];
-        need[u] = own_n[u] >= 0 && !(ccp[own_n[u]] >= KPP_PRUNE * old[u]);
+        need[u] = own_n[u] >= 0 && !(ccv[u] >= KPP_PRUNE * old[u]);
       } else {
         old[u] = 0.f;
         need[u] = base + (int64_t)u * RPW < r1;
