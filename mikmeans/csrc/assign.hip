@@ -224,7 +224,7 @@ static hipError_t launch_t(const AssignArgs& a, hipStream_t s) {
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)assign_kernel<T, DPAD, P>,
+    (void)hipFuncSetAttribute((const void*)assign_kernel<T, DPAD, P>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }

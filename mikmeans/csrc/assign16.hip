@@ -347,7 +347,7 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_>,
+    (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }

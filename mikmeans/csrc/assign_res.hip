@@ -219,7 +219,7 @@ static hipError_t launch_res_t(const AssignArgs& a, unsigned long long* keys, hi
   const int tpp = (kt + passes - 1) / passes;  // balanced passes
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)assign_res_kernel<T, DPAD, P>,
+    (void)hipFuncSetAttribute((const void*)assign_res_kernel<T, DPAD, P>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)RES_LDS_MAX);
     attr = true;
   }

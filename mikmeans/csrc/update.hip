@@ -497,7 +497,7 @@ static hipError_t launch_nt(const UpdateArgs& a, int ldc, hipStream_t s) {
   const int64_t rows_per_chunk = (a.N + a.n_chunks - 1) / a.n_chunks;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)update_kernel<T, SW, MODE, NT, NBF, PER>,
+    (void)hipFuncSetAttribute((const void*)update_kernel<T, SW, MODE, NT, NBF, PER>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)UPD_LDS_MAX);
     attr = true;
   }
