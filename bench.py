@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """Headline benchmark: Lloyd iterations/sec at N=1e8, D=128, K=1024, bf16 (BASELINE.json).
 
-Driver contract: ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is
-launched by ``torch.distributed.run`` (one rank per GPU, RCCL over xGMI).  The
+Driver contract: ``python bench.py --gpus N --steps K --warmup W``; for N>1 it runs
+one rank per GPU (RCCL over xGMI): under ``torch.distributed.run`` it joins that job,
+and started plainly it launches its own N-rank ``torch.distributed.run`` child (the
+parent never touches the GPU).  By default even N=1 joins a real one-rank RCCL
+process group, so every N runs the same collective path.  The
 dataset is 1e8 synthetic Gaussian-blob points in total (1024 blobs, generated on
 device, each rank its own contiguous row range; identical data for any world
 size), centroids are K random data rows.  One timed step is one full Lloyd
@@ -56,7 +59,29 @@ def main(argv=None):
                          "(incremental M-step) from the same start and report it as an extra field")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: gloo rehearsal of the multi-rank path (tests; tiny --n)")
+    ap.add_argument("--pg", default="force", choices=["force", "auto"],
+                    help="force: even one rank joins a real process group (RCCL on GPU), so N=1 "
+                         "runs the same collective path as N=8; auto: no group when WORLD_SIZE=1")
+    ap.add_argument("--timeout", type=float, default=120.0,
+                    help="collective timeout in seconds (a dead rank fails the job after this long)")
     args = ap.parse_args(argv)
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # Self-launch: this parent has not touched the GPU (no HIP call yet); it starts
+        # one rank per GPU as a torch.distributed.run child and exits with its code.
+        from mikmeans.parallel.launch import launch_self
+
+        return launch_self(args.gpus, [os.path.abspath(__file__), *(sys.argv[1:] if argv is None else argv)])
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+        return 2
+    if args.pg == "force" and world_env == 1:
+        from mikmeans.parallel.launch import free_port
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MIKMEANS_FORCE_PG="1")
 
     import mikmeans
     from mikmeans.data.blobs import make_blobs, blob_centers
@@ -67,10 +92,9 @@ def main(argv=None):
     cfg = dict(CONFIGS[args.config])
     if args.n:
         cfg["n"] = args.n
-    comm = Comm.from_env(args.device)
+    comm = Comm.from_env(args.device, timeout_s=args.timeout)
     world = comm.world
-    if args.gpus != world and comm.rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    assert world == args.gpus, (world, args.gpus)
     dev = comm.device
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     dtype = torch.bfloat16 if cfg["dtype"] == "bfloat16" else torch.float32
@@ -147,10 +171,12 @@ def main(argv=None):
                 "parallelism": f"dp{world}",
                 **({"mstep": "incremental"} if args.incremental else {}),
             },
+            "comm": {"backend": comm.backend, "world_size": comm.world, "process_group": comm.grouped},
             **extra,
         }
         print(json.dumps(out), flush=True)
     comm.close()
+    return 0
 
 
 def _timed_steps(eng, comm, warmup: int, steps: int, sync) -> float:
@@ -222,4 +248,4 @@ def _bench_minibatch(args, cfg, comm, dtype):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

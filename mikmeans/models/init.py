@@ -135,13 +135,15 @@ def _kpp_gpu(X, centers, K, comm: Comm, u, L, prune: bool = True):
 
     if n:
         C.kpp_d2(X, centers[0], True, d2, bs, rpb)
-    W = comm.world
+    # multi-rank selection whenever a process group exists (also a forced 1-rank group:
+    # the one-GPU rehearsal of the RCCL path issues the same collectives as W=8)
+    multi = comm.grouped
     for k in range(1, K):
         for t in range(L):
             uk = u[(k - 1) * L + t: (k - 1) * L + t + 1]
             # the sampled row lands straight in centers[k] on one rank (L == 1)
-            row = centers[k] if (L == 1 and W == 1) else crow
-            if W == 1:
+            row = centers[k] if (L == 1 and not multi) else crow
+            if not multi:
                 C.kpp_sample(bs, d2, rpb, uk, X, row, None, 1, None, 0)  # target = u * total, on device
             else:
                 tot = bs.sum().reshape(1) if n else torch.zeros(1, dtype=torch.float64, device=dev)

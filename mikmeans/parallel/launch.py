@@ -1,14 +1,18 @@
 """Local multi-process launcher (one process per rank) for CPU/gloo runs and tests.
 
-GPU jobs use ``torchrun --nproc-per-node N`` (one rank per GPU, RCCL); this helper
-spawns ``world`` CPU ranks on 127.0.0.1 with the gloo backend so the exact same
-distributed code paths (sharding, packed all-reduce, k-means++ owner selection,
-checkpoint broadcast, room replication) run without a GPU.
+GPU jobs run one rank per GPU (RCCL): ``launch_self`` starts a script as an N-rank
+``torch.distributed.run`` child with optional fresh-process restarts (bench.py and
+``mikmeans launch`` use it); ``spawn_local`` runs a function on ``world`` CPU ranks on
+127.0.0.1 with the gloo backend so the exact same distributed code paths (sharding,
+packed all-reduce, k-means++ owner selection, checkpoint broadcast, room replication)
+run without a GPU.
 """
 from __future__ import annotations
 
 import os
 import socket
+import subprocess
+import sys
 import tempfile
 import traceback
 
@@ -38,6 +42,36 @@ def _worker(rank, world, port, fn, args, outdir):
         raise
     finally:
         comm.close()
+
+
+def torchrun_cmd(nproc: int, script_argv: list[str], port: int | None = None) -> list[str]:
+    """``python -m torch.distributed.run`` for ``nproc`` local ranks on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port or free_port()), *script_argv]
+
+
+def launch_self(nproc: int, script_argv: list[str], max_restarts: int = 0, env: dict | None = None) -> int:
+    """Start ``script_argv`` (a script path plus its arguments) as an ``nproc``-rank job and
+    return its exit code -- the MI355X analogue of the reference meshing every tab on page
+    load (app.mjs:70-118, called at :583).
+
+    The caller must not have initialised the GPU: the job runs as a CHILD process (never an
+    exec of this one).  A failed job is relaunched up to ``max_restarts`` times as a fresh
+    process tree; a script that checkpoints resumes from its last checkpoint then
+    (``mikmeans fit --resume auto``), so a lost rank costs at most the work since it.
+    """
+    env = dict(os.environ if env is None else env)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    rc = 1
+    for attempt in range(max_restarts + 1):
+        cmd = torchrun_cmd(nproc, script_argv)
+        if attempt:
+            print(f"[mikmeans launch] job failed (rc={rc}); restart {attempt}/{max_restarts}", file=sys.stderr,
+                  flush=True)
+        rc = subprocess.call(cmd, env=env)
+        if rc == 0:
+            break
+    return rc
 
 
 def spawn_local(fn, world: int, *args, timeout: float = 300.0):

@@ -18,8 +18,10 @@ step() {  # step NAME TIMEOUT CMD...
 for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step pytest_gpu 1200 python -m pytest tests -x -q -m gpu ;;
+    tests) step pytest_gpu 1200 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread ;;
+    rccl) step pytest_rccl 300 python -u -m pytest tests/test_gpu_rccl.py -x -v --timeout 120 --timeout-method thread ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
+    benchauto) step bench_nopg 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 --pg auto --no-also-incremental ;;
     bench2) step bench_cfg2 300 python bench.py --config cfg2 --steps 50 --warmup 5 ;;
     bench4) step bench_cfg4 300 python bench.py --config cfg4 --steps 20 --warmup 3 ;;
     bench5) step bench_cfg5 300 python bench.py --config cfg5 --steps 20 --warmup 3 ;;
