@@ -228,7 +228,8 @@ def _bench_minibatch(args, cfg, comm, dtype):
     stream = BlobStream(N, D, K, b, seed=args.seed, dtype=dtype, device=comm.device, rank=comm.rank,
                         world=comm.world, with_norms=True,  # row norms fused into the generator
                         prefetch=args.prefetch)  # batch j+1 generated on a side stream during step j
-    eng = MiniBatchEngine(K, D, b, dtype=dtype, device=comm.device, comm=comm)
+    # the generator's value bound fixes the fixed-point scales up front (no per-step clamp check)
+    eng = MiniBatchEngine(K, D, b, dtype=dtype, device=comm.device, comm=comm, value_bound=stream.value_bound)
     first = next(stream)
     eng.set_centers(init_random(first, D, K, b * comm.world, comm.rank * b, comm, args.seed))
     for _ in range(args.warmup):

@@ -423,10 +423,16 @@ class MiniBatchKMeans(_Serving):
         init_n = min(n, self.init_size or max(3 * self.batch_size, 3 * self.n_clusters))
         sample_idx = torch.randperm(n, generator=g)[:init_n].to(device)
         eng.set_centers(self._init_centers(Xt[sample_idx]))
-        steps = self.max_steps or max(1, math.ceil(self.max_iter * n / self.batch_size))
+        # the step count must be the same on every rank (each step is a collective): derive
+        # it from the global row count, never from this rank's shard size
+        n_global, _ = _shard_info(n, comm, device)
+        steps = self.max_steps or max(1, math.ceil(self.max_iter * n_global / (self.batch_size * comm.world)))
         for s in range(steps):
-            idx = torch.randint(0, n, (min(self.batch_size, n),), generator=g).to(device)
-            eng.partial_fit(Xt[idx])
+            if n:
+                idx = torch.randint(0, n, (min(self.batch_size, n),), generator=g).to(device)
+                eng.partial_fit(Xt[idx])
+            else:
+                eng.partial_fit(Xt[:0])       # empty shard: still joins the step's all-reduce
             if self.tol > 0 and (s + 1) % 10 == 0:
                 if float(eng.shift.sum()) <= self.tol:
                     break
@@ -438,6 +444,8 @@ class MiniBatchKMeans(_Serving):
         """Fit on an iterator of per-rank batches (e.g. :class:`~mikmeans.data.blobs.BlobStream`)."""
         first = init_batch if init_batch is not None else next(iter(stream))
         eng = self._engine(first.shape[1], first.device)
+        if getattr(stream, "value_bound", None) is not None and eng.gpu and eng.col_exp is None:
+            eng.value_bound = float(stream.value_bound)   # bounded stream: no per-step clamp check
         eng.set_centers(self._init_centers(first.to(self.dtype)))
         for _ in range(steps):
             Xb = next(stream)

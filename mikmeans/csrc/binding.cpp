@@ -136,7 +136,8 @@ void check_i64(const Tensor& t, const char* name, int64_t numel_min) {
 
 void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab,
             const Tensor& cnt_slab, int64_t n_chunks, const c10::optional<Tensor>& weights,
-            const Tensor& col_exp, int64_t cnt_exp, bool clamp) {
+            const Tensor& col_exp, int64_t cnt_exp, bool clamp,
+            const c10::optional<Tensor>& clamp_count, const c10::optional<Tensor>& col_exp2) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   const int64_t N = X.size(0);
@@ -159,6 +160,15 @@ void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab
   a.slab = (long long*)slab.data_ptr<int64_t>(); a.cnt_slab = (long long*)cnt_slab.data_ptr<int64_t>();
   a.weights = opt_ptr<const float>(weights);
   a.col_exp = col_exp.data_ptr<int32_t>(); a.cnt_exp = (int)cnt_exp; a.clamp = clamp ? 1 : 0;
+  if (clamp_count.has_value()) {
+    check_i32(*clamp_count, "clamp_count", 1);
+    a.clamp_count = clamp_count->data_ptr<int32_t>();
+  }
+  if (col_exp2.has_value()) {
+    TORCH_CHECK(sw > 0 && !clamp, "mikmeans: the residual pass needs the LDS path and no clamp");
+    check_i32(*col_exp2, "col_exp2", D);
+    a.col_exp2 = col_exp2->data_ptr<int32_t>();
+  }
   hip_check(mk::launch_update(dt, a, stream()), "update");
 }
 
@@ -243,6 +253,21 @@ void reduce(const Tensor& slab, const Tensor& cnt_slab, int64_t n_chunks, int64_
             "reduce");
 }
 
+// Wide-range column lo sums: out[k*nw + j] = 2^-exps[j] * sum_c slab[c][k][cols[j]].
+void reduce_cols(const Tensor& slab, int64_t n_chunks, int64_t K, int64_t D, const Tensor& cols,
+                 const Tensor& exps, const Tensor& out) {
+  check_i64(slab, "slab", n_chunks * K * D);
+  const int64_t nw = cols.numel();
+  check_i32(cols, "cols", nw);
+  check_i32(exps, "exps", nw);
+  check_f64(out, "out", K * nw);
+  // (column indices are validated once by the engine: no host read here, the call is graph-captured)
+  hip_check(mk::launch_reduce_cols((const long long*)slab.data_ptr<int64_t>(), (int)n_chunks, (int)K, (int)D,
+                                   cols.data_ptr<int32_t>(), exps.data_ptr<int32_t>(), (int)nw,
+                                   out.data_ptr<double>(), stream()),
+            "reduce_cols");
+}
+
 void finalize(int64_t mode, const c10::optional<Tensor>& packed, const Tensor& Cold,
               const c10::optional<Tensor>& Cnew, const c10::optional<Tensor>& frozen,
               const c10::optional<Tensor>& mb_counts, const Tensor& pack, const Tensor& cn,
@@ -295,15 +320,17 @@ void row_sqnorm(const Tensor& X, const Tensor& out) {
 }
 
 // out: int32 [D] zero-filled by the caller; receives max |x[:, d]| as float bit patterns.
-void col_absmax(const Tensor& X, const Tensor& out) {
+void col_absmax(const Tensor& X, const Tensor& out, const c10::optional<Tensor>& sumsq) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   check_cuda(out, "out");
   TORCH_CHECK(out.scalar_type() == at::kInt && out.is_contiguous() && out.numel() == X.size(1),
               "mikmeans: col_absmax out must be int32 [D]");
   TORCH_CHECK(X.size(1) / vec_of(dt) <= 64, "mikmeans: col_absmax supports D <= 64 16-B pieces");
+  if (sumsq.has_value()) check_f64(*sumsq, "sumsq", X.size(1));
   hip_check(mk::launch_col_absmax(dt, X.data_ptr(), X.size(0), (int)X.size(1), ldx,
-                                  reinterpret_cast<uint32_t*>(out.data_ptr<int32_t>()), stream()),
+                                  reinterpret_cast<uint32_t*>(out.data_ptr<int32_t>()), stream(),
+                                  opt_ptr<double>(sumsq)),
             "col_absmax");
 }
 
@@ -434,14 +461,19 @@ std::string js_array(const Tensor& t) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mikmeans native ops (gfx950 HIP kernels + host helpers)";
   m.def("assign", &assign, "fused MFMA distance + argmin (K2)");
-  m.def("update", &update, "LDS-privatised per-cluster sums/counts (K3)");
+  m.def("update", &update, "LDS-privatised per-cluster sums/counts (K3)", py::arg("X"), py::arg("labels"),
+        py::arg("K"), py::arg("slab"), py::arg("cnt_slab"), py::arg("n_chunks"), py::arg("weights"),
+        py::arg("col_exp"), py::arg("cnt_exp"), py::arg("clamp"), py::arg("clamp_count") = py::none(),
+        py::arg("col_exp2") = py::none());
+  m.def("reduce_cols", &reduce_cols, "lo sums of the wide-range columns (residual pass)");
   m.def("reduce", &reduce, "slab reduction into the packed f64 all-reduce message");
   m.def("label_delta", &label_delta, "changed-row list for the incremental M-step");
   m.def("update_delta", &update_delta, "incremental M-step scatter-add (+new / -old label)");
   m.def("reduce_delta", &reduce_delta, "slab reduction into running totals + packed message");
   m.def("finalize", &finalize, "new centroids, shift, fragment re-pack (K4)");
   m.def("row_sqnorm", &row_sqnorm, "row squared norms (K1)");
-  m.def("col_absmax", &col_absmax, "per-column max |x| as f32 bit patterns (fixed-point scales)");
+  m.def("col_absmax", &col_absmax, "per-column max |x| as f32 bit patterns (+ optional f64 sum |x|; fixed-point scales)",
+        py::arg("X"), py::arg("out"), py::arg("sumabs") = py::none());
   m.def("kpp_d2", &kpp_d2, "k-means++ D^2 update (K5; triangle-inequality pruned with owner/cc)",
         py::arg("X"), py::arg("c"), py::arg("first"), py::arg("d2"), py::arg("block_sums"),
         py::arg("rows_per_block"), py::arg("owner") = py::none(), py::arg("cc") = py::none(),

@@ -144,17 +144,30 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
 // per row (power of two >= the row's 16-byte pieces, <= 64), 256/L rows per pass, four
 // independent row loads in flight per lane; |x| compared as bit patterns (non-negative
 // floats order like unsigned integers, and a NaN's pattern exceeds +inf's, so NaN
-// propagates like torch.aminmax).  One global atomicMax per (block, column).
-template <typename T>
+// propagates like torch.aminmax).  One global atomicMax per (block, column).  SQ: also
+// the per-column sum of |x| (f32 per lane, one f64 atomicAdd per (block, column)), from
+// which the engine flags wide-range columns (max >> mean |x|) for the residual pass.
+template <typename T, bool SQ>
 __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X, int64_t N, int NP,
-                                                         int L, int64_t ldx, uint32_t* __restrict__ out) {
+                                                         int L, int64_t ldx, uint32_t* __restrict__ out,
+                                                         double* __restrict__ sumsq) {
   constexpr int V = Elem<T>::V;
   const int p = threadIdx.x & (L - 1);
   const int R = 256 / L;
   const int64_t step = (int64_t)gridDim.x * R;
   uint32_t m[V];
+  float q[V];
 #pragma unroll
-  for (int e = 0; e < V; ++e) m[e] = 0u;
+  for (int e = 0; e < V; ++e) { m[e] = 0u; q[e] = 0.f; }
+  auto take = [&](const u32x4& w) {
+    float f[V];
+    unpack16(w, f, (T*)nullptr);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      m[e] = max(m[e], __float_as_uint(f[e]) & 0x7fffffffu);
+      if constexpr (SQ) q[e] += fabsf(f[e]);
+    }
+  };
   if (p < NP) {
     int64_t i = (int64_t)blockIdx.x * R + threadIdx.x / L;
     const T* base = X + (int64_t)p * V;
@@ -163,23 +176,16 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
 #pragma unroll
       for (int u = 0; u < 4; ++u) w[u] = *(const u32x4*)(base + (i + u * step) * ldx);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float f[V];
-        unpack16(w[u], f, (T*)nullptr);
-#pragma unroll
-        for (int e = 0; e < V; ++e) m[e] = max(m[e], __float_as_uint(f[e]) & 0x7fffffffu);
-      }
+      for (int u = 0; u < 4; ++u) take(w[u]);
     }
-    for (; i < N; i += step) {
-      float f[V];
-      unpack16(*(const u32x4*)(base + i * ldx), f, (T*)nullptr);
-#pragma unroll
-      for (int e = 0; e < V; ++e) m[e] = max(m[e], __float_as_uint(f[e]) & 0x7fffffffu);
-    }
+    for (; i < N; i += step) take(*(const u32x4*)(base + i * ldx));
   }
   for (int o = L; o < 64; o <<= 1)
 #pragma unroll
-    for (int e = 0; e < V; ++e) m[e] = max(m[e], (uint32_t)__shfl_xor((int)m[e], o, 64));
+    for (int e = 0; e < V; ++e) {
+      m[e] = max(m[e], (uint32_t)__shfl_xor((int)m[e], o, 64));
+      if constexpr (SQ) q[e] += __shfl_xor(q[e], o, 64);
+    }
   __shared__ uint32_t red[4][64 * V];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane < L)
@@ -190,10 +196,22 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
     const uint32_t v = max(max(red[0][j], red[1][j]), max(red[2][j], red[3][j]));
     if (v) atomicMax(out + j, v);
   }
+  if constexpr (SQ) {
+    __syncthreads();
+    float* rf = (float*)&red[0][0];
+    if (lane < L)
+#pragma unroll
+      for (int e = 0; e < V; ++e) rf[wv * 64 * V + lane * V + e] = q[e];
+    __syncthreads();
+    for (int j = threadIdx.x; j < NP * V; j += 256) {
+      const double v = (double)rf[j] + rf[64 * V + j] + rf[128 * V + j] + rf[192 * V + j];
+      if (v != 0.0) atomicAdd(sumsq + j, v);
+    }
+  }
 }
 
 hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
-                             hipStream_t s) {
+                             hipStream_t s, double* sumsq) {
   const int V = dtype == DT_BF16 ? 8 : 4;
   const int NP = D / V;
   if (N <= 0 || D % V || NP > 64 || NP < 1) return N <= 0 ? hipSuccess : hipErrorInvalidValue;
@@ -202,12 +220,14 @@ hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t
   const int R = 256 / L;
   int64_t nb = (N + R - 1) / R;
   if (nb > 2048) nb = 2048;  // 8 per CU; each streams its rows with 4 loads in flight per lane
-  if (dtype == DT_BF16)
-    hipLaunchKernelGGL(col_absmax_kernel<uint16_t>, dim3((unsigned)nb), dim3(256), 0, s,
-                       (const uint16_t*)X, N, NP, L, ldx, out);
-  else
-    hipLaunchKernelGGL(col_absmax_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s,
-                       (const float*)X, N, NP, L, ldx, out);
+  const dim3 g((unsigned)nb), b(256);
+  if (dtype == DT_BF16) {
+    if (sumsq) hipLaunchKernelGGL((col_absmax_kernel<uint16_t, true>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, sumsq);
+    else hipLaunchKernelGGL((col_absmax_kernel<uint16_t, false>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, sumsq);
+  } else {
+    if (sumsq) hipLaunchKernelGGL((col_absmax_kernel<float, true>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, sumsq);
+    else hipLaunchKernelGGL((col_absmax_kernel<float, false>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, sumsq);
+  }
   return hipGetLastError();
 }
 

@@ -74,7 +74,12 @@ struct UpdateArgs {
   const float* weights;  // optional per-row weights (sample_weight)
   const int* col_exp;    // [D] column d's contributions are rne(x * w * 2^col_exp[d]), |.| <= 2^20
   int cnt_exp;           // counts scale 2^cnt_exp (0 when unweighted)
-  int clamp;             // saturate contributions outside +-2^21 (streamed data)
+  int clamp;             // saturate contributions outside +-2^20 (streamed data) ...
+  int* clamp_count = nullptr;  // ... and count the workgroups that did (optional)
+  // Residual (lo) pass of wide-range columns (optional): contributions are
+  // rne((x*w*2^col_exp - rne(x*w*2^col_exp)) * 2^(col_exp2 - col_exp)) on columns with
+  // col_exp2 > -200, nothing elsewhere; slices without such a column are skipped.
+  const int* col_exp2 = nullptr;
   // Incremental M-step (optional): rows whose label changed since the last M-step, as
   // (row, previous label) pairs from launch_label_delta.  Each is added to its new
   // label and subtracted from its old one; when *dcount > dcap the list overflowed
@@ -103,6 +108,9 @@ hipError_t launch_reduce(const long long* slab, const long long* cnt_slab, int n
                          int dcap = 0);
 // With `tot` ([K*D + K] int64, persistent across iterations): tot += slab sums (or
 // tot = slab sums when *dcount > dcap), and the message is built from tot.
+// out[k*nw + j] = 2^-exps[j] * sum_c slab[c][k][cols[j]]  (wide-column lo sums)
+hipError_t launch_reduce_cols(const long long* slab, int n_chunks, int K, int D, const int* cols,
+                              const int* exps, int nw, double* out, hipStream_t s);
 
 // ---- finalize (new centroids + shift + re-pack) -------------------------------
 enum FinalizeMode : int { FIN_PACK_ONLY = 0, FIN_LLOYD = 1, FIN_MINIBATCH = 2 };
@@ -122,7 +130,7 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 
 // ---- row squared norms -------------------------------------------------------
 hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
-                             hipStream_t s);
+                             hipStream_t s, double* sumsq = nullptr);
 hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t ldx, float* out,
                              hipStream_t s);
 

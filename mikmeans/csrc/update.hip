@@ -70,12 +70,26 @@ __device__ __forceinline__ void unpack_any(const typename LoadT<BYTES>::type& w,
 }
 
 // bits of (1.5*2^23 + rne(v * sc)); exact while |v * sc| <= 2^22.  CLAMP saturates
-// out-of-range contributions (streams whose scale came from an earlier batch).
+// out-of-range contributions at +-2^20 (streams whose scale came from an earlier
+// batch), the bound FX_LIM's no-wrap guarantee assumes; the caller tracks the raw
+// range (rlo, rhi) so a batch that clamped is reported instead of kept silently.
+constexpr float FX_QMAX = 1048576.f;  // 2^FX_BITS
 template <bool CLAMP>
-__device__ __forceinline__ uint32_t fx_bits(float v, float sc) {
-  float r = __builtin_fmaf(v, sc, FX_MAGIC);
-  if constexpr (CLAMP) r = __builtin_amdgcn_fmed3f(r, FX_MAGIC - 2097152.f, FX_MAGIC + 2097152.f);
+__device__ __forceinline__ float fx_raw(float v, float sc) { return __builtin_fmaf(v, sc, FX_MAGIC); }
+template <bool CLAMP>
+__device__ __forceinline__ uint32_t fx_clamp(float r) {
+  if constexpr (CLAMP) r = __builtin_amdgcn_fmed3f(r, FX_MAGIC - FX_QMAX, FX_MAGIC + FX_QMAX);
   return __float_as_uint(r);
+}
+template <bool CLAMP>
+__device__ __forceinline__ uint32_t fx_bits(float v, float sc) { return fx_clamp<CLAMP>(fx_raw<CLAMP>(v, sc)); }
+// Residual pass (wide-range columns): bits of 1.5*2^23 + rne((v*sc - rne(v*sc)) * sc2).
+// v*sc - rne(v*sc) is exact in f32 (|.| <= 1/2), so the hi pass (col_exp) plus this lo
+// pass (col_exp + 20) quantise x to 2^-41 of its column maximum instead of 2^-21.
+__device__ __forceinline__ uint32_t fx_bits_resid(float v, float sc, float sc2) {
+  const float hi = __builtin_fmaf(v, sc, FX_MAGIC) - FX_MAGIC;
+  const float res = __builtin_fmaf(v, sc, -hi);
+  return __float_as_uint(__builtin_fmaf(res, sc2, FX_MAGIC));
 }
 
 __device__ __forceinline__ long long fx_q(float v, float sc) {
@@ -192,7 +206,7 @@ __device__ void upd_flush_all(const UpdateArgs& a, const UpdLayout& L, char* m, 
   }
 }
 
-enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8, UPD_NTLOAD = 16 };
+enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8, UPD_NTLOAD = 16, UPD_RESID = 32 };
 
 constexpr int upd_ksh(int np) { return np >= 32 ? 0 : np == 16 ? 1 : np == 8 ? 2 : np == 4 ? 3 : np == 2 ? 4 : 5; }
 __host__ __device__ static inline size_t upd_lds_bytes(int K, int ldc, bool weighted) {
@@ -211,6 +225,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   constexpr bool W = MODE & (UPD_WEIGHTED | UPD_DELTA);  // per-row signed weights
   constexpr bool SWZ = MODE & UPD_SWZ;
   constexpr bool NTL = MODE & UPD_NTLOAD;                // non-temporal X stream (A/B)
+  constexpr bool RESID = MODE & UPD_RESID;               // lo pass of the wide-range columns
   constexpr int ES = sizeof(T);
   constexpr int PB = (SW * ES >= 16) ? 16 : SW * ES;  // bytes per lane load
   constexpr int V = PB / ES;                           // elements per lane load (even)
@@ -234,6 +249,11 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   const int j = b >> 3;
   const int slice = j % n_slices;
   const int chunk = (j / n_slices) * 8 + (b & 7);
+  if constexpr (RESID) {  // slices without a wide-range column have nothing to add
+    bool any = false;
+    for (int c = slice * SW; c < slice * SW + SW && c < a.D; ++c) any |= a.col_exp2[c] > -200;
+    if (!any) return;
+  }
 
   {
     unsigned long long* z = cells;
@@ -265,9 +285,15 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   const bool counter = lp == 0;
   const bool wcounter = W && counter && slice == 0;
   const float cscale = ldexpf(1.f, a.cnt_exp);
-  float sc[V];
+  float sc[V], sc2[V];
 #pragma unroll
-  for (int e = 0; e < V; ++e) sc[e] = (col + e < a.D) ? ldexpf(1.f, a.col_exp[col + e]) : 0.f;
+  for (int e = 0; e < V; ++e) {
+    sc[e] = (col + e < a.D) ? ldexpf(1.f, a.col_exp[col + e]) : 0.f;
+    // lo-pass scale 2^(col_exp2 - col_exp): 2^20 on wide columns, 0 elsewhere
+    sc2[e] = (RESID && col + e < a.D && a.col_exp2[col + e] > -200)
+                 ? ldexpf(1.f, a.col_exp2[col + e] - a.col_exp[col + e]) : 0.f;
+  }
+  float rlo = FX_MAGIC, rhi = FX_MAGIC;  // raw contribution range seen (CLAMP: clamp report)
 
   // Row mapping: in a period starting at `base`, lane (lr, lp) owns the UNR
   // consecutive rows base + lr*UNR + u, so runs of equal labels (sorted or
@@ -355,8 +381,17 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
       for (int e = 0; e < V; e += 2) {
         const float s0 = W ? sc[e] * wt_[u] : sc[e];
         const float s1 = W ? sc[e + 1] * wt_[u] : sc[e + 1];
-        v[e / 2] = (unsigned long long)fx_bits<CLAMP>(f[e], s0) |
-                   ((unsigned long long)fx_bits<CLAMP>(f[e + 1], s1) << 32);
+        if constexpr (RESID)
+          v[e / 2] = (unsigned long long)fx_bits_resid(f[e], s0, sc2[e]) |
+                     ((unsigned long long)fx_bits_resid(f[e + 1], s1, sc2[e + 1]) << 32);
+        else {
+          const float r0 = fx_raw<CLAMP>(f[e], s0), r1 = fx_raw<CLAMP>(f[e + 1], s1);
+          if constexpr (CLAMP) {
+            rlo = fminf(fminf(rlo, r0), r1);
+            rhi = fmaxf(fmaxf(rhi, r0), r1);
+          }
+          v[e / 2] = (unsigned long long)fx_clamp<CLAMP>(r0) | ((unsigned long long)fx_clamp<CLAMP>(r1) << 32);
+        }
       }
       if constexpr (W)
         if (wcounter)  // weighted counts: one add per row (slice 0 only)
@@ -409,6 +444,12 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
     }
   }
   upd_flush_all<SW>(a, L, smem, slice, chunk);
+  if constexpr (CLAMP) {
+    if (a.clamp_count) {
+      const unsigned long long any = __ballot(!(rlo >= FX_MAGIC - FX_QMAX && rhi <= FX_MAGIC + FX_QMAX));
+      if (any && (threadIdx.x & 63) == __builtin_ctzll(any)) atomicAdd(a.clamp_count, 1);
+    }
+  }
 }
 
 // Fallback for K too large to privatise even 2 columns: direct int64 global atomics
@@ -550,6 +591,15 @@ template <typename T, int SW>
 static hipError_t launch_clamp(const UpdateArgs& a, int ldc, hipStream_t s) {
   const int mode = (a.clamp ? UPD_CLAMP : 0) | (a.weights ? UPD_WEIGHTED : 0) |
                    (ldc == SW / 2 ? UPD_SWZ : 0);
+  if (a.col_exp2) {  // residual (lo) pass of the wide-range columns: never clamped / incremental
+    if (a.clamp || a.dlist) return hipErrorInvalidValue;
+    switch (mode) {
+      case 0: return launch_sw<T, SW, UPD_RESID>(a, ldc, s);
+      case 2: return launch_sw<T, SW, UPD_RESID | UPD_WEIGHTED>(a, ldc, s);
+      case 4: return launch_sw<T, SW, UPD_RESID | UPD_SWZ>(a, ldc, s);
+      default: return launch_sw<T, SW, UPD_RESID | UPD_WEIGHTED | UPD_SWZ>(a, ldc, s);
+    }
+  }
   if (a.dlist) {  // incremental M-step (Lloyd: never clamped; weights read at run time)
     if (a.clamp) return hipErrorInvalidValue;
     return (mode & UPD_SWZ) ? launch_sw<T, SW, UPD_DELTA | UPD_SWZ>(a, ldc, s)
@@ -591,6 +641,7 @@ hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s) {
   const int sw = choose_sw(dtype, a.K, a.D, a.weights != nullptr || a.dlist != nullptr, &ldc);
   if (sw > 0 && a.n_chunks % 8) return hipErrorInvalidValue;
   if (a.dlist && sw == 0) return hipErrorInvalidValue;  // no incremental global fallback
+  if (a.col_exp2 && sw == 0) return hipErrorInvalidValue;  // residual pass needs the LDS path
   return dtype == DT_BF16 ? launch_update_t<uint16_t>(a, s, sw, ldc)
                           : launch_update_t<float>(a, s, sw, ldc);
 }
@@ -658,6 +709,33 @@ hipError_t launch_reduce(const long long* slab, const long long* cnt_slab, int n
   const unsigned nb = (unsigned)((total + 255) / 256);
   hipLaunchKernelGGL(reduce_kernel, dim3(nb), dim3(256), 0, s, slab, cnt_slab, n_chunks, K, D,
                      col_exp, ldexp(1.0, -cnt_exp), slots, packed, tot, dcount, dcap);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// launch_reduce_cols: out[k*nw + j] = 2^-exps[j] * sum_c slab[c][k][cols[j]] (f64, exact:
+// integer partials below 2^53) -- the lo sums of the wide-range columns, appended to the
+// all-reduce message and added onto the hi sums after it.
+__global__ __launch_bounds__(256) void reduce_cols_kernel(const long long* __restrict__ slab, int n_chunks,
+                                                          int K, int D, const int* __restrict__ cols,
+                                                          const int* __restrict__ exps, int nw,
+                                                          double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)K * nw) return;
+  const int k = (int)(e / nw), j = (int)(e % nw);
+  const int64_t KD = (int64_t)K * D;
+  const long long* src = slab + (int64_t)k * D + cols[j];
+  long long acc = 0;
+  for (int c = 0; c < n_chunks; ++c) acc += src[(int64_t)c * KD];
+  out[e] = ldexp((double)acc, -exps[j]);
+}
+
+hipError_t launch_reduce_cols(const long long* slab, int n_chunks, int K, int D, const int* cols,
+                              const int* exps, int nw, double* out, hipStream_t s) {
+  const int64_t total = (int64_t)K * nw;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, slab,
+                     n_chunks, K, D, cols, exps, nw, out);
   return hipGetLastError();
 }
 

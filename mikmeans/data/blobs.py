@@ -145,7 +145,7 @@ class BlobStream:
                  seed=0, dtype=torch.float32, device="cpu", rank=0, world=1, offset=0,
                  with_norms: bool = False, prefetch: bool = False):
         self.n_total, self.d, self.batch = n_total, d, batch
-        self.std, self.seed, self.dtype = std, seed, dtype
+        self.std, self.seed, self.dtype, self.box = std, seed, dtype, box
         self.device = torch.device(device)
         self.rank, self.world, self.offset = rank, world, offset
         self.centers = blob_centers(n_centers, d, box, seed, device=self.device)
@@ -163,6 +163,13 @@ class BlobStream:
         self._pf = None          # (X, norms, ready event) of the batch generated ahead
         self._pool = []
         self._side = torch.cuda.Stream(device=self.device) if self.prefetch else None
+
+    @property
+    def value_bound(self) -> float:
+        """A bound on |x| of every generated value: centres lie in [-box, box], the
+        Box-Muller normals in [-5.78, 5.78] (uniforms are >= 2^-24, -2 ln 2^-24 < 33.3),
+        plus one bf16 rounding step."""
+        return float((self.box + 6.0 * abs(self.std)) * (1.0 + 2.0**-7))
 
     def __iter__(self):
         return self

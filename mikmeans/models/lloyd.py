@@ -159,15 +159,28 @@ class LloydEngine:
         if self.n:
             C.row_sqnorm(self.X, self.xn)
         # fixed-point scale of the M-step accumulators (X is static for the fit)
-        from ..ops import fixed_exps
+        from ..ops import MStepScales, mstep_scales
 
-        # (global column maxima: every rank uses the same scale -> exact, world-size independent sums)
-        self.col_exp, self.cnt_exp = fixed_exps(self.X, self.weights, comm=self.comm)
+        # (global column maxima: every rank uses the same scale -> exact, world-size independent
+        # sums; columns whose max is far above their RMS also get a residual lo pass)
+        n_glob = torch.tensor([float(self.n)], dtype=torch.float64, device=dev)
+        self.comm.allreduce_(n_glob)
+        self.scales = mstep_scales(self.X, self.weights, comm=self.comm, n_global=int(n_glob.item()))
+        if self.scales.nw and C.update_slice_width(self.dt, self.K, self.Dp, self.weights is not None) == 0:
+            self.scales = MStepScales(self.scales.col_exp, self.scales.cnt_exp, [], dev)
+        self.col_exp, self.cnt_exp = self.scales.col_exp, self.scales.cnt_exp
+        if self.scales.nw:
+            # message tail: the wide columns' lo sums [K, nw], added onto the hi sums after the all-reduce
+            self.packed = torch.zeros(self.K * self.Dp + self.K + 2 + self.K * self.scales.nw,
+                                      dtype=torch.float64, device=dev)
         if self.weights is not None:
             self.mind = torch.empty(self.n, dtype=torch.float32, device=dev)
         self.delta = None
         if self.incremental:
-            if self.segments > 1 or self.n >= 2**31 or C.update_slice_width(self.dt, self.K, self.Dp, True) == 0:
+            if self.scales.nw:
+                native.warn_once(f"{self.scales.nw} wide-range column(s): residual M-step pass, full passes "
+                                 "instead of the incremental M-step")
+            elif self.segments > 1 or self.n >= 2**31 or C.update_slice_width(self.dt, self.K, self.Dp, True) == 0:
                 native.warn_once("incremental M-step unavailable for this shape/overlap mode; using full passes")
             else:
                 cap = max(1, min(self.n, int(self.n * self.delta_cap)))
@@ -287,8 +300,18 @@ class LloydEngine:
                 self.packed[KD + self.K] = (self.mind.double() * self.weights.double()).sum()
         else:
             self.packed.zero_()
+        sc = self.scales
+        if sc.nw and self.n:  # residual (lo) pass of the wide-range columns into the message tail
+            C.update(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks, self.weights,
+                     self.col_exp, self.cnt_exp, False, col_exp2=sc.col_exp2)
+            C.reduce_cols(self.slab, self.n_chunks, self.K, self.Dp, sc.wide_cols, sc.wide_exps,
+                          self.packed[KD + self.K + 2:])
         with _phase("mikmeans.allreduce"):
             self.comm.allreduce_(self.packed)
+        if sc.nw:
+            from ..ops import add_wide_lo
+
+            add_wide_lo(self.packed, self.K, self.Dp, sc)
         with _phase("mikmeans.finalize"):
             self._relocate_empty()
             self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts)

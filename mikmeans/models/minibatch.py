@@ -36,7 +36,8 @@ class MiniBatchEngine:
         self.vcount = torch.zeros(self.K, dtype=torch.float64, device=self.device)
         self.shift = torch.zeros(self.K, dtype=torch.float32, device=self.device)
         self.counts = torch.zeros(self.K, dtype=torch.float32, device=self.device)
-        self.packed = torch.zeros(self.K * self.Dp + self.K + 2, dtype=torch.float64, device=self.device)
+        # [K*D sums | K counts | inertia | changed | clamped-workgroup count]
+        self.packed = torch.zeros(self.K * self.Dp + self.K + 3, dtype=torch.float64, device=self.device)
         self.frozen = None
         if frozen is not None:
             self.frozen = torch.as_tensor(frozen, dtype=torch.uint8).reshape(-1).to(self.device)
@@ -57,8 +58,14 @@ class MiniBatchEngine:
             self.n_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, self.batch)
             self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.int64, device=dev)
             self.cnt_slab = torch.empty(self.n_chunks * self.K, dtype=torch.int64, device=dev)
-            self.col_exp = None  # fixed-point scales, set from the first batch (x8 headroom)
+            # fixed-point scales: from the first batch (x8 headroom) or the given value bound; a
+            # later batch beyond them is detected on device (clamp count) and redone with scales
+            # grown from its own column maxima -- never saturated silently
+            self.col_exp = None
+            self.bound = None    # per-column |x| bound [D] f64 the scales were made for
+            self.rescales = 0    # batches redone with a wider scale
             self.value_bound = value_bound
+            self.clampc = torch.zeros(1, dtype=torch.int32, device=dev)
             self.labels = torch.empty(self.batch, dtype=torch.int32, device=dev)
             self.xn = torch.empty(self.batch, dtype=torch.float32, device=dev)
 
@@ -86,6 +93,35 @@ class MiniBatchEngine:
         self.C, self.Cnew = self.Cnew, self.C
         self.steps += 1
 
+    def _set_bound(self, Xb, grow: bool = False):
+        from ..ops import col_max_abs, fixed_exps
+
+        if self.value_bound is not None:
+            bound = torch.full((self.Dp,), float(self.value_bound), dtype=torch.float64, device=self.device)
+        else:
+            # all-zero columns get the finest scale; a later nonzero value there is a clamp -> regrow
+            bound = 8.0 * col_max_abs(Xb).clamp_min(1e-30)
+            if grow and self.bound is not None:
+                bound = torch.maximum(bound, self.bound)
+        self.col_exp, _ = fixed_exps(Xb, None, comm=self.comm, bound=bound)   # bound all-reduced (MAX)
+        self.bound = bound
+
+    def _mstep(self, Xb, lab):
+        C = self._C
+        KD = self.K * self.Dp
+        if Xb.shape[0]:
+            # a given value bound cannot be exceeded: no clamp, no count (the plain kernel)
+            bounded = self.value_bound is not None
+            C.update(Xb, lab, self.K, self.slab, self.cnt_slab, self.n_chunks, None, self.col_exp, 0,
+                     not bounded, clamp_count=None if bounded else self.clampc)
+            C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
+                     self.col_exp, 0)
+            self.packed[KD + self.K + 2] = self.clampc[0].double()
+            self.clampc.zero_()
+        else:
+            self.packed.zero_()
+        self.comm.allreduce_(self.packed)
+
     def _step_gpu(self, Xb, norms=None):
         C = self._C
         Xb = pad_columns(Xb.to(self.device), self.dtype)
@@ -93,29 +129,28 @@ class MiniBatchEngine:
         if b > self.batch:
             raise ValueError(f"batch of {b} rows exceeds the engine's batch_size {self.batch}")
         if self.col_exp is None:
-            # one host read for the whole stream: per column |x| <= 8 x (first batch's max) or the
-            # given bound; contributions beyond it saturate (clamp) instead of wrapping
-            from ..ops import col_max_abs, fixed_exps
-
-            if self.value_bound is not None:
-                bound = torch.full((self.Dp,), float(self.value_bound), dtype=torch.float64)
-            else:
-                bound = 8.0 * col_max_abs(Xb).clamp_min(1e-30)
-            self.col_exp, _ = fixed_exps(Xb, None, comm=self.comm, bound=bound)
+            self._set_bound(Xb)
+        lab = self.labels[:b]
         if b:
-            lab = self.labels[:b]
             if norms is not None and norms.shape[0] >= b and norms.dtype == torch.float32 and norms.is_cuda:
                 xn = norms[:b].contiguous()
             else:
                 xn = self.xn[:b]
                 C.row_sqnorm(Xb, xn)
             self.pk.assign(Xb, xn, lab, None, self.slots, False)
-            C.update(Xb, lab, self.K, self.slab, self.cnt_slab, self.n_chunks, None, self.col_exp, 0, True)
-            C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
-                     self.col_exp, 0)
-        else:
-            self.packed.zero_()
-        self.comm.allreduce_(self.packed)
+        self._mstep(Xb, lab)
+        if self.value_bound is None:
+            # one host read per step: the all-reduced clamp count is the same on every rank,
+            # so all ranks agree to redo this batch with scales grown from its maxima
+            KD = self.K * self.Dp
+            if float(self.packed[KD + self.K + 2].item()) > 0:
+                inertia = self.packed[KD + self.K].clone()
+                self.rescales += 1
+                self._set_bound(Xb, grow=True)
+                self._mstep(Xb, lab)
+                self.packed[KD + self.K] = inertia   # the assign's slots were consumed by the first reduce
+                if float(self.packed[KD + self.K + 2].item()) > 0:
+                    raise RuntimeError("mini-batch M-step still saturates after rescaling (non-finite data?)")
         self.pk.finalize(2, self.packed, self.C, self.Cnew, self.frozen, self.vcount, self.shift,
                          self.counts)
 

@@ -93,6 +93,16 @@ class OrderedMeta:
         return dict(self.items())
 
 
+def _js_strict_ne(a, b) -> bool:
+    """JavaScript ``a !== b`` for JSON values: objects/arrays compare by identity, a
+    boolean never equals a number, 3 === 3.0."""
+    if isinstance(a, (dict, list)) or isinstance(b, (dict, list)):
+        return a is not b
+    if isinstance(a, bool) != isinstance(b, bool):
+        return True
+    return a != b
+
+
 class Room:
     def __init__(self, room_id: str | None = None, *, user: str | None = None, seed: int | None = None,
                  clock=None, max_centroids: int = MAX_CENTROIDS, seed_jessica: bool = True):
@@ -105,6 +115,9 @@ class Room:
         self.centroids: list[dict] = []
         self.meta = OrderedMeta()
         self._last_iter = None
+        # the #mode <select>'s value: syncMeta (app.mjs:299) copies a truthy meta mode into
+        # it; hardReset reads it back (app.mjs:231)
+        self._mode_select = "learn"
         self.log: list[tuple] = []  # applied operations (for replication)
         if seed_jessica:
             self.ensure_jessica_once()
@@ -295,24 +308,45 @@ class Room:
         self.dedupe_seeds()
         self.log.append(("populate_test_data",))
 
-    def hard_reset(self, mode: str = "learn"):
+    def hard_reset(self, mode: str | None = None):
+        """Clear the board, re-seed Jessica (app.mjs:225-237).  The mode written is the
+        current mode selector's value (``mode`` overrides it), and the iteration hook then
+        runs as the reference's observer does after the transaction (app.mjs:498-505):
+        resetting from a nonzero iteration snapshots the fresh board as ``prevSnapshot``."""
+        mode = self._mode_select if mode is None else mode
         for k in self.meta.keys():
             if str(k).startswith("pos:"):
                 self.meta.delete(k)
         self.cards = []
         self.centroids = []
         self.meta.set("iteration", 0)
-        self.meta.set("mode", mode or "learn")
+        self._set_meta_mode(mode or "learn")
         self.meta.set("seededJessica", False)
         self.cards.append({**JESSICA, "traits": list(JESSICA["traits"]), "assignedTo": None, "createdBy": "seed"})
         self.meta.set("seededJessica", True)
         self.meta.delete("prevSnapshot")
-        self._last_iter = 0
+        self._iteration_hook()
         self.log.append(("hard_reset", mode))
 
     # ------------------------------------------------------------- meta / iter
-    def set_mode(self, mode: str):
+    MODES = ("learn", "playtest", "custom")   # the <select>'s options (index.html:125-127)
+
+    def _set_meta_mode(self, mode):
         self.meta.set("mode", mode)
+        if mode:  # syncMeta: a truthy mode is copied into the select ("" if no option matches)
+            self._mode_select = mode if mode in self.MODES else ""
+
+    def _iteration_hook(self):
+        """The meta observer (app.mjs:498-505), run after any transaction that set
+        ``iteration``: when it differs from the last seen value (JS ``!==``; arrays and
+        objects never compare equal), the current metrics become ``prevSnapshot``."""
+        cur = self.meta.get("iteration")
+        if _js_strict_ne(cur, self._last_iter):
+            self.meta.set("prevSnapshot", self.snapshot_metrics())
+            self._last_iter = cur
+
+    def set_mode(self, mode: str):
+        self._set_meta_mode(mode)
 
     def set_iteration(self, value):
         """Advance the iteration label; on change, freeze the current metrics as
@@ -322,9 +356,7 @@ class Room:
         except (TypeError, ValueError):
             it = 0
         self.meta.set("iteration", it)
-        if it != self._last_iter:
-            self.meta.set("prevSnapshot", self.snapshot_metrics())
-            self._last_iter = it
+        self._iteration_hook()
 
     # ---------------------------------------------------------------- metrics
     def members(self, cid: str) -> list[dict]:
@@ -395,9 +427,16 @@ class Room:
         meta = data.get("meta")
         if isinstance(meta, dict):
             for k, v in meta.items():
-                self.meta.set(k, v)
+                if k == "mode":
+                    self._set_meta_mode(v)
+                else:
+                    self.meta.set(k, v)
+            # the observer runs at the end of the import transaction, before dedupeSeeds
+            # (app.mjs:272-279): an imported iteration that differs from the last seen one
+            # overwrites the imported prevSnapshot with the (pre-dedupe) board's metrics
+            if "iteration" in meta:
+                self._iteration_hook()
         self.dedupe_seeds()
-        self._last_iter = self.meta.get("iteration")
         self.log.append(("import",))
 
     @classmethod

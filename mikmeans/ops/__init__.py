@@ -159,19 +159,43 @@ def max_abs(X: torch.Tensor) -> float:
     return max(abs(float(mn)), abs(float(mx)))
 
 
+def _native_colstats_ok(X: torch.Tensor) -> bool:
+    v = 16 // X.element_size()
+    return (X.is_cuda and X.dtype in (torch.float32, torch.bfloat16) and X.dim() == 2 and X.stride(1) == 1
+            and X.shape[1] % v == 0 and X.shape[1] // v <= 64 and (X.shape[0] <= 1 or X.stride(0) % v == 0)
+            and X.data_ptr() % 16 == 0)
+
+
 def col_max_abs(X: torch.Tensor) -> torch.Tensor:
     """Per-column max |x| as float64 ``[D]`` (no |X| temporary)."""
+    return col_stats(X, sumsq=False)[0]
+
+
+def col_stats(X: torch.Tensor, sumsq: bool = True):
+    """``(max |x|, sum |x|)`` per column as float64 ``[D]`` tensors (the second is None
+    unless ``sumsq``): one streaming pass on the GPU (csrc/finalize.hip col_absmax)."""
     if X.shape[0] == 0:
-        return torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
-    if X.is_cuda and X.dtype in (torch.float32, torch.bfloat16):
-        v = 16 // X.element_size()
-        if (X.dim() == 2 and X.stride(1) == 1 and X.shape[1] % v == 0 and X.shape[1] // v <= 64
-                and (X.shape[0] <= 1 or X.stride(0) % v == 0) and X.data_ptr() % 16 == 0):
-            out = torch.zeros(X.shape[1], dtype=torch.int32, device=X.device)
-            require().col_absmax(X, out)   # one streaming pass (csrc/finalize.hip)
-            return out.view(torch.float32).double()
+        z = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
+        return z, (z.clone() if sumsq else None)
+    if _native_colstats_ok(X):
+        out = torch.zeros(X.shape[1], dtype=torch.int32, device=X.device)
+        ss = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device) if sumsq else None
+        require().col_absmax(X, out, ss)
+        return out.view(torch.float32).double(), ss
     mn, mx = torch.aminmax(X, dim=0)
-    return torch.maximum(mn.double().abs(), mx.double().abs())
+    m = torch.maximum(mn.double().abs(), mx.double().abs())
+    ss = None
+    if sumsq:
+        ss = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
+        for i in range(0, X.shape[0], 1 << 20):
+            ss += X[i : i + (1 << 20)].to(torch.float64).abs().sum(0)
+    return m, ss
+
+
+# A column whose max |x| exceeds WIDE_RATIO x its mean |x| gets the residual (lo) M-step pass:
+# its contributions are then exact to 2^-41 (not 2^-21) of the column maximum, so one
+# outlier no longer coarsens every other point's contribution (csrc/update.hip UPD_RESID).
+WIDE_RATIO = 256.0
 
 
 def fixed_exps(X: torch.Tensor, weights: torch.Tensor | None = None, comm=None, bound=None):
@@ -182,18 +206,72 @@ def fixed_exps(X: torch.Tensor, weights: torch.Tensor | None = None, comm=None, 
     weighted counts.  ``bound`` (per-column float64 ``[D]``) overrides the data's
     column maxima; with ``comm`` the maxima are all-reduced so every rank uses the
     same scale (exact, world-size independent sums)."""
+    sc = mstep_scales(X, weights, comm=comm, bound=bound, wide_ratio=0)
+    return sc.col_exp, sc.cnt_exp
+
+
+class MStepScales:
+    """Fixed-point scales of one fit's M-step plus its wide-range columns.
+
+    ``col_exp``/``cnt_exp`` as in :func:`fixed_exps`; ``wide_cols`` (int32 ``[nw]``) are
+    the columns with max |x| > ``wide_ratio`` x mean |x|, ``wide_exps`` their lo-pass
+    exponents (``col_exp + 20``) and ``col_exp2`` the kernel's per-column form (-1000
+    = no lo pass)."""
+
+    def __init__(self, col_exp, cnt_exp, wide_cols, device):
+        self.col_exp, self.cnt_exp = col_exp, cnt_exp
+        wc = sorted(int(c) for c in wide_cols)
+        ce = col_exp.cpu()
+        self.wide_cols = torch.tensor(wc, dtype=torch.int32, device=device)
+        self.wide_exps = torch.tensor([int(ce[c]) + 20 for c in wc], dtype=torch.int32, device=device)
+        e2 = torch.full_like(ce, -1000)
+        for c in wc:
+            e2[c] = int(ce[c]) + 20
+        self.col_exp2 = e2.to(device)
+        self.nw = len(wc)
+
+
+def mstep_scales(X: torch.Tensor, weights: torch.Tensor | None = None, comm=None, bound=None,
+                 n_global: int | None = None, wide_ratio: float | None = None) -> MStepScales:
+    """Scales of the fixed-point M-step (global over ranks) and the wide-range columns."""
     C = require()
-    m = col_max_abs(X) if bound is None else bound.to(device=X.device, dtype=torch.float64)
+    ratio = WIDE_RATIO if wide_ratio is None else float(wide_ratio)
+    want_ss = bound is None and ratio > 0
+    if bound is None:
+        m, ss = col_stats(X, sumsq=want_ss)
+    else:
+        m, ss = bound.to(device=X.device, dtype=torch.float64), None
     wm = torch.zeros(1, dtype=torch.float64, device=X.device)
     if weights is not None and weights.numel():
         wm[0] = max_abs(weights)
     if comm is not None:
         comm.allreduce_max_(m)
         comm.allreduce_max_(wm)
+        if ss is not None:
+            comm.allreduce_(ss)
     w = float(wm.item()) if weights is not None else 1.0
-    exps = [C.fixed_exp(v * w) for v in m.cpu().tolist()]
+    mh = m.cpu()
+    exps = [C.fixed_exp(v * w) for v in mh.tolist()]
     col_exp = torch.tensor(exps, dtype=torch.int32, device=X.device)
-    return col_exp, (C.fixed_exp(w) if weights is not None else 0)
+    wide = []
+    if ss is not None:
+        n = n_global if n_global is not None else X.shape[0]
+        mean_abs = ss.cpu() / max(int(n), 1)
+        wide = [d for d in range(len(exps)) if mh[d] > 0 and mh[d] > ratio * mean_abs[d]
+                and exps[d] + 20 <= 126]  # the lo scale must stay a normal float
+    return MStepScales(col_exp, C.fixed_exp(w) if weights is not None else 0, wide, X.device)
+
+
+def add_wide_lo(packed: torch.Tensor, K: int, D: int, sc: MStepScales) -> None:
+    """After the all-reduce: add the wide columns' lo sums (message tail) onto their hi
+    sums -- one f64 rounding of two exact integer-valued totals, so world-size invariant."""
+    if not sc.nw:
+        return
+    KD = K * D
+    lo = packed[KD + K + 2 : KD + K + 2 + K * sc.nw].view(K, sc.nw)
+    pv = packed[:KD].view(K, D)
+    idx = sc.wide_cols.long()
+    pv.index_copy_(1, idx, pv.index_select(1, idx) + lo)
 
 
 def cluster_sums(X: torch.Tensor, labels: torch.Tensor, K: int, weights: torch.Tensor | None = None):
@@ -207,11 +285,17 @@ def cluster_sums(X: torch.Tensor, labels: torch.Tensor, K: int, weights: torch.T
     nch = C.update_n_chunks(dt, K, D, n, weights is not None)
     slab = torch.empty(nch * K * D, dtype=torch.int64, device=X.device)
     cnt = torch.empty(nch * K, dtype=torch.int64, device=X.device)
-    packed = torch.empty(K * D + K + 2, dtype=torch.float64, device=X.device)
     lab = labels.to(torch.int32).contiguous()
     w = weights.to(torch.float32).contiguous() if weights is not None else None
-    ce_col, ce = fixed_exps(Xp, w)
-    C.update(Xp, lab, K, slab, cnt, nch, w, ce_col, ce, False)
-    C.reduce(slab, cnt, nch, K, D, None, packed, ce_col, ce)
+    sc = mstep_scales(Xp, w, n_global=n)
+    if sc.nw and C.update_slice_width(dt, K, D, w is not None) == 0:
+        sc = MStepScales(sc.col_exp, sc.cnt_exp, [], X.device)  # global-atomic fallback: no lo pass
+    packed = torch.zeros(K * D + K + 2 + K * sc.nw, dtype=torch.float64, device=X.device)
+    C.update(Xp, lab, K, slab, cnt, nch, w, sc.col_exp, sc.cnt_exp, False)
+    C.reduce(slab, cnt, nch, K, D, None, packed, sc.col_exp, sc.cnt_exp)
+    if sc.nw:
+        C.update(Xp, lab, K, slab, cnt, nch, w, sc.col_exp, sc.cnt_exp, False, col_exp2=sc.col_exp2)
+        C.reduce_cols(slab, nch, K, D, sc.wide_cols, sc.wide_exps, packed[K * D + K + 2 :])
+        add_wide_lo(packed, K, D, sc)
     sums = packed[: K * D].view(K, D)[:, : X.shape[1]]
     return sums, packed[K * D : K * D + K]

@@ -19,6 +19,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step pytest_gpu 1200 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread ;;
+    mstep) step pytest_mstep 300 python -u -m pytest tests/test_gpu_mstep.py -x -v --timeout 120 --timeout-method thread ;;
     rccl) step pytest_rccl 300 python -u -m pytest tests/test_gpu_rccl.py -x -v --timeout 120 --timeout-method thread ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
     benchauto) step bench_nopg 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 --pg auto --no-also-incremental ;;

@@ -134,3 +134,22 @@ def test_comm_collectives_world4():
     for o in outs:
         assert o["sum"] == 10 and o["max"] == 3 and o["b"] == "hello"
         assert o["g"].tolist() == [[0, 0], [1, 10], [2, 20], [3, 30]] and o["o"] == [0, 1, 2, 3]
+
+
+def _minibatch_fit_uneven(comm):
+    import mikmeans
+
+    n = 1025
+    X = _data()[:n]
+    s, e = shard_range(n, comm.rank, comm.world)   # shards of 342 / 342 / 341 rows
+    km = mikmeans.MiniBatchKMeans(4, batch_size=64, max_iter=1, seed=2, comm=comm).fit(X[s:e])
+    return {"C": km.cluster_centers_.clone(), "steps": km.n_steps_}
+
+
+def test_minibatch_fit_uneven_shards_same_step_count():
+    """Ranks with different shard sizes must issue the same number of step collectives
+    (steps came from the rank-local n and could deadlock)."""
+    outs = spawn_local(_minibatch_fit_uneven, 3)
+    assert len({o["steps"] for o in outs}) == 1
+    for o in outs:
+        assert torch.equal(o["C"], outs[0]["C"])

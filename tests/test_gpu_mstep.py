@@ -1,0 +1,129 @@
+"""M-step robustness on the GPU: wide-range (outlier) columns, mini-batch scale growth.
+
+The fixed-point scatter-add (csrc/update.hip) quantises every contribution on a
+per-column grid derived from the column maximum.  These tests pin the two ways that
+grid can be wrong -- a single huge outlier coarsening every other row of its column
+(residual lo pass) and a streamed batch exceeding the first batch's range (device
+clamp count + rescale) -- against float64 oracles.
+"""
+import pytest
+import torch
+
+from mikmeans import ops
+from mikmeans.data import blobs as B
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _oracle_means(X, labels, K):
+    Xd = X.double().cpu()
+    lab = labels.long().cpu()
+    s = torch.zeros(K, X.shape[1], dtype=torch.float64).index_add_(0, lab, Xd)
+    c = torch.bincount(lab, minlength=K).double()
+    return s, c
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_outlier_column_sums_exact(native, dtype, weighted):
+    n, d, K = 100_000, 64, 16
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(n, d, generator=g)
+    X[1234, 3] = 1.0e6            # one outlier in an N(0,1) column
+    X[777, 40] = -3.0e5
+    X = X.to(dtype)
+    labels = torch.randint(0, K, (n,), generator=g, dtype=torch.int32)
+    w = torch.rand(n, generator=g) + 0.5 if weighted else None
+    sc = ops.mstep_scales(X.to(DEV), w.to(DEV) if w is not None else None, n_global=n)
+    assert sorted(sc.wide_cols.cpu().tolist()) == [3, 40]
+    s, c = ops.cluster_sums(X.to(DEV), labels.to(DEV), K, w.to(DEV) if w is not None else None)
+    Xd = X.double() * (w.double()[:, None] if weighted else 1.0)
+    s_ref = torch.zeros(K, d, dtype=torch.float64).index_add_(0, labels.long(), Xd)
+    c_ref = torch.zeros(K, dtype=torch.float64).index_add_(0, labels.long(),
+                                                           w.double() if weighted else torch.ones(n, dtype=torch.float64))
+    # centroid error (sum / count) within 1e-5 absolute of the f64 oracle in every column
+    err = ((s.cpu() / c.cpu()[:, None]) - (s_ref / c_ref[:, None])).abs().max().item()
+    assert err <= 1e-5, err
+    torch.testing.assert_close(c.cpu(), c_ref, rtol=1e-6, atol=1e-6)
+
+
+def test_outlier_lloyd_step_matches_f64(native):
+    from mikmeans.models.lloyd import LloydEngine
+
+    n, d, K = 60_000, 32, 8
+    X = B.make_blobs(n, d, K, seed=4)
+    X[100, 5] = 1.0e6
+    C0 = X[torch.arange(K) * 1000 + 7].clone()
+    eng = LloydEngine(X.to(DEV), K, incremental=False).set_centers(C0)
+    assert eng.scales.nw == 1
+    eng.step()
+    labels = eng.labels.cpu()
+    s, c = _oracle_means(X, labels, K)
+    exp = torch.where(c[:, None] > 0, s / c.clamp_min(1)[:, None], C0.double())
+    # within 1e-5 of the f64 oracle, beyond the f32 rounding of the centre itself
+    err = ((eng.centers.cpu().double() - exp).abs() - exp.abs() * 2.0**-24).max().item()
+    assert err <= 1e-5, err
+    # the incremental default falls back to full passes with wide columns and agrees bitwise
+    eng2 = LloydEngine(X.to(DEV), K, incremental=True).set_centers(C0)
+    eng2.step()
+    assert torch.equal(eng.centers, eng2.centers)
+
+
+def test_outlier_lloyd_graph_replay(native):
+    from mikmeans.models.lloyd import LloydEngine
+
+    X = B.make_blobs(40_000, 64, 10, seed=6, dtype=torch.bfloat16, device=DEV)
+    X[5, 9] = 5.0e5
+    C0 = X[:10].float()
+    ea = LloydEngine(X, 10).set_centers(C0)
+    eb = LloydEngine(X, 10).set_centers(C0).capture()
+    for _ in range(3):
+        ea.step()
+        eb.step()
+    torch.cuda.synchronize()
+    assert ea.scales.nw == 1 and torch.equal(ea.centers, eb.centers)
+
+
+def test_update_clamp_count(native):
+    C = native
+    n, d, K = 20_000, 32, 4
+    X = torch.randn(n, d, device=DEV)
+    lab = torch.randint(0, K, (n,), device=DEV, dtype=torch.int32)
+    nch = C.update_n_chunks(ops.dtype_code(torch.float32), K, d, n, False)
+    slab = torch.empty(nch * K * d, dtype=torch.int64, device=DEV)
+    cnt = torch.empty(nch * K, dtype=torch.int64, device=DEV)
+    # scale made for |x| <= 0.5: rows beyond it are clamped and counted, rows within are not
+    col_exp, _ = ops.fixed_exps(X[:1], None, bound=torch.full((d,), 0.5, dtype=torch.float64))
+    cc = torch.zeros(1, dtype=torch.int32, device=DEV)
+    C.update(X, lab, K, slab, cnt, nch, None, col_exp, 0, True, clamp_count=cc)
+    assert int(cc.item()) > 0
+    cc.zero_()
+    col_exp, _ = ops.fixed_exps(X, None)
+    C.update(X, lab, K, slab, cnt, nch, None, col_exp, 0, True, clamp_count=cc)
+    assert int(cc.item()) == 0
+
+
+@pytest.mark.parametrize("case", ["growing", "zero_first"])
+def test_minibatch_rescales_instead_of_saturating(native, case):
+    """A later batch 20x the first batch's range, or a column that is all zero in the
+    first batch: the GPU engine must match the CPU engine (no silent saturation)."""
+    from mikmeans.models.minibatch import MiniBatchEngine
+
+    d, K, b = 32, 6, 2048
+    g = torch.Generator().manual_seed(1)
+    batches = [torch.randn(b, d, generator=g) for _ in range(8)]
+    if case == "growing":
+        batches[4] = batches[4] * 20.0
+    else:
+        batches[0][:, 7] = 0.0
+    C0 = batches[0][:K].clone()
+    ec = MiniBatchEngine(K, d, b)
+    eg = MiniBatchEngine(K, d, b, device=DEV)
+    ec.set_centers(C0)
+    eg.set_centers(C0)
+    for xb in batches:
+        ec.partial_fit(xb)
+        eg.partial_fit(xb.to(DEV))
+    assert eg.rescales >= 1
+    torch.testing.assert_close(eg.centers.cpu(), ec.centers, rtol=1e-4, atol=1e-4)

@@ -221,3 +221,55 @@ def test_cli_room_utilities(tmp_path, capsys):
     assert out[1] in ("Heads", "Tails")
     assert re.fullmatch(r"d12 → ([1-9]|1[0-2])", out[2])
     assert out[3] == "Suggested order:"
+
+
+def test_hard_reset_keeps_current_mode_and_runs_iteration_hook():
+    """hardReset writes the mode selector's value (app.mjs:231) and, when the iteration
+    was nonzero, the observer snapshots the fresh board (app.mjs:230, :498-505)."""
+    r = make_room()
+    r.populate_test_data()
+    a = r.add_centroid("A")
+    r.drop_card("seed:t1", a["id"], 0.5, 0.5)
+    r.set_mode("custom")
+    r.set_iteration(3)
+    r.hard_reset()
+    assert r.meta.get("mode") == "custom" and r.meta.get("iteration") == 0
+    snap = r.meta.get("prevSnapshot")
+    assert snap == r.snapshot_metrics() and snap["counts"] == {}
+    # from iteration 0 the key stays deleted (no change -> no snapshot)
+    r.hard_reset()
+    assert r.meta.get("prevSnapshot") is None and "prevSnapshot" not in r.meta
+    # a mode outside the select's options leaves the select blank -> "learn"
+    r.set_mode("weird")
+    r.hard_reset()
+    assert r.meta.get("mode") == "learn"
+    text = r.export_json()
+    assert '"prevSnapshot"' not in text
+
+
+def test_import_with_new_iteration_overwrites_prev_snapshot():
+    """After an import that changes ``iteration`` the reference's observer replaces the
+    imported prevSnapshot with the imported board's metrics, before dedupeSeeds."""
+    src = make_room()
+    src.populate_test_data()
+    a = src.add_centroid("A")
+    src.drop_card("seed:t1", a["id"], 0.5, 0.5)
+    src.set_iteration(5)
+    src.drop_card("seed:t2", a["id"], 0.5, 0.5)   # board differs from the stored snapshot
+    obj = src.export_obj()
+    obj = {**obj, "cards": obj["cards"] + [dict(obj["cards"][1])]}   # a duplicate seed card
+    text = jsjson.stringify(obj, 2)
+    r = make_room()
+    r.set_iteration(2)
+    r.import_json(text)
+    snap = r.meta.get("prevSnapshot")
+    assert snap != src.meta.get("prevSnapshot")
+    # the snapshot saw the duplicate seed card (pre-dedupe: t1, t2 and t1 again); the board
+    # itself is deduplicated afterwards
+    assert snap["counts"] == {a["id"]: 3} and r._last_iter == 5
+    assert len(r.cards) == len(src.cards) and r.snapshot_metrics()["counts"] == {a["id"]: 2}
+    # same iteration -> the imported snapshot is kept
+    r2 = make_room()
+    r2.set_iteration(5)
+    r2.import_json(src.export_json())
+    assert r2.meta.get("prevSnapshot") == src.meta.get("prevSnapshot")
