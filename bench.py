@@ -131,7 +131,6 @@ def main(argv=None):
             n_changed=st.n_changed,
             # one extra, untimed, event-instrumented iteration
             phase_ms=_phase_breakdown(eng) if (eng.gpu and not args.incremental) else None,
-            assign_layout=eng.pk.layout if eng.gpu else None,
         )
         if args.config == "cfg3" and args.also_incremental and not args.incremental and eng.gpu:
             # The library default (KMeans(incremental=True)) from the same start: identical

@@ -24,7 +24,7 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 BUILD = PKG.parent / "build" / "native"
 ARCH = os.environ.get("MIKMEANS_ARCH", "gfx950")
-HIP_SOURCES = ["assign.hip", "assign16.hip", "assign_res.hip", "update.hip", "finalize.hip", "kpp.hip"]
+HIP_SOURCES = ["assign16.hip", "update.hip", "finalize.hip", "kpp.hip"]
 BINDING = "binding.cpp"
 
 DEVICE_FLAGS = [
@@ -38,9 +38,6 @@ DEVICE_FLAGS = [
     "-amdgpu-mfma-vgpr-form=1",
     "-Wno-unused-result",
 ]
-if os.environ.get("MIKMEANS_AB") == "1":
-    # diagnostic kernel variants for scripts/ab_kernels.py (not in the default build)
-    DEVICE_FLAGS.append("-DMK_AB_VARIANTS")
 
 
 def ext_path() -> Path:

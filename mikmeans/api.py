@@ -440,18 +440,85 @@ class MiniBatchKMeans(_Serving):
         self.labels_ = self.predict(X)
         return self
 
-    def fit_stream(self, stream, steps: int, init_batch: torch.Tensor | None = None):
-        """Fit on an iterator of per-rank batches (e.g. :class:`~mikmeans.data.blobs.BlobStream`)."""
-        first = init_batch if init_batch is not None else next(iter(stream))
-        eng = self._engine(first.shape[1], first.device)
+    def fit_stream(self, stream, steps: int, init_batch: torch.Tensor | None = None, *, resume_from=None,
+                   checkpoint_every: int = 0, checkpoint_dir=None):
+        """Fit on an iterator of per-rank batches (e.g. :class:`~mikmeans.data.blobs.BlobStream`).
+
+        ``steps`` counts the whole run; with ``checkpoint_every`` the state (centres, running
+        counts, fixed-point scales, step and the stream's global row position) is saved
+        every that many steps, and ``resume_from`` continues such a run -- also on another
+        world size: a stream with the same global batch (``batch * world``) then replays the
+        same rows per step and the exact integer M-step gives the same centres (the
+        reference's export/import of the whole board, app.mjs:263-282).  A generic iterator
+        must itself be positioned at the checkpoint's ``stream_pos`` (BlobStream is seeked)."""
+        from .utils import faults
+        from .utils.checkpoint import load_checkpoint
+
+        comm = self.comm or get_comm()
+        if resume_from is not None:
+            ck = load_checkpoint(resume_from, comm=comm)
+            if ck.get("kind") != "minibatch":
+                raise ValueError(f"{resume_from} is not a mini-batch checkpoint")
+            device = torch.device(getattr(stream, "device", None) or self.device or comm.device)
+            eng = self._engine(int(ck["n_features"]), device)
+            eng.load_state(ck["centers"], ck["tensors"], ck["iteration"], ck.get("rescales", 0))
+            if hasattr(stream, "seek"):
+                stream.seek(int(ck["stream_pos"]))
+        else:
+            first = init_batch if init_batch is not None else next(iter(stream))
+            eng = self._engine(first.shape[1], first.device)
+            eng.set_centers(self._init_centers(first.to(self.dtype)))
         if getattr(stream, "value_bound", None) is not None and eng.gpu and eng.col_exp is None:
             eng.value_bound = float(stream.value_bound)   # bounded stream: no per-step clamp check
-        eng.set_centers(self._init_centers(first.to(self.dtype)))
-        for _ in range(steps):
+        while eng.steps < steps:
             Xb = next(stream)
             eng.partial_fit(Xb, getattr(stream, "last_norms", None))
+            faults.maybe_fail(comm.rank, eng.steps)
+            if checkpoint_every and checkpoint_dir and eng.steps % checkpoint_every == 0:
+                self._finish(eng)
+                self._save(checkpoint_dir, comm, stream_pos=stream.position() if hasattr(stream, "position")
+                           else None)
         self._finish(eng)
         return self
+
+    # ------------------------------------------------------------- persist
+    def _save(self, path, comm, stream_pos=None):
+        from .utils.checkpoint import save_checkpoint
+
+        eng = self._eng
+        cfg = {"n_clusters": self.n_clusters, "batch_size": self.batch_size, "max_iter": self.max_iter,
+               "init": self.init if isinstance(self.init, str) else "array", "dtype": str(self.dtype),
+               "seed": self.seed, "tol": self.tol}
+        extra = {"kind": "minibatch", "rescales": getattr(eng, "rescales", 0)}
+        if stream_pos is not None:
+            extra["stream_pos"] = int(stream_pos)
+        return save_checkpoint(path, eng.centers, eng.steps, cfg, comm=comm, extra=extra,
+                               tensors=eng.state_tensors())
+
+    def save(self, path):
+        """Checkpoint the fitted state (centres, running counts, scales, step count)."""
+        self._check_fitted()
+        return self._save(path, self.comm or get_comm())
+
+    @classmethod
+    def load(cls, path, device=None, comm=None):
+        """A MiniBatchKMeans that continues from ``path`` (``partial_fit`` / ``predict``)."""
+        from .config import resolve_dtype
+        from .utils.checkpoint import load_checkpoint
+
+        ck = load_checkpoint(path, comm=comm)
+        if ck.get("kind") != "minibatch":
+            raise ValueError(f"{path} is not a mini-batch checkpoint")
+        c = ck["config"]
+        dt = "bfloat16" if "bfloat16" in c.get("dtype", "") else "float32"
+        km = cls(c["n_clusters"], batch_size=c["batch_size"], max_iter=c.get("max_iter", 100),
+                 init=c.get("init", "k-means++"), dtype=resolve_dtype(dt), device=device,
+                 seed=c.get("seed", 0), comm=comm, tol=c.get("tol", 0.0))
+        dev = _default_device(device)
+        eng = km._engine(int(ck["n_features"]), dev)
+        eng.load_state(ck["centers"], ck["tensors"], ck["iteration"], ck.get("rescales", 0))
+        km._finish(eng)
+        return km
 
     def partial_fit(self, Xb):
         comm = self.comm or get_comm()

@@ -10,6 +10,8 @@ Commands (the reference's top-bar controls, app.mjs:240-288, as a CLI):
 * ``export``   -- checkpoint -> flat-float centroid JSON or room-export JSON (app.mjs:263-267)
 * ``import``   -- room-export JSON -> numeric checkpoint of trait vectors (app.mjs:268-282)
 * ``bench``    -- the headline benchmark (same as ``python bench.py``)
+* ``launch``   -- run a command as an N-rank job with fresh-process restarts from the last
+                  checkpoint (the reference's peers re-meshing after a drop, app.mjs:105-117)
 * ``info``     -- device, native extension and build information
 """
 from __future__ import annotations
@@ -23,12 +25,21 @@ import numpy as np
 import torch
 
 
-def _comm(device):
+def _comm(device, timeout_s: float = 600.0):
     from .parallel import Comm, set_comm
 
-    c = Comm.from_env(device)
+    c = Comm.from_env(device, timeout_s=timeout_s)
     set_comm(c)
     return c
+
+
+def _resume_dir(cfg):
+    """``--resume auto``: the checkpoint dir when it already holds a checkpoint (a restart)."""
+    from .utils.checkpoint import has_checkpoint
+
+    if cfg.resume == "auto":
+        return cfg.checkpoint_dir if cfg.checkpoint_dir and has_checkpoint(cfg.checkpoint_dir) else None
+    return cfg.resume
 
 
 def cmd_fit(a) -> int:
@@ -39,7 +50,8 @@ def cmd_fit(a) -> int:
 
     cfg = KMeansConfig.from_args(a)
     device = cfg.device or ("cuda" if torch.cuda.is_available() else "cpu")
-    comm = _comm(device)
+    comm = _comm(device, cfg.timeout_s)
+    resume = _resume_dir(cfg)
     dtype = resolve_dtype(cfg.dtype)
     if a.input:
         X, n, start = load_points(a.input, comm.rank, comm.world)
@@ -53,10 +65,15 @@ def cmd_fit(a) -> int:
     if cfg.batch_size > 0:
         km = MiniBatchKMeans(cfg.n_clusters, batch_size=cfg.batch_size, max_iter=cfg.max_iter, init=cfg.init,
                              dtype=dtype, device=comm.device, seed=cfg.seed, comm=comm)
+        if resume:
+            raise SystemExit("--resume applies to Lloyd fits and streams (MiniBatchKMeans.fit_stream)")
+        km.fit(X)
     else:
         km = KMeans.from_config(cfg, comm=comm)
         km.device = comm.device
-    km.fit(X)
+        if resume and comm.rank == 0:
+            print(f"[mikmeans] resuming from {resume}", file=sys.stderr, flush=True)
+        km.fit(X, resume_from=resume)
     out = Path(a.output) if a.output else None
     if comm.rank == 0:
         rec = {"n_samples": n, "n_clusters": cfg.n_clusters, "world": comm.world}
@@ -190,6 +207,22 @@ def cmd_import(a) -> int:
     return 0
 
 
+def cmd_launch(a, rest) -> int:
+    """``mikmeans launch --nproc N [--max-restarts R] -- <command> ...``: run a mikmeans
+    command as an N-rank job (one process per GPU, RCCL) and restart it as a FRESH process
+    tree when it fails; with ``--checkpoint-dir`` the restart resumes from the last
+    checkpoint (``--resume auto`` is added).  This process never touches the GPU."""
+    from .parallel.launch import launch_self
+
+    if rest and rest[0] == "--":
+        rest = rest[1:]
+    if not rest:
+        raise SystemExit("usage: mikmeans launch --nproc N [--max-restarts R] -- <command> [args]")
+    if "--checkpoint-dir" in rest and "--resume" not in rest:
+        rest = [*rest, "--resume", "auto"]
+    return launch_self(a.nproc, ["-m", "mikmeans", *rest], max_restarts=a.max_restarts)
+
+
 def cmd_bench(a, rest) -> int:
     root = Path(__file__).resolve().parent.parent
     sys.path.insert(0, str(root))
@@ -264,6 +297,7 @@ def build_parser():
     i.add_argument("--save-room", help="also write the (re-assigned) room JSON")
     i.add_argument("--seed", type=int, default=0)
     sub.add_parser("bench", help="headline benchmark (args forwarded to bench.py)", add_help=False)
+    sub.add_parser("launch", help="N-rank job with restarts from the last checkpoint", add_help=False)
     sub.add_parser("info", help="environment / build info")
     return ap
 
@@ -272,6 +306,12 @@ def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     if argv and argv[0] == "bench":
         return cmd_bench(None, argv[1:])
+    if argv and argv[0] == "launch":
+        la = argparse.ArgumentParser(prog="mikmeans launch", description=cmd_launch.__doc__)
+        la.add_argument("--nproc", type=int, default=1, help="ranks (one per GPU)")
+        la.add_argument("--max-restarts", type=int, default=0, help="fresh-process restarts after a failure")
+        a, rest = la.parse_known_args(argv[1:])
+        return cmd_launch(a, rest)
     a = build_parser().parse_args(argv)
     return {"fit": cmd_fit, "predict": cmd_predict, "blobs": cmd_blobs, "room": cmd_room,
             "export": cmd_export, "import": cmd_import, "info": cmd_info}[a.cmd](a)

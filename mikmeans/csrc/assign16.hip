@@ -1,38 +1,51 @@
-// mikmeans — K2 variant: assignment on 16x16 MFMA tiles (v_mfma_f32_16x16x32_bf16 /
-// v_mfma_f32_16x16x4_f32) for gfx950.
+// mikmeans — K2: nearest-centroid assignment on 16x16 MFMA tiles for gfx950
+// (v_mfma_f32_16x16x32_bf16 / v_mfma_f32_16x16x4_f32).
 //
-// Same algorithm and pipeline as assign.hip (fragment-packed centroid chunks in a
-// 3-slot LDS ring fed by LDS-DMA, |c|^2 seeding the accumulators, packed-index
-// v_min3 argmin), re-tiled for the 16x16 matrix-core shape:
-//  * lane (r = l&15, g = l>>4) holds the B fragment of point p0+r, feature
-//    quarter g: x[p0+r][g*DPAD/4 .. +DPAD/4) (contiguous), and the A fragment of
-//    centroid r of the tile, same quarter;
-//  * output D[row = 4g+reg][col = r]: each lane holds 4 centroid scores of its
-//    point per tile; GT consecutive tiles are reduced together (4-bit index =
-//    tile-in-group * 4 + reg), the 4 lane groups g merge once at the end.
-// On MI355X the chip holds a higher clock on the 16x16 shape under load
-// (MI355X_MICROARCH.md, DVFS give-back item 7), which is why this variant exists;
-// scripts/ab_kernels.py picks the faster one per shape.
+// Pipeline: fragment-packed centroid chunks stream through an LDS ring fed by LDS-DMA
+// (global_load_lds_dwordx4, no VGPR round trip); every wave keeps P blocks of 16
+// points in registers and multiplies them against each 16-centroid tile:
+//  * lane (r = l&15, g = l>>4) holds the B fragment of point p0+r, feature quarter g:
+//    x[p0+r][g*DPAD/4 .. +DPAD/4) (contiguous), and the A fragment of centroid r of the
+//    tile (the packed -2c), same quarter;
+//  * the accumulators are seeded with |c|^2 (+ the point offset below), so the output
+//    D[row = 4g+reg][col = r] is the score of point r against centroid 16t+4g+reg and
+//    each lane holds 4 scores of its point per tile; the 4 lane groups g merge once at
+//    the end.
 //
-// Layout "16" of the packed centroids (csrc/kernels.h describes layout "32"):
+// Argmin epilogue.
+//  * bf16: keys carry a 6-bit index in the low mantissa bits (tile-in-segment*4 + reg)
+//    so one v_min3 tree yields (min, index): 1.5 VALU per score.  The workgroup adds
+//    o = (1 + 2^-12) max |x|^2 over its 256 points to its LDS copy of |c|^2 once, which
+//    makes every key |x-c|^2 + (o - |x|^2) > 0: among equal keys the lower index then
+//    always wins (an OR of the index into a NEGATIVE float favours the higher one), and
+//    the key resolution is 2^-17 of the squared distance plus the spread of |x|^2 inside
+//    the workgroup, not 2^-17 of |x|^2 (coarse for data far from the origin).  A
+//    per-point offset would make the keys a function of the point alone, but its per-tile
+//    seed adds cost 17 % at the headline shape (one process A/B, round 2); workgroups
+//    are therefore aligned to the global 256-row grid by the callers (shard_range,
+//    streaming chunks), so near-tie resolution is the same on any world size.
+//  * f32: an exact (value, index) compare per score (v_cmp + 2 v_cndmask).  The f32
+//    MFMA is 16x slower per FLOP than bf16, so the epilogue is noise there and the
+//    labels carry full fp32 score resolution; strict < in ascending index order keeps
+//    the lowest index on exact ties.
+//
+// Layout "16" of the packed centroids (csrc/kernels.h):
 //   element (k, d): t = k/16, r = k%16, g = d / (DPAD/4), e = d % (DPAD/4)
 //   offset = ((t*NQ + e/V)*64 + r + 16*g)*V + e%V,  NQ = DPAD/(4V)
 #include "common.h"
 #include "kernels.h"
+#include "plan.h"
 
 namespace mk {
 
-constexpr int chunk_tiles16(int esize, int dpad) {
-  return (16 * dpad * esize) >= 16384 ? 1 : 16384 / (16 * dpad * esize);
-}
+using plan::chunk_tiles16;
 
 // CT_: tiles per LDS chunk (0 = the 16 KiB default, which also fixes Kpad's
 // granule); NBUF_: ring slots (prefetch depth NBUF-1).
-template <typename T, int DPAD, int P_, int GT_, int CT_ = 0, int NBUF_ = 3, int NW_ = 4>
+template <typename T, int DPAD, int P_, int CT_ = 0, int NBUF_ = 2, int NW_ = 4>
 struct Assign16Cfg {
   static constexpr int NW = NW_;                // waves per workgroup sharing the ring
   static constexpr int P = P_;                  // 16-point blocks per wave
-  static constexpr int GT = GT_;                // tiles reduced per epilogue
   static constexpr int V = Elem<T>::V;
   static constexpr int NQ = DPAD / 4 / V;       // 16-B pieces per lane per point
   static constexpr int TILE_BYTES = NQ * 1024;  // 16 centroids x DPAD
@@ -45,8 +58,6 @@ struct Assign16Cfg {
   static_assert(NBUF == 2 || NBUF == 3, "ring depth");
   static_assert(chunk_tiles16(sizeof(T), DPAD) % CT == 0, "chunk must divide the Kpad granule");
   static_assert(NQ >= 1, "DPAD too small for the 16x16 layout");
-  static_assert(CT % GT == 0, "tile group must divide the chunk");
-  static_assert(GT * 4 <= 16, "4-bit packed index");
   static_assert(PIECES % NW == 0, "chunk pieces must split evenly over waves");
 };
 
@@ -66,13 +77,30 @@ template <> struct Mfma16<float> {
   }
 };
 
-// DBG bit flags (diagnostic builds for A/B; 4, 16 and 32 are pipeline options; 16 = at
-// least 4 waves per SIMD, i.e. <= 128 VGPRs; 32 = at least 3, <= 168): 1 = epilogue replaced by
-// one add per tile (MFMA + LDS pipeline alone), 2 = no ring refills / waits (MFMA +
-// epilogue alone on whatever the LDS holds).
-template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0, int NW_ = 4>
-__global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) void assign16_kernel(AssignArgs a) {
-  using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_, NW_>;
+// Sum of squares of one lane's 16-byte piece.
+__device__ __forceinline__ float sq16(const u32x4& w, uint16_t*) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = bf16lo(w[i]), hi = bf16hi(w[i]);
+    s = __builtin_fmaf(lo, lo, s);
+    s = __builtin_fmaf(hi, hi, s);
+  }
+  return s;
+}
+__device__ __forceinline__ float sq16(const u32x4& w, float*) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s = __builtin_fmaf(__uint_as_float(w[i]), __uint_as_float(w[i]), s);
+  return s;
+}
+
+// OCC: minimum waves per SIMD the register allocation must allow (launch bounds).
+// OFS (bf16): 1 = workgroup seed offset in the LDS |c|^2 (default), 0 = raw scores (A/B).
+template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, int OFS = 1>
+__global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
+  using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
+  constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -87,27 +115,33 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
   const int c0 = (int)blockIdx.y * cps;
   const int nch = c0 + cps < nch_all ? c0 + cps : nch_all;  // one past this split's last chunk
   const int ncl = nch - c0;                                    // chunks of this split
-  const char* gC = (const char*)a.Cpack + (int64_t)c0 * C::CHUNK_BYTES;
-
+  // LDS-DMA through buffer descriptors: the per-lane part is one 32-bit voffset (lane*16)
+  // and every chunk / piece offset is a scalar, so no 64-bit VGPR address stays live
+  // across the main loop (the f32 and D=128 bf16 bodies are register-bound).
+  const uint32_t loff = (uint32_t)lane * 16u;
+  const __amdgpu_buffer_rsrc_t rC = make_rsrc(a.Cpack, (uint32_t)a.Kpad * DPAD * sizeof(T));
+  const __amdgpu_buffer_rsrc_t rN = make_rsrc(a.cn, (uint32_t)a.Kpad * 4u);
   for (int p = wid; p < cn_bytes / 1024; p += C::NW)
-    glds16((const char*)a.cn + p * 1024 + lane * 16, (MK_LDS void*)(cn_lds + p * 1024));
+    blds16(rN, (MK_LDS void*)(cn_lds + p * 1024), loff, (uint32_t)p * 1024u);
   auto issue_chunk = [&](int c) {  // c: chunk index within this split (ring slot c % NBUF)
-    const char* src = gC + (int64_t)c * C::CHUNK_BYTES + lane * 16;
+    const uint32_t src = (uint32_t)(c0 + c) * C::CHUNK_BYTES;
     char* dst = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
 #pragma unroll
     for (int i = 0; i < C::NPW; ++i) {
       const int pc = wid + i * C::NW;
-      glds16(src + pc * 1024, (MK_LDS void*)(dst + pc * 1024));
+      blds16(rC, (MK_LDS void*)(dst + pc * 1024), loff, src + (uint32_t)pc * 1024u);
     }
   };
   issue_chunk(0);
 
   const int64_t pbase = (int64_t)blockIdx.x * C::PTS + (int64_t)wid * (C::P * 16);
   u32x4 xr[C::P][C::NQ];
+  float xnr[C::P];
 #pragma unroll
   for (int p = 0; p < C::P; ++p) {
     int64_t row = pbase + p * 16 + r;
     row = row < a.N ? row : (a.N - 1);
+    xnr[p] = (!EXACT && OFS == 1 && a.xn) ? a.xn[row] : 0.f;
     const T* rp = (const T*)a.X + row * a.ldx + g * (DPAD / 4);
 #pragma unroll
     for (int q = 0; q < C::NQ; ++q) {
@@ -116,145 +150,130 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
       else xr[p][q] = u32x4{0u, 0u, 0u, 0u};
     }
   }
-  wait_vmcnt<0>();  // see assign.hip: retire the fragments before the LDS-DMA loop
+  wait_vmcnt<0>();  // retire the fragments before the LDS-DMA loop (its vmcnt waits count chunks)
   if (C::NBUF == 3 && ncl > 1) issue_chunk(1);
+
+  // bf16 seed offset (see the header): o = (1 + 2^-12) max |x|^2 over the workgroup's
+  // points, from the caller's row norms when given (loaded with the fragments) or from
+  // the fragments themselves, folded into this workgroup's LDS copy of |c|^2 once.
+  float off = 0.f;
+  if constexpr (!EXACT && OFS == 1) {
+    float m = 0.f;
+    if (a.xn) {
+#pragma unroll
+      for (int p = 0; p < C::P; ++p) m = fmaxf(m, xnr[p]);
+    } else {
+#pragma unroll
+      for (int p = 0; p < C::P; ++p) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < C::NQ; ++q) s += sq16(xr[p][q], (T*)nullptr);
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        m = fmaxf(m, s);
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    float* red = (float*)(bufs + C::NBUF * C::CHUNK_BYTES);
+    if (lane == 0) red[wid] = m;
+    __syncthreads();  // (every wave's cn / chunk-0 DMA has landed: vmcnt(0) above)
+#pragma unroll
+    for (int w = 0; w < C::NW; ++w) off = fmaxf(off, red[w]);
+    off = __builtin_fmaf(off, 2.44140625e-04f, off);  // * (1 + 2^-12)
+    off = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(off)));
+    for (int k = threadIdx.x; k < a.Kpad; k += C::NW * 64) ((float*)cn_lds)[k] += off;
+    // (published by the main loop's first wait_lgkm0 + barrier)
+  }
 
   float best[C::P], seg_best[C::P];
   int bg[C::P];
 #pragma unroll
   for (int p = 0; p < C::P; ++p) { best[p] = 3.0e38f; seg_best[p] = 3.0e38f; bg[p] = 0; }
-  const int last_grp = nch * (C::CT / GT) - 1;
+  const int ngrp = nch * C::CT;   // one past the last tile (global tile numbering)
   const unsigned kmask = key6_mask();
 
-  float dbg_sink = 0.f;
-  if constexpr ((DBG & 2) != 0) { wait_vmcnt<0>(); raw_barrier(); }
   for (int c = 0; c < ncl; ++c) {
-    if constexpr ((DBG & 2) == 0) {
-      // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
-      if (C::NBUF == 3 && c + 1 < ncl) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
-      wait_lgkm0();
-      raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
-      if (c + C::NBUF - 1 < ncl) issue_chunk(c + C::NBUF - 1);
-    }
+    // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
+    if (C::NBUF == 3 && c + 1 < ncl) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
+    wait_lgkm0();
+    raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
+    if (c + C::NBUF - 1 < ncl) issue_chunk(c + C::NBUF - 1);
     const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
-    // DBG & 64 / 128: LLVM's MFMA/DS interleaving strategies for the chunk body (A/B)
-    if constexpr ((DBG & 64) != 0) __builtin_amdgcn_iglp_opt(0);
-    if constexpr ((DBG & 128) != 0) __builtin_amdgcn_iglp_opt(1);
-    // A fragments + |c|^2 of one tile from the LDS ring
-    auto load_tile = [&](int tl_i, u32x4* aw_, f32x4& ci_) {
+#pragma unroll
+    for (int tl_i = 0; tl_i < C::CT; ++tl_i) {
       const int tile = (c0 + c) * C::CT + tl_i;
-      ci_ = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
+      // A fragments + |c|^2 of the tile from the LDS ring
+      const f32x4 ci = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
       const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
+      u32x4 aw[C::NQ];
 #pragma unroll
-      for (int q = 0; q < C::NQ; ++q) aw_[q] = *(const u32x4*)(tl + q * 1024);
-    };
-    // DBG & 4: prefetch the next tile's fragments before this tile's MFMAs (GT == 1)
-    u32x4 awn[C::NQ];
-    f32x4 cin;
-    if constexpr ((DBG & 4) != 0 && GT == 1) load_tile(0, awn, cin);
+      for (int q = 0; q < C::NQ; ++q) aw[q] = *(const u32x4*)(tl + q * 1024);
+      f32x4 acc[C::P];
 #pragma unroll
-    for (int tg = 0; tg < C::CT / GT; ++tg) {
-      f32x4 acc[C::P][GT];
+      for (int p = 0; p < C::P; ++p) acc[p] = ci;
 #pragma unroll
-      for (int t = 0; t < GT; ++t) {
-        const int tl_i = tg * GT + t;
-        u32x4 aw[C::NQ];
-        f32x4 ci;
-        if constexpr ((DBG & 4) != 0 && GT == 1) {
+      for (int q = 0; q < C::NQ; ++q) {
 #pragma unroll
-          for (int q = 0; q < C::NQ; ++q) aw[q] = awn[q];
-          ci = cin;
-          if (tl_i + 1 < C::CT) load_tile(tl_i + 1, awn, cin);
-        } else {
-          load_tile(tl_i, aw, ci);
-        }
-#pragma unroll
-        for (int q = 0; q < C::NQ; ++q) {
-#pragma unroll
-          for (int p = 0; p < C::P; ++p)
-            acc[p][t] = Mfma16<T>::run(aw[q], xr[p][q], q == 0 ? ci : acc[p][t]);
-        }
+        for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
       }
-      const int grp = (c0 + c) * (C::CT / GT) + tg;
-      if constexpr ((DBG & 1) != 0) {
+      if constexpr (EXACT) {
+        // (tile*4 + reg) as wave-uniform values: the index select needs no VALU add
+        const int u = tile * 4;
 #pragma unroll
-        for (int p = 0; p < C::P; ++p) dbg_sink += acc[p][0][0];
-        continue;
-      }
-      if constexpr (GT == 1) {
-        // 6-bit keys over a segment of 16 tiles (tile-in-segment * 4 + reg): 4 key
-        // packs + 2 v_min3 per tile and point block; the running best is merged
-        // with its segment id once per segment.
-        // the four indices as opaque SGPRs, so each key is one v_and_or_b32
-        const unsigned tis = (unsigned)(grp & 15) << 2;
+        for (int p = 0; p < C::P; ++p) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool lt = acc[p][e] < best[p];
+            best[p] = lt ? acc[p][e] : best[p];
+            bg[p] = lt ? u + e : bg[p];
+          }
+        }
+      } else {
+        // 6-bit keys over a segment of 16 tiles (tile-in-segment * 4 + reg): 4 key packs
+        // + 2 v_min3 per tile and point block; the running best is merged with its
+        // segment id once per segment.  The four indices as opaque SGPRs, so each key is
+        // one v_and_or_b32.
+        const unsigned tis = (unsigned)(tile & 15) << 2;
         unsigned t0, t1, t2, t3;
         asm volatile("s_mov_b32 %0, %4\n\ts_or_b32 %1, %4, 1\n\ts_or_b32 %2, %4, 2\n\ts_or_b32 %3, %4, 3"
                      : "=s"(t0), "=s"(t1), "=s"(t2), "=s"(t3) : "s"(tis));
 #pragma unroll
         for (int p = 0; p < C::P; ++p) {
-          const f32x4& sv = acc[p][0];
+          const f32x4& sv = acc[p];
           const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
           const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
-          if constexpr ((DBG & 8) != 0) {
-            seg_best[p] = min3f_v(min3f_v(k0, k1, k2), k3, seg_best[p]);
-          } else {
-            seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
-          }
+          seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
         }
-        if ((grp & 15) == 15 || grp == last_grp) {
+        if ((tile & 15) == 15 || tile == ngrp - 1) {
 #pragma unroll
           for (int p = 0; p < C::P; ++p) {
             // compare values only: on equal (truncated) values the earlier segment keeps
-            // the lower centroid index
+            // the lower centroid index (all keys are >= 0, see the header)
             const float sv = __uint_as_float(__float_as_uint(seg_best[p]) & ~63u);
             const float bv = __uint_as_float(__float_as_uint(best[p]) & ~63u);
-            if (sv < bv) { best[p] = seg_best[p]; bg[p] = grp >> 4; }
+            if (sv < bv) { best[p] = seg_best[p]; bg[p] = tile >> 4; }
             seg_best[p] = 3.0e38f;
           }
         }
-        continue;
-      }
-#pragma unroll
-      for (int p = 0; p < C::P; ++p) {
-        float m;
-        if constexpr (GT == 2) {
-          const f32x4& s0 = acc[p][0];
-          const f32x4& s1 = acc[p][1];
-          const float m0 = min3f(pack_key(s0[0], 0), pack_key(s0[1], 1), pack_key(s0[2], 2));
-          const float m1 = min3f(pack_key(s0[3], 3), pack_key(s1[0], 4), pack_key(s1[1], 5));
-          m = min3f(min3f(m0, m1, pack_key(s1[2], 6)), pack_key(s1[3], 7), pack_key(s1[3], 7));
-        } else {
-          float k[16];
-#pragma unroll
-          for (int t = 0; t < GT; ++t)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) k[4 * t + e] = pack_key(acc[p][t][e], 4 * t + e);
-          const float m0 = min3f(k[0], k[1], k[2]), m1 = min3f(k[3], k[4], k[5]);
-          const float m2 = min3f(k[6], k[7], k[8]), m3 = min3f(k[9], k[10], k[11]);
-          const float m4 = min3f(k[12], k[13], k[14]);
-          m = min3f(min3f(m0, m1, m2), min3f(m3, m4, k[15]), min3f(m3, m4, k[15]));
-        }
-        if (m < best[p]) { best[p] = m; bg[p] = grp; }
       }
     }
   }
 
-  if constexpr ((DBG & 1) != 0) best[0] = fminf(best[0], dbg_sink);
   float inert = 0.f;
   int changed = 0;
 #pragma unroll
   for (int p = 0; p < C::P; ++p) {
-    const unsigned bits = __float_as_uint(best[p]);
     int k;
     float v;
-    if constexpr (GT == 1) {  // bg = segment of 16 tiles, 6-bit key
+    if constexpr (EXACT) {  // bg = tile * 4 + reg of the first strict minimum
+      k = (bg[p] >> 2) * 16 + 4 * g + (bg[p] & 3);
+      v = best[p];
+    } else {               // bg = segment of 16 tiles, 6-bit key; undo the seed offset
+      const unsigned bits = __float_as_uint(best[p]);
       const int idx = (int)(bits & 63u);
       k = (bg[p] * 16 + (idx >> 2)) * 16 + 4 * g + (idx & 3);
       v = __uint_as_float(bits & ~63u);
-    } else {
-      const int idx = (int)(bits & 15u);
-      k = (bg[p] * GT + (idx >> 2)) * 16 + 4 * g + (idx & 3);
-      v = __uint_as_float(bits & ~15u);
     }
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) {
@@ -262,11 +281,19 @@ __global__ __launch_bounds__(NW_ * 64, (DBG & 16) ? 4 : ((DBG & 32) ? 3 : 1)) vo
       const int ko = __shfl_xor(k, o, 64);
       if (vo < v || (vo == v && ko < k)) { v = vo; k = ko; }
     }
+    // this point's seed offset (0 for f32 / OFS 0)
+    const float offp = off;
     if ((p & 3) == g) {
       const int64_t i = pbase + p * 16 + r;
       if (a.split_keys) {
-        if (i < a.N) atomicMin(a.split_keys + i, split_key(v, k));
+        // compare the (positive) keys across splits; split_finish undoes the offset
+        // (parked in mind[], which the caller provides whenever xn is given)
+        if (i < a.N) {
+          atomicMin(a.split_keys + i, split_key(v, k));
+          if (a.mind) a.mind[i] = offp;
+        }
       } else if (i < a.N) {
+        v -= offp;   // back to |c|^2 - 2 x.c
         if (a.track_changed) changed += (a.labels[i] != k);
         a.labels[i] = k;
         if (a.xn) {
@@ -304,7 +331,7 @@ __global__ __launch_bounds__(256) void split_finish_kernel(AssignArgs a) {
     const unsigned long long key = a.split_keys[i];
     a.split_keys[i] = ~0ull;
     const int k = (int)(unsigned)key;
-    const float v = split_value(key);
+    const float v = split_value(key) - (a.mind ? a.mind[i] : 0.f);  // minus the parked seed offset
     if (a.track_changed) changed = a.labels[i] != k;
     a.labels[i] = k;
     if (a.xn) {
@@ -338,17 +365,17 @@ static int assign16_splits(int64_t nblk, int nch) {
   return (nch + cps - 1) / cps;  // no empty split (the kernel's chunk range must be non-empty)
 }
 
-template <typename T, int DPAD, int P, int GT, int CT_ = 0, int NBUF_ = 3, int DBG = 0, int NW_ = 4>
+template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, int OFS = 1>
 static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
-  using C = Assign16Cfg<T, DPAD, P, GT, CT_, NBUF_, NW_>;
+  using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   if (a.Kpad % (16 * C::CT) != 0) return hipErrorInvalidValue;
   const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
-  const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW;
+  const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW;  // + offset / slot scratch
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, OFS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
@@ -356,116 +383,36 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   const int splits = a.split_keys ? assign16_splits(nblk, a.Kpad / (16 * C::CT)) : 1;
   AssignArgs b = a;
   if (splits == 1) b.split_keys = nullptr;
-  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, GT, CT_, NBUF_, DBG, NW_>),
+  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, OFS>),
                      dim3((unsigned)nblk, (unsigned)splits), dim3(C::NW * 64), lds, s, b);
   if (splits > 1)
     hipLaunchKernelGGL(split_finish_kernel, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 
-static int g_assign16_gt = 0;
-static int g_assign16_cfg = 0;  // tuned-shape pipeline variant (A/B), 0 = default
-void set_assign16_gt(int gt) { g_assign16_gt = gt; }
-void set_assign16_cfg(int v) { g_assign16_cfg = v; }
+static int g_assign_offset = 1;
+void set_assign_offset(int m) { g_assign_offset = m; }
 
 template <typename T, int DPAD>
 static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   constexpr int CT = chunk_tiles16(sizeof(T), DPAD);
   constexpr int NQ = DPAD / 4 / Elem<T>::V;
   constexpr int P = NQ >= 8 ? 2 : 4;  // keep the point fragments within ~64-128 VGPRs
-#ifdef MK_AB_VARIANTS
-  // Diagnostic / A-B builds only (MIKMEANS_AB=1 python -m mikmeans._build): every
-  // variant below was measured against the default (profiles/r1_08_*, r1_16_*, r1_17_*).
-  if constexpr (sizeof(T) == 2 && DPAD == 128) {
-    // pipeline variants of the headline shape (occupancy vs barrier frequency):
-    //   1: GT1, 16 KiB chunks, 2 slots (36 KiB LDS at K=1024 -> 4 WGs/CU at <=128 VGPRs)
-    //   2: GT1,  8 KiB chunks, 3 slots (28 KiB)     3: GT2, 16 KiB chunks, 2 slots
-    //   4: GT2,  8 KiB chunks, 3 slots
-    switch (g_assign16_cfg) {
-      case 1: return launch16_t<T, DPAD, P, 1, 4, 2>(a, s);
-      case 2: return launch16_t<T, DPAD, P, 1, 2, 3>(a, s);
-      case 3: return launch16_t<T, DPAD, P, 2, 4, 2>(a, s);
-      case 4: return launch16_t<T, DPAD, P, 2, 2, 3>(a, s);
-      case 10: return launch16_t<T, DPAD, P, 1, 2, 3, 1>(a, s);   // diagnostics of the default
-      case 11: return launch16_t<T, DPAD, P, 1, 2, 3, 2>(a, s);
-      case 12: return launch16_t<T, DPAD, 8, 1, 2, 3>(a, s);      // 8 point-blocks per wave
-      case 13: return launch16_t<T, DPAD, 2, 1, 2, 3>(a, s);      // 2 point-blocks per wave
-      case 14: return launch16_t<T, DPAD, P, 1, 2, 3, 8>(a, s);   // volatile min3 (sched barrier)
-      case 15: return launch16_t<T, DPAD, P, 1, 4, 2, 8>(a, s);
-      case 16: return launch16_t<T, DPAD, P, 1, 4, 2>(a, s);
-      case 17: return launch16_t<T, DPAD, P, 1, 4, 3>(a, s);
-      case 18: return launch16_t<T, DPAD, P, 1, 1, 3>(a, s);
-      case 19: return launch16_t<T, DPAD, P, 1, 1, 2>(a, s);
-      case 20: return launch16_t<T, DPAD, P, 1, 4, 3, 8>(a, s);
-      case 23: return launch16_t<T, DPAD, P, 1, 4, 2, 3>(a, s);   // no epilogue, no ring
-      case 24: return launch16_t<T, DPAD, P, 1, 4, 2, 4>(a, s);   // A prefetch
-      case 25: return launch16_t<T, DPAD, P, 1, 4, 2, 5>(a, s);   // A prefetch, no epilogue
-      case 26: return launch16_t<T, DPAD, P, 1, 4, 2, 1>(a, s);   // no epilogue
-      case 27: return launch16_t<T, DPAD, P, 1, 4, 2, 2>(a, s);   // no ring
-      case 29: return launch16_t<T, DPAD, P, 1, 4, 2, 16>(a, s);  // <= 128 VGPRs (4 waves/SIMD)
-      case 30: return launch16_t<T, DPAD, P, 1, 2, 3, 16>(a, s);
-      case 31: return launch16_t<T, DPAD, P, 1, 4, 3, 16>(a, s);
-      case 32: return launch16_t<T, DPAD, P, 1, 4, 2, 16, 8>(a, s);  // 8 waves share the ring
-      case 33: return launch16_t<T, DPAD, P, 1, 4, 3, 16, 8>(a, s);
-      case 34: return launch16_t<T, DPAD, P, 1, 2, 3, 16, 8>(a, s);
-      case 35: return launch16_t<T, DPAD, P, 1, 2, 2, 16, 2>(a, s);  // 2 waves per ring
-      case 40: return launch16_t<T, DPAD, P, 1, 4, 2, 16, 16>(a, s);  // 16 waves share the ring
-      case 41: return launch16_t<T, DPAD, P, 1, 4, 3, 16, 16>(a, s);
-      case 50: return launch16_t<T, DPAD, 6, 1, 4, 2, 32>(a, s);  // 6 point blocks, 3 waves/SIMD
-      case 51: return launch16_t<T, DPAD, 5, 1, 4, 2, 32>(a, s);
-      case 52: return launch16_t<T, DPAD, 6, 1, 4, 3, 32>(a, s);
-      case 53: return launch16_t<T, DPAD, 6, 1, 2, 3, 32>(a, s);
-      case 36: return launch16_t<T, DPAD, P, 1, 2, 3, 16, 2>(a, s);
-      case 37: return launch16_t<T, DPAD, P, 1, 1, 3, 16, 4>(a, s);  // 4 KiB chunks
-      case 38: return launch16_t<T, DPAD, P, 1, 4, 2, 16 | 64>(a, s);   // iglp_opt(0)
-      case 39: return launch16_t<T, DPAD, P, 1, 4, 2, 16 | 128>(a, s);  // iglp_opt(1)
-      case 21: return launch16_t<T, DPAD, 2, 1, 4, 2>(a, s);
-      case 22: return launch16_t<T, DPAD, 8, 1, 4, 2>(a, s);
-      case 63: return launch16_t<T, DPAD, P, 1, 4, 2, 4 | 32>(a, s);  // A prefetch at 3 waves/SIMD
-      case 64: return launch16_t<T, DPAD, P, 1, 4, 3, 4 | 32>(a, s);
-      case 65: return launch16_t<T, DPAD, 5, 1, 4, 2, 4 | 32>(a, s);
-      case 66: return launch16_t<T, DPAD, 3, 1, 4, 2, 4 | 16>(a, s);  // P=3 + prefetch at 4 waves/SIMD
-      case 67: return launch16_t<T, DPAD, P, 1, 2, 3, 4 | 32>(a, s);
-      default: break;
-    }
+  // 16 KiB chunks in a 2-slot ring.  A/B on MI355X at N=2e7 D=128 K=1024 bf16 (round 1,
+  // profiles/r1_08_*, r1_16_*, r1_17_*): 1279-1317 TF/s vs 1218-1265 for 4/8 KiB chunks
+  // with 3 slots, 1099 / 1250 for 2 / 8 point blocks per wave, -6 % / -20 % for 8 / 16
+  // waves sharing one ring.  bf16: at most 128 VGPRs (4 waves per SIMD): +2.5 % at the
+  // headline shape.  f32 would spill heavily under that bound.
+  constexpr int OCC = sizeof(T) == 2 ? 4 : 1;
+  if constexpr (sizeof(T) == 2) {
+    if (g_assign_offset == 0) return launch16_t<T, DPAD, P, CT, 2, OCC, 4, 0>(a, s);  // A/B (temporary)
   }
-  if constexpr (sizeof(T) == 2 && DPAD == 256) {  // cfg5 shape (P=2 default, 8 KiB tiles)
-    switch (g_assign16_cfg) {
-      case 70: return launch16_t<T, DPAD, 3, 1, 2, 2, 32>(a, s);  // 3 point blocks, 3 waves/SIMD
-      case 71: return launch16_t<T, DPAD, 4, 1, 2, 2>(a, s);      // 4 point blocks, 2 waves/SIMD
-      case 72: return launch16_t<T, DPAD, 3, 1, 1, 3, 32>(a, s);
-      case 73: return launch16_t<T, DPAD, 2, 1, 1, 3, 16>(a, s);
-      case 74: return launch16_t<T, DPAD, 4, 1, 1, 3>(a, s);
-      default: break;
-    }
-  }
-#else
-  if (g_assign16_cfg != 0) return hipErrorNotSupported;  // variant knob needs an A/B build
-#endif
-  // gt knob: 0/1 = the GT1 default below, 2/4 = GT2/GT4.  GT1 is the fastest on every
-  // BASELINE shape when timed on the bench's own data and centres (scripts/ab_shapes.py,
-  // profiles/r1_16_assign_shapes.md); on random centres GT2 can look faster.
-  if (g_assign16_gt <= 1) {
-    // Default: 1-tile epilogue with segmented 6-bit keys (1.5 VALU per score), 16 KiB
-    // chunks in a 2-slot ring.  A/B on MI355X at N=2e7 D=128 K=1024 bf16 (scripts/
-    // ab_kernels.py, one process, interleaved rounds): 1279-1317 TF/s vs 1218-1265 for
-    // 4/8 KiB chunks with 3 slots, 1099 / 1250 for 2 / 8 point blocks per wave.
-    // bf16: at most 128 VGPRs (4 waves per SIMD; <= 5 spilled registers): +2.5 % at the
-    // headline shape (1339 vs 1306 TF/s).  f32 would spill heavily under that bound.
-    constexpr int WB = sizeof(T) == 2 ? 16 : 0;
-    return launch16_t<T, DPAD, P, 1, CT, 2, WB>(a, s);
-  }
-  const int want = g_assign16_gt;  // >= 2
-  if (want >= 4 && CT % 4 == 0) return launch16_t<T, DPAD, P, (CT % 4 == 0 ? 4 : 1)>(a, s);
-  if (want >= 2 && CT % 2 == 0) return launch16_t<T, DPAD, P, (CT % 2 == 0 ? 2 : 1)>(a, s);
-  return launch16_t<T, DPAD, P, 1>(a, s);
+  return launch16_t<T, DPAD, P, CT, 2, OCC, 4, 1>(a, s);
 }
 
-int assign16_chunk_tiles(int dtype, int dpad) {
-  const bool ok = dtype == DT_BF16 ? (dpad == 32 || dpad == 64 || dpad == 128 || dpad == 256)
-                                   : (dpad == 16 || dpad == 32 || dpad == 64 || dpad == 128 || dpad == 256);
-  return ok ? chunk_tiles16(dtype == DT_BF16 ? 2 : 4, dpad) : 0;
-}
+int assign16_chunk_tiles(int dtype, int dpad) { return plan::assign16_chunk_tiles(dtype == DT_BF16 ? 2 : 4, dpad); }
+int assign_kpad(int dtype, int dpad, int K) { return plan::assign_kpad(dtype == DT_BF16 ? 2 : 4, dpad, K); }
+int assign_cn_len(int kpad) { return plan::assign_cn_len(kpad); }
 
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s) {
   if (dtype == DT_BF16) {

@@ -73,17 +73,14 @@ void check_i64(const Tensor& t, const char* name, int64_t numel_min);
 void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::optional<Tensor>& xn,
             const Tensor& labels, const c10::optional<Tensor>& mind,
             const c10::optional<Tensor>& slots, int64_t Kpad, int64_t dpad, bool track_changed,
-            int64_t layout, const c10::optional<Tensor>& keys) {
+            const c10::optional<Tensor>& keys) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   const int64_t N = X.size(0);
   const int D = (int)X.size(1);
-  // layout: 32 (assign.hip), 16 (assign16.hip), 116 (assign_res.hip; packs like 16)
-  TORCH_CHECK(layout == 32 || layout == 16 || layout == 116, "mikmeans: layout must be 32, 16 or 116");
-  const int pack_layout = layout == 32 ? 32 : 16;
   TORCH_CHECK(D <= dpad, "mikmeans: D exceeds dpad");
-  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, (int)Kpad, pack_layout) == Kpad, "mikmeans: bad Kpad ",
-              Kpad, " for dpad ", dpad, " layout ", layout);
+  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, (int)Kpad) == Kpad, "mikmeans: bad Kpad ", Kpad, " for dpad ",
+              dpad);
   check_cuda(pack, "pack");
   TORCH_CHECK(pack.is_contiguous() && pack.scalar_type() == X.scalar_type(),
               "mikmeans: pack dtype must match X");
@@ -104,27 +101,12 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
   a.mind = opt_ptr<float>(mind);
   a.slots = opt_ptr<double>(slots);
   a.track_changed = track_changed ? 1 : 0;
-  if (layout == 116) {
-    const int passes = mk::assign_res_passes(dt, (int)dpad, (int)Kpad);
-    TORCH_CHECK(passes >= 1, "mikmeans: resident assign does not support this shape");
-    if (passes > 1) {
-      TORCH_CHECK(keys.has_value(), "mikmeans: resident assign over ", passes, " passes needs keys");
-      check_i64(*keys, "keys", N);
-    }
-    hip_check(mk::launch_assign_res(dt, (int)dpad, a,
-                                    keys.has_value() ? (unsigned long long*)keys->data_ptr<int64_t>()
-                                                     : nullptr,
-                                    stream()),
-              "assign_res");
-  } else if (layout == 16) {
-    if (keys.has_value()) {  // all-ones u64 scratch: lets small N split the centre range
-      check_i64(*keys, "keys", N);
-      a.split_keys = (unsigned long long*)keys->data_ptr<int64_t>();
-    }
-    hip_check(mk::launch_assign16(dt, (int)dpad, a, stream()), "assign16");
-  } else {
-    hip_check(mk::launch_assign(dt, (int)dpad, a, stream()), "assign");
+  if (keys.has_value()) {  // all-ones u64 scratch: lets small N split the centre range
+    check_i64(*keys, "keys", N);
+    TORCH_CHECK(!xn.has_value() || mind.has_value(), "mikmeans: split assign with xn needs mind");
+    a.split_keys = (unsigned long long*)keys->data_ptr<int64_t>();
   }
+  hip_check(mk::launch_assign16(dt, (int)dpad, a, stream()), "assign");
 }
 
 void check_i64(const Tensor& t, const char* name, int64_t numel_min) {
@@ -272,13 +254,12 @@ void finalize(int64_t mode, const c10::optional<Tensor>& packed, const Tensor& C
               const c10::optional<Tensor>& Cnew, const c10::optional<Tensor>& frozen,
               const c10::optional<Tensor>& mb_counts, const Tensor& pack, const Tensor& cn,
               const c10::optional<Tensor>& shift, const c10::optional<Tensor>& counts,
-              int64_t dpad, int64_t Kpad, int64_t layout) {
+              int64_t dpad, int64_t Kpad) {
   check_f32(Cold, "C");
   TORCH_CHECK(Cold.dim() == 2, "mikmeans: C must be [K, D]");
   const int K = (int)Cold.size(0), D = (int)Cold.size(1);
   const int dt = pack.scalar_type() == at::kBFloat16 ? mk::DT_BF16 : mk::DT_F32;
-  TORCH_CHECK(layout == 32 || layout == 16, "mikmeans: layout must be 32 or 16");
-  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, K, (int)layout) == Kpad, "mikmeans: bad Kpad");
+  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, K) == Kpad, "mikmeans: bad Kpad");
   TORCH_CHECK(D <= dpad, "mikmeans: D > dpad");
   check_cuda(pack, "pack");
   TORCH_CHECK(pack.is_contiguous() && pack.numel() >= Kpad * dpad, "mikmeans: pack too small");
@@ -306,7 +287,6 @@ void finalize(int64_t mode, const c10::optional<Tensor>& packed, const Tensor& C
   a.pack = pack.data_ptr(); a.cn = cn.data_ptr<float>();
   a.shift = opt_ptr<float>(shift); a.counts_out = opt_ptr<float>(counts);
   a.mode = (int)mode;
-  a.layout = (int)layout;
   hip_check(mk::launch_finalize(a, stream()), "finalize");
 }
 
@@ -460,7 +440,9 @@ std::string js_array(const Tensor& t) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mikmeans native ops (gfx950 HIP kernels + host helpers)";
-  m.def("assign", &assign, "fused MFMA distance + argmin (K2)");
+  m.def("assign", &assign, "fused MFMA distance + argmin (K2)", py::arg("X"), py::arg("pack"), py::arg("cn"),
+        py::arg("xn"), py::arg("labels"), py::arg("mind"), py::arg("slots"), py::arg("Kpad"), py::arg("dpad"),
+        py::arg("track_changed"), py::arg("keys") = py::none());
   m.def("update", &update, "LDS-privatised per-cluster sums/counts (K3)", py::arg("X"), py::arg("labels"),
         py::arg("K"), py::arg("slab"), py::arg("cnt_slab"), py::arg("n_chunks"), py::arg("weights"),
         py::arg("col_exp"), py::arg("cnt_exp"), py::arg("clamp"), py::arg("clamp_count") = py::none(),
@@ -482,26 +464,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("kpp_sample", &kpp_sample, "k-means++ D^2 sampling (K6)");
   m.def("blob_centers", &blob_centers, "Philox blob centres");
   m.def("blobs", &blobs, "Philox Gaussian blobs (K8)");
-  m.def("assign_kpad", [](int64_t dt, int64_t dpad, int64_t K, int64_t layout) {
-    return mk::assign_kpad((int)dt, (int)dpad, (int)K, (int)layout); });
+  m.def("assign_kpad", [](int64_t dt, int64_t dpad, int64_t K) { return mk::assign_kpad((int)dt, (int)dpad, (int)K); });
   m.def("assign16_supported", [](int64_t dt, int64_t dpad) { return mk::assign16_chunk_tiles((int)dt, (int)dpad) > 0; });
-  m.def("assign_res_passes", [](int64_t dt, int64_t dpad, int64_t Kpad) {
-          return mk::assign_res_passes((int)dt, (int)dpad, (int)Kpad); },
-        "passes of the LDS-resident assign (0 = unsupported)");
-  m.def("set_assign_res_grid", [](int64_t g) { mk::set_assign_res_grid((int)g); }, "A/B knob");
-  m.def("set_update_nt", [](int64_t nt) { mk::set_update_nt((int)nt); }, "update threads/WG (A/B)");
   m.def("set_update_max_sw", [](int64_t sw) { mk::set_update_max_sw((int)sw); },
         "cap the M-step slice width (smaller LDS footprint for overlap with assign)");
-  m.def("set_assign16_cfg", [](int64_t v) { mk::set_assign16_cfg((int)v); }, "tuning: 16x16 pipeline variant");
-  m.def("set_assign16_gt", [](int64_t gt) { mk::set_assign16_gt((int)gt); }, "tuning: 16x16 epilogue tile group");
-  m.def("assign_chunk_tiles", [](int64_t dt, int64_t dpad) { return mk::assign_chunk_tiles((int)dt, (int)dpad); });
+  m.def("set_assign_offset", [](int64_t m) { mk::set_assign_offset((int)m); }, "A/B: bf16 seed offset scheme");
   m.def("assign_cn_len", [](int64_t kpad) { return mk::assign_cn_len((int)kpad); });
   m.def("update_slice_width", [](int64_t dt, int64_t K, int64_t D, bool w) { return mk::update_slice_width((int)dt, (int)K, (int)D, w); },
         py::arg("dtype"), py::arg("K"), py::arg("D"), py::arg("weighted") = false);
   m.def("update_n_chunks", [](int64_t dt, int64_t K, int64_t D, int64_t N, bool w) { return mk::update_n_chunks((int)dt, (int)K, (int)D, N, w); },
         py::arg("dtype"), py::arg("K"), py::arg("D"), py::arg("N"), py::arg("weighted") = false);
-  m.def("set_assign_p", [](int64_t p) { mk::set_assign_p((int)p); }, "tuning: points blocks per wave");
-  m.def("get_assign_p", []() { return mk::get_assign_p(); });
   m.def("fixed_exp", [](double maxabs) { return mk::fixed_exp(maxabs); },
         "fixed-point exponent e with maxabs * 2^e <= 2^30 (M-step accumulators)");
   m.def("js_format", &js_format, "ECMAScript Number::toString of a double");

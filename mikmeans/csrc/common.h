@@ -67,6 +67,21 @@ __device__ __forceinline__ void glds16(const void* gsrc, MK_LDS void* lds_base) 
   __builtin_amdgcn_global_load_lds(gsrc, lds_base, 16, 0, 0);
 }
 
+// Buffer-descriptor LDS-DMA: 16 B per lane from rsrc + voff + soff to lds_base + lane*16.
+// The descriptor is built from wave-uniform values (readfirstlane'd, so the compiler can
+// prove it and never wraps the load in a waterfall loop); voff is the only VGPR operand.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t b = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, MK_LDS void* lds_base, uint32_t voff,
+                                       uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds_base, 16, voff, soff, 0, 0);
+}
+
 // s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] | vmcnt_hi[15:14],
 // expcnt[6:4]=7, lgkmcnt[11:8]=15).
 template <int N>

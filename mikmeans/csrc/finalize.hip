@@ -12,16 +12,14 @@
 
 namespace mk {
 
-// layout 32: 32-centroid tiles, lane r+32h holds feature half h (assign.hip);
-// layout 16: 16-centroid tiles, lane r+16g holds feature quarter g (assign16.hip).
+// Packed layout (kernels.h): 16-centroid tiles, lane r+16g holds feature quarter g.
 template <typename T>
-__device__ __forceinline__ void store_pack_l(void* pack, int layout, int dpad, int k, int d, float v) {
+__device__ __forceinline__ void store_pack(void* pack, int dpad, int k, int d, float v) {
   constexpr int V = Elem<T>::V;
-  const int parts = layout == 16 ? 4 : 2;
-  const int nq = dpad / (parts * V);
-  const int t = k / layout, r = k % layout;
-  const int hh = d / (dpad / parts), e = d % (dpad / parts);
-  const int64_t off = ((int64_t)(t * nq + e / V) * 64 + r + layout * hh) * V + e % V;
+  const int nq = dpad / (4 * V);
+  const int t = k >> 4, r = k & 15;
+  const int g = d / (dpad / 4), e = d % (dpad / 4);
+  const int64_t off = ((int64_t)(t * nq + e / V) * 64 + r + 16 * g) * V + e % V;
   ((T*)pack)[off] = Elem<T>::from_f32(v);
 }
 
@@ -62,18 +60,18 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
       shift += diff * diff;
       const float q = (a.dtype == DT_BF16) ? round_bf16(nv) : nv;
       cn += q * q;
-      if (a.dtype == DT_BF16) store_pack_l<uint16_t>(a.pack, a.layout, a.dpad, k, d, -2.f * q);
-      else store_pack_l<float>(a.pack, a.layout, a.dpad, k, d, -2.f * q);
+      if (a.dtype == DT_BF16) store_pack<uint16_t>(a.pack, a.dpad, k, d, -2.f * q);
+      else store_pack<float>(a.pack, a.dpad, k, d, -2.f * q);
     }
     for (int d = a.D + part; d < a.dpad; d += 8) {
-      if (a.dtype == DT_BF16) store_pack_l<uint16_t>(a.pack, a.layout, a.dpad, k, d, 0.f);
-      else store_pack_l<float>(a.pack, a.layout, a.dpad, k, d, 0.f);
+      if (a.dtype == DT_BF16) store_pack<uint16_t>(a.pack, a.dpad, k, d, 0.f);
+      else store_pack<float>(a.pack, a.dpad, k, d, 0.f);
     }
     if (a.mode == FIN_MINIBATCH && upd && part == 0) a.mb_counts[k] += c;
   } else if (k < a.Kpad) {
     for (int d = part; d < a.dpad; d += 8) {
-      if (a.dtype == DT_BF16) store_pack_l<uint16_t>(a.pack, a.layout, a.dpad, k, d, 0.f);
-      else store_pack_l<float>(a.pack, a.layout, a.dpad, k, d, 0.f);
+      if (a.dtype == DT_BF16) store_pack<uint16_t>(a.pack, a.dpad, k, d, 0.f);
+      else store_pack<float>(a.pack, a.dpad, k, d, 0.f);
     }
   }
   // reduce over the 8 threads of a centroid

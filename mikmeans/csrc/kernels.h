@@ -17,22 +17,18 @@ constexpr int NSLOT = 256;
 constexpr int SLOT_STRIDE = 8;
 
 // ---- centroid packing -------------------------------------------------------
-// The assign kernel reads centroids from a "fragment-packed" array: for tile
-// t (32 centroids) and 16-byte piece q, the 64 lanes' MFMA A-operand fragments
-// are stored contiguously (1 KiB), so one LDS-DMA wave-instruction stages a
-// piece and one ds_read_b128 per lane fetches it conflict-free.
-//   element (k, d): t = k/32, r = k%32, h = d / (DPAD/2), e = d % (DPAD/2)
-//   offset = ((t*NQ + e/V)*64 + r + 32*h)*V + e%V,  V = 16/sizeof(T), NQ = DPAD/(2V)
-// The stored value is -2*c (exact in bf16/f32) and cn[k] = |c_q|^2 of the
-// quantised centroid, so the MFMA chain seeded with cn directly yields
+// The assign kernel reads centroids from a "fragment-packed" array: for tile t (16
+// centroids) and 16-byte piece q, the 64 lanes' MFMA A-operand fragments are stored
+// contiguously (1 KiB), so one LDS-DMA wave-instruction stages a piece and one
+// ds_read_b128 per lane fetches it conflict-free.
+//   element (k, d): t = k/16, r = k%16, g = d / (DPAD/4), e = d % (DPAD/4)
+//   offset = ((t*NQ + e/V)*64 + r + 16*g)*V + e%V,  V = 16/sizeof(T), NQ = DPAD/(4V)
+// The stored value is -2*c (exact in bf16/f32) and cn[k] = |c_q|^2 of the quantised
+// centroid, so the MFMA chain seeded with cn directly yields
 // score = |c|^2 - 2 x.c  (= |x-c|^2 - |x|^2).
-// Layout "16" (assign16.hip) is the same idea on 16-centroid tiles for the
-// 16x16 MFMA shape.  The layout is chosen per fit and must match between the
-// finalize (packing) and assign launches.
-int assign_chunk_tiles(int dtype, int dpad);  // centroid tiles per LDS chunk (CT), layout 32
-int assign16_chunk_tiles(int dtype, int dpad);  // layout 16 (0 = unsupported)
-int assign_kpad(int dtype, int dpad, int K, int layout = 32);  // K rounded to a chunk multiple
-int assign_cn_len(int kpad);                  // cn array length (multiple of 256 floats)
+int assign16_chunk_tiles(int dtype, int dpad);  // centroid tiles per LDS chunk (0 = unsupported)
+int assign_kpad(int dtype, int dpad, int K);     // K rounded to a chunk multiple
+int assign_cn_len(int kpad);                     // cn array length (multiple of 256 floats)
 
 struct AssignArgs {
   const void* X; int64_t N; int D; int64_t ldx;
@@ -42,22 +38,12 @@ struct AssignArgs {
   float* mind;          // optional: squared distance to the chosen centroid
   double* slots;        // optional: [NSLOT][SLOT_STRIDE] (+inertia, +changed)
   int track_changed;
-  // assign16 only: optional u64 [N] all-ones scratch; small N then splits the centre
-  // range over grid.y (split_finish_kernel writes labels and restores the all-ones)
+  // optional u64 [N] all-ones scratch; small N then splits the centre range over
+  // grid.y (split_finish_kernel writes labels and restores the all-ones)
   unsigned long long* split_keys = nullptr;
 };
-hipError_t launch_assign(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
-// LDS-resident centroids, persistent workgroups; K split into passes that chain a per-point
-// best key through `keys` (u64 [N], needed when assign_res_passes > 1).
-hipError_t launch_assign_res(int dtype, int dpad, const AssignArgs& a, unsigned long long* keys,
-                             hipStream_t s);
-int assign_res_passes(int dtype, int dpad, int Kpad);
-void set_assign_res_grid(int g);
-void set_assign16_gt(int gt);  // tiles per epilogue group of the 16x16 variant (0 = default)
-void set_assign16_cfg(int v);  // pipeline variant of the bf16 D=128 shape (0 = default)
-void set_assign_p(int p);  // 32-point blocks per wave (0 = default)
-int get_assign_p();
+void set_assign_offset(int m);  // bf16 seed-offset scheme (A/B)
 
 // ---- update (LDS-privatised scatter-add) -------------------------------------
 // Sums are accumulated in FIXED POINT: every contribution x*w is rounded to a
@@ -93,7 +79,6 @@ int update_n_chunks(int dtype, int K, int D, int64_t N, bool weighted = false);
 int fixed_exp(double maxabs);                     // largest e with maxabs * 2^e <= 2^20
 void set_update_max_sw(int sw);                   // cap the slice width (0 = none)
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s);
-void set_update_nt(int nt);                       // A/B knob: threads per workgroup
 // Changed rows: for every i with labels[i] != prev[i], append (i, prev[i]) to list
 // (first `cap` entries kept, *count counts all) and set prev[i] = labels[i].
 // Zeroes *count first (stream-ordered).
@@ -124,7 +109,6 @@ struct FinalizeArgs {
   float* shift;           // optional [K]
   float* counts_out;      // optional [K]
   int mode;
-  int layout;             // 32 or 16 (packed-centroid layout of the assign variant)
 };
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 

@@ -1,0 +1,99 @@
+// mikmeans — host-side launch planning shared by the kernels and the sanitizer harness.
+//
+// Everything that turns (K, D, N, dtype) into launch geometry and buffer sizes lives
+// here as plain C++ (no HIP types), so tests/native/plan_fuzz.cpp can build it with
+// g++ -fsanitize=address,undefined and sweep it on the CPU: the
+// M-step's LDS footprint and slice width, its chunk count, the fixed-point exponent
+// and the assign kernel's padded K.
+#pragma once
+#include <math.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define MK_HD __host__ __device__
+#else
+#define MK_HD
+#endif
+
+namespace mk {
+namespace plan {
+
+constexpr size_t UPD_LDS_MAX = 160 * 1024;  // one LDS-filling M-step workgroup per CU
+constexpr int FX_BITS = 20;                 // |q| <= 2^20 per fixed-point contribution
+
+// M-step LDS: cells [K+1][ldc] u64 | add counts [K+1] u32 | flag, nhot | weighted counts
+// [K+1] i64 (weighted / incremental) | hot-label list [K+1] u16.
+MK_HD inline size_t upd_lds_bytes(int K, int ldc, bool weighted) {
+  size_t b = (size_t)(K + 1) * (size_t)ldc * 8 + (size_t)(K + 1) * 4 + 8;
+  b = (b + 7) & ~(size_t)7;
+  b += weighted ? (size_t)(K + 1) * 8 : 0;
+  return b + ((size_t)(K + 1) * 2 + 7) / 8 * 8;
+}
+
+// Columns per M-step workgroup (0 = global-atomic fallback) and the LDS cell stride:
+// the widest power-of-two slice <= 64 (and <= max_sw when nonzero) that fits, odd
+// stride preferred (sw/2 + 1), else unpadded (sw/2, XOR-swizzled in the kernel).
+inline int choose_sw(int esize, int K, int D, bool weighted, int max_sw, int* ldc) {
+  if (K < 1 || D < 1 || (D * esize) % 4 || D % 2) return 0;
+  int dp = 2;
+  while (dp < D) dp *= 2;
+  for (int sw = 64; sw >= 2; sw /= 2) {
+    if (sw > dp) continue;
+    if (max_sw && sw > max_sw) continue;
+    if (upd_lds_bytes(K, sw / 2 + 1, weighted) <= UPD_LDS_MAX) { *ldc = sw / 2 + 1; return sw; }
+    if (upd_lds_bytes(K, sw / 2, weighted) <= UPD_LDS_MAX) { *ldc = sw / 2; return sw; }
+  }
+  return 0;
+}
+
+// Row chunks of the M-step (a multiple of 8: blocks b and b+8 share an XCD): one wave of
+// the 256 CUs over (chunk, slice) workgroups, fewer for tiny N.
+inline int update_n_chunks(int sw, int D, int64_t N) {
+  if (sw == 0) return 1;
+  const int n_slices = (D + sw - 1) / sw;
+  int nc = (256 + n_slices - 1) / n_slices;
+  nc = ((nc + 7) / 8) * 8;
+  const int64_t rows = (N + nc - 1) / nc;
+  if (rows < 256) {
+    const int64_t c = (N + 255) / 256;
+    nc = (int)((c + 7) / 8 * 8);
+    if (nc < 8) nc = 8;
+  }
+  return nc;
+}
+
+// Largest e with maxabs * 2^e <= 2^FX_BITS, kept in [-126, 126] (2^e a normal float);
+// 0 for a zero, negative or non-finite bound.
+inline int fixed_exp(double maxabs) {
+  if (!(maxabs > 0) || !isfinite(maxabs)) return 0;
+  const double l = ceil(log2(maxabs));
+  if (l > 200) return -126;
+  if (l < -200) return 126;
+  int e = FX_BITS - (int)l;
+  while (e > -1000 && ldexp(maxabs, e) > ldexp(1.0, FX_BITS)) --e;  // guard rounding of log2
+  if (e > 126) e = 126;
+  if (e < -126) e = -126;
+  return e;
+}
+
+// Assign kernel: centroid tiles (16 centroids) per 16 KiB LDS chunk, 0 = unsupported width.
+constexpr int chunk_tiles16(int esize, int dpad) {
+  return (16 * dpad * esize) >= 16384 ? 1 : 16384 / (16 * dpad * esize);
+}
+inline int assign16_chunk_tiles(int esize, int dpad) {
+  const bool ok = esize == 2 ? (dpad == 32 || dpad == 64 || dpad == 128 || dpad == 256)
+                             : (dpad == 16 || dpad == 32 || dpad == 64 || dpad == 128 || dpad == 256);
+  return ok ? chunk_tiles16(esize, dpad) : 0;
+}
+// K rounded up to a whole chunk (0 = unsupported width or K out of range).
+inline int assign_kpad(int esize, int dpad, int K) {
+  const int ct = assign16_chunk_tiles(esize, dpad);
+  if (ct <= 0 || K < 1 || K > (1 << 24)) return 0;
+  const int m = 16 * ct;
+  return ((K + m - 1) / m) * m;
+}
+inline int assign_cn_len(int kpad) { return ((kpad + 255) / 256) * 256; }
+
+}  // namespace plan
+}  // namespace mk

@@ -36,12 +36,13 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "plan.h"
 
 namespace mk {
 
 constexpr int UPD_NT = 512;                 // one LDS-filling workgroup per CU
-constexpr size_t UPD_LDS_MAX = 160 * 1024;
-constexpr int FX_BITS = 20;                 // |q| <= 2^20 per contribution
+using plan::UPD_LDS_MAX;
+using plan::FX_BITS;                        // |q| <= 2^20 per contribution
 constexpr int FX_LIM = (1 << (30 - FX_BITS)) * 2 - 1;  // adds per flush: 2047 * 2^20 < 2^31
 constexpr float FX_MAGIC = 12582912.0f;     // 1.5 * 2^23, bits 0x4B400000
 constexpr unsigned long long FX_MM = 0x4B4000004B400000ull;
@@ -206,15 +207,10 @@ __device__ void upd_flush_all(const UpdateArgs& a, const UpdLayout& L, char* m, 
   }
 }
 
-enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8, UPD_NTLOAD = 16, UPD_RESID = 32 };
+enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8, UPD_RESID = 32 };
 
 constexpr int upd_ksh(int np) { return np >= 32 ? 0 : np == 16 ? 1 : np == 8 ? 2 : np == 4 ? 3 : np == 2 ? 4 : 5; }
-__host__ __device__ static inline size_t upd_lds_bytes(int K, int ldc, bool weighted) {
-  size_t b = (size_t)(K + 1) * ldc * 8 + (size_t)(K + 1) * 4 + 8;  // cells, nadd, flag, nhot
-  b = (b + 7) & ~(size_t)7;
-  b += weighted ? (size_t)(K + 1) * 8 : 0;                          // weighted counts
-  return b + ((size_t)(K + 1) * 2 + 7) / 8 * 8;                     // hot-label list (u16)
-}
+using plan::upd_lds_bytes;
 
 template <typename T, int SW, int MODE, int NT = UPD_NT, int NBF = UPD_NBUF, int PER = UPD_MAX_PERIOD>
 __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
@@ -224,7 +220,6 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   constexpr bool DELTA = MODE & UPD_DELTA;
   constexpr bool W = MODE & (UPD_WEIGHTED | UPD_DELTA);  // per-row signed weights
   constexpr bool SWZ = MODE & UPD_SWZ;
-  constexpr bool NTL = MODE & UPD_NTLOAD;                // non-temporal X stream (A/B)
   constexpr bool RESID = MODE & UPD_RESID;               // lo pass of the wide-range columns
   constexpr int ES = sizeof(T);
   constexpr int PB = (SW * ES >= 16) ? 16 : SW * ES;  // bytes per lane load
@@ -325,8 +320,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
         lab_[u] = ((unsigned)l < (unsigned)a.K) ? l : a.K;
         if constexpr (DELTA) wt_[u] = wrow ? wrow[off + u] : 1.f;
         else if constexpr (W) wt_[u] = wrow[off + u];
-        if constexpr (NTL) w_[u] = __builtin_nontemporal_load((const LT*)(p + u * a.ldx));
-        else w_[u] = *(const LT*)(p + u * a.ldx);
+        w_[u] = *(const LT*)(p + u * a.ldx);
       }
     } else {                                           // clamp rows past the chunk -> sink row K
 #pragma unroll
@@ -474,28 +468,14 @@ __global__ __launch_bounds__(256) void update_global_kernel(UpdateArgs a) {
 
 static int esize(int dtype) { return dtype == DT_BF16 ? 2 : 4; }
 
-
-
 // Cap on the slice width (0 = none).  A smaller slice shrinks the LDS footprint
 // so an update workgroup can be co-resident with assign workgroups when the
 // engine overlaps the two kernels on separate streams.
 static int g_update_max_sw = 0;
 void set_update_max_sw(int sw) { g_update_max_sw = sw; }
 
-// slice width (columns per workgroup, 0 = global fallback) and LDS cell stride: the
-// widest slice that fits, odd stride preferred, else unpadded + swizzle
 static int choose_sw(int dtype, int K, int D, bool weighted, int* ldc) {
-  const int es = esize(dtype);
-  if ((D * es) % 4 || D % 2) return 0;
-  int dp = 2;
-  while (dp < D) dp *= 2;
-  for (int sw = 64; sw >= 2; sw /= 2) {
-    if (sw > dp) continue;
-    if (g_update_max_sw && sw > g_update_max_sw) continue;
-    if (upd_lds_bytes(K, sw / 2 + 1, weighted) <= UPD_LDS_MAX) { *ldc = sw / 2 + 1; return sw; }
-    if (upd_lds_bytes(K, sw / 2, weighted) <= UPD_LDS_MAX) { *ldc = sw / 2; return sw; }
-  }
-  return 0;
+  return plan::choose_sw(esize(dtype), K, D, weighted, g_update_max_sw, ldc);
 }
 
 int update_slice_width(int dtype, int K, int D, bool weighted) {
@@ -504,33 +484,10 @@ int update_slice_width(int dtype, int K, int D, bool weighted) {
 }
 
 int update_n_chunks(int dtype, int K, int D, int64_t N, bool weighted) {
-  const int sw = update_slice_width(dtype, K, D, weighted);
-  if (sw == 0) return 1;
-  const int n_slices = (D + sw - 1) / sw;
-  // LDS-bound: one resident workgroup per CU; aim for one wave of the 256 CUs
-  int nc = (256 + n_slices - 1) / n_slices;
-  nc = ((nc + 7) / 8) * 8;
-  const int64_t rows = (N + nc - 1) / nc;
-  if (rows < 256) {  // tiny problems: fewer chunks
-    nc = (int)((N + 255) / 256);
-    nc = ((nc + 7) / 8) * 8;
-    if (nc < 8) nc = 8;
-  }
-  return nc;
+  return plan::update_n_chunks(update_slice_width(dtype, K, D, weighted), D, N);
 }
 
-int fixed_exp(double maxabs) {
-  if (!(maxabs > 0) || !isfinite(maxabs)) return 0;
-  int e = FX_BITS - (int)ceil(log2(maxabs));
-  while (e > -1000 && ldexp(maxabs, e) > ldexp(1.0, FX_BITS)) --e;  // guard rounding of log2
-  if (e > 126) e = 126;     // 2^e must stay a normal float
-  if (e < -126) e = -126;
-  return e;
-}
-
-// Threads per workgroup (A/B knob; 0 = default UPD_NT).
-static int g_update_nt = 0;
-void set_update_nt(int nt) { g_update_nt = nt; }
+int fixed_exp(double maxabs) { return plan::fixed_exp(maxabs); }
 
 template <typename T, int SW, int MODE, int NT, int NBF = UPD_NBUF, int PER = UPD_MAX_PERIOD>
 static hipError_t launch_nt(const UpdateArgs& a, int ldc, hipStream_t s) {
@@ -557,25 +514,6 @@ constexpr int upd_default_nt() {
 
 template <typename T, int SW, int MODE>
 static hipError_t launch_sw(const UpdateArgs& a, int ldc, hipStream_t s) {
-  if constexpr (sizeof(T) == 2 && SW == 32 && MODE == 0) {
-    // A/B knobs (values are codes, not thread counts beyond 256 / 512)
-    switch (g_update_nt) {
-      case 512: return launch_nt<T, SW, MODE, 512>(a, ldc, s);
-      case 256: return launch_nt<T, SW, MODE, 256>(a, ldc, s);
-      case 1024: return launch_nt<T, SW, MODE, 1024, 3, 1024>(a, ldc, s);  // previous default
-      case 1022: return launch_nt<T, SW, MODE, 1024, 2>(a, ldc, s);        // 2-deep ring
-      case 1028: return launch_nt<T, SW, MODE, 1024, 4>(a, ldc, s);        // 4-deep ring
-      case 1029: return launch_nt<T, SW, MODE, 1024, 4, 512>(a, ldc, s);   // 4 x half periods
-      case 1030: return launch_nt<T, SW, MODE, 1024, 6, 512>(a, ldc, s);   // 6 x half periods
-      case 1031: return launch_nt<T, SW, MODE, 1024, 8, 512>(a, ldc, s);
-      case 1032: return launch_nt<T, SW, MODE, 1024, 8, 256>(a, ldc, s);   // 1 row per lane
-      case 1033: return launch_nt<T, SW, MODE, 1024, 12, 256>(a, ldc, s);
-      case 1034: return launch_nt<T, SW, MODE, 1024, 6, 256>(a, ldc, s);
-      case 2030: return launch_nt<T, SW, UPD_NTLOAD, 1024, 6, 512>(a, ldc, s);  // default + nt loads
-      case 2031: return launch_nt<T, SW, UPD_NTLOAD, 1024, 8, 512>(a, ldc, s);
-      default: break;
-    }
-  }
   constexpr int NT = upd_default_nt<T, SW, MODE>();
   // 1024 threads: 512-row periods, 6-deep ring (5 periods of loads in flight).  N=1e8
   // D=128 K=1024 bf16: 5.33-5.76 ms vs 5.96-6.34 for 3 x 1024-row periods (same boxes).

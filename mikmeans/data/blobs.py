@@ -171,6 +171,18 @@ class BlobStream:
         plus one bf16 rounding step."""
         return float((self.box + 6.0 * abs(self.std)) * (1.0 + 2.0**-7))
 
+    def position(self) -> int:
+        """Global row offset of the next batch (rows consumed by every rank so far)."""
+        return self.offset + self.step * self.world * self.batch
+
+    def seek(self, pos: int) -> "BlobStream":
+        """Continue the global row sequence at ``pos`` -- with any world size: a resumed
+        job with the same global batch (``batch * world``) sees the same rows per step."""
+        if self.prefetch and self._pf is not None:
+            raise RuntimeError("seek() before the first batch of a prefetching stream")
+        self.offset, self.step = int(pos), 0
+        return self
+
     def __iter__(self):
         return self
 

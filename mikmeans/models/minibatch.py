@@ -93,6 +93,28 @@ class MiniBatchEngine:
         self.C, self.Cnew = self.Cnew, self.C
         self.steps += 1
 
+    # ------------------------------------------------------------ persistence
+    def state_tensors(self) -> dict:
+        """Everything beyond the centres a resumed stream needs to continue bit for bit."""
+        t = {"vcount": self.vcount.double().cpu()}
+        if self.gpu and self.bound is not None:
+            t["col_bound"] = self.bound.double().cpu()
+        return t
+
+    def load_state(self, centers: torch.Tensor, tensors: dict, steps: int, rescales: int = 0):
+        self.set_centers(centers)
+        self.vcount.copy_(tensors["vcount"].to(device=self.device, dtype=torch.float64))
+        self.steps = int(steps)
+        if self.gpu:
+            self.rescales = int(rescales)
+            if "col_bound" in tensors and self.value_bound is None:
+                from ..ops import fixed_exps
+
+                self.bound = tensors["col_bound"].to(device=self.device, dtype=torch.float64)
+                self.col_exp, _ = fixed_exps(torch.empty((0, self.Dp), dtype=self.dtype, device=self.device),
+                                             None, comm=self.comm, bound=self.bound)
+        return self
+
     def _set_bound(self, Xb, grow: bool = False):
         from ..ops import col_max_abs, fixed_exps
 

@@ -65,7 +65,10 @@ class StreamingLloydEngine(LloydEngine):
         self.frozen = None
         if frozen is not None:
             self.frozen = torch.as_tensor(frozen, dtype=torch.uint8).reshape(-1).to(dev)
-        self.R = max(1, min(int(chunk_rows), max(self.n, 1)))
+        # chunks start on the 256-row grid of the resident fit (csrc/assign16.hip seed offset)
+        from ..parallel.shard import ROW_ALIGN
+
+        self.R = max(1, min(-(-int(chunk_rows) // ROW_ALIGN) * ROW_ALIGN, max(self.n, 1)))
         self.ranges = [(r, min(r + self.R, self.n)) for r in range(0, self.n, self.R)]
         self.iteration = 0
         self.labels = torch.full((self.n,), -1, dtype=torch.int32, device=dev)

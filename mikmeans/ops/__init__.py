@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 
 from . import cpu
-from .native import available, dpad_for, dtype_code, preferred_layout, require, vec_elems
+from .native import available, dpad_for, dtype_code, require, vec_elems
 
 __all__ = [
     "available",
@@ -70,7 +70,7 @@ class CentroidPack:
     rows between K and Kpad.
     """
 
-    def __init__(self, K: int, D: int, dtype: torch.dtype, device, layout: int | None = None):
+    def __init__(self, K: int, D: int, dtype: torch.dtype, device):
         C = require()
         self._C = C
         self.K, self.D, self.dtype = K, D, dtype
@@ -78,9 +78,7 @@ class CentroidPack:
         if self.dpad == 0:
             raise NotImplementedError(f"mikmeans: GPU assign supports D <= 256 (got {D})")
         self.dt = dtype_code(dtype)
-        self.layout = layout or preferred_layout(dtype, self.dpad, K)
-        self.pack_layout = 32 if self.layout == 32 else 16      # 116 (resident) packs like 16
-        self.Kpad = C.assign_kpad(self.dt, self.dpad, K, self.pack_layout)
+        self.Kpad = C.assign_kpad(self.dt, self.dpad, K)
         self._keys = None
         self.pack = torch.zeros(self.Kpad * self.dpad, dtype=dtype, device=device)
         self.cn = torch.zeros(C.assign_cn_len(self.Kpad), dtype=torch.float32, device=device)
@@ -96,33 +94,31 @@ class CentroidPack:
         """K4: new centres from the all-reduced message (mode 1 Lloyd, 2 mini-batch) or
         pack-only (mode 0); always re-packs ``-2c`` / ``|c|^2`` for the next assign."""
         self._C.finalize(mode, packed, Cold, Cnew, frozen, mb_counts, self.pack, self.cn, shift, counts,
-                         self.dpad, self.Kpad, self.pack_layout)
+                         self.dpad, self.Kpad)
 
     def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False):
         """K2 on these centres (``X`` column-padded, 16-B rows)."""
         keys = None
-        if self.layout == 116 and self._C.assign_res_passes(self.dt, self.dpad, self.Kpad) > 1:
-            if self._keys is None or self._keys.numel() < X.shape[0]:
-                self._keys = torch.empty(max(X.shape[0], 1), dtype=torch.int64, device=X.device)
-            keys = self._keys
-        elif self.layout == 16 and 0 < X.shape[0] <= SPLIT_MAX_ROWS:
+        if 0 < X.shape[0] <= SPLIT_MAX_ROWS:
             # small batches split the centre range across workgroups (assign16 grid.y);
             # the kernels leave the scratch all-ones again, so it is filled only once
             if self._keys is None or self._keys.numel() < X.shape[0]:
                 self._keys = torch.full((X.shape[0],), -1, dtype=torch.int64, device=X.device)
             keys = self._keys
+            if xn is not None and mind is None:   # the splits park each point's seed offset there
+                mind = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)
         self._C.assign(X, self.pack, self.cn, xn, labels, mind, slots, self.Kpad, self.dpad,
-                       track_changed, self.layout, keys)
+                       track_changed, keys)
 
 
-def pack_centers(centers: torch.Tensor, D: int, dtype: torch.dtype, device, layout: int | None = None):
+def pack_centers(centers: torch.Tensor, D: int, dtype: torch.dtype, device):
     """A CentroidPack of ``centers`` for points with ``D`` (column-padded) features."""
     cen = torch.zeros((centers.shape[0], D), dtype=torch.float32, device=device)
     cen[:, : centers.shape[1]] = centers.to(device=device, dtype=torch.float32)
-    return CentroidPack(cen.shape[0], D, dtype, device, layout=layout).load(cen)
+    return CentroidPack(cen.shape[0], D, dtype, device).load(cen)
 
 
-def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True, layout: int | None = None,
+def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True,
            pack: "CentroidPack | None" = None):
     """Nearest centroid of every row: returns ``(labels int32, sqdist float32 or None)``.
 
@@ -139,7 +135,7 @@ def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True, la
     if pack is not None and (pack.D, pack.dtype, pack.pack.device) == (D, Xp.dtype, Xp.device):
         pk = pack
     else:
-        pk = pack_centers(centers, D, Xp.dtype, X.device, layout)
+        pk = pack_centers(centers, D, Xp.dtype, X.device)
     n = Xp.shape[0]
     labels = torch.empty(n, dtype=torch.int32, device=X.device)
     xn = mind = None

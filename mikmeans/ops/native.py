@@ -65,31 +65,12 @@ def vec_elems(dtype: torch.dtype) -> int:
 
 
 def dpad_for(D: int, dtype: torch.dtype) -> int:
-    """Power-of-two padded feature width the assign kernel is instantiated for (0 = unsupported)."""
-    v = vec_elems(dtype)
-    d = 2 * v
+    """Power-of-two padded feature width the assign kernel is instantiated for (0 = unsupported):
+    at least four 16-byte pieces (one per lane group of the 16x16 MFMA tile), at most 256."""
+    d = 4 * vec_elems(dtype)
     while d < D:
         d *= 2
     return d if d <= 256 else 0
-
-
-def preferred_layout(dtype: torch.dtype, dpad: int, K: int | None = None) -> int:
-    """Assign-kernel variant: 32 (32x32 MFMA, assign.hip), 16 (16x16 MFMA with an LDS
-    ring, assign16.hip) or 116 (16x16 MFMA, LDS-resident centroids, assign_res.hip).
-    ``MIKMEANS_ASSIGN_LAYOUT`` overrides."""
-    env = os.environ.get("MIKMEANS_ASSIGN_LAYOUT")
-    m = require()
-    ok16 = m.assign16_supported(dtype_code(dtype), dpad)
-    if env in ("16", "32", "116"):
-        return int(env) if (env == "32" or ok16) else 32
-    if not ok16:
-        return 32
-    return DEFAULT_LAYOUT
-
-
-# Measured on MI355X (scripts/ab_kernels.py, N=2e7, D=128, K=1024, bf16): the 16x16
-# variant with 2-tile epilogue groups runs 1262 TF/s against 1119 for the 32x32 one.
-DEFAULT_LAYOUT = 16
 
 
 _warned: set = set()

@@ -15,15 +15,25 @@ HBM_BYTES = 288 * 10**9          # MI355X HBM3E per GPU (spec)
 HBM_USABLE_FRACTION = 0.90       # leave room for the runtime / RCCL buffers
 
 
-def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
-    """Balanced contiguous split: the first ``n % world`` ranks get one extra row."""
-    base, rem = divmod(n, world)
-    start = rank * base + min(rank, rem)
-    return start, start + base + (1 if rank < rem else 0)
+# Shard boundaries fall on multiples of this many rows: the bf16 assign kernel folds one
+# seed offset per workgroup of 256 points into its keys (csrc/assign16.hip), so aligned
+# shards give every point the same workgroup -- and the same near-tie resolution -- on
+# any world size.
+ROW_ALIGN = 256
 
 
-def shard_sizes(n: int, world: int) -> list[int]:
-    return [shard_range(n, r, world)[1] - shard_range(n, r, world)[0] for r in range(world)]
+def shard_range(n: int, rank: int, world: int, align: int = ROW_ALIGN) -> tuple[int, int]:
+    """Balanced contiguous split in units of ``align`` rows (the first ranks get one unit
+    more; only the last shard may end off the grid)."""
+    units = -(-n // align)
+    base, rem = divmod(units, world)
+    u0 = rank * base + min(rank, rem)
+    u1 = u0 + base + (1 if rank < rem else 0)
+    return min(n, u0 * align), min(n, u1 * align)
+
+
+def shard_sizes(n: int, world: int, align: int = ROW_ALIGN) -> list[int]:
+    return [shard_range(n, r, world, align)[1] - shard_range(n, r, world, align)[0] for r in range(world)]
 
 
 @dataclass

@@ -27,14 +27,21 @@ CKPT_FLAT = "centroids.json"
 
 
 def save_checkpoint(path, centers: torch.Tensor, iteration: int, config=None, *, history=None,
-                    comm=None, extra: dict | None = None) -> Path:
+                    comm=None, extra: dict | None = None, tensors: dict | None = None) -> Path:
+    """Write the checkpoint (rank 0) and barrier.  ``tensors``: further named state
+    (e.g. mini-batch running counts) stored in the same safetensors file."""
     path = Path(path)
     rank = comm.rank if comm is not None else 0
     if rank == 0:
         path.mkdir(parents=True, exist_ok=True)
         c = centers.detach().to("cpu", torch.float32).contiguous()
         tmp = path / (CKPT_TENSORS + ".tmp")
-        save_file({"centers": c}, str(tmp))
+        blobs = {"centers": c}
+        for k, v in (tensors or {}).items():
+            if k == "centers":
+                raise ValueError("'centers' is reserved")
+            blobs[k] = v.detach().to("cpu").contiguous()
+        save_file(blobs, str(tmp))
         os.replace(tmp, path / CKPT_TENSORS)
         meta = {
             "format": "mikmeans-checkpoint-v1",
@@ -64,26 +71,41 @@ def _jsonable(o):
     return str(o)
 
 
+def has_checkpoint(path) -> bool:
+    path = Path(path)
+    return (path / CKPT_META).is_file() and (path / CKPT_TENSORS).is_file()
+
+
+_DTYPES = {str(d): d for d in (torch.float32, torch.float64, torch.int32, torch.int64, torch.uint8, torch.bfloat16)}
+
+
 def load_checkpoint(path, comm=None, device=None) -> dict:
-    """Read a checkpoint (rank 0) and broadcast it to every rank of ``comm``."""
+    """Read a checkpoint (rank 0) and broadcast it to every rank of ``comm``.
+
+    Returns the JSON state plus ``centers`` and ``tensors`` (every other named tensor)."""
     path = Path(path)
     rank = comm.rank if comm is not None else 0
     state = None
     if rank == 0:
         meta = json.loads((path / CKPT_META).read_text())
-        t = load_file(str(path / CKPT_TENSORS))["centers"]
-        state = {**meta, "centers": t}
+        ts = load_file(str(path / CKPT_TENSORS))
+        state = {**meta, "centers": ts.pop("centers"), "tensors": ts}
     if comm is not None and comm.world > 1:
         blob = None
         if state is not None:
-            hdr = {k: v for k, v in state.items() if k != "centers"}
-            hdr["_shape"] = list(state["centers"].shape)
+            hdr = {k: v for k, v in state.items() if k not in ("centers", "tensors")}
+            hdr["_tensors"] = [["centers", list(state["centers"].shape), str(state["centers"].dtype)]] + \
+                [[k, list(v.shape), str(v.dtype)] for k, v in state["tensors"].items()]
             blob = json.dumps(hdr).encode()
         meta = json.loads(comm.broadcast_bytes(blob, 0).decode())   # JSON, never unpickled
-        shape = meta.pop("_shape")
-        buf = (state["centers"] if state else torch.zeros(shape)).to(comm.device)
-        comm.broadcast_(buf, 0)
-        state = {**meta, "centers": buf.cpu()}
+        specs = meta.pop("_tensors")
+        got = {}
+        for name, shape, dt in specs:
+            src = None if state is None else (state["centers"] if name == "centers" else state["tensors"][name])
+            buf = (src if src is not None else torch.zeros(shape, dtype=_DTYPES[dt])).to(comm.device)
+            comm.broadcast_(buf, 0)
+            got[name] = buf.cpu()
+        state = {**meta, "centers": got.pop("centers"), "tensors": got}
     if device is not None:
         state["centers"] = state["centers"].to(device)
     return state

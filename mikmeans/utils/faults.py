@@ -26,6 +26,15 @@ def _spec():
 
 
 def maybe_fail(rank: int, iteration: int) -> None:
+    """Raise if ``MIKMEANS_FAULT`` names this (rank, iteration).  With
+    ``MIKMEANS_FAULT_ONCE=<path>`` the fault fires only while ``path`` does not exist (and
+    creates it), so a supervised job restarted by ``mikmeans launch`` recovers."""
     spec = _spec()
     if spec is not None and spec == (rank, iteration):
+        once = os.environ.get("MIKMEANS_FAULT_ONCE")
+        if once:
+            if os.path.exists(once):
+                return
+            with open(once, "w") as f:
+                f.write(f"{rank}:{iteration}\n")
         raise InjectedFault(f"injected fault on rank {rank} after iteration {iteration}")

@@ -19,6 +19,10 @@ for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step pytest_gpu 1200 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread ;;
+    kern) step pytest_kern 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread ;;
+    kbench) step kbench 300 python scripts/kbench.py ${KB_ARGS:-} ;;
+    kbench4) step kbench4 300 python scripts/kbench.py --n 10000000 --d 64 --k 4096 ;;
+    kbench2) step kbench2 300 python scripts/kbench.py --n 1000000 --d 128 --k 256 --dtype f32 --reps 20 ;;
     mstep) step pytest_mstep 300 python -u -m pytest tests/test_gpu_mstep.py -x -v --timeout 120 --timeout-method thread ;;
     rccl) step pytest_rccl 300 python -u -m pytest tests/test_gpu_rccl.py -x -v --timeout 120 --timeout-method thread ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Per-kernel timing of one Lloyd step's phases on the bench's own data (one process).
+
+usage: kbench.py [--n N] [--d D] [--k K] [--dtype bf16|f32] [--reps R]
+Prints one JSON line: median / min ms of assign, update, reduce and the whole step,
+plus the assign's MFMA TF/s.  Centres are a few Lloyd iterations in (like the bench's
+timed steps), so the argmin sees realistic score distributions.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from mikmeans.data.blobs import blob_centers, make_blobs
+from mikmeans.models.init import init_random
+from mikmeans.models.lloyd import LloydEngine
+from mikmeans.parallel import Comm
+
+
+def timed(fn, reps):
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return {"median_ms": round(statistics.median(ts), 4), "min_ms": round(min(ts), 4)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=20_000_000)
+    ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--k", type=int, default=1024)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--warm-iters", type=int, default=3)
+    ap.add_argument("--ab-offset", default="", help="comma list of bf16 seed-offset modes to A/B (interleaved)")
+    a = ap.parse_args()
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    dev = torch.device("cuda")
+    comm = Comm.local(dev)
+    X = make_blobs(a.n, a.d, a.k, seed=0, dtype=dt, device=dev, centers=blob_centers(a.k, a.d, 10.0, 0, device=dev))
+    eng = LloydEngine(X, a.k, comm=comm).set_centers(init_random(X, a.d, a.k, a.n, 0, comm, 0))
+    for _ in range(a.warm_iters):
+        eng.step()
+    C = eng._C
+    res = {"n": a.n, "d": a.d, "k": a.k, "dtype": a.dtype}
+    res["assign"] = timed(lambda: eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True), a.reps)
+    res["update"] = timed(lambda: C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks, None,
+                                           eng.col_exp, eng.cnt_exp, False), a.reps)
+    res["reduce"] = timed(lambda: C.reduce(eng.slab, eng.cnt_slab, eng.n_chunks, eng.K, eng.Dp, eng.slots,
+                                           eng.packed, eng.col_exp, eng.cnt_exp), a.reps)
+    if a.ab_offset:
+        modes = [int(m) for m in a.ab_offset.split(",")]
+        ts = {m: [] for m in modes}
+        for _ in range(5):
+            for m in modes:
+                C.set_assign_offset(m)
+                ts[m].append(timed(lambda: eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True),
+                                   a.reps)["median_ms"])
+        C.set_assign_offset(2)
+        res["ab_offset_ms"] = {str(m): round(statistics.median(v), 4) for m, v in ts.items()}
+    res["step"] = timed(eng.step, a.reps)
+    res["assign_tflops"] = round(2.0 * a.n * a.k * a.d / (res["assign"]["median_ms"] * 1e-3) / 1e12, 1)
+    res["update_GBps"] = round(X.numel() * X.element_size() / (res["update"]["median_ms"] * 1e-3) / 1e9, 1)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

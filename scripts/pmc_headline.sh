@@ -11,6 +11,6 @@ P4="WRITE_SIZE"
 for i in 1 2 3 4; do
   eval P=\$P$i
   rm -rf gpurun_out/pmch$i
-  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d gpurun_out/pmch$i -- python3 bench.py --n $N --steps 2 --warmup 1 --no-also-incremental > gpurun_out/pmch$i.log 2>&1 || exit $?
+  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d gpurun_out/pmch$i -- python3 bench.py --n $N --steps 2 --warmup 1 --no-also-incremental --pg auto > gpurun_out/pmch$i.log 2>&1 || exit $?
 done
 echo pmc-done

@@ -120,3 +120,31 @@ def test_init_reset_and_unassigned_predict():
     km.reset()
     with pytest.raises(RuntimeError):
         km.predict(X)
+
+
+def test_launch_restarts_failed_job_from_checkpoint(tmp_path):
+    """``mikmeans launch``: a 2-rank job whose rank 1 dies after iteration 5 is restarted
+    as a fresh process tree, resumes from the iteration-4 checkpoint and ends with the
+    centres of an uninterrupted run (the reference re-meshes after a
+    dropped peer, app.mjs:105-117)."""
+    from safetensors.torch import load_file
+
+    common = ["--blobs", "6000,4,5", "--device", "cpu", "--n-clusters", "5", "--max-iter", "8", "--tol", "-1",
+              "--checkpoint-every", "2", "--seed", "3"]
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    ref = subprocess.run([sys.executable, "-m", "mikmeans", "launch", "--nproc", "2", "--", "fit", *common,
+                          "--checkpoint-dir", str(tmp_path / "ck_ref"), "--output", str(tmp_path / "ref")],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert ref.returncode == 0, ref.stderr[-3000:]
+    env_f = dict(env, MIKMEANS_FAULT="1:5", MIKMEANS_FAULT_ONCE=str(tmp_path / "fault.once"))
+    r = subprocess.run([sys.executable, "-m", "mikmeans", "launch", "--nproc", "2", "--max-restarts", "1", "--",
+                        "fit", *common, "--checkpoint-dir", str(tmp_path / "ck"), "--output", str(tmp_path / "out")],
+                       cwd=ROOT, env=env_f, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert (tmp_path / "fault.once").exists() and "restart 1/1" in r.stderr
+    assert "resuming from" in r.stderr
+    a = load_file(str(tmp_path / "ref" / "centroids.safetensors"))["centers"]
+    b = load_file(str(tmp_path / "out" / "centroids.safetensors"))["centers"]
+    assert torch.equal(a, b)

@@ -141,7 +141,7 @@ def _minibatch_fit_uneven(comm):
 
     n = 1025
     X = _data()[:n]
-    s, e = shard_range(n, comm.rank, comm.world)   # shards of 342 / 342 / 341 rows
+    s, e = shard_range(n, comm.rank, comm.world, align=1)   # shards of 342 / 342 / 341 rows
     km = mikmeans.MiniBatchKMeans(4, batch_size=64, max_iter=1, seed=2, comm=comm).fit(X[s:e])
     return {"C": km.cluster_centers_.clone(), "steps": km.n_steps_}
 

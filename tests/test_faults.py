@@ -39,3 +39,51 @@ def test_rank_failure_then_resume_with_other_world(tmp_path, monkeypatch):
             assert r["n_iter"] == ITERS
             assert torch.equal(r["C"], ref["C"])           # exact: integer-sum M-step, any world size
             assert r["inertia"] == pytest.approx(ref["inertia"], rel=1e-12)
+
+
+def _mb_stream(comm, ckdir, resume, batch_global, steps):
+    from mikmeans import MiniBatchKMeans
+    from mikmeans.data.blobs import BlobStream
+
+    b = batch_global // comm.world
+    st = BlobStream(10**6, 8, 6, b, std=2.0, seed=3, rank=comm.rank, world=comm.world)
+    km = MiniBatchKMeans(6, batch_size=b, seed=1, comm=comm, init="random", device="cpu")
+    km.fit_stream(st, steps, resume_from=ckdir if resume else None, checkpoint_every=2, checkpoint_dir=ckdir)
+    return {"C": km.cluster_centers_, "steps": km.n_steps_, "counts": km.counts_}
+
+
+def test_minibatch_stream_failure_then_resume_with_other_world(tmp_path, monkeypatch):
+    """Kill a rank mid-stream (W=2), resume from the last checkpoint on W=4 with the same
+    global batch: the stream replays the same rows per step, the centres match the
+    uninterrupted single-rank run bit for bit (VERDICT r1 #8)."""
+    from mikmeans.parallel import Comm
+    from mikmeans.utils.checkpoint import load_checkpoint
+
+    ref = _mb_stream(Comm.local(), str(tmp_path / "ref"), False, 1024, 10)
+    ck = str(tmp_path / "ck")
+    monkeypatch.setenv("MIKMEANS_FAULT", "1:5")
+    with pytest.raises(Exception):
+        spawn_local(_mb_stream, 2, ck, False, 1024, 10)
+    monkeypatch.delenv("MIKMEANS_FAULT")
+    st = load_checkpoint(ck)
+    assert st["iteration"] == 4 and st["kind"] == "minibatch" and st["stream_pos"] == 5 * 1024
+    res = spawn_local(_mb_stream, 4, ck, True, 1024, 10)
+    for r in res:
+        assert r["steps"] == 10
+        assert torch.equal(r["C"], ref["C"])
+        assert torch.equal(r["counts"], ref["counts"])
+
+
+def test_minibatch_save_load_roundtrip(tmp_path):
+    import mikmeans
+    from mikmeans.data.blobs import make_blobs
+
+    X = make_blobs(4096, 5, 4, seed=2)
+    km = mikmeans.MiniBatchKMeans(4, batch_size=512, seed=0, device="cpu").fit(X)
+    km.save(tmp_path / "mb")
+    km2 = mikmeans.MiniBatchKMeans.load(tmp_path / "mb", device="cpu")
+    assert torch.equal(km2.cluster_centers_, km.cluster_centers_)
+    assert torch.equal(km2.counts_, km.counts_) and km2.n_steps_ == km.n_steps_
+    km.partial_fit(X[:512])
+    km2.partial_fit(X[:512])
+    assert torch.equal(km2.cluster_centers_, km.cluster_centers_)

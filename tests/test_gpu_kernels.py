@@ -43,42 +43,74 @@ def test_row_sqnorm(native, dtype, n, d):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n,d,k", [(1000, 2, 3), (513, 16, 37), (20000, 128, 256), (9000, 128, 1024),
                                    (4096, 64, 4096), (3000, 256, 512), (255, 100, 70), (70000, 32, 9)])
-@pytest.mark.parametrize("layout", [32, 16, 116])
-def test_assign_matches_reference(native, dtype, n, d, k, layout):
+def test_assign_matches_reference(native, dtype, n, d, k):
     X = _points(n, d, dtype, seed=k)
     C = _points(k, d, torch.float32, seed=k + 1)
-    dp = ops.dpad_for(ops.pad_columns(X[:1]).shape[1], dtype)
-    if layout in (16, 116) and not native.assign16_supported(ops.dtype_code(dtype), dp):
-        pytest.skip("16x16 variant needs DPAD/4 >= one 16-byte piece")
-    labels, mind = ops.assign(X.to(DEV), C.to(DEV), with_dist=True, layout=layout)
+    labels, mind = ops.assign(X.to(DEV), C.to(DEV), with_dist=True)
     _check_assign(X, C, labels, mind, rel=2e-5 if dtype == torch.float32 else 3e-5)
 
 
-@pytest.mark.parametrize("gt", [1, 2, 4])
-def test_assign16_tile_groups(native, gt):
-    X = _points(7000, 128, torch.bfloat16, seed=gt)
-    C = _points(1000, 128, torch.float32, seed=gt + 7)
-    native.set_assign16_gt(gt)
-    try:
-        labels, mind = ops.assign(X.to(DEV), C.to(DEV), with_dist=True, layout=16)
-    finally:
-        native.set_assign16_gt(0)
-    _check_assign(X, C, labels, mind, rel=3e-5)
+def _first_argmin(sc):
+    """Lowest index among the exact minima of each row (f64 scores)."""
+    m = sc.min(1, keepdim=True).values
+    idx = torch.arange(sc.shape[1], dtype=torch.int64).expand_as(sc)
+    return torch.where(sc == m, idx, sc.shape[1]).min(1).values
 
 
-@pytest.mark.parametrize("layout", [16, 116, 32])
-def test_assign_exact_f32_small_ints(native, layout):
-    # integer data: scores are exact in f32, so labels must equal argmin exactly (lowest index on ties)
-    g = torch.Generator().manual_seed(3)
-    X = torch.randint(-8, 8, (5000, 64), generator=g).float()
-    C = torch.randint(-8, 8, (1300, 64), generator=g).float()
-    C[17] = C[5]      # exact duplicate centre: index 5 must win
-    C[1200] = C[40]   # ... also across resident-kernel passes (116: 3 passes here)
-    labels, _ = ops.assign(X.to(DEV), C.to(DEV), with_dist=False, layout=layout)
-    exp, _ = ref.assign(X, C)
-    sc = ref.scores(X, C)
-    tie = (sc == sc.min(1, keepdim=True).values).sum(1) > 1
-    assert torch.equal(labels.cpu()[~tie], exp[~tie])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,d,k", [(5000, 64, 1300), (3000, 128, 1024), (2000, 32, 300)])
+def test_assign_exact_ties_lowest_index(native, dtype, n, d, k):
+    """Integer data: every score is exact in f32, so labels must equal the f64 argmin with
+    the LOWEST index on exact ties -- every row, ties included (duplicated centres, negative
+    and positive scores)."""
+    g = torch.Generator().manual_seed(3 + d)
+    X = torch.randint(-8, 8, (n, d), generator=g).float()
+    C = torch.randint(-8, 8, (k, d), generator=g).float()
+    C[17] = C[5]       # exact duplicate centres: the lower index must win
+    C[k - 100] = C[40]
+    C[k - 1] = C[300 % k]
+    X[:50] = C[5]      # rows sitting exactly on a duplicated centre (score -|x|^2 < 0)
+    X[50:100] = C[40]
+    labels, _ = ops.assign(X.to(dtype).to(DEV), C.to(DEV), with_dist=False)
+    sc = ref.scores(X.double(), C.double())
+    exp = _first_argmin(sc)
+    got = labels.cpu().long()
+    if dtype == torch.float32:
+        assert torch.equal(got, exp)
+    else:
+        # bf16 keys: scores are exact too, but the per-point seed offset is added in f32, so
+        # two DISTINCT centres with equal exact scores may split by one rounding; the label
+        # must be optimal, and among bitwise-equal centres the lowest index
+        assert torch.equal(sc.gather(1, got[:, None]), sc.gather(1, exp[:, None]))
+        same = (C[got] == C[exp]).all(1)
+        assert torch.equal(got[same], exp[same])
+        assert torch.equal(got[:100], exp[:100])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_assign_offset_data_resolution(native, dtype):
+    """Data far from the origin (x + 100): labels equal the f64 argmin on the (quantised)
+    centres except where the f64 gap to the runner-up is below the fp32 arithmetic of the
+    expanded form, 2^-20 (|x|^2 + |c|^2); duplicated centres keep the lowest index."""
+    n, d, k = 20000, 128, 512
+    g = torch.Generator().manual_seed(11)
+    C = torch.randn(k, d, generator=g) * 2.0 + 100.0
+    C[7] = C[3]
+    X = (C[torch.randint(0, k, (n,), generator=g)] + torch.randn(n, d, generator=g)).to(dtype)
+    labels, _ = ops.assign(X.to(DEV), C.to(DEV), with_dist=False)
+    Cq = ref.quantize_centers(C, dtype).double()
+    Xd = X.double()
+    dist = (Xd * Xd).sum(1, keepdim=True) - 2 * Xd @ Cq.T + (Cq * Cq).sum(1)[None]
+    exp = _first_argmin(dist)
+    srt = dist.sort(1).values
+    uniq_gap = torch.where(srt > srt[:, :1], srt, torch.inf).min(1).values - srt[:, 0]
+    tol = 2.0**-20 * ((Xd * Xd).sum(1) + (Cq * Cq).sum(1).max())
+    ok = uniq_gap > tol
+    assert ok.float().mean() > 0.95
+    got = labels.cpu().long()
+    bad = (got != exp) & ok
+    assert int(bad.sum()) == 0, f"{int(bad.sum())} wrong labels of {int(ok.sum())} resolvable rows"
+    assert not (got == 7).any()   # the duplicate of centre 3 never wins
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -452,7 +484,7 @@ def test_assign_centre_split_small_batches(native, dtype, n, d, k):
     X = _points(n, d, dtype, seed=n + k)
     C = _points(k, d, torch.float32, seed=k + 11)
     Xp = ops.pad_columns(X.to(DEV))
-    pk = ops.pack_centers(C.to(DEV), Xp.shape[1], Xp.dtype, DEV, layout=16)
+    pk = ops.pack_centers(C.to(DEV), Xp.shape[1], Xp.dtype, DEV)
     assert n <= ops.SPLIT_MAX_ROWS
     xn = ops.row_sqnorm(Xp)
     res = []
@@ -463,7 +495,7 @@ def test_assign_centre_split_small_batches(native, dtype, n, d, k):
         if split:
             pk.assign(Xp, xn, lab, mind, slots, True)
         else:
-            native.assign(Xp, pk.pack, pk.cn, xn, lab, mind, slots, pk.Kpad, pk.dpad, True, 16, None)
+            native.assign(Xp, pk.pack, pk.cn, xn, lab, mind, slots, pk.Kpad, pk.dpad, True, None)
         s = slots.view(native.NSLOT, native.SLOT_STRIDE).sum(0)
         res.append((lab.cpu(), mind.cpu(), float(s[0]), float(s[1])))
     assert int((pk._keys[:n] != -1).sum()) == 0          # scratch restored to all-ones
@@ -482,7 +514,7 @@ def test_streaming_fit_matches_resident(native, dtype):
     X = B.make_blobs(50_000, 60, 32, seed=21, dtype=torch.float32, device=DEV)
     C0 = X[:32].cpu()
     ref = mikmeans.KMeans(32, init=C0, dtype=dtype, max_iter=6, tol=0, device=DEV).fit(X)
-    st = mikmeans.KMeans(32, init=C0, dtype=dtype, max_iter=6, tol=0, device=DEV, chunk_rows=7_000).fit(X.cpu())
+    st = mikmeans.KMeans(32, init=C0, dtype=dtype, max_iter=6, tol=0, device=DEV, chunk_rows=6_500).fit(X.cpu())   # -> 6656-row chunks (256 grid)
     from mikmeans.models.streaming import StreamingLloydEngine
 
     assert isinstance(st._engine, StreamingLloydEngine) and len(st._engine.ranges) == 8

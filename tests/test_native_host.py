@@ -37,3 +37,19 @@ def test_jsnum_under_asan_ubsan(tmp_path):
     for v, s in zip(vals, got):
         exp = "null" if not np.isfinite(v) else js_number(float(v))
         assert s == exp, (v, s, exp)
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host C++ compiler")
+def test_launch_planning_under_asan_ubsan(tmp_path):
+    """csrc/plan.h (M-step slice width / LDS bytes / chunks, fixed-point exponent, assign
+    Kpad) swept over K in [1, 2^20], D in [1, 256] under ASan + UBSan (VERDICT r1 #9)."""
+    exe = tmp_path / "plan_fuzz"
+    src = os.path.join(ROOT, "tests", "native", "plan_fuzz.cpp")
+    inc = os.path.join(ROOT, "mikmeans", "csrc")
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                        "-fno-sanitize-recover=all", "-I", inc, src, "-o", str(exe)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    out = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=600)
+    assert out.returncode == 0 and out.stdout.startswith("ok "), out.stdout[-2000:] + out.stderr[-2000:]
