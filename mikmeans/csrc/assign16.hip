@@ -96,8 +96,7 @@ __device__ __forceinline__ float sq16(const u32x4& w, float*) {
 }
 
 // OCC: minimum waves per SIMD the register allocation must allow (launch bounds).
-// OFS (bf16): 1 = workgroup seed offset in the LDS |c|^2 (default), 0 = raw scores (A/B).
-template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, int OFS = 1>
+template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4>
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
@@ -141,7 +140,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   for (int p = 0; p < C::P; ++p) {
     int64_t row = pbase + p * 16 + r;
     row = row < a.N ? row : (a.N - 1);
-    xnr[p] = (!EXACT && OFS == 1 && a.xn) ? a.xn[row] : 0.f;
+    xnr[p] = (!EXACT && a.xn) ? a.xn[row] : 0.f;
     const T* rp = (const T*)a.X + row * a.ldx + g * (DPAD / 4);
 #pragma unroll
     for (int q = 0; q < C::NQ; ++q) {
@@ -157,7 +156,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   // points, from the caller's row norms when given (loaded with the fragments) or from
   // the fragments themselves, folded into this workgroup's LDS copy of |c|^2 once.
   float off = 0.f;
-  if constexpr (!EXACT && OFS == 1) {
+  if constexpr (!EXACT) {
     float m = 0.f;
     if (a.xn) {
 #pragma unroll
@@ -200,15 +199,20 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
     if (c + C::NBUF - 1 < ncl) issue_chunk(c + C::NBUF - 1);
     const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
+    // A fragments + |c|^2 of a tile from the LDS ring
+    auto load_a = [&](int tl_i, u32x4* aw_, f32x4& ci_) {
+      const int tile = (c0 + c) * C::CT + tl_i;
+      ci_ = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
+      const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
+#pragma unroll
+      for (int q = 0; q < C::NQ; ++q) aw_[q] = *(const u32x4*)(tl + q * 1024);
+    };
 #pragma unroll
     for (int tl_i = 0; tl_i < C::CT; ++tl_i) {
       const int tile = (c0 + c) * C::CT + tl_i;
-      // A fragments + |c|^2 of the tile from the LDS ring
-      const f32x4 ci = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
-      const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
       u32x4 aw[C::NQ];
-#pragma unroll
-      for (int q = 0; q < C::NQ; ++q) aw[q] = *(const u32x4*)(tl + q * 1024);
+      f32x4 ci;
+      load_a(tl_i, aw, ci);
       f32x4 acc[C::P];
 #pragma unroll
       for (int p = 0; p < C::P; ++p) acc[p] = ci;
@@ -281,7 +285,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       const int ko = __shfl_xor(k, o, 64);
       if (vo < v || (vo == v && ko < k)) { v = vo; k = ko; }
     }
-    // this point's seed offset (0 for f32 / OFS 0)
+    // this point's seed offset (0 for f32)
     const float offp = off;
     if ((p & 3) == g) {
       const int64_t i = pbase + p * 16 + r;
@@ -365,7 +369,7 @@ static int assign16_splits(int64_t nblk, int nch) {
   return (nch + cps - 1) / cps;  // no empty split (the kernel's chunk range must be non-empty)
 }
 
-template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, int OFS = 1>
+template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4>
 static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   if (a.Kpad % (16 * C::CT) != 0) return hipErrorInvalidValue;
@@ -374,7 +378,7 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, OFS>,
+    (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
@@ -383,31 +387,30 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   const int splits = a.split_keys ? assign16_splits(nblk, a.Kpad / (16 * C::CT)) : 1;
   AssignArgs b = a;
   if (splits == 1) b.split_keys = nullptr;
-  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, OFS>),
+  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_>),
                      dim3((unsigned)nblk, (unsigned)splits), dim3(C::NW * 64), lds, s, b);
   if (splits > 1)
     hipLaunchKernelGGL(split_finish_kernel, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 
-static int g_assign_offset = 1;
-void set_assign_offset(int m) { g_assign_offset = m; }
-
+// The workgroup's point count (NW*P*16) must divide parallel/shard.py ROW_ALIGN (1536).
 template <typename T, int DPAD>
 static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   constexpr int CT = chunk_tiles16(sizeof(T), DPAD);
   constexpr int NQ = DPAD / 4 / Elem<T>::V;
-  constexpr int P = NQ >= 8 ? 2 : 4;  // keep the point fragments within ~64-128 VGPRs
-  // 16 KiB chunks in a 2-slot ring.  A/B on MI355X at N=2e7 D=128 K=1024 bf16 (round 1,
-  // profiles/r1_08_*, r1_16_*, r1_17_*): 1279-1317 TF/s vs 1218-1265 for 4/8 KiB chunks
-  // with 3 slots, 1099 / 1250 for 2 / 8 point blocks per wave, -6 % / -20 % for 8 / 16
-  // waves sharing one ring.  bf16: at most 128 VGPRs (4 waves per SIMD): +2.5 % at the
-  // headline shape.  f32 would spill heavily under that bound.
-  constexpr int OCC = sizeof(T) == 2 ? 4 : 1;
-  if constexpr (sizeof(T) == 2) {
-    if (g_assign_offset == 0) return launch16_t<T, DPAD, P, CT, 2, OCC, 4, 0>(a, s);  // A/B (temporary)
-  }
-  return launch16_t<T, DPAD, P, CT, 2, OCC, 4, 1>(a, s);
+  // 16 KiB chunks in a 2-slot ring.  A/B on MI355X (one process, interleaved rounds; round 1
+  // profiles/r1_08_*, r1_16_*, r1_17_*, round 2 profiles/r2_04_assign_ab.md):
+  //  * bf16 D=128: 4 point blocks per wave at <= 128 VGPRs (4 waves/SIMD) -- 3 / 5 blocks,
+  //    3 waves/SIMD, 8/16 waves per ring, 4/8 KiB chunks x 3 slots and next-tile fragment
+  //    loads under the MFMAs are all slower;
+  //  * bf16 D=64: 8 point blocks at 3 waves/SIMD, -5 % against 4 blocks at 4;
+  //  * bf16 D=256: 3 point blocks at 3 waves/SIMD, -4 % against 2 at 4;
+  //  * f32: the register file sets 4 (D <= 64) or 2 blocks at one wave per SIMD minimum.
+  constexpr int P = sizeof(T) == 2 ? (DPAD == 64 ? 8 : DPAD == 256 ? 3 : 4) : (NQ >= 8 ? 2 : 4);
+  constexpr int OCC = sizeof(T) == 2 ? ((DPAD == 64 || DPAD == 256) ? 3 : 4) : 1;
+  static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
+  return launch16_t<T, DPAD, P, CT, 2, OCC>(a, s);
 }
 
 int assign16_chunk_tiles(int dtype, int dpad) { return plan::assign16_chunk_tiles(dtype == DT_BF16 ? 2 : 4, dpad); }

@@ -468,7 +468,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("assign16_supported", [](int64_t dt, int64_t dpad) { return mk::assign16_chunk_tiles((int)dt, (int)dpad) > 0; });
   m.def("set_update_max_sw", [](int64_t sw) { mk::set_update_max_sw((int)sw); },
         "cap the M-step slice width (smaller LDS footprint for overlap with assign)");
-  m.def("set_assign_offset", [](int64_t m) { mk::set_assign_offset((int)m); }, "A/B: bf16 seed offset scheme");
   m.def("assign_cn_len", [](int64_t kpad) { return mk::assign_cn_len((int)kpad); });
   m.def("update_slice_width", [](int64_t dt, int64_t K, int64_t D, bool w) { return mk::update_slice_width((int)dt, (int)K, (int)D, w); },
         py::arg("dtype"), py::arg("K"), py::arg("D"), py::arg("weighted") = false);

@@ -43,7 +43,6 @@ struct AssignArgs {
   unsigned long long* split_keys = nullptr;
 };
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
-void set_assign_offset(int m);  // bf16 seed-offset scheme (A/B)
 
 // ---- update (LDS-privatised scatter-add) -------------------------------------
 // Sums are accumulated in FIXED POINT: every contribution x*w is rounded to a

@@ -65,12 +65,15 @@ def init_random(X, D, K, n_global, start, comm: Comm, seed: int) -> torch.Tensor
 
 def init_kmeanspp(X: torch.Tensor, D: int, K: int, n_global: int, start: int, comm: Comm, seed: int,
                   n_local_trials: int = 1, xn: torch.Tensor | None = None,
-                  prune: bool | None = None) -> torch.Tensor:
+                  prune: bool | None = None, owner_path: bool | None = None) -> torch.Tensor:
     """k-means++ seeding; returns replicated f32 centres [K, D].
 
     ``X`` may be column-padded (only the first ``D`` columns are real).  ``prune``
     (GPU; default on, ``MIKMEANS_KPP_PRUNE=0`` turns it off) skips the rows the
     triangle inequality rules out of each D^2 pass; the centres are bit-identical.
+    ``owner_path`` (GPU): draw through the multi-rank owner selection (all-gather of the
+    potentials, owner kernel, all-reduce of the row) -- default only when world > 1; a
+    one-rank RCCL group can force it to rehearse the collectives.
     """
     if prune is None:
         prune = os.environ.get("MIKMEANS_KPP_PRUNE", "1") not in ("0", "")
@@ -84,7 +87,8 @@ def init_kmeanspp(X: torch.Tensor, D: int, K: int, n_global: int, start: int, co
     # every random number up front: the GPU loop then never waits for the host
     u = torch.as_tensor(rng.random((K - 1) * L), dtype=torch.float64)
     if X.is_cuda:
-        _kpp_gpu(X, centers, K, comm, u.to(X.device), L, prune)
+        multi = comm.world > 1 if owner_path is None else bool(owner_path)
+        _kpp_gpu(X, centers, K, comm, u.to(X.device), L, prune, multi)
     else:
         _kpp_cpu(X, centers, K, comm, u, L)
     return centers[:, :D].contiguous()
@@ -107,7 +111,7 @@ def _local_target(totals_all: torch.Tensor, u: torch.Tensor, rank: int) -> tuple
     return torch.where(owner, local, torch.full_like(local, -1.0)), total
 
 
-def _kpp_gpu(X, centers, K, comm: Comm, u, L, prune: bool = True):
+def _kpp_gpu(X, centers, K, comm: Comm, u, L, prune: bool = True, multi: bool = False):
     C = native.require()
     n = X.shape[0]
     dev = X.device
@@ -135,9 +139,6 @@ def _kpp_gpu(X, centers, K, comm: Comm, u, L, prune: bool = True):
 
     if n:
         C.kpp_d2(X, centers[0], True, d2, bs, rpb)
-    # multi-rank selection whenever a process group exists (also a forced 1-rank group:
-    # the one-GPU rehearsal of the RCCL path issues the same collectives as W=8)
-    multi = comm.grouped
     for k in range(1, K):
         for t in range(L):
             uk = u[(k - 1) * L + t: (k - 1) * L + t + 1]

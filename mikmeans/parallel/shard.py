@@ -16,10 +16,10 @@ HBM_USABLE_FRACTION = 0.90       # leave room for the runtime / RCCL buffers
 
 
 # Shard boundaries fall on multiples of this many rows: the bf16 assign kernel folds one
-# seed offset per workgroup of 256 points into its keys (csrc/assign16.hip), so aligned
-# shards give every point the same workgroup -- and the same near-tie resolution -- on
-# any world size.
-ROW_ALIGN = 256
+# seed offset per workgroup of 128..512 points into its keys (csrc/assign16.hip; every
+# workgroup size divides 1536), so aligned shards give every point the same workgroup --
+# and the same near-tie resolution -- on any world size.
+ROW_ALIGN = 1536
 
 
 def shard_range(n: int, rank: int, world: int, align: int = ROW_ALIGN) -> tuple[int, int]:

@@ -42,7 +42,6 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--warm-iters", type=int, default=3)
-    ap.add_argument("--ab-offset", default="", help="comma list of bf16 seed-offset modes to A/B (interleaved)")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     dev = torch.device("cuda")
@@ -58,16 +57,6 @@ def main():
                                            eng.col_exp, eng.cnt_exp, False), a.reps)
     res["reduce"] = timed(lambda: C.reduce(eng.slab, eng.cnt_slab, eng.n_chunks, eng.K, eng.Dp, eng.slots,
                                            eng.packed, eng.col_exp, eng.cnt_exp), a.reps)
-    if a.ab_offset:
-        modes = [int(m) for m in a.ab_offset.split(",")]
-        ts = {m: [] for m in modes}
-        for _ in range(5):
-            for m in modes:
-                C.set_assign_offset(m)
-                ts[m].append(timed(lambda: eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True),
-                                   a.reps)["median_ms"])
-        C.set_assign_offset(2)
-        res["ab_offset_ms"] = {str(m): round(statistics.median(v), 4) for m, v in ts.items()}
     res["step"] = timed(eng.step, a.reps)
     res["assign_tflops"] = round(2.0 * a.n * a.k * a.d / (res["assign"]["median_ms"] * 1e-3) / 1e12, 1)
     res["update_GBps"] = round(X.numel() * X.element_size() / (res["update"]["median_ms"] * 1e-3) / 1e9, 1)

@@ -163,10 +163,10 @@ def test_blobs_shard_invariance():
 
 
 def test_shard_plan():
-    assert shard_sizes(10, 3) == [10, 0, 0]                  # one 256-row unit
+    assert shard_sizes(10, 3) == [10, 0, 0]                  # one 1536-row unit
     assert [shard_range(10, r, 3, align=1) for r in range(3)] == [(0, 4), (4, 7), (7, 10)]
-    assert [shard_range(1000, r, 3) for r in range(3)] == [(0, 512), (512, 768), (768, 1000)]
-    assert shard_sizes(10**8, 8)[0] % 256 == 0 and sum(shard_sizes(10**8, 8)) == 10**8
+    assert [shard_range(4000, r, 3) for r in range(3)] == [(0, 1536), (1536, 3072), (3072, 4000)]
+    assert shard_sizes(10**8, 8)[0] % 1536 == 0 and sum(shard_sizes(10**8, 8)) == 10**8
     p = plan(10**8, 128, 1024, world=1, itemsize=2)
     assert p.fits and p.bytes_points == 25_600_000_000
     big = plan(10**9, 256, 512, world=1, itemsize=2)

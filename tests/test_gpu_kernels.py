@@ -514,10 +514,12 @@ def test_streaming_fit_matches_resident(native, dtype):
     X = B.make_blobs(50_000, 60, 32, seed=21, dtype=torch.float32, device=DEV)
     C0 = X[:32].cpu()
     ref = mikmeans.KMeans(32, init=C0, dtype=dtype, max_iter=6, tol=0, device=DEV).fit(X)
-    st = mikmeans.KMeans(32, init=C0, dtype=dtype, max_iter=6, tol=0, device=DEV, chunk_rows=6_500).fit(X.cpu())   # -> 6656-row chunks (256 grid)
+    st = mikmeans.KMeans(32, init=C0, dtype=dtype, max_iter=6, tol=0, device=DEV, chunk_rows=6_000).fit(X.cpu())
     from mikmeans.models.streaming import StreamingLloydEngine
+    from mikmeans.parallel.shard import ROW_ALIGN
 
-    assert isinstance(st._engine, StreamingLloydEngine) and len(st._engine.ranges) == 8
+    R = -(-6_000 // ROW_ALIGN) * ROW_ALIGN     # chunks start on the shard grid
+    assert isinstance(st._engine, StreamingLloydEngine) and len(st._engine.ranges) == -(-50_000 // R)
     assert st.n_iter_ == ref.n_iter_
     assert torch.equal(st.cluster_centers_, ref.cluster_centers_)
     assert torch.equal(st.labels_, ref.labels_)

@@ -93,7 +93,7 @@ def test_rccl_kmeanspp_multi_rank_path(rccl, trials):
     n, d, k = 40_000, 64, 48
     X = B.make_blobs(n, d, 30, seed=2, dtype=torch.bfloat16, device=DEV)
     a = init_kmeanspp(X, d, k, n, 0, Comm.local(DEV), seed=5, n_local_trials=trials)
-    b = init_kmeanspp(X, d, k, n, 0, rccl, seed=5, n_local_trials=trials)
+    b = init_kmeanspp(X, d, k, n, 0, rccl, seed=5, n_local_trials=trials, owner_path=True)
     # the owner path draws with target - 0 on the only rank: same row every step
     assert torch.equal(a, b)
 
