@@ -57,6 +57,8 @@ def main():
                                            eng.col_exp, eng.cnt_exp, False), a.reps)
     res["reduce"] = timed(lambda: C.reduce(eng.slab, eng.cnt_slab, eng.n_chunks, eng.K, eng.Dp, eng.slots,
                                            eng.packed, eng.col_exp, eng.cnt_exp), a.reps)
+    from mikmeans.ops import col_stats
+    res["col_absmax"] = timed(lambda: col_stats(eng.X, sumsq=False), a.reps)   # streaming-read reference
     res["step"] = timed(eng.step, a.reps)
     res["assign_tflops"] = round(2.0 * a.n * a.k * a.d / (res["assign"]["median_ms"] * 1e-3) / 1e12, 1)
     res["update_GBps"] = round(X.numel() * X.element_size() / (res["update"]["median_ms"] * 1e-3) / 1e9, 1)
