@@ -64,6 +64,9 @@ def main(argv=None):
                          "runs the same collective path as N=8; auto: no group when WORLD_SIZE=1")
     ap.add_argument("--timeout", type=float, default=120.0,
                     help="collective timeout in seconds (a dead rank fails the job after this long)")
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
+                    help="replay each Lloyd iteration as one captured hipGraph (the same kernels and RCCL "
+                         "all-reduce, one launch); falls back to eager launches if capture fails")
     args = ap.parse_args(argv)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -119,6 +122,7 @@ def main(argv=None):
         sync()
         extra["init_s"] = round(time.perf_counter() - t0, 3)
         eng = LloydEngine(X, K, comm=comm, incremental=args.incremental).set_centers(C0)
+        extra["graph"] = _capture(eng, args.graph)
         elapsed = _timed_steps(eng, comm, args.warmup, args.steps, sync)
         ms = elapsed * 1e3 / args.steps
         value = args.steps / elapsed
@@ -139,6 +143,7 @@ def main(argv=None):
             C_full = eng.centers.clone()
             del eng
             inc = LloydEngine(X, K, comm=comm, incremental=True).set_centers(C0)
+            _capture(inc, args.graph)
             el_inc = _timed_steps(inc, comm, args.warmup, args.steps, sync)
             extra["incremental_mstep"] = {
                 "value": args.steps / el_inc,
@@ -176,6 +181,25 @@ def main(argv=None):
         print(json.dumps(out), flush=True)
     comm.close()
     return 0
+
+
+def _capture(eng, want: bool) -> bool:
+    """hipGraph-capture one Lloyd iteration (bitwise the eager step: tests/test_gpu_rccl.py);
+    every rank decides together, so either all replay graphs or none does."""
+    ok = torch.tensor([1.0 if (want and eng.gpu) else 0.0], dtype=torch.float64, device=eng.device)
+    if ok.item():
+        try:
+            eng.capture()
+            ok[0] = 1.0 if getattr(eng, "_graphs", None) is not None else 0.0
+        except Exception as e:  # noqa: BLE001 -- fall back to eager launches
+            print(f"[bench] graph capture failed ({e!r}); eager steps", file=sys.stderr, flush=True)
+            eng._graphs = None
+            ok[0] = 0.0
+    eng.comm.allreduce_(ok)                 # SUM over ranks: all must have captured
+    if ok.item() < eng.comm.world:
+        eng._graphs = None
+        return False
+    return True
 
 
 def _timed_steps(eng, comm, warmup: int, steps: int, sync) -> float:
