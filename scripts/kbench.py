@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--warm-iters", type=int, default=3)
+    ap.add_argument("--slice-probe", action="store_true")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     dev = torch.device("cuda")
@@ -59,6 +60,16 @@ def main():
                                            eng.packed, eng.col_exp, eng.cnt_exp), a.reps)
     from mikmeans.ops import col_stats
     res["col_absmax"] = timed(lambda: col_stats(eng.X, sumsq=False), a.reps)   # streaming-read reference
+    if a.slice_probe and a.d == 128:
+        # EXPERIMENT: the same bytes as contiguous 64-B "rows" (what a slice-blocked layout of
+        # X would give the M-step): X viewed as [4n, 32], random labels
+        X4 = eng.X.reshape(-1, 32)
+        lab4 = torch.randint(0, a.k, (X4.shape[0],), dtype=torch.int32, device=dev)
+        nc4 = C.update_n_chunks(eng.dt, a.k, 32, X4.shape[0], False)
+        slab4 = torch.empty(nc4 * a.k * 32, dtype=torch.int64, device=dev)
+        cnt4 = torch.empty(nc4 * a.k, dtype=torch.int64, device=dev)
+        ce4 = eng.col_exp[:32].contiguous()
+        res["update_contig64"] = timed(lambda: C.update(X4, lab4, a.k, slab4, cnt4, nc4, None, ce4, 0, False), a.reps)
     res["step"] = timed(eng.step, a.reps)
     res["assign_tflops"] = round(2.0 * a.n * a.k * a.d / (res["assign"]["median_ms"] * 1e-3) / 1e12, 1)
     res["update_GBps"] = round(X.numel() * X.element_size() / (res["update"]["median_ms"] * 1e-3) / 1e9, 1)
