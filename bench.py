@@ -64,9 +64,11 @@ def main(argv=None):
                          "runs the same collective path as N=8; auto: no group when WORLD_SIZE=1")
     ap.add_argument("--timeout", type=float, default=120.0,
                     help="collective timeout in seconds (a dead rank fails the job after this long)")
-    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
-                    help="replay each Lloyd iteration as one captured hipGraph (the same kernels and RCCL "
-                         "all-reduce, one launch); falls back to eager launches if capture fails")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="replay each Lloyd iteration as one captured hipGraph (the same kernels and the RCCL "
+                         "all-reduce, one launch; eager fallback if capture fails).  auto: on for one rank "
+                         "(cfg2's 0.7 ms steps gain ~1 %%); off for N > 1, where the host already runs "
+                         "far ahead of ~3 ms steps")
     args = ap.parse_args(argv)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -122,7 +124,8 @@ def main(argv=None):
         sync()
         extra["init_s"] = round(time.perf_counter() - t0, 3)
         eng = LloydEngine(X, K, comm=comm, incremental=args.incremental).set_centers(C0)
-        extra["graph"] = _capture(eng, args.graph)
+        use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+        extra["graph"] = _capture(eng, use_graph)
         elapsed = _timed_steps(eng, comm, args.warmup, args.steps, sync)
         ms = elapsed * 1e3 / args.steps
         value = args.steps / elapsed
@@ -143,7 +146,7 @@ def main(argv=None):
             C_full = eng.centers.clone()
             del eng
             inc = LloydEngine(X, K, comm=comm, incremental=True).set_centers(C0)
-            _capture(inc, args.graph)
+            _capture(inc, use_graph)
             el_inc = _timed_steps(inc, comm, args.warmup, args.steps, sync)
             extra["incremental_mstep"] = {
                 "value": args.steps / el_inc,
