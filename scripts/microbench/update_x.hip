@@ -1,0 +1,749 @@
+// mikmeans — K3: Lloyd M-step scatter-add (per-cluster sums and counts) for gfx950.
+//
+// sums[k,:] += w_i x_i, counts[k] += w_i for k = labels[i].
+//
+// Why this shape (measured on MI355X, scripts/microbench/lds_atomics.hip):
+//  * global float atomics run at ~1.3 TB/s of added bytes chip-wide, so a direct
+//    scatter of N=1e8 x D=128 f32 adds (51 GB) would take ~40 ms per iteration;
+//  * LDS ds_add_f32 costs ~169 cycles per wave-instruction whatever the bank
+//    pattern; integer LDS adds are ~20x faster and are bound by moving their
+//    address + data dwords from VGPRs to the LDS (2 cycles per dword).
+// So every workgroup privatises a [K][SW] slice of the sums in LDS as FIXED-POINT
+// integers, TWO columns per 64-bit cell: a contribution q = rne(x * w * 2^e_col)
+// (|q| <= 2^20, per-column exponent e_col from the global column max) is formed
+// by ONE fma against the magic constant 1.5*2^23, whose result's bit pattern is
+// 0x4B400000 + q; the bit patterns of two adjacent columns are added as one
+// ds_add_u64 (3 dwords for 2 elements).  Modulo 2^64 the cell then holds
+//   sum(q_a) + sum(q_b) * 2^32 + n * 0x4B400000 * (1 + 2^32)
+// where n is the number of adds since the last flush (counted per label), and as
+// long as |sum(q)| < 2^31 for both columns the two sums decode exactly.  Each
+// label's add count is tracked; before any can reach 2^11 the workgroup flushes
+// its slice (decode, add into its int64 slab rows, zero) and carries on.
+// Integer addition is exact and associative: the M-step is bitwise identical for
+// any atomic order, chunking or world size; the quantisation error per point is
+// <= 2^-21 max|x_col|.
+//
+// D is split into column slices so a slice fits LDS; every workgroup streams its
+// contiguous chunk of rows with 4..16-byte loads.  Grid mapping is XCD-aware:
+// blocks b and b+8 share an XCD on MI355X, so the n_slices workgroups that read
+// the same rows (different column slices of the same lines) get block ids
+// congruent mod 8 and meet in one 4 MB L2.
+//
+// Reference parity: the reference's "update step" is re-deriving the dashboard
+// after humans move cards (app.mjs:481-496 snapshotMetrics counts); counts here
+// are exactly those per-centroid counts.
+#include <math.h>
+
+#include "../../mikmeans/csrc/common.h"
+#include "../../mikmeans/csrc/kernels.h"
+#include "../../mikmeans/csrc/plan.h"
+
+namespace mku {
+using mk::u32x4; using mk::f32x4; using mk::unpack16; using mk::bf16lo; using mk::bf16hi; using mk::Elem;
+using mk::wait_lgkm0; using mk::raw_barrier; using mk::UpdateArgs; using mk::DT_BF16; using mk::DT_F32;
+using mk::wave_sum; using mk::NSLOT; using mk::SLOT_STRIDE;
+namespace plan = mk::plan;
+// EXPERIMENT bits (not in the product kernel): 256 no per-period barrier / flush check,
+// 512 no LDS adds (values kept live)
+
+
+constexpr int UPD_NT = 512;                 // one LDS-filling workgroup per CU
+using plan::UPD_LDS_MAX;
+using plan::FX_BITS;                        // |q| <= 2^20 per contribution
+constexpr int FX_LIM = (1 << (30 - FX_BITS)) * 2 - 1;  // adds per flush: 2047 * 2^20 < 2^31
+constexpr float FX_MAGIC = 12582912.0f;     // 1.5 * 2^23, bits 0x4B400000
+constexpr unsigned long long FX_MM = 0x4B4000004B400000ull;
+constexpr int UPD_MAX_PERIOD = 1024;        // rows between flush checks
+constexpr int UPD_NBUF = 3;                 // period buffers in the prefetch ring
+
+template <int BYTES> struct LoadT;
+template <> struct LoadT<16> { typedef u32x4 type; };
+template <> struct LoadT<8> { typedef uint2 type; };
+template <> struct LoadT<4> { typedef uint32_t type; };
+
+template <typename T, int BYTES>
+__device__ __forceinline__ void unpack_any(const typename LoadT<BYTES>::type& w, float* o) {
+  if constexpr (BYTES == 16) {
+    unpack16(w, o, (T*)nullptr);
+  } else {
+    constexpr int NW = BYTES / 4;
+    uint32_t d[NW];
+    if constexpr (NW == 1) d[0] = w; else { d[0] = w.x; d[1] = w.y; }
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      if constexpr (sizeof(T) == 2) { o[2 * i] = bf16lo(d[i]); o[2 * i + 1] = bf16hi(d[i]); }
+      else o[i] = __uint_as_float(d[i]);
+    }
+  }
+}
+
+// bits of (1.5*2^23 + rne(v * sc)); exact while |v * sc| <= 2^22.  CLAMP saturates
+// out-of-range contributions at +-2^20 (streams whose scale came from an earlier
+// batch), the bound FX_LIM's no-wrap guarantee assumes; the caller tracks the raw
+// range (rlo, rhi) so a batch that clamped is reported instead of kept silently.
+constexpr float FX_QMAX = 1048576.f;  // 2^FX_BITS
+template <bool CLAMP>
+__device__ __forceinline__ float fx_raw(float v, float sc) { return __builtin_fmaf(v, sc, FX_MAGIC); }
+template <bool CLAMP>
+__device__ __forceinline__ uint32_t fx_clamp(float r) {
+  if constexpr (CLAMP) r = __builtin_amdgcn_fmed3f(r, FX_MAGIC - FX_QMAX, FX_MAGIC + FX_QMAX);
+  return __float_as_uint(r);
+}
+template <bool CLAMP>
+__device__ __forceinline__ uint32_t fx_bits(float v, float sc) { return fx_clamp<CLAMP>(fx_raw<CLAMP>(v, sc)); }
+// Residual pass (wide-range columns): bits of 1.5*2^23 + rne((v*sc - rne(v*sc)) * sc2).
+// v*sc - rne(v*sc) is exact in f32 (|.| <= 1/2), so the hi pass (col_exp) plus this lo
+// pass (col_exp + 20) quantise x to 2^-41 of its column maximum instead of 2^-21.
+__device__ __forceinline__ uint32_t fx_bits_resid(float v, float sc, float sc2) {
+  const float hi = __builtin_fmaf(v, sc, FX_MAGIC) - FX_MAGIC;
+  const float res = __builtin_fmaf(v, sc, -hi);
+  return __float_as_uint(__builtin_fmaf(res, sc2, FX_MAGIC));
+}
+
+__device__ __forceinline__ long long fx_q(float v, float sc) {
+  return (long long)(int)(fx_bits<true>(v, sc) - 0x4B400000u);
+}
+
+// LDS: cells [K+1][LDc] u64 (row K is a sink for rows outside the chunk, so the hot
+// loop has no per-row branch) | add counts [K+1] u32 | flag | weighted counts [K+1] i64
+// (weighted fits only).  With an odd stride (LDc = SW/2 + 1) rows start on scattered
+// banks; where only LDc = SW/2 fits, the pair index is XOR-swizzled by label bits
+// instead (swz), which scatters the banks of one instruction the same way.
+struct UpdLayout {
+  int K, LDc, np, ksh;
+  bool swz;
+  __device__ unsigned long long* cells(char* m) const { return (unsigned long long*)m; }
+  __device__ unsigned* nadd(char* m) const { return (unsigned*)(cells(m) + (size_t)(K + 1) * LDc); }
+  __device__ int* flag(char* m) const { return (int*)(nadd(m) + K + 1); }
+  __device__ long long* wcnt(char* m) const {
+    return (long long*)(((uintptr_t)(flag(m) + 2) + 7) & ~(uintptr_t)7);
+  }
+  __device__ int* nhot(char* m) const { return flag(m) + 1; }
+  // list of labels being flushed (u16), after the weighted counts when present
+  __device__ unsigned short* hot(char* m, bool weighted) const {
+    return (unsigned short*)(wcnt(m) + (weighted ? K + 1 : 0));
+  }
+  // cell position of pair p of label k
+  __device__ int pos(int k, int p) const { return swz ? (p ^ ((k >> ksh) & (np - 1))) : p; }
+};
+
+// nadd[k]: adds since label k's last flush in bits 0..30; bit 31 = "k's slab row
+// already holds a partial sum" (then a flush adds instead of storing).
+constexpr unsigned NADD_MASK = 0x7fffffffu, NADD_WRITTEN = 0x80000000u;
+
+// Mid-chunk flush of every label whose add count reached `thresh`: list them, then
+// decode their cells with one (label, pair) per thread so the slab read-modify-writes
+// of a label are contiguous across lanes.  Called by all threads after an LDS barrier.
+// counts come from the signed 64-bit per-label counters (weighted or incremental
+// M-step) instead of the add counts
+__device__ __forceinline__ bool upd_wcounts(const UpdateArgs& a) { return a.weights || a.dlist; }
+
+template <int SW>
+__device__ void upd_flush_hot(const UpdateArgs& a, const UpdLayout& L, char* m, int slice, int chunk,
+                              unsigned thresh) {
+  constexpr int NP = SW / 2;
+  const bool W = mku::upd_wcounts(a);
+  unsigned* nadd = L.nadd(m);
+  unsigned short* hot = L.hot(m, W);
+  if (threadIdx.x == 0) *L.nhot(m) = 0;
+  __syncthreads();
+  for (int k = threadIdx.x; k < a.K; k += blockDim.x)
+    if ((nadd[k] & NADD_MASK) >= thresh) hot[atomicAdd(L.nhot(m), 1)] = (unsigned short)k;
+  __syncthreads();
+  const int nh = *L.nhot(m);
+  const int cols = (a.D - slice * SW) < SW ? (a.D - slice * SW) : SW;
+  unsigned long long* cells = L.cells(m);
+  for (int e = threadIdx.x; e < nh * NP; e += blockDim.x) {
+    const int k = hot[e / NP], p = e % NP;
+    const unsigned na = nadd[k];
+    const int q = k * L.LDc + L.pos(k, p);
+    const unsigned long long T = cells[q] - (unsigned long long)(na & NADD_MASK) * FX_MM;
+    cells[q] = 0;
+    const int lo = (int)(uint32_t)T;
+    const long long hi = (long long)(T - (unsigned long long)(long long)lo) >> 32;
+    if (2 * p < cols) {
+      long long* dst = a.slab + (int64_t)chunk * a.K * a.D + (int64_t)k * a.D + slice * SW + 2 * p;
+      if (na & NADD_WRITTEN) { dst[0] += lo; dst[1] += hi; }
+      else { dst[0] = lo; dst[1] = hi; }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nh; i += blockDim.x) {
+    const int k = hot[i];
+    const unsigned na = nadd[k];
+    if (slice == 0) {
+      const long long c = W ? L.wcnt(m)[k] : (long long)(na & NADD_MASK);
+      long long* cd = a.cnt_slab + (int64_t)chunk * a.K + k;
+      if (na & NADD_WRITTEN) *cd += c; else *cd = c;
+    }
+    if (W) L.wcnt(m)[k] = 0;
+    nadd[k] = NADD_WRITTEN;
+  }
+  if (threadIdx.x == 0) *L.flag(m) = 0;
+  __syncthreads();
+}
+
+// Final flush of every label, one (label, cell) per thread so the slab writes coalesce.
+template <int SW>
+__device__ void upd_flush_all(const UpdateArgs& a, const UpdLayout& L, char* m, int slice, int chunk) {
+  constexpr int NP = SW / 2;
+  unsigned long long* cells = L.cells(m);
+  const unsigned* nadd = L.nadd(m);
+  __syncthreads();
+  long long* slab = a.slab + (int64_t)chunk * a.K * a.D + slice * SW;
+  const int cols = (a.D - slice * SW) < SW ? (a.D - slice * SW) : SW;
+  for (int e = threadIdx.x; e < a.K * NP; e += blockDim.x) {
+    const int k = e / NP, p = e % NP;
+    const unsigned na = nadd[k];
+    const unsigned long long T = cells[k * L.LDc + L.pos(k, p)] - (unsigned long long)(na & NADD_MASK) * FX_MM;
+    const int lo = (int)(uint32_t)T;
+    const long long hi = (long long)(T - (unsigned long long)(long long)lo) >> 32;
+    if (2 * p < cols) {
+      long long* dst = slab + (int64_t)k * a.D + 2 * p;
+      if (na & NADD_WRITTEN) { dst[0] += lo; dst[1] += hi; }
+      else { dst[0] = lo; dst[1] = hi; }
+    }
+  }
+  if (slice == 0) {
+    for (int k = threadIdx.x; k < a.K; k += blockDim.x) {
+      const unsigned na = nadd[k];
+      const long long c = mku::upd_wcounts(a) ? L.wcnt(m)[k] : (long long)(na & NADD_MASK);
+      long long* dst = a.cnt_slab + (int64_t)chunk * a.K + k;
+      if (na & NADD_WRITTEN) *dst += c; else *dst = c;
+    }
+  }
+}
+
+enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8, UPD_RESID = 32 };
+
+constexpr int upd_ksh(int np) { return np >= 32 ? 0 : np == 16 ? 1 : np == 8 ? 2 : np == 4 ? 3 : np == 2 ? 4 : 5; }
+using plan::upd_lds_bytes;
+
+template <typename T, int SW, int MODE, int NT = UPD_NT, int NBF = UPD_NBUF, int PER = UPD_MAX_PERIOD>
+__global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
+                                                        int64_t rows_per_chunk) {
+  // (rows_per_chunk is recomputed from the list length in incremental mode)
+  constexpr bool CLAMP = MODE & UPD_CLAMP;
+  constexpr bool DELTA = MODE & UPD_DELTA;
+  constexpr bool W = MODE & (UPD_WEIGHTED | UPD_DELTA);  // per-row signed weights
+  constexpr bool SWZ = MODE & UPD_SWZ;
+  constexpr bool RESID = MODE & UPD_RESID;               // lo pass of the wide-range columns
+  constexpr int ES = sizeof(T);
+  constexpr int PB = (SW * ES >= 16) ? 16 : SW * ES;  // bytes per lane load
+  constexpr int V = PB / ES;                           // elements per lane load (even)
+  constexpr int LPR = SW / V;                          // lanes per row
+  constexpr int RPP = NT / LPR;                        // rows per pass
+  constexpr int UNR = (PER / RPP) < 8 ? (PER / RPP) : 8;
+  constexpr int PERIOD = RPP * UNR;
+  constexpr unsigned THRESH = FX_LIM - PERIOD + 1;     // flush before any label passes FX_LIM
+  constexpr int NP = SW / 2;
+  constexpr int LDC = SWZ ? NP : NP + 1;                // unpadded + swizzle, or odd stride
+  constexpr int KSH = upd_ksh(NP);
+  static_assert(V % 2 == 0 && UNR >= 1 && FX_LIM >= PERIOD, "update tiling");
+  typedef typename LoadT<PB>::type LT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const UpdLayout L{a.K, LDC, NP, KSH, SWZ};
+  unsigned long long* cells = L.cells(smem);
+  long long* wcnt = L.wcnt(smem);
+  unsigned* nadd = L.nadd(smem);
+
+  const int b = blockIdx.x;
+  const int j = b >> 3;
+  const int slice = j % n_slices;
+  const int chunk = (j / n_slices) * 8 + (b & 7);
+  if constexpr (RESID) {  // slices without a wide-range column have nothing to add
+    bool any = false;
+    for (int c = slice * SW; c < slice * SW + SW && c < a.D; ++c) any |= a.col_exp2[c] > -200;
+    if (!any) return;
+  }
+
+  {
+    unsigned long long* z = cells;
+    const int nz = (int)((upd_lds_bytes(a.K, LDC, W) + 7) / 8);
+    for (int e = threadIdx.x; e < nz; e += NT) z[e] = 0;
+  }
+
+  // Incremental mode: the rows are the 2*c entries of the changed-row list (c adds
+  // to the new labels, then c subtractions from the old ones) unless it overflowed.
+  int64_t nrows = a.N;
+  int dc = 0;
+  bool full = true;
+  if constexpr (DELTA) {
+    dc = *a.dcount;
+    full = dc > a.dcap;
+    if (!full) {
+      nrows = 2 * (int64_t)dc;
+      rows_per_chunk = (nrows + a.n_chunks - 1) / a.n_chunks;
+    }
+  }
+  const int64_t row0 = (int64_t)chunk * rows_per_chunk;
+  int64_t row1 = row0 + rows_per_chunk;
+  if (row1 > nrows) row1 = nrows;
+  const int lr = threadIdx.x / LPR, lp = threadIdx.x % LPR;
+  const int col = slice * SW + lp * V;
+  const bool colok = col < a.D;
+  const bool all_cols = (a.D % SW) == 0;               // kernel-uniform
+  const int colc = colok ? col : 0;
+  const bool counter = lp == 0;
+  const bool wcounter = W && counter && slice == 0;
+  const float cscale = ldexpf(1.f, a.cnt_exp);
+  float sc[V], sc2[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    sc[e] = (col + e < a.D) ? ldexpf(1.f, a.col_exp[col + e]) : 0.f;
+    // lo-pass scale 2^(col_exp2 - col_exp): 2^20 on wide columns, 0 elsewhere
+    sc2[e] = (RESID && col + e < a.D && a.col_exp2[col + e] > -200)
+                 ? ldexpf(1.f, a.col_exp2[col + e] - a.col_exp[col + e]) : 0.f;
+  }
+  float rlo = FX_MAGIC, rhi = FX_MAGIC;  // raw contribution range seen (CLAMP: clamp report)
+
+  // Row mapping: in a period starting at `base`, lane (lr, lp) owns the UNR
+  // consecutive rows base + lr*UNR + u, so runs of equal labels (sorted or
+  // converged data) merge in registers before they reach the LDS, and the loads
+  // of one lane are one address plus immediate offsets.
+  const T* xrow = (const T*)a.X + (row0 + (int64_t)lr * UNR) * a.ldx + colc;
+  const int* lrow = a.labels + row0 + lr * UNR;
+  const float* wrow = a.weights ? a.weights + row0 + lr * UNR : nullptr;
+  auto load = [&](int64_t base, LT* w_, int* lab_, float* wt_) {
+    const int64_t off = base - row0;
+    if (DELTA && !full) {                              // gather the listed rows
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int64_t j0 = base + (int64_t)lr * UNR + u;
+        const int64_t j = j0 < row1 ? j0 : row1 - 1;
+        const bool neg = j >= dc;
+        const int2 e = a.dlist[neg ? j - dc : j];
+        const int l = neg ? e.y : a.labels[e.x];
+        lab_[u] = (j0 < row1 && (unsigned)l < (unsigned)a.K) ? l : a.K;
+        const float wv = a.weights ? a.weights[e.x] : 1.f;
+        wt_[u] = neg ? -wv : wv;
+        w_[u] = *(const LT*)((const T*)a.X + (int64_t)e.x * a.ldx + colc);
+      }
+    } else if (base + PERIOD <= row1) {                // whole period (all but the last)
+      const T* p = xrow + off * a.ldx;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int l = lrow[off + u];
+        lab_[u] = ((unsigned)l < (unsigned)a.K) ? l : a.K;
+        if constexpr (DELTA) wt_[u] = wrow ? wrow[off + u] : 1.f;
+        else if constexpr (W) wt_[u] = wrow[off + u];
+        w_[u] = *(const LT*)(p + u * a.ldx);
+      }
+    } else {                                           // clamp rows past the chunk -> sink row K
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int64_t i0 = base + (int64_t)lr * UNR + u;
+        const int64_t i = i0 < row1 ? i0 : row1 - 1;
+        const int l = a.labels[i];
+        lab_[u] = (i0 < row1 && (unsigned)l < (unsigned)a.K) ? l : a.K;
+        if constexpr (DELTA) wt_[u] = a.weights ? a.weights[i] : 1.f;
+        else if constexpr (W) wt_[u] = a.weights[i];
+        w_[u] = *(const LT*)((const T*)a.X + i * a.ldx + colc);
+      }
+    }
+    if (!all_cols && !colok) {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) w_[u] = LT{};
+    }
+  };
+
+  // Accumulate one period; sets the flush flag when a label's add count nears FX_LIM.
+  auto accumulate = [&](const LT* w_, const int* lab_, const float* wt_) {
+    unsigned seen = 0;
+    unsigned long long acc[V / 2];
+    int cur = lab_[0];
+    unsigned run = 0;
+    auto emit = [&]() {
+      if constexpr ((MODE & 512) != 0) {
+#pragma unroll
+        for (int c = 0; c < V / 2; ++c) asm volatile("" :: "v"(acc[c]));
+        return;
+      }
+      unsigned long long* dst = cells + cur * LDC;
+      if constexpr (SWZ) {
+        const int f = (cur >> KSH) & (NP - 1);
+#pragma unroll
+        for (int c = 0; c < V / 2; ++c)
+          __hip_atomic_fetch_add(dst + ((lp * (V / 2) + c) ^ f), acc[c], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+#pragma unroll
+        for (int c = 0; c < V / 2; ++c)
+          __hip_atomic_fetch_add(dst + lp * (V / 2) + c, acc[c], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (counter) {
+        const unsigned old = __hip_atomic_fetch_add(nadd + cur, run, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP) & NADD_MASK;
+        if (cur < a.K) seen = old + run > seen ? old + run : seen;  // the sink never flushes
+      }
+    };
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      float f[V];
+      unpack_any<T, PB>(w_[u], f);
+      unsigned long long v[V / 2];
+#pragma unroll
+      for (int e = 0; e < V; e += 2) {
+        const float s0 = W ? sc[e] * wt_[u] : sc[e];
+        const float s1 = W ? sc[e + 1] * wt_[u] : sc[e + 1];
+        if constexpr (RESID)
+          v[e / 2] = (unsigned long long)fx_bits_resid(f[e], s0, sc2[e]) |
+                     ((unsigned long long)fx_bits_resid(f[e + 1], s1, sc2[e + 1]) << 32);
+        else {
+          const float r0 = fx_raw<CLAMP>(f[e], s0), r1 = fx_raw<CLAMP>(f[e + 1], s1);
+          if constexpr (CLAMP) {
+            rlo = fminf(fminf(rlo, r0), r1);
+            rhi = fmaxf(fmaxf(rhi, r0), r1);
+          }
+          v[e / 2] = (unsigned long long)fx_clamp<CLAMP>(r0) | ((unsigned long long)fx_clamp<CLAMP>(r1) << 32);
+        }
+      }
+      if constexpr (W)
+        if (wcounter)  // weighted counts: one add per row (slice 0 only)
+          __hip_atomic_fetch_add(wcnt + lab_[u], (long long)__float2int_rn(wt_[u] * cscale),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (u == 0) {
+#pragma unroll
+        for (int c = 0; c < V / 2; ++c) acc[c] = v[c];
+        run = 1;
+      } else {
+        if (lab_[u] != cur) {  // label changes: emit the run so far
+          emit();
+          cur = lab_[u];
+          run = 0;
+#pragma unroll
+          for (int c = 0; c < V / 2; ++c) acc[c] = 0;
+        }
+#pragma unroll
+        for (int c = 0; c < V / 2; ++c) acc[c] += v[c];
+        ++run;
+      }
+    }
+    emit();
+    if constexpr (!(MODE & 256)) {
+    if (seen >= THRESH) *L.flag(smem) = 1;
+    // LDS-only barrier: the prefetched global loads stay in flight
+    wait_lgkm0();
+    raw_barrier();
+    }
+  };
+
+  // NB-deep ring of period buffers: NB-1 periods of loads in flight while one accumulates
+  constexpr int NB = NBF;
+  LT wb[NB][UNR];
+  int lb[NB][UNR];
+  float tb[NB][UNR];
+#pragma unroll
+  for (int s = 0; s < NB - 1; ++s)
+    if (row0 + (int64_t)s * PERIOD < row1) load(row0 + (int64_t)s * PERIOD, wb[s], lb[s], tb[s]);
+  __syncthreads();
+  for (int64_t base = row0; base < row1; base += (int64_t)NB * PERIOD) {
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+      const int64_t pb = base + (int64_t)s * PERIOD;
+      if (pb < row1) {
+        const int64_t nb = pb + (int64_t)(NB - 1) * PERIOD;
+        const int ns = (s + NB - 1) % NB;  // static after unrolling
+        if (nb < row1) load(nb, wb[ns], lb[ns], tb[ns]);
+        accumulate(wb[s], lb[s], tb[s]);
+        if constexpr (!(MODE & 256))
+          if (*L.flag(smem)) mku::upd_flush_hot<SW>(a, L, smem, slice, chunk, THRESH / 2);  // batch near-hot labels too
+      }
+    }
+  }
+  mku::upd_flush_all<SW>(a, L, smem, slice, chunk);
+  if constexpr (CLAMP) {
+    if (a.clamp_count) {
+      const unsigned long long any = __ballot(!(rlo >= FX_MAGIC - FX_QMAX && rhi <= FX_MAGIC + FX_QMAX));
+      if (any && (threadIdx.x & 63) == __builtin_ctzll(any)) atomicAdd(a.clamp_count, 1);
+    }
+  }
+}
+
+// Fallback for K too large to privatise even 2 columns: direct int64 global atomics
+// (same fixed-point contributions, so results match the LDS path bit for bit).
+template <typename T>
+__global__ __launch_bounds__(256) void update_global_kernel(UpdateArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= a.N) return;
+  const int k = a.labels[i];
+  if ((unsigned)k >= (unsigned)a.K) return;
+  const float wt = a.weights ? a.weights[i] : 1.f;
+  const T* xr = (const T*)a.X + i * a.ldx;
+  for (int d = lane; d < a.D; d += 64)
+    atomicAdd((unsigned long long*)(a.slab + (int64_t)k * a.D + d),
+              (unsigned long long)fx_q(Elem<T>::to_f32(xr[d]), ldexpf(1.f, a.col_exp[d]) * wt));
+  if (lane == 0)
+    atomicAdd((unsigned long long*)(a.cnt_slab + k),
+              (unsigned long long)(a.weights ? (long long)__float2int_rn(wt * ldexpf(1.f, a.cnt_exp))
+                                             : 1ll));
+}
+
+static int esize(int dtype) { return dtype == DT_BF16 ? 2 : 4; }
+
+// Cap on the slice width (0 = none).  A smaller slice shrinks the LDS footprint
+// so an update workgroup can be co-resident with assign workgroups when the
+// engine overlaps the two kernels on separate streams.
+static int g_update_max_sw = 0;
+void set_update_max_sw(int sw) { g_update_max_sw = sw; }
+
+static int choose_sw(int dtype, int K, int D, bool weighted, int* ldc) {
+  return plan::choose_sw(esize(dtype), K, D, weighted, g_update_max_sw, ldc);
+}
+
+int update_slice_width(int dtype, int K, int D, bool weighted) {
+  int ldc;
+  return choose_sw(dtype, K, D, weighted, &ldc);
+}
+
+int update_n_chunks(int dtype, int K, int D, int64_t N, bool weighted) {
+  return plan::update_n_chunks(update_slice_width(dtype, K, D, weighted), D, N);
+}
+
+int fixed_exp(double maxabs) { return plan::fixed_exp(maxabs); }
+
+template <typename T, int SW, int MODE, int NT, int NBF = UPD_NBUF, int PER = UPD_MAX_PERIOD>
+hipError_t launch_nt(const UpdateArgs& a, int ldc, hipStream_t s) {
+  const int n_slices = (a.D + SW - 1) / SW;
+  const int64_t rows_per_chunk = (a.N + a.n_chunks - 1) / a.n_chunks;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)update_kernel<T, SW, MODE, NT, NBF, PER>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)UPD_LDS_MAX);
+    attr = true;
+  }
+  hipLaunchKernelGGL((update_kernel<T, SW, MODE, NT, NBF, PER>), dim3(a.n_chunks * n_slices), dim3(NT),
+                     upd_lds_bytes(a.K, ldc, (MODE & (UPD_WEIGHTED | UPD_DELTA)) != 0), s, a, n_slices,
+                     rows_per_chunk);
+  return hipGetLastError();
+}
+
+// 1024 threads (4 waves per SIMD, <= 128 VGPRs) where the period buffers fit without
+// spilling; measured at N=1e8 D=128 K=1024 bf16: 5.67 ms vs 5.89 (512) vs 6.74 (256).
+template <typename T, int SW, int MODE>
+constexpr int upd_default_nt() {
+  return (sizeof(T) == 2 && SW <= 32 && !(MODE & (UPD_WEIGHTED | UPD_DELTA))) ? 1024 : UPD_NT;
+}
+
+template <typename T, int SW, int MODE>
+static hipError_t launch_sw(const UpdateArgs& a, int ldc, hipStream_t s) {
+  constexpr int NT = upd_default_nt<T, SW, MODE>();
+  // 1024 threads: 512-row periods, 6-deep ring (5 periods of loads in flight).  N=1e8
+  // D=128 K=1024 bf16: 5.33-5.76 ms vs 5.96-6.34 for 3 x 1024-row periods (same boxes).
+  constexpr int ES = sizeof(T);
+  constexpr int V = ((SW * ES >= 16) ? 16 : SW * ES) / ES;
+  constexpr int RPP = NT / (SW / V);
+  constexpr int PER = RPP > 512 ? RPP : 512;
+  if constexpr (NT == 1024) return mku::launch_nt<T, SW, MODE, 1024, 6, PER>(a, ldc, s);
+  else return mku::launch_nt<T, SW, MODE, NT>(a, ldc, s);
+}
+
+template <typename T, int SW>
+static hipError_t launch_clamp(const UpdateArgs& a, int ldc, hipStream_t s) {
+  const int mode = (a.clamp ? UPD_CLAMP : 0) | (a.weights ? UPD_WEIGHTED : 0) |
+                   (ldc == SW / 2 ? UPD_SWZ : 0);
+  if (a.col_exp2) {  // residual (lo) pass of the wide-range columns: never clamped / incremental
+    if (a.clamp || a.dlist) return hipErrorInvalidValue;
+    switch (mode) {
+      case 0: return mku::launch_sw<T, SW, UPD_RESID>(a, ldc, s);
+      case 2: return mku::launch_sw<T, SW, UPD_RESID | UPD_WEIGHTED>(a, ldc, s);
+      case 4: return mku::launch_sw<T, SW, UPD_RESID | UPD_SWZ>(a, ldc, s);
+      default: return mku::launch_sw<T, SW, UPD_RESID | UPD_WEIGHTED | UPD_SWZ>(a, ldc, s);
+    }
+  }
+  if (a.dlist) {  // incremental M-step (Lloyd: never clamped; weights read at run time)
+    if (a.clamp) return hipErrorInvalidValue;
+    return (mode & UPD_SWZ) ? mku::launch_sw<T, SW, UPD_DELTA | UPD_SWZ>(a, ldc, s)
+                            : mku::launch_sw<T, SW, UPD_DELTA>(a, ldc, s);
+  }
+  switch (mode) {
+    case 0: return mku::launch_sw<T, SW, 0>(a, ldc, s);
+    case 1: return mku::launch_sw<T, SW, 1>(a, ldc, s);
+    case 2: return mku::launch_sw<T, SW, 2>(a, ldc, s);
+    case 3: return mku::launch_sw<T, SW, 3>(a, ldc, s);
+    case 4: return mku::launch_sw<T, SW, 4>(a, ldc, s);
+    case 5: return mku::launch_sw<T, SW, 5>(a, ldc, s);
+    case 6: return mku::launch_sw<T, SW, 6>(a, ldc, s);
+    default: return mku::launch_sw<T, SW, 7>(a, ldc, s);
+  }
+}
+
+template <typename T>
+static hipError_t launch_update_t(const UpdateArgs& a, hipStream_t s, int sw, int ldc) {
+  switch (sw) {
+    case 64: return mku::launch_clamp<T, 64>(a, ldc, s);
+    case 32: return mku::launch_clamp<T, 32>(a, ldc, s);
+    case 16: return mku::launch_clamp<T, 16>(a, ldc, s);
+    case 8: return mku::launch_clamp<T, 8>(a, ldc, s);
+    case 4: return mku::launch_clamp<T, 4>(a, ldc, s);
+    case 2: return mku::launch_clamp<T, 2>(a, ldc, s);
+    case 0:
+      // caller zeroed slab[K*D] + cnt_slab[K] (n_chunks == 1)
+      hipLaunchKernelGGL((update_global_kernel<T>), dim3((unsigned)((a.N + 3) / 4)), dim3(256), 0,
+                         s, a);
+      return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s) {
+  if (a.N <= 0) return hipSuccess;
+  int ldc = 0;
+  const int sw = choose_sw(dtype, a.K, a.D, a.weights != nullptr || a.dlist != nullptr, &ldc);
+  if (sw > 0 && a.n_chunks % 8) return hipErrorInvalidValue;
+  if (a.dlist && sw == 0) return hipErrorInvalidValue;  // no incremental global fallback
+  if (a.col_exp2 && sw == 0) return hipErrorInvalidValue;  // residual pass needs the LDS path
+  return dtype == DT_BF16 ? mku::launch_update_t<uint16_t>(a, s, sw, ldc)
+                          : mku::launch_update_t<float>(a, s, sw, ldc);
+}
+
+// ---------------------------------------------------------------------------
+// launch_reduce: packed[k*D+d] = 2^-exp[d] * sum_c slab[c][k][d] (f64, exact: every
+// partial is an integer below 2^53), counts likewise,
+// plus the assign kernel's inertia / changed slots (which it then re-zeroes).
+__global__ __launch_bounds__(256) void reduce_kernel(const long long* __restrict__ slab,
+                                                     const long long* __restrict__ cnt_slab,
+                                                     int n_chunks, int K, int D,
+                                                     const int* __restrict__ col_exp,
+                                                     double inv_c, double* slots, double* packed,
+                                                     long long* tot, const int* dcount, int dcap) {
+  const int64_t KD = (int64_t)K * D;
+  const int64_t total = KD + K;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < total && tot) {  // incremental: running integer totals (exact, order-free)
+    const long long* src = e < KD ? slab + e : cnt_slab + (e - KD);
+    const int64_t stride = e < KD ? KD : K;
+    long long acc = 0;
+    for (int c = 0; c < n_chunks; ++c) acc += src[(int64_t)c * stride];
+    const long long t = (*dcount > dcap) ? acc : tot[e] + acc;
+    tot[e] = t;
+    packed[e] = e < KD ? ldexp((double)t, -col_exp[e % D]) : (double)t * inv_c;
+  } else if (e < total) {
+    double acc = 0.0;
+    if (e < KD) {
+      for (int c = 0; c < n_chunks; ++c) acc += (double)slab[(int64_t)c * KD + e];
+      acc = ldexp(acc, -col_exp[e % D]);
+    } else {
+      const int64_t k = e - KD;
+      for (int c = 0; c < n_chunks; ++c) acc += (double)cnt_slab[(int64_t)c * K + k];
+      acc *= inv_c;
+    }
+    packed[e] = acc;
+  }
+  if (blockIdx.x == gridDim.x - 1) {
+    __shared__ double red[4][2];
+    double si = 0, sc = 0;
+    if (slots) {
+      for (int i = threadIdx.x; i < NSLOT; i += 256) {
+        si += slots[i * SLOT_STRIDE + 0];
+        sc += slots[i * SLOT_STRIDE + 1];
+        slots[i * SLOT_STRIDE + 0] = 0.0;
+        slots[i * SLOT_STRIDE + 1] = 0.0;
+      }
+    }
+    si = wave_sum(si);
+    sc = wave_sum(sc);
+    if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6][0] = si; red[threadIdx.x >> 6][1] = sc; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      packed[total + 0] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+      packed[total + 1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    }
+  }
+}
+
+hipError_t launch_reduce(const long long* slab, const long long* cnt_slab, int n_chunks, int K,
+                         int D, const int* col_exp, int cnt_exp, double* slots, double* packed,
+                         hipStream_t s, long long* tot, const int* dcount, int dcap) {
+  if (tot && !dcount) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)K * D + K;
+  const unsigned nb = (unsigned)((total + 255) / 256);
+  hipLaunchKernelGGL(reduce_kernel, dim3(nb), dim3(256), 0, s, slab, cnt_slab, n_chunks, K, D,
+                     col_exp, ldexp(1.0, -cnt_exp), slots, packed, tot, dcount, dcap);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// launch_reduce_cols: out[k*nw + j] = 2^-exps[j] * sum_c slab[c][k][cols[j]] (f64, exact:
+// integer partials below 2^53) -- the lo sums of the wide-range columns, appended to the
+// all-reduce message and added onto the hi sums after it.
+__global__ __launch_bounds__(256) void reduce_cols_kernel(const long long* __restrict__ slab, int n_chunks,
+                                                          int K, int D, const int* __restrict__ cols,
+                                                          const int* __restrict__ exps, int nw,
+                                                          double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)K * nw) return;
+  const int k = (int)(e / nw), j = (int)(e % nw);
+  const int64_t KD = (int64_t)K * D;
+  const long long* src = slab + (int64_t)k * D + cols[j];
+  long long acc = 0;
+  for (int c = 0; c < n_chunks; ++c) acc += src[(int64_t)c * KD];
+  out[e] = ldexp((double)acc, -exps[j]);
+}
+
+hipError_t launch_reduce_cols(const long long* slab, int n_chunks, int K, int D, const int* cols,
+                              const int* exps, int nw, double* out, hipStream_t s) {
+  const int64_t total = (int64_t)K * nw;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(reduce_cols_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, slab,
+                     n_chunks, K, D, cols, exps, nw, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// launch_label_delta: the changed-row list of the incremental M-step.  Each thread
+// checks LD_R rows (coalesced, stride 256); a workgroup reserves its list range with
+// one global atomic.  List order is not deterministic, but the M-step sums are
+// integers, so the result is.
+constexpr int LD_R = 16;
+
+__global__ __launch_bounds__(256) void label_delta_kernel(const int32_t* __restrict__ labels,
+                                                          int32_t* __restrict__ prev, int64_t N,
+                                                          int2* __restrict__ list, int cap,
+                                                          int* count) {
+  __shared__ int wg_n, wg_base;
+  if (threadIdx.x == 0) wg_n = 0;
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * 256 * LD_R + threadIdx.x;
+  int lab[LD_R], old[LD_R];
+  unsigned m = 0;
+#pragma unroll
+  for (int t = 0; t < LD_R; ++t) {
+    const int64_t i = b0 + t * 256;
+    if (i < N) {
+      lab[t] = labels[i];
+      old[t] = prev[i];
+      if (lab[t] != old[t]) m |= 1u << t;
+    }
+  }
+  const int n = __popc(m);
+  const int off = n ? atomicAdd(&wg_n, n) : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) wg_base = wg_n ? atomicAdd(count, wg_n) : 0;
+  __syncthreads();
+  int pos = wg_base + off;
+#pragma unroll
+  for (int t = 0; t < LD_R; ++t) {
+    if (m >> t & 1u) {
+      const int64_t i = b0 + t * 256;
+      prev[i] = lab[t];
+      if (pos < cap) list[pos] = make_int2((int)i, old[t]);
+      ++pos;
+    }
+  }
+}
+
+hipError_t launch_label_delta(const int32_t* labels, int32_t* prev, int64_t N, int2* list, int cap,
+                              int* count, hipStream_t s) {
+  if (N >= (int64_t)1 << 31) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(count, 0, sizeof(int), s);
+  if (e != hipSuccess || N <= 0) return e;
+  const int64_t per = 256 * LD_R;
+  hipLaunchKernelGGL(label_delta_kernel, dim3((unsigned)((N + per - 1) / per)), dim3(256), 0, s,
+                     labels, prev, N, list, cap, count);
+  return hipGetLastError();
+}
+
+}  // namespace mku
