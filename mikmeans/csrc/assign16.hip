@@ -96,7 +96,9 @@ __device__ __forceinline__ float sq16(const u32x4& w, float*) {
 }
 
 // OCC: minimum waves per SIMD the register allocation must allow (launch bounds).
-template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4>
+// FULLD: D == DPAD, so no fragment piece needs a column check.  The per-piece check costs
+// 7 % at D=256 K=512 even when every piece passes it (profiles/r2_08_assign_clock_study.md).
+template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false>
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
@@ -145,7 +147,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
 #pragma unroll
     for (int q = 0; q < C::NQ; ++q) {
       const int col = g * (DPAD / 4) + q * C::V;
-      if (col < a.D) xr[p][q] = *(const u32x4*)(rp + q * C::V);
+      if (FULLD || col < a.D) xr[p][q] = *(const u32x4*)(rp + q * C::V);
       else xr[p][q] = u32x4{0u, 0u, 0u, 0u};
     }
   }
@@ -378,7 +380,9 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_>,
+    (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
@@ -387,8 +391,12 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   const int splits = a.split_keys ? assign16_splits(nblk, a.Kpad / (16 * C::CT)) : 1;
   AssignArgs b = a;
   if (splits == 1) b.split_keys = nullptr;
-  hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_>),
-                     dim3((unsigned)nblk, (unsigned)splits), dim3(C::NW * 64), lds, s, b);
+  if (a.D == DPAD)
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true>),
+                       dim3((unsigned)nblk, (unsigned)splits), dim3(C::NW * 64), lds, s, b);
+  else
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false>),
+                       dim3((unsigned)nblk, (unsigned)splits), dim3(C::NW * 64), lds, s, b);
   if (splits > 1)
     hipLaunchKernelGGL(split_finish_kernel, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, s, b);
   return hipGetLastError();

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "assign_x.h"
+#include "assign_copy.h"
 
 #define CK(x)                                                                              \
   do {                                                                                     \
@@ -57,6 +58,20 @@ typedef hipError_t (*LaunchFn)(const mk::AssignArgs&, hipStream_t);
 struct Variant { const char* name; LaunchFn fn; };
 
 static hipError_t v_prod128(const mk::AssignArgs& a, hipStream_t s) { return mk::launch_assign16(mk::DT_BF16, 128, a, s); }
+static double* g_slots = nullptr;
+// the Lloyd engine's call: previous labels read (changed count), inertia/changed slots
+static hipError_t v_prod128_lloyd(const mk::AssignArgs& a, hipStream_t s) {
+  mk::AssignArgs b = a; b.track_changed = 1; b.slots = g_slots;
+  return mk::launch_assign16(mk::DT_BF16, 128, b, s);
+}
+static hipError_t v_prod128_lloyd_nomind(const mk::AssignArgs& a, hipStream_t s) {
+  mk::AssignArgs b = a; b.track_changed = 1; b.slots = g_slots; b.mind = nullptr;
+  return mk::launch_assign16(mk::DT_BF16, 128, b, s);
+}
+static hipError_t v_prod128_nomind(const mk::AssignArgs& a, hipStream_t s) {
+  mk::AssignArgs b = a; b.mind = nullptr;
+  return mk::launch_assign16(mk::DT_BF16, 128, b, s);
+}
 static hipError_t v_prod64(const mk::AssignArgs& a, hipStream_t s) { return mk::launch_assign16(mk::DT_BF16, 64, a, s); }
 static hipError_t v_prod256(const mk::AssignArgs& a, hipStream_t s) { return mk::launch_assign16(mk::DT_BF16, 256, a, s); }
 
@@ -126,10 +141,20 @@ int main(int argc, char** argv) {
   a.xn = xn; a.labels = labels; a.mind = mind; a.slots = nullptr; a.track_changed = 0;
 
   std::vector<Variant> vs;
-  if (D == 128) vs.push_back({"prod", v_prod128});
+  CK(hipMalloc(&g_slots, mk::NSLOT * mk::SLOT_STRIDE * 8));
+  CK(hipMemset(g_slots, 0, mk::NSLOT * mk::SLOT_STRIDE * 8));
+  if (D == 128) {
+    vs.push_back({"prod", v_prod128});
+    vs.push_back({"prod_lloyd", v_prod128_lloyd});
+    vs.push_back({"prod_lloyd_nomind", v_prod128_lloyd_nomind});
+    vs.push_back({"prod_nomind", v_prod128_nomind});
+  }
   if (D == 64) vs.push_back({"prod", v_prod64});
   if (D == 256) vs.push_back({"prod", v_prod256});
   mkx::add_variants(D, vs);
+  if (D == 256) vs.push_back({"old_head", mkc::launch_old<256, 3, 2, 3>});
+  if (D == 128) vs.push_back({"old_head", mkc::launch_old<128, 4, 4, 4>});
+  if (D == 64) vs.push_back({"old_head", mkc::launch_old<64, 8, 8, 3>});
   vs.push_back({"prod_again", vs[0].fn});
 
   // reference labels

@@ -312,7 +312,6 @@ static hipError_t launch_x(const AssignArgs& a, hipStream_t s) {
 
 template <typename VS>
 static void add_variants(int D, VS& vs) {
-  if (D == 128) vs.push_back({"x_p4o4_m0", launch_x<128, 4, 4, 0>});
   if (D == 64) vs.push_back({"x64_p8o3_m0", launch_x<64, 8, 3, 0>});
   if (D == 256) {
     vs.push_back({"x256_p3o3_m0", launch_x<256, 3, 3, 0>});
