@@ -507,21 +507,26 @@ static hipError_t launch_nt(const UpdateArgs& a, int ldc, hipStream_t s) {
 
 // 1024 threads (4 waves per SIMD, <= 128 VGPRs) where the period buffers fit without
 // spilling; measured at N=1e8 D=128 K=1024 bf16: 5.67 ms vs 5.89 (512) vs 6.74 (256).
+// 64-column slices (K <= ~600) take a 3-deep ring to stay under 128 VGPRs: 1.64 ms vs
+// 1.95 at 512 threads for the cfg5 batch (N=16.8M D=256 K=512; profiles/r2_05_update_study.md).
+// (The clamped 64-column body would spill 32+ VGPRs at 1024 threads, so it keeps 512.)
 template <typename T, int SW, int MODE>
 constexpr int upd_default_nt() {
-  return (sizeof(T) == 2 && SW <= 32 && !(MODE & (UPD_WEIGHTED | UPD_DELTA))) ? 1024 : UPD_NT;
+  return (sizeof(T) == 2 && (SW <= 32 || (SW == 64 && !(MODE & UPD_CLAMP))) &&
+          !(MODE & (UPD_WEIGHTED | UPD_DELTA))) ? 1024 : UPD_NT;
 }
 
 template <typename T, int SW, int MODE>
 static hipError_t launch_sw(const UpdateArgs& a, int ldc, hipStream_t s) {
   constexpr int NT = upd_default_nt<T, SW, MODE>();
-  // 1024 threads: 512-row periods, 6-deep ring (5 periods of loads in flight).  N=1e8
-  // D=128 K=1024 bf16: 5.33-5.76 ms vs 5.96-6.34 for 3 x 1024-row periods (same boxes).
+  // 1024 threads: 512-row periods, 6-deep ring (5 periods of loads in flight; 3-deep for
+  // 64-column slices).  N=1e8 D=128 K=1024 bf16: 5.33-5.76 ms vs 5.96-6.34 for 3 x
+  // 1024-row periods (same boxes).
   constexpr int ES = sizeof(T);
   constexpr int V = ((SW * ES >= 16) ? 16 : SW * ES) / ES;
   constexpr int RPP = NT / (SW / V);
   constexpr int PER = RPP > 512 ? RPP : 512;
-  if constexpr (NT == 1024) return launch_nt<T, SW, MODE, 1024, 6, PER>(a, ldc, s);
+  if constexpr (NT == 1024) return launch_nt<T, SW, MODE, 1024, (SW <= 32 ? 6 : 3), PER>(a, ldc, s);
   else return launch_nt<T, SW, MODE, NT>(a, ldc, s);
 }
 

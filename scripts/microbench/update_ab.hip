@@ -44,9 +44,9 @@ typedef hipError_t (*Fn)(const mk::UpdateArgs&, int, hipStream_t);
 struct Var { const char* name; Fn fn; };
 
 static hipError_t prod(const mk::UpdateArgs& a, int, hipStream_t s) { return mk::launch_update(mk::DT_BF16, a, s); }
-template <int MODE, int NT, int NBF, int PER>
+template <int MODE, int NT, int NBF, int PER, int SW = 32>
 static hipError_t xv(const mk::UpdateArgs& a, int ldc, hipStream_t s) {
-  return mku::launch_nt<uint16_t, 32, MODE, NT, NBF, PER>(a, ldc, s);
+  return mku::launch_nt<uint16_t, SW, MODE, NT, NBF, PER>(a, ldc, s);
 }
 
 int main(int argc, char** argv) {
@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
   const int reps = argc > 5 ? atoi(argv[5]) : 5;
   int ldc = 0;
   const int sw = mk::plan::choose_sw(2, K, D, false, 0, &ldc);
-  if (sw != 32) { fprintf(stderr, "harness variants assume slice width 32 (got %d)\n", sw); return 2; }
+  if (sw != 32 && sw != 64) { fprintf(stderr, "harness variants assume slice width 32 or 64 (got %d)\n", sw); return 2; }
   const int nc = mk::update_n_chunks(mk::DT_BF16, K, D, N);
   uint16_t* X; int32_t* lab; long long *slab, *cnt; int* cexp;
   CK(hipMalloc(&X, N * D * 2));
@@ -76,16 +76,21 @@ int main(int argc, char** argv) {
   a.X = X; a.N = N; a.D = D; a.ldx = D; a.labels = lab; a.K = K; a.n_chunks = nc;
   a.slab = slab; a.cnt_slab = cnt; a.weights = nullptr; a.col_exp = cexp; a.cnt_exp = 0; a.clamp = 0;
 
-  std::vector<Var> vs = {
-      {"prod", prod},
-      {"x_same", xv<0, 1024, 6, 512>},
-      {"x_nobar", xv<256, 1024, 6, 512>},
-      {"x_nolds", xv<512, 1024, 6, 512>},
-      {"x_nobar_nolds", xv<768, 1024, 6, 512>},
-      {"x_nb8", xv<0, 1024, 8, 512>},
-      {"x_per1024", xv<0, 1024, 4, 1024>},
-      {"x_nt512", xv<0, 512, 6, 512>},
-  };
+  std::vector<Var> vs;
+  vs.push_back({"prod", prod});
+  if (sw == 32) {
+    vs.push_back({"x_same", xv<0, 1024, 6, 512>});
+    vs.push_back({"x_nolds", xv<512, 1024, 6, 512>});
+  } else {
+    vs.push_back({"x_same", xv<0, 512, 3, 1024, 64>});
+    vs.push_back({"x_nt1024_nb3", xv<0, 1024, 3, 512, 64>});
+    vs.push_back({"x_nt1024_nb4", xv<0, 1024, 4, 512, 64>});
+    vs.push_back({"x_nt512_nb4", xv<0, 512, 4, 1024, 64>});
+    vs.push_back({"x_nt512_nb6_p512", xv<0, 512, 6, 512, 64>});
+    vs.push_back({"x_nt1024_nb6", xv<0, 1024, 6, 512, 64>});
+    vs.push_back({"x_nolds", xv<512, 512, 3, 1024, 64>});
+  }
+
   // reference: column sums over all chunks
   auto totals = [&](std::vector<long long>& t) {
     std::vector<long long> h((size_t)nc * K * D);
