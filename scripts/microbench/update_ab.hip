@@ -80,8 +80,16 @@ int main(int argc, char** argv) {
   vs.push_back({"prod", prod});
   if (sw == 32) {
     vs.push_back({"x_same", xv<0, 1024, 6, 512>});
-    vs.push_back({"x_nolds", xv<512, 1024, 6, 512>});
+    vs.push_back({"x_nb4", xv<0, 1024, 4, 512>});
+    vs.push_back({"x_nb5", xv<0, 1024, 5, 512>});
+    vs.push_back({"x_p256_nb8", xv<0, 1024, 8, 256>});
+    vs.push_back({"x_p256_nb12", xv<0, 1024, 12, 256>});
+    vs.push_back({"x_p256_nb6", xv<0, 1024, 6, 256>});
+    vs.push_back({"x_clamp", xv<1, 1024, 6, 512>});
   } else {
+    vs.push_back({"x_clamp_nt512_nb3", xv<1, 512, 3, 1024, 64>});
+    vs.push_back({"x_clamp_nt1024_nb2", xv<1, 1024, 2, 512, 64>});
+    vs.push_back({"x_clamp_nt512_nb2", xv<1, 512, 2, 1024, 64>});
     vs.push_back({"x_same", xv<0, 512, 3, 1024, 64>});
     vs.push_back({"x_nt1024_nb3", xv<0, 1024, 3, 512, 64>});
     vs.push_back({"x_nt1024_nb4", xv<0, 1024, 4, 512, 64>});
