@@ -145,16 +145,10 @@ int main(int argc, char** argv) {
   CK(hipMemset(g_slots, 0, mk::NSLOT * mk::SLOT_STRIDE * 8));
   if (D == 128) {
     vs.push_back({"prod", v_prod128});
-    vs.push_back({"prod_lloyd", v_prod128_lloyd});
-    vs.push_back({"prod_lloyd_nomind", v_prod128_lloyd_nomind});
-    vs.push_back({"prod_nomind", v_prod128_nomind});
   }
   if (D == 64) vs.push_back({"prod", v_prod64});
   if (D == 256) vs.push_back({"prod", v_prod256});
   mkx::add_variants(D, vs);
-  if (D == 256) vs.push_back({"old_head", mkc::launch_old<256, 3, 2, 3>});
-  if (D == 128) vs.push_back({"old_head", mkc::launch_old<128, 4, 4, 4>});
-  if (D == 64) vs.push_back({"old_head", mkc::launch_old<64, 8, 8, 3>});
   vs.push_back({"prod_again", vs[0].fn});
 
   // reference labels

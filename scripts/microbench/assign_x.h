@@ -13,7 +13,7 @@
 namespace mkx {
 using namespace mk;
 
-template <int DPAD, int P, int OCC, int MODE, int NW = 4>
+template <int DPAD, int P, int OCC, int MODE, int NW = 4, int NBUF = 2>
 __global__ __launch_bounds__(NW * 64, OCC) void assign_x_kernel(AssignArgs a) {
   constexpr int V = 8;
   constexpr int NQ = DPAD / 4 / V;
@@ -23,7 +23,6 @@ __global__ __launch_bounds__(NW * 64, OCC) void assign_x_kernel(AssignArgs a) {
   constexpr int PIECES = CHUNK_BYTES / 1024;
   constexpr int NPW = PIECES / NW;
   constexpr int PTS = NW * P * 16;
-  constexpr int NBUF = 2;
   constexpr bool SKEW = MODE & 1, SGB = MODE & 2, PF = MODE & 4;
   constexpr bool STAMP = MODE & 8;   // per-workgroup (s_memtime, s_memrealtime) at start/end
   constexpr bool NOEPI = MODE & 16;
@@ -32,6 +31,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void assign_x_kernel(AssignArgs a) {
   // point blocks where some lane's tile minimum is <= its threshold, seeded with the score
   // to the previous label's centre (VALU dot product + rounding margin)
   constexpr bool GATE = MODE & 64;
+  constexpr bool NOWAIT = MODE & 512;  // ablation: ring refills issued but never waited for (racy)
+  constexpr bool NORING = MODE & 256;  // ablation: no ring refills after the first two chunks (stale C)
   constexpr bool DUMP = MODE & 128;  // debug: mind[i] = seed (unfudged) + |x|^2  // next tile's fragments read into the same registers before the epilogue  // ablation: no argmin epilogue (accumulators kept live)
   unsigned long long t_beg = 0, r_beg = 0;
   if constexpr (STAMP) { t_beg = __builtin_amdgcn_s_memtime(); r_beg = __builtin_amdgcn_s_memrealtime(); }
@@ -57,7 +58,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void assign_x_kernel(AssignArgs a) {
       blds16(rC, (MK_LDS void*)(dst + pc * 1024), loff, src + (uint32_t)pc * 1024u);
     }
   };
-  issue_chunk(0);
+#pragma unroll
+  for (int c = 0; c < NBUF - 1; ++c)
+    if (c < a.Kpad / (16 * CT)) issue_chunk(c);
 
   const int64_t pbase = (int64_t)blockIdx.x * PTS + (int64_t)wid * (P * 16);
   u32x4 xr[P][NQ];
@@ -157,10 +160,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void assign_x_kernel(AssignArgs a) {
   int tprev = -1;
 
   for (int c = 0; c < nch; ++c) {
-    wait_vmcnt<0>();
+    if constexpr (NOWAIT) { if (c < 1) wait_vmcnt<0>(); }
+    else if constexpr (NBUF > 2) { if (c + NBUF - 2 < nch) wait_vmcnt<(NBUF - 2) * NPW>(); else wait_vmcnt<0>(); }
+    else wait_vmcnt<0>();
     wait_lgkm0();
     raw_barrier();
-    if (c + 1 < nch) issue_chunk(c + 1);
+    if (c + NBUF - 1 < nch && (!NORING || c + 1 < 2)) issue_chunk(c + NBUF - 1);
     const char* buf = bufs + (c % NBUF) * CHUNK_BYTES;
     u32x4 awn[NQ];
     f32x4 cin;
@@ -293,26 +298,34 @@ __global__ __launch_bounds__(NW * 64, OCC) void assign_x_kernel(AssignArgs a) {
   }
 }
 
-template <int DPAD, int P, int OCC, int MODE>
+template <int DPAD, int P, int OCC, int MODE, int NW = 4, int NBUF = 2>
 static hipError_t launch_x(const AssignArgs& a, hipStream_t s) {
   constexpr int CT = plan::chunk_tiles16(2, DPAD);
   constexpr int CHUNK_BYTES = CT * (DPAD / 32) * 1024;
   const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
-  const size_t lds = cn_bytes + 2 * CHUNK_BYTES + 64;
+  const size_t lds = cn_bytes + NBUF * CHUNK_BYTES + 16 * NW;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)assign_x_kernel<DPAD, P, OCC, MODE>,
+    (void)hipFuncSetAttribute((const void*)assign_x_kernel<DPAD, P, OCC, MODE, NW, NBUF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  const int64_t nblk = (a.N + 4 * P * 16 - 1) / (4 * P * 16);
-  hipLaunchKernelGGL((assign_x_kernel<DPAD, P, OCC, MODE>), dim3((unsigned)nblk), dim3(256), lds, s, a);
+  const int64_t nblk = (a.N + NW * P * 16 - 1) / (NW * P * 16);
+  hipLaunchKernelGGL((assign_x_kernel<DPAD, P, OCC, MODE, NW, NBUF>), dim3((unsigned)nblk), dim3(NW * 64), lds, s, a);
   return hipGetLastError();
 }
 
 template <typename VS>
 static void add_variants(int D, VS& vs) {
   if (D == 64) vs.push_back({"x64_p8o3_m0", launch_x<64, 8, 3, 0>});
+  if (D == 128) {
+    vs.push_back({"x_p4o4_m0", launch_x<128, 4, 4, 0>});
+    vs.push_back({"x_p4o4_st", launch_x<128, 4, 4, 8>});
+    vs.push_back({"x_p4o4_nw8", launch_x<128, 4, 4, 0, 8, 2>});
+    vs.push_back({"x_p4o4_nw8_nb3", launch_x<128, 4, 4, 0, 8, 3>});
+    vs.push_back({"x_p4o4_nw16_nb3", launch_x<128, 4, 4, 0, 16, 3>});
+    vs.push_back({"x_p4o4_nw16_nb4", launch_x<128, 4, 4, 0, 16, 4>});
+  }
   if (D == 256) {
     vs.push_back({"x256_p3o3_m0", launch_x<256, 3, 3, 0>});
     vs.push_back({"x256_p3o3_early", launch_x<256, 3, 3, 32>});
