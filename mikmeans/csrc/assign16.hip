@@ -209,12 +209,25 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
 #pragma unroll
       for (int q = 0; q < C::NQ; ++q) aw_[q] = *(const u32x4*)(tl + q * 1024);
     };
+    // EARLY (bf16 D=64): the next tile's fragments are read right after this tile's
+    // MFMAs are issued, so their LDS latency hides under the argmin epilogue (+2 % at D=64
+    // in one-process A/B, profiles/r2_08_assign_clock_study.md; no gain at D=128)
+    constexpr bool EARLY = !EXACT && DPAD == 64;
+    u32x4 awe[C::NQ];
+    f32x4 cie;
+    if constexpr (EARLY) load_a(0, awe, cie);
 #pragma unroll
     for (int tl_i = 0; tl_i < C::CT; ++tl_i) {
       const int tile = (c0 + c) * C::CT + tl_i;
       u32x4 aw[C::NQ];
       f32x4 ci;
-      load_a(tl_i, aw, ci);
+      if constexpr (EARLY) {
+#pragma unroll
+        for (int q = 0; q < C::NQ; ++q) aw[q] = awe[q];
+        ci = cie;
+      } else {
+        load_a(tl_i, aw, ci);
+      }
       f32x4 acc[C::P];
 #pragma unroll
       for (int p = 0; p < C::P; ++p) acc[p] = ci;
@@ -222,6 +235,10 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       for (int q = 0; q < C::NQ; ++q) {
 #pragma unroll
         for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
+      }
+      if constexpr (EARLY) {
+        if (tl_i + 1 < C::CT) load_a(tl_i + 1, awe, cie);
+        __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (EXACT) {
         // (tile*4 + reg) as wave-uniform values: the index select needs no VALU add

@@ -4,7 +4,9 @@
 namespace mkc {
 using namespace mk;
 // OCC: minimum waves per SIMD the register allocation must allow (launch bounds).
-template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4>
+// FULLD: D == DPAD, so no fragment piece needs a column check.  The per-piece check costs
+// 7 % at D=256 K=512 even when every piece passes it (profiles/r2_08_assign_clock_study.md).
+template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false>
 __global__ __launch_bounds__(NW_ * 64, OCC) void old_kernel(AssignArgs a) {
   using C = mk::Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
@@ -53,7 +55,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void old_kernel(AssignArgs a) {
 #pragma unroll
     for (int q = 0; q < C::NQ; ++q) {
       const int col = g * (DPAD / 4) + q * C::V;
-      if (col < a.D) xr[p][q] = *(const u32x4*)(rp + q * C::V);
+      if (FULLD || col < a.D) xr[p][q] = *(const u32x4*)(rp + q * C::V);
       else xr[p][q] = u32x4{0u, 0u, 0u, 0u};
     }
   }
@@ -241,13 +243,13 @@ static hipError_t launch_old(const AssignArgs& a, hipStream_t s) {
   const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)old_kernel<uint16_t, DPAD, P, CT, 2, OCC, 4>,
+    (void)hipFuncSetAttribute((const void*)old_kernel<uint16_t, DPAD, P, CT, 2, OCC, 4, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
   AssignArgs b = a; b.split_keys = nullptr;
-  hipLaunchKernelGGL((old_kernel<uint16_t, DPAD, P, CT, 2, OCC, 4>), dim3((unsigned)nblk, 1), dim3(256), lds, s, b);
+  hipLaunchKernelGGL((old_kernel<uint16_t, DPAD, P, CT, 2, OCC, 4, true>), dim3((unsigned)nblk, 1), dim3(256), lds, s, b);
   return hipGetLastError();
 }
 }  // namespace mkc

@@ -321,10 +321,7 @@ static void add_variants(int D, VS& vs) {
   if (D == 128) {
     vs.push_back({"x_p4o4_m0", launch_x<128, 4, 4, 0>});
     vs.push_back({"x_p4o4_st", launch_x<128, 4, 4, 8>});
-    vs.push_back({"x_p4o4_nw8", launch_x<128, 4, 4, 0, 8, 2>});
-    vs.push_back({"x_p4o4_nw8_nb3", launch_x<128, 4, 4, 0, 8, 3>});
-    vs.push_back({"x_p4o4_nw16_nb3", launch_x<128, 4, 4, 0, 16, 3>});
-    vs.push_back({"x_p4o4_nw16_nb4", launch_x<128, 4, 4, 0, 16, 4>});
+
   }
   if (D == 256) {
     vs.push_back({"x256_p3o3_m0", launch_x<256, 3, 3, 0>});
