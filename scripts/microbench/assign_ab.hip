@@ -150,6 +150,7 @@ int main(int argc, char** argv) {
   if (D == 256) vs.push_back({"prod", v_prod256});
   mkx::add_variants(D, vs);
   if (D == 64) vs.push_back({"old_head", mkc::launch_old<64, 8, 8, 3>});
+  if (D == 256) vs.push_back({"old_head", mkc::launch_old<256, 3, 2, 3>});
   if (D == 128) vs.push_back({"old_head", mkc::launch_old<128, 4, 4, 4>});
   vs.push_back({"prod_again", vs[0].fn});
 
