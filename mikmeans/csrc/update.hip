@@ -511,12 +511,18 @@ static hipError_t launch_nt(const UpdateArgs& a, int ldc, hipStream_t s) {
 // 1.95 at 512 threads for the cfg5 batch (N=16.8M D=256 K=512; profiles/r2_05_update_study.md).
 // The clamped 64-column body (mini-batch without a value bound) takes a 2-deep ring:
 // 1.79 ms vs 2.02 at 512 threads; a 3-deep one would spill 32 VGPRs.
+// f32, 64-column slices, plain adds: 1024 threads with a 2-deep ring, 1.80 vs 2.02 ms at
+// N=2e7 D=128 K=256 (0.121 vs 0.126 at cfg2's N=1e6; profiles/r2_05_update_study.md).
 template <typename T, int SW, int MODE>
 constexpr int upd_default_nt() {
-  return (sizeof(T) == 2 && SW <= 64 && !(MODE & (UPD_WEIGHTED | UPD_DELTA))) ? 1024 : UPD_NT;
+  if constexpr (sizeof(T) == 4)
+    return (SW == 64 && !(MODE & (UPD_WEIGHTED | UPD_DELTA | UPD_CLAMP | UPD_RESID))) ? 1024 : UPD_NT;
+  return (SW <= 64 && !(MODE & (UPD_WEIGHTED | UPD_DELTA))) ? 1024 : UPD_NT;
 }
-template <int SW, int MODE>
-constexpr int upd_ring_1024() { return SW <= 32 ? 6 : (MODE & UPD_CLAMP) ? 2 : 3; }
+template <typename T, int SW, int MODE>
+constexpr int upd_ring_1024() {
+  return sizeof(T) == 4 ? 2 : SW <= 32 ? 6 : (MODE & UPD_CLAMP) ? 2 : 3;
+}
 
 template <typename T, int SW, int MODE>
 static hipError_t launch_sw(const UpdateArgs& a, int ldc, hipStream_t s) {
@@ -528,7 +534,7 @@ static hipError_t launch_sw(const UpdateArgs& a, int ldc, hipStream_t s) {
   constexpr int V = ((SW * ES >= 16) ? 16 : SW * ES) / ES;
   constexpr int RPP = NT / (SW / V);
   constexpr int PER = RPP > 512 ? RPP : 512;
-  if constexpr (NT == 1024) return launch_nt<T, SW, MODE, 1024, upd_ring_1024<SW, MODE>(), PER>(a, ldc, s);
+  if constexpr (NT == 1024) return launch_nt<T, SW, MODE, 1024, upd_ring_1024<T, SW, MODE>(), PER>(a, ldc, s);
   else return launch_nt<T, SW, MODE, NT>(a, ldc, s);
 }
 

@@ -28,7 +28,8 @@ __device__ __forceinline__ uint32_t hsh(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16; return x;
 }
 __device__ __forceinline__ float unif(uint32_t h) { return (h >> 8) * (1.0f / 16777216.0f); }
-__global__ void gen_kernel(uint16_t* X, int32_t* lab, int64_t i0, int D, int K) {
+template <typename T>
+__global__ void gen_kernel(T* X, int32_t* lab, int64_t i0, int D, int K) {
   const int64_t i = i0 + blockIdx.x;
   const uint32_t b = hsh((uint32_t)i * 2654435761u);
   if (threadIdx.x == 0) lab[blockIdx.x] = (int32_t)(b % (uint32_t)K);
@@ -36,17 +37,19 @@ __global__ void gen_kernel(uint16_t* X, int32_t* lab, int64_t i0, int D, int K) 
     const float c = (unif(hsh((b % 4096u) * 7919u + d * 104729u + 17u)) - 0.5f) * 20.f;
     const uint32_t h = hsh(hsh((uint32_t)i ^ 0x9e3779b9u) + (uint32_t)d * 0x85ebca6bu);
     const float n = unif(h) + unif(hsh(h + 1)) + unif(hsh(h + 2)) + unif(hsh(h + 3)) - 2.f;
-    X[(int64_t)blockIdx.x * D + d] = mk::f32_to_bf16(c + 1.7f * n);
+    if constexpr (sizeof(T) == 2) X[(int64_t)blockIdx.x * D + d] = mk::f32_to_bf16(c + 1.7f * n);
+    else X[(int64_t)blockIdx.x * D + d] = c + 1.7f * n;
   }
 }
 
 typedef hipError_t (*Fn)(const mk::UpdateArgs&, int, hipStream_t);
 struct Var { const char* name; Fn fn; };
 
-static hipError_t prod(const mk::UpdateArgs& a, int, hipStream_t s) { return mk::launch_update(mk::DT_BF16, a, s); }
-template <int MODE, int NT, int NBF, int PER, int SW = 32>
+static int g_dt = mk::DT_BF16;
+static hipError_t prod(const mk::UpdateArgs& a, int, hipStream_t s) { return mk::launch_update(g_dt, a, s); }
+template <int MODE, int NT, int NBF, int PER, int SW = 32, typename T = uint16_t>
 static hipError_t xv(const mk::UpdateArgs& a, int ldc, hipStream_t s) {
-  return mku::launch_nt<uint16_t, SW, MODE, NT, NBF, PER>(a, ldc, s);
+  return mku::launch_nt<T, SW, MODE, NT, NBF, PER>(a, ldc, s);
 }
 
 int main(int argc, char** argv) {
@@ -55,19 +58,23 @@ int main(int argc, char** argv) {
   const int K = argc > 3 ? atoi(argv[3]) : 1024;
   const int rounds = argc > 4 ? atoi(argv[4]) : 4;
   const int reps = argc > 5 ? atoi(argv[5]) : 5;
+  const bool f32 = argc > 6 && atoi(argv[6]) == 1;
+  g_dt = f32 ? mk::DT_F32 : mk::DT_BF16;
+  const int es = f32 ? 4 : 2;
   int ldc = 0;
-  const int sw = mk::plan::choose_sw(2, K, D, false, 0, &ldc);
+  const int sw = mk::plan::choose_sw(es, K, D, false, 0, &ldc);
   if (sw != 32 && sw != 64) { fprintf(stderr, "harness variants assume slice width 32 or 64 (got %d)\n", sw); return 2; }
-  const int nc = mk::update_n_chunks(mk::DT_BF16, K, D, N);
-  uint16_t* X; int32_t* lab; long long *slab, *cnt; int* cexp;
-  CK(hipMalloc(&X, N * D * 2));
+  const int nc = mk::update_n_chunks(g_dt, K, D, N);
+  void* X; int32_t* lab; long long *slab, *cnt; int* cexp;
+  CK(hipMalloc(&X, N * D * es));
   CK(hipMalloc(&lab, N * 4));
   CK(hipMalloc(&slab, (size_t)nc * K * D * 8));
   CK(hipMalloc(&cnt, (size_t)nc * K * 8));
   CK(hipMalloc(&cexp, D * 4));
   for (int64_t i0 = 0; i0 < N; i0 += (1 << 24)) {
     const int64_t n = std::min<int64_t>(1 << 24, N - i0);
-    gen_kernel<<<dim3((unsigned)n), 64>>>(X + i0 * D, lab + i0, i0, D, K);
+    if (f32) gen_kernel<float><<<dim3((unsigned)n), 64>>>((float*)X + i0 * D, lab + i0, i0, D, K);
+    else gen_kernel<uint16_t><<<dim3((unsigned)n), 64>>>((uint16_t*)X + i0 * D, lab + i0, i0, D, K);
   }
   std::vector<int> he(D, mk::plan::fixed_exp(16.0));
   CK(hipMemcpy(cexp, he.data(), D * 4, hipMemcpyHostToDevice));
@@ -78,7 +85,12 @@ int main(int argc, char** argv) {
 
   std::vector<Var> vs;
   vs.push_back({"prod", prod});
-  if (sw == 32) {
+  if (f32 && sw == 64) {
+    vs.push_back({"f_same", xv<0, 512, 3, 1024, 64, float>});
+    vs.push_back({"f_nt1024_nb2", xv<0, 1024, 2, 512, 64, float>});
+    vs.push_back({"f_nt1024_nb3", xv<0, 1024, 3, 512, 64, float>});
+    vs.push_back({"f_nt512_nb2", xv<0, 512, 2, 1024, 64, float>});
+  } else if (sw == 32) {
     vs.push_back({"x_same", xv<0, 1024, 6, 512>});
     vs.push_back({"x_nb4", xv<0, 1024, 4, 512>});
     vs.push_back({"x_nb5", xv<0, 1024, 5, 512>});
@@ -139,8 +151,8 @@ int main(int argc, char** argv) {
     auto t = times[v];
     std::sort(t.begin(), t.end());
     const double med = t[t.size() / 2];
-    printf("N=%lld D=%d K=%d %-16s median %.4f ms  min %.4f ms  %.0f GB/s\n", (long long)N, D, K, vs[v].name, med,
-           t[0], N * D * 2.0 / (med * 1e-3) / 1e9);
+    printf("%s N=%lld D=%d K=%d %-16s median %.4f ms  min %.4f ms  %.0f GB/s\n", f32 ? "f32" : "bf16", (long long)N, D, K, vs[v].name, med,
+           t[0], N * D * (double)es / (med * 1e-3) / 1e9);
   }
   fflush(stdout);
   return 0;
