@@ -77,6 +77,52 @@ inline int fixed_exp(double maxabs) {
   return e;
 }
 
+// K-split M-step (plain full passes: unweighted, not incremental, not the residual pass).
+// KS workgroups share a row chunk; workgroup j owns labels [j*kq, (j+1)*kq) and every
+// column, and takes whole rows (LPR lanes x 16 B), so each wave-instruction reads full
+// 128-B lines instead of the column-slice kernel's 64-B row pieces.
+struct KsPlan {
+  int ks;   // workgroups per row chunk (power of two)
+  int kq;   // labels per workgroup
+  int lpr;  // lanes per row (power of two <= 64): 16-B pieces of a (column-padded) row
+  int ldc;  // u64 cells per label (2 columns each, + 1 for an odd bank stride)
+  int gm;   // row groups of loads kept in flight per wave and period
+};
+constexpr int KS_NT = 1024;                         // threads per workgroup
+constexpr size_t KS_LIST_BYTES = 2 * (KS_NT / 64) * 64 * 4;  // per-wave match lists, 2 periods
+MK_HD inline size_t ks_lds_bytes(int kq, int ldc) {
+  return (size_t)kq * (size_t)ldc * 8 + (size_t)kq * 4 + 16 + KS_LIST_BYTES;
+}
+inline bool choose_ks(int esize, int K, int D, KsPlan* p) {
+  if (K < 2 || D < 2 || D % 2 || (D * esize) % 4) return false;
+  const int v = 16 / esize;
+  int lpr = 1;
+  while (lpr * v < D) lpr *= 2;
+  if (lpr > 64 || lpr < 8) return false;            // rows past 1 KiB, or rows of 64 B or less
+  const int ldc = lpr * v / 2 + 1;
+  // prefer ~4 row groups of matches per wave and period (LPR / KS of them on average)
+  int ks = lpr / 4 > 1 ? lpr / 4 : 1;
+  while (ks > K) ks /= 2;                            // no workgroup without labels
+  for (;;) {
+    const int kq = (K + ks - 1) / ks;
+    if (ks_lds_bytes(kq, ldc) <= UPD_LDS_MAX) {
+      if (ks < 2) return false;                      // one workgroup would scan every row alone
+      p->ks = ks; p->kq = kq; p->lpr = lpr; p->ldc = ldc;
+      p->gm = (lpr / ks) >= 2 ? 6 : 3;
+      return true;
+    }
+    if (ks >= 64) return false;
+    ks *= 2;
+  }
+}
+// Row chunks for the K-split grid: at least the column-slice kernel's count for the same
+// shape (so both kernels fill the chip with one slab layout), a multiple of 8.
+inline int update_n_chunks_ks(int ks, int nc_slice) {
+  int nc = (256 + ks - 1) / ks;
+  nc = ((nc + 7) / 8) * 8;
+  return nc > nc_slice ? nc : nc_slice;
+}
+
 // Assign kernel: centroid tiles (16 centroids) per 16 KiB LDS chunk, 0 = unsupported width.
 constexpr int chunk_tiles16(int esize, int dpad) {
   return (16 * dpad * esize) >= 16384 ? 1 : 16384 / (16 * dpad * esize);

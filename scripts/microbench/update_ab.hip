@@ -63,7 +63,7 @@ int main(int argc, char** argv) {
   const int es = f32 ? 4 : 2;
   int ldc = 0;
   const int sw = mk::plan::choose_sw(es, K, D, false, 0, &ldc);
-  if (sw != 32 && sw != 64) { fprintf(stderr, "harness variants assume slice width 32 or 64 (got %d)\n", sw); return 2; }
+  printf("slice width %d, n_chunks from production %d\n", sw, mk::update_n_chunks(g_dt, K, D, N));
   const int nc = mk::update_n_chunks(g_dt, K, D, N);
   void* X; int32_t* lab; long long *slab, *cnt; int* cexp;
   CK(hipMalloc(&X, N * D * es));
@@ -85,32 +85,11 @@ int main(int argc, char** argv) {
 
   std::vector<Var> vs;
   vs.push_back({"prod", prod});
-  if (f32 && sw == 64) {
-    vs.push_back({"f_same", xv<0, 512, 3, 1024, 64, float>});
-    vs.push_back({"f_nt1024_nb2", xv<0, 1024, 2, 512, 64, float>});
-    vs.push_back({"f_nt1024_nb3", xv<0, 1024, 3, 512, 64, float>});
-    vs.push_back({"f_nt512_nb2", xv<0, 512, 2, 1024, 64, float>});
-  } else if (sw == 32) {
-    vs.push_back({"x_same", xv<0, 1024, 6, 512>});
-    vs.push_back({"x_nb4", xv<0, 1024, 4, 512>});
-    vs.push_back({"x_nb5", xv<0, 1024, 5, 512>});
-    vs.push_back({"x_p256_nb8", xv<0, 1024, 8, 256>});
-    vs.push_back({"x_p256_nb12", xv<0, 1024, 12, 256>});
-    vs.push_back({"x_p256_nb6", xv<0, 1024, 6, 256>});
-    vs.push_back({"x_clamp", xv<1, 1024, 6, 512>});
-  } else {
-    vs.push_back({"x_clamp_nt512_nb3", xv<1, 512, 3, 1024, 64>});
-    vs.push_back({"x_clamp_nt1024_nb2", xv<1, 1024, 2, 512, 64>});
-    vs.push_back({"x_clamp_nt512_nb2", xv<1, 512, 2, 1024, 64>});
-    vs.push_back({"x_same", xv<0, 512, 3, 1024, 64>});
-    vs.push_back({"x_nt1024_nb3", xv<0, 1024, 3, 512, 64>});
-    vs.push_back({"x_nt1024_nb4", xv<0, 1024, 4, 512, 64>});
-    vs.push_back({"x_nt512_nb4", xv<0, 512, 4, 1024, 64>});
-    vs.push_back({"x_nt512_nb6_p512", xv<0, 512, 6, 512, 64>});
-    vs.push_back({"x_nt1024_nb6", xv<0, 1024, 6, 512, 64>});
-    vs.push_back({"x_nolds", xv<512, 512, 3, 1024, 64>});
-  }
-
+  // the column-slice kernel as production had it before the K-split kernel
+  if (!f32 && sw == 32) vs.push_back({"slice_old", xv<0, 1024, 6, 512, 32>});
+  if (!f32 && sw == 64) vs.push_back({"slice_old", xv<0, 1024, 3, 512, 64>});
+  if (!f32 && sw == 8) vs.push_back({"slice_old", xv<4, 1024, 6, 1024, 8>});
+  if (f32 && sw == 64) vs.push_back({"slice_old", xv<0, 1024, 2, 512, 64, float>});
   // reference: column sums over all chunks
   auto totals = [&](std::vector<long long>& t) {
     std::vector<long long> h((size_t)nc * K * D);

@@ -49,6 +49,23 @@ int main() {
           }
         }
       }
+      for (int es : {2, 4}) {   // K-split M-step plan
+        KsPlan kp{};
+        ++cases;
+        if (!choose_ks(es, K, D, &kp)) continue;
+        const int v = 16 / es;
+        if (kp.ks < 2 || kp.ks > 64 || (kp.ks & (kp.ks - 1))) return fail("ks pow2", K, D, kp.ks);
+        if ((long long)kp.kq * kp.ks < K || (long long)kp.kq * (kp.ks / 2) >= K) return fail("kq cover", K, kp.ks, kp.kq);
+        if (kp.lpr < 8 || kp.lpr > 64 || (kp.lpr & (kp.lpr - 1))) return fail("lpr", D, es, kp.lpr);
+        if (kp.lpr * v < D || (kp.lpr / 2) * v >= D) return fail("lpr cover", D, es, kp.lpr);
+        if (kp.ldc != kp.lpr * v / 2 + 1 || kp.ldc % 2 == 0) return fail("ks ldc", D, es, kp.ldc);
+        if (ks_lds_bytes(kp.kq, kp.ldc) > UPD_LDS_MAX) return fail("ks lds", K, D, kp.kq);
+        if (kp.gm != 3 && kp.gm != 6) return fail("ks gm", K, D, kp.gm);
+        for (int ncs : {8, 32, 64, 128}) {
+          const int nc = update_n_chunks_ks(kp.ks, ncs);
+          if (nc % 8 || nc < ncs || (long long)nc * kp.ks < 256) return fail("ks n_chunks", kp.ks, ncs, nc);
+        }
+      }
       for (int es : {2, 4}) {
         for (int dpad : {8, 16, 32, 64, 128, 256, 512}) {
           const int kp = assign_kpad(es, dpad, K);

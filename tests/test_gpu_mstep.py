@@ -127,3 +127,55 @@ def test_minibatch_rescales_instead_of_saturating(native, case):
         eg.partial_fit(xb.to(DEV))
     assert eg.rescales >= 1
     torch.testing.assert_close(eg.centers.cpu(), ec.centers, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("case", ["uniform", "one_label", "sorted", "unassigned"])
+@pytest.mark.parametrize("d,k", [(128, 1024), (64, 4096)])
+def test_cluster_sums_ksplit_matches_slice_kernel(native, case, d, k):
+    """The K-split M-step (plain full passes at shapes whose column slices are under 128 B,
+    csrc/update.hip update_ks_kernel) against the column-slice kernel, which unit weights
+    select: the same fixed-point contributions, so the sums must agree bit for bit --
+    through hot-label flushes (one label), whole-wave matches that overflow the in-flight
+    row groups (sorted labels) and rows without a label (-1)."""
+    C = native
+    assert C.update_slice_width(ops.dtype_code(torch.bfloat16), k, d, False) * 2 < 128
+    n = 300_000
+    g = torch.Generator().manual_seed(d + k)
+    X = (torch.randn(n, d, generator=g) * 3 + 1).to(torch.bfloat16)
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32)
+    if case == "one_label":
+        lab.fill_(k - 1)
+    elif case == "sorted":
+        lab = lab.sort().values
+    elif case == "unassigned":
+        lab[::3] = -1
+    Xd, ld = X.to(DEV), lab.to(DEV)
+    sums, counts = ops.cluster_sums(Xd, ld, k)
+    ws, _ = ops.cluster_sums(Xd, ld, k, torch.ones(n, device=DEV))
+    assert torch.equal(sums, ws)
+    valid = lab >= 0
+    assert torch.equal(counts.cpu().long(), torch.bincount(lab[valid].long(), minlength=k))
+    again, _ = ops.cluster_sums(Xd, ld, k)          # atomics in another order: same bits
+    assert torch.equal(again, sums)
+
+
+def test_ksplit_clamp_count(native):
+    """Clamped K-split pass (mini-batch streams): out-of-range rows are counted."""
+    C = native
+    n, d, K = 50_000, 128, 1024
+    X = torch.randn(n, d, device=DEV).to(torch.bfloat16)
+    lab = torch.randint(0, K, (n,), device=DEV, dtype=torch.int32)
+    dt = ops.dtype_code(torch.bfloat16)
+    assert C.update_slice_width(dt, K, d, False) * 2 < 128
+    nch = C.update_n_chunks(dt, K, d, n, False)
+    slab = torch.empty(nch * K * d, dtype=torch.int64, device=DEV)
+    cnt = torch.empty(nch * K, dtype=torch.int64, device=DEV)
+    col_exp, _ = ops.fixed_exps(X[:1], None, bound=torch.full((d,), 0.5, dtype=torch.float64))
+    cc = torch.zeros(1, dtype=torch.int32, device=DEV)
+    C.update(X, lab, K, slab, cnt, nch, None, col_exp, 0, True, clamp_count=cc)
+    assert int(cc.item()) > 0
+    cc.zero_()
+    col_exp, _ = ops.fixed_exps(X, None)
+    C.update(X, lab, K, slab, cnt, nch, None, col_exp, 0, True, clamp_count=cc)
+    assert int(cc.item()) == 0
+    assert int(cnt.view(nch, K).sum()) == n
