@@ -108,7 +108,13 @@ inline bool choose_ks(int esize, int K, int D, KsPlan* p) {
     if (ks_lds_bytes(kq, ldc) <= UPD_LDS_MAX) {
       if (ks < 2) return false;                      // one workgroup would scan every row alone
       p->ks = ks; p->kq = kq; p->lpr = lpr; p->ldc = ldc;
-      p->gm = (lpr / ks) >= 2 ? 6 : 3;
+      // row groups in flight: the owned rows of a wave's 64 (mean m = 64/ks) plus 2.5
+      // standard deviations, in groups of 64/lpr rows; too few sends rows to the
+      // synchronous overflow path, too many issues masked loads (headline 6, cfg4 2:
+      // profiles/r2_05_update_study.md)
+      const double m = 64.0 / ks;
+      const int g = (int)ceil((m + 2.5 * sqrt(m)) / (64.0 / lpr));
+      p->gm = g <= 2 ? 2 : g <= 3 ? 3 : 6;
       return true;
     }
     if (ks >= 64) return false;

@@ -804,7 +804,8 @@ static hipError_t launch_ks_t(const UpdateArgs& a, const plan::KsPlan& kp, hipSt
 template <typename T, int LPR>
 static hipError_t launch_ks_l(const UpdateArgs& a, const plan::KsPlan& kp, hipStream_t s) {
   if (kp.gm == 6) return a.clamp ? launch_ks_t<T, LPR, 6, true>(a, kp, s) : launch_ks_t<T, LPR, 6, false>(a, kp, s);
-  return a.clamp ? launch_ks_t<T, LPR, 3, true>(a, kp, s) : launch_ks_t<T, LPR, 3, false>(a, kp, s);
+  if (kp.gm == 3) return a.clamp ? launch_ks_t<T, LPR, 3, true>(a, kp, s) : launch_ks_t<T, LPR, 3, false>(a, kp, s);
+  return a.clamp ? launch_ks_t<T, LPR, 2, true>(a, kp, s) : launch_ks_t<T, LPR, 2, false>(a, kp, s);
 }
 
 template <typename T>

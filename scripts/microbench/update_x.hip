@@ -354,11 +354,6 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
     int cur = lab_[0];
     unsigned run = 0;
     auto emit = [&]() {
-      if constexpr ((MODE & 512) != 0) {
-#pragma unroll
-        for (int c = 0; c < V / 2; ++c) asm volatile("" :: "v"(acc[c]));
-        return;
-      }
       unsigned long long* dst = cells + cur * LDC;
       if constexpr (SWZ) {
         const int f = (cur >> KSH) & (NP - 1);
@@ -421,12 +416,10 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
       }
     }
     emit();
-    if constexpr (!(MODE & 256)) {
     if (seen >= THRESH) *L.flag(smem) = 1;
     // LDS-only barrier: the prefetched global loads stay in flight
     wait_lgkm0();
     raw_barrier();
-    }
   };
 
   // NB-deep ring of period buffers: NB-1 periods of loads in flight while one accumulates
@@ -447,8 +440,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
         const int ns = (s + NB - 1) % NB;  // static after unrolling
         if (nb < row1) load(nb, wb[ns], lb[ns], tb[ns]);
         accumulate(wb[s], lb[s], tb[s]);
-        if constexpr (!(MODE & 256))
-          if (*L.flag(smem)) mku::upd_flush_hot<SW>(a, L, smem, slice, chunk, THRESH / 2);  // batch near-hot labels too
+        if (*L.flag(smem)) mku::upd_flush_hot<SW>(a, L, smem, slice, chunk, THRESH / 2);  // batch near-hot labels too
       }
     }
   }
@@ -457,6 +449,191 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
     if (a.clamp_count) {
       const unsigned long long any = __ballot(!(rlo >= FX_MAGIC - FX_QMAX && rhi <= FX_MAGIC + FX_QMAX));
       if (any && (threadIdx.x & 63) == __builtin_ctzll(any)) atomicAdd(a.clamp_count, 1);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K-split M-step (plan::choose_ks): for plain full passes (unweighted, not incremental,
+// not the residual pass) whenever the column-slice kernel above would need more than one
+// slice.  KS workgroups share a row chunk; workgroup j owns labels [j*kq, j*kq + kn) in
+// every column.  Each period of KS_NT rows:
+//   1. every thread holds one row's label (loaded two periods ahead);
+//   2. each wave compacts its rows whose label it owns into a wave-private LDS list
+//      (ballot + mbcnt, no atomics);
+//   3. the wave reads those rows WHOLE, LPR lanes x 16 B per row (RG = 64/LPR rows per
+//      instruction: full 128-B lines, where the slice kernel reads 64-B pieces of 16 rows),
+//      GM row groups of the NEXT period in flight while this period's groups accumulate;
+//   4. the same fixed-point ds_add_u64 pairs as the slice kernel, so the sums are bitwise
+//      identical (integer adds in any order); the per-period barrier and hot-label flush
+//      bound every label's adds below FX_LIM.
+// The slab layout ([n_chunks][K][D] int64 + [n_chunks][K] counts) and the reduce are
+// shared with the slice kernel.
+template <typename T>
+__device__ void ks_flush(const UpdateArgs& a, char* m, int kq, int kn, int ldc, int npair, int k0,
+                         int chunk, unsigned thresh) {
+  unsigned long long* cells = (unsigned long long*)m;
+  unsigned* nadd = (unsigned*)(cells + (size_t)kq * ldc);
+  const int tot = kn * npair;
+  for (int e = threadIdx.x; e < tot; e += blockDim.x) {
+    const int kl = e / npair, p = e % npair;
+    const unsigned na = nadd[kl];
+    if ((na & NADD_MASK) < thresh) continue;
+    const int q = kl * ldc + p;
+    const unsigned long long T_ = cells[q] - (unsigned long long)(na & NADD_MASK) * FX_MM;
+    cells[q] = 0;
+    const int lo = (int)(uint32_t)T_;
+    const long long hi = (long long)(T_ - (unsigned long long)(long long)lo) >> 32;
+    if (2 * p < a.D) {
+      long long* dst = a.slab + (int64_t)chunk * a.K * a.D + (int64_t)(k0 + kl) * a.D + 2 * p;
+      if (na & NADD_WRITTEN) { dst[0] += lo; if (2 * p + 1 < a.D) dst[1] += hi; }
+      else { dst[0] = lo; if (2 * p + 1 < a.D) dst[1] = hi; }
+    }
+  }
+  __syncthreads();
+  for (int kl = threadIdx.x; kl < kn; kl += blockDim.x) {
+    const unsigned na = nadd[kl];
+    if ((na & NADD_MASK) < thresh) continue;
+    long long* cd = a.cnt_slab + (int64_t)chunk * a.K + k0 + kl;
+    if (na & NADD_WRITTEN) *cd += (long long)(na & NADD_MASK); else *cd = (long long)(na & NADD_MASK);
+    nadd[kl] = NADD_WRITTEN;
+  }
+  __syncthreads();
+}
+
+template <typename T, int LPR, int GM, bool CLAMP>
+__global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, int ks, int kq, int ldc,
+                                                                int64_t rows_per_chunk) {
+  constexpr int NT = plan::KS_NT;
+  constexpr int V = 16 / (int)sizeof(T);
+  constexpr int RG = 64 / LPR;                      // rows per wave-instruction
+  constexpr int NPL = V / 2;                        // cell pairs per lane
+  constexpr int NPAIR = LPR * NPL;
+  constexpr unsigned THRESH = FX_LIM - NT + 1;      // a period adds <= NT rows to a label
+  static_assert(LPR >= 1 && LPR <= 64 && (LPR & (LPR - 1)) == 0, "lanes per row");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  unsigned long long* cells = (unsigned long long*)smem;
+  unsigned* nadd = (unsigned*)(cells + (size_t)kq * ldc);
+  int* flag = (int*)(nadd + kq);
+  unsigned* lists = (unsigned*)(flag + 4);          // [2 periods][NT/64 waves][64]
+
+  const int b = blockIdx.x, jb = b >> 3;
+  const int ksi = jb % ks;
+  const int chunk = (jb / ks) * 8 + (b & 7);
+  const int k0 = ksi * kq;
+  const int kn = a.K - k0 < kq ? a.K - k0 : kq;    // labels this workgroup owns
+  if (kn <= 0 || chunk >= a.n_chunks) return;       // (uniform: before any barrier)
+  for (int e = threadIdx.x; e < kq * ldc; e += NT) cells[e] = 0;
+  for (int e = threadIdx.x; e < kq; e += NT) nadd[e] = 0;
+  if (threadIdx.x == 0) *flag = 0;
+  __syncthreads();
+
+  const int64_t row0 = (int64_t)chunk * rows_per_chunk;
+  int64_t row1 = row0 + rows_per_chunk;
+  if (row1 > a.N) row1 = a.N;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int rr = lane / LPR, cc = lane % LPR;
+  const int col = cc * V;
+  const bool colok = col < a.D;
+  float sc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) sc[e] = (col + e < a.D) ? ldexpf(1.f, a.col_exp[col + e]) : 0.f;
+  float rlo = FX_MAGIC, rhi = FX_MAGIC;
+  unsigned seen = 0;
+  const T* xcol = (const T*)a.X + (colok ? col : 0);
+  const int64_t rsafe = row0 < row1 ? row0 : 0;    // a valid row for masked lanes
+
+  auto label_at = [&](int64_t i) -> int { return i < row1 ? a.labels[i] : -1; };
+  // rows [base + wid*64, +64) of this wave: compact the owned ones into lst, return the count
+  auto compact = [&](int lab, unsigned* lst) -> int {
+    const unsigned rel = (unsigned)(lab - k0);
+    const bool m = rel < (unsigned)kn;
+    const unsigned long long bal = __ballot(m);
+    const int pos = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+    if (m) lst[pos] = (unsigned)lane | (rel << 6);
+    return (int)__popcll(bal);
+  };
+  // one row group per instruction: entries [g0 + j*RG, +RG) of lst; label -1 = no row
+  auto issue = [&](const unsigned* lst, int cnt, int64_t wbase, int g0, u32x4* xb, int* lb) {
+#pragma unroll
+    for (int j = 0; j < GM; ++j) {
+      const int e = g0 + j * RG + rr;
+      const bool v = e < cnt;
+      const unsigned ent = lst[v ? e : 0];
+      const int64_t row = v ? wbase + (int64_t)(ent & 63u) : rsafe;
+      xb[j] = *(const u32x4*)(xcol + row * a.ldx);
+      lb[j] = v ? (int)(ent >> 6) : -1;
+    }
+  };
+  auto accumulate = [&](const u32x4& w, int kl) {
+    float f[V];
+    unpack16(colok ? w : u32x4{0u, 0u, 0u, 0u}, f, (T*)nullptr);
+    unsigned long long* dst = cells + kl * ldc + cc * NPL;
+#pragma unroll
+    for (int e = 0; e < V; e += 2) {
+      const float r0 = fx_raw<CLAMP>(f[e], sc[e]), r1 = fx_raw<CLAMP>(f[e + 1], sc[e + 1]);
+      if constexpr (CLAMP) {
+        rlo = fminf(fminf(rlo, r0), r1);
+        rhi = fmaxf(fmaxf(rhi, r0), r1);
+      }
+      const unsigned long long v = (unsigned long long)fx_clamp<CLAMP>(r0) |
+                                   ((unsigned long long)fx_clamp<CLAMP>(r1) << 32);
+      __hip_atomic_fetch_add(dst + e / 2, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (cc == 0) {
+      const unsigned old = __hip_atomic_fetch_add(nadd + kl, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP) & NADD_MASK;
+      seen = old + 1 > seen ? old + 1 : seen;
+    }
+  };
+
+  unsigned* lbuf0 = lists + wid * 64;
+  unsigned* lbuf1 = lists + (NT / 64) * 64 + wid * 64;
+  // prologue: period 0 compacted and its first groups in flight, period 1's labels loaded
+  int lab_next = label_at(row0 + NT + threadIdx.x);
+  int cnt = compact(label_at(row0 + threadIdx.x), lbuf0);
+  u32x4 xa[GM];
+  int la[GM];
+  issue(lbuf0, cnt, row0 + wid * 64, 0, xa, la);
+  for (int64_t base = row0; base < row1; base += NT) {
+    const int lab_nn = label_at(base + 2 * NT + threadIdx.x);
+    const int cnt_n = compact(lab_next, lbuf1);
+    u32x4 xb[GM];
+    int lb[GM];
+    issue(lbuf1, cnt_n, base + NT + wid * 64, 0, xb, lb);
+#pragma unroll
+    for (int j = 0; j < GM; ++j)
+      if (la[j] >= 0) accumulate(xa[j], la[j]);
+    // rare: more owned rows than GM groups hold -- the rest synchronously
+    for (int g0 = GM * RG; g0 < cnt; g0 += RG) {
+      const int e = g0 + rr;
+      if (e < cnt) {
+        const unsigned ent = lbuf0[e];
+        const u32x4 w = *(const u32x4*)(xcol + (base + wid * 64 + (int64_t)(ent & 63u)) * a.ldx);
+        accumulate(w, (int)(ent >> 6));
+      }
+    }
+    if (seen >= THRESH) *flag = 1;
+    __syncthreads();
+    if (*flag) {
+      mku::ks_flush<T>(a, smem, kq, kn, ldc, NPAIR, k0, chunk, THRESH / 2);
+      if (threadIdx.x == 0) *flag = 0;
+      seen = 0;
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < GM; ++j) { xa[j] = xb[j]; la[j] = lb[j]; }
+    cnt = cnt_n;
+    lab_next = lab_nn;
+    unsigned* t = lbuf0; lbuf0 = lbuf1; lbuf1 = t;
+  }
+  __syncthreads();
+  mku::ks_flush<T>(a, smem, kq, kn, ldc, NPAIR, k0, chunk, 0u);
+  if constexpr (CLAMP) {
+    if (a.clamp_count) {
+      const unsigned long long any = __ballot(!(rlo >= FX_MAGIC - FX_QMAX && rhi <= FX_MAGIC + FX_QMAX));
+      if (any && lane == __builtin_ctzll(any)) atomicAdd(a.clamp_count, 1);
     }
   }
 }
@@ -498,8 +675,23 @@ int update_slice_width(int dtype, int K, int D, bool weighted) {
   return choose_sw(dtype, K, D, weighted, &ldc);
 }
 
+static int esize(int dtype);
+
+// The K-split kernel serves plain full passes where the slice kernel needs 2+ slices of
+// under 128 B per row: N=1e8 D=128 K=1024 bf16 (64-B pieces) 5.20 -> 4.67 ms, N=1e7 D=64
+// K=4096 (16-B pieces) 0.62 -> 0.44 ms; with 128-B or wider pieces (cfg5's 64 bf16
+// columns, cfg2's 64 f32 columns) the slice kernel already reads whole lines and is as fast
+// or faster (profiles/r2_05_update_study.md).
+static bool use_ks(int dtype, int K, int D, bool weighted, plan::KsPlan* kp) {
+  if (weighted) return false;
+  const int sw = update_slice_width(dtype, K, D, false);
+  return sw > 0 && sw < D && sw * esize(dtype) < 128 && plan::choose_ks(esize(dtype), K, D, kp);
+}
+
 int update_n_chunks(int dtype, int K, int D, int64_t N, bool weighted) {
-  return plan::update_n_chunks(update_slice_width(dtype, K, D, weighted), D, N);
+  const int nc = plan::update_n_chunks(update_slice_width(dtype, K, D, weighted), D, N);
+  plan::KsPlan kp;
+  return use_ks(dtype, K, D, weighted, &kp) ? plan::update_n_chunks_ks(kp.ks, nc) : nc;
 }
 
 int fixed_exp(double maxabs) { return plan::fixed_exp(maxabs); }
@@ -522,21 +714,34 @@ hipError_t launch_nt(const UpdateArgs& a, int ldc, hipStream_t s) {
 
 // 1024 threads (4 waves per SIMD, <= 128 VGPRs) where the period buffers fit without
 // spilling; measured at N=1e8 D=128 K=1024 bf16: 5.67 ms vs 5.89 (512) vs 6.74 (256).
+// 64-column slices (K <= ~600) take a 3-deep ring to stay under 128 VGPRs: 1.64 ms vs
+// 1.95 at 512 threads for the cfg5 batch (N=16.8M D=256 K=512; profiles/r2_05_update_study.md).
+// The clamped 64-column body (mini-batch without a value bound) takes a 2-deep ring:
+// 1.79 ms vs 2.02 at 512 threads; a 3-deep one would spill 32 VGPRs.
+// f32, 64-column slices, plain adds: 1024 threads with a 2-deep ring, 1.80 vs 2.02 ms at
+// N=2e7 D=128 K=256 (0.121 vs 0.126 at cfg2's N=1e6; profiles/r2_05_update_study.md).
 template <typename T, int SW, int MODE>
 constexpr int upd_default_nt() {
-  return (sizeof(T) == 2 && SW <= 32 && !(MODE & (UPD_WEIGHTED | UPD_DELTA))) ? 1024 : UPD_NT;
+  if constexpr (sizeof(T) == 4)
+    return (SW == 64 && !(MODE & (UPD_WEIGHTED | UPD_DELTA | UPD_CLAMP | UPD_RESID))) ? 1024 : UPD_NT;
+  return (SW <= 64 && !(MODE & (UPD_WEIGHTED | UPD_DELTA))) ? 1024 : UPD_NT;
+}
+template <typename T, int SW, int MODE>
+constexpr int upd_ring_1024() {
+  return sizeof(T) == 4 ? 2 : SW <= 32 ? 6 : (MODE & UPD_CLAMP) ? 2 : 3;
 }
 
 template <typename T, int SW, int MODE>
 static hipError_t launch_sw(const UpdateArgs& a, int ldc, hipStream_t s) {
   constexpr int NT = upd_default_nt<T, SW, MODE>();
-  // 1024 threads: 512-row periods, 6-deep ring (5 periods of loads in flight).  N=1e8
-  // D=128 K=1024 bf16: 5.33-5.76 ms vs 5.96-6.34 for 3 x 1024-row periods (same boxes).
+  // 1024 threads: 512-row periods, 6-deep ring (5 periods of loads in flight; 3-deep for
+  // 64-column slices).  N=1e8 D=128 K=1024 bf16: 5.33-5.76 ms vs 5.96-6.34 for 3 x
+  // 1024-row periods (same boxes).
   constexpr int ES = sizeof(T);
   constexpr int V = ((SW * ES >= 16) ? 16 : SW * ES) / ES;
   constexpr int RPP = NT / (SW / V);
   constexpr int PER = RPP > 512 ? RPP : 512;
-  if constexpr (NT == 1024) return mku::launch_nt<T, SW, MODE, 1024, 6, PER>(a, ldc, s);
+  if constexpr (NT == 1024) return mku::launch_nt<T, SW, MODE, 1024, upd_ring_1024<T, SW, MODE>(), PER>(a, ldc, s);
   else return mku::launch_nt<T, SW, MODE, NT>(a, ldc, s);
 }
 
@@ -588,8 +793,45 @@ static hipError_t launch_update_t(const UpdateArgs& a, hipStream_t s, int sw, in
   return hipErrorInvalidValue;
 }
 
+template <typename T, int LPR, int GM, bool CLAMP>
+hipError_t launch_ks_t(const UpdateArgs& a, const plan::KsPlan& kp, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)update_ks_kernel<T, LPR, GM, CLAMP>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)UPD_LDS_MAX);
+    attr = true;
+  }
+  const int64_t rows_per_chunk = (a.N + a.n_chunks - 1) / a.n_chunks;
+  hipLaunchKernelGGL((update_ks_kernel<T, LPR, GM, CLAMP>), dim3((unsigned)(a.n_chunks * kp.ks)),
+                     dim3(plan::KS_NT), plan::ks_lds_bytes(kp.kq, kp.ldc), s, a, kp.ks, kp.kq, kp.ldc,
+                     rows_per_chunk);
+  return hipGetLastError();
+}
+
+template <typename T, int LPR>
+static hipError_t launch_ks_l(const UpdateArgs& a, const plan::KsPlan& kp, hipStream_t s) {
+  if (kp.gm == 6) return a.clamp ? mku::launch_ks_t<T, LPR, 6, true>(a, kp, s) : mku::launch_ks_t<T, LPR, 6, false>(a, kp, s);
+  return a.clamp ? mku::launch_ks_t<T, LPR, 3, true>(a, kp, s) : mku::launch_ks_t<T, LPR, 3, false>(a, kp, s);
+}
+
+template <typename T>
+static hipError_t launch_ks(const UpdateArgs& a, const plan::KsPlan& kp, hipStream_t s) {
+  switch (kp.lpr) {
+    case 8: return mku::launch_ks_l<T, 8>(a, kp, s);
+    case 16: return mku::launch_ks_l<T, 16>(a, kp, s);
+    case 32: return mku::launch_ks_l<T, 32>(a, kp, s);
+    case 64: return mku::launch_ks_l<T, 64>(a, kp, s);
+  }
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s) {
   if (a.N <= 0) return hipSuccess;
+  plan::KsPlan kp;
+  if (!a.dlist && !a.col_exp2 && use_ks(dtype, a.K, a.D, a.weights != nullptr, &kp)) {
+    if (a.n_chunks % 8) return hipErrorInvalidValue;
+    return dtype == DT_BF16 ? mku::launch_ks<uint16_t>(a, kp, s) : mku::launch_ks<float>(a, kp, s);
+  }
   int ldc = 0;
   const int sw = choose_sw(dtype, a.K, a.D, a.weights != nullptr || a.dlist != nullptr, &ldc);
   if (sw > 0 && a.n_chunks % 8) return hipErrorInvalidValue;

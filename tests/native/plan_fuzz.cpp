@@ -60,7 +60,7 @@ int main() {
         if (kp.lpr * v < D || (kp.lpr / 2) * v >= D) return fail("lpr cover", D, es, kp.lpr);
         if (kp.ldc != kp.lpr * v / 2 + 1 || kp.ldc % 2 == 0) return fail("ks ldc", D, es, kp.ldc);
         if (ks_lds_bytes(kp.kq, kp.ldc) > UPD_LDS_MAX) return fail("ks lds", K, D, kp.kq);
-        if (kp.gm != 3 && kp.gm != 6) return fail("ks gm", K, D, kp.gm);
+        if (kp.gm != 2 && kp.gm != 3 && kp.gm != 6) return fail("ks gm", K, D, kp.gm);
         for (int ncs : {8, 32, 64, 128}) {
           const int nc = update_n_chunks_ks(kp.ks, ncs);
           if (nc % 8 || nc < ncs || (long long)nc * kp.ks < 256) return fail("ks n_chunks", kp.ks, ncs, nc);
