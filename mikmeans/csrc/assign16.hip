@@ -4,9 +4,13 @@
 // Pipeline: fragment-packed centroid chunks stream through an LDS ring fed by LDS-DMA
 // (global_load_lds_dwordx4, no VGPR round trip); every wave keeps P blocks of 16
 // points in registers and multiplies them against each 16-centroid tile:
-//  * lane (r = l&15, g = l>>4) holds the B fragment of point p0+r, feature quarter g:
-//    x[p0+r][g*DPAD/4 .. +DPAD/4) (contiguous), and the A fragment of centroid r of the
-//    tile (the packed -2c), same quarter;
+//  * lane (r = l&15, g = l>>4) holds the B fragments of point p0+r, piece q covering
+//    features [(4q+g)V, +V) (V = 16 B of elements), and the A fragments of centroid r
+//    of the tile (the packed -2c), same features.  Interleaving the lane groups' pieces
+//    makes each fragment load read 64 contiguous bytes per point (16 rows per wave
+//    instruction); giving each lane group a contiguous quarter of the row instead made
+//    every load touch 64 cache lines, and the loads cost a fixed ~27 % of the D=256
+//    K=512 assign (profiles/r2_08_assign_clock_study.md);
 //  * the accumulators are seeded with |c|^2 (+ the point offset below), so the output
 //    D[row = 4g+reg][col = r] is the score of point r against centroid 16t+4g+reg and
 //    each lane holds 4 scores of its point per tile; the 4 lane groups g merge once at
@@ -30,8 +34,8 @@
 //    the lowest index on exact ties.
 //
 // Layout "16" of the packed centroids (csrc/kernels.h):
-//   element (k, d): t = k/16, r = k%16, g = d / (DPAD/4), e = d % (DPAD/4)
-//   offset = ((t*NQ + e/V)*64 + r + 16*g)*V + e%V,  NQ = DPAD/(4V)
+//   element (k, d): t = k/16, r = k%16, q = d / (4V), g = (d / V) % 4
+//   offset = ((t*NQ + q)*64 + r + 16*g)*V + d%V,  NQ = DPAD/(4V)
 #include "common.h"
 #include "kernels.h"
 #include "plan.h"
@@ -143,11 +147,11 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     int64_t row = pbase + p * 16 + r;
     row = row < a.N ? row : (a.N - 1);
     xnr[p] = (!EXACT && a.xn) ? a.xn[row] : 0.f;
-    const T* rp = (const T*)a.X + row * a.ldx + g * (DPAD / 4);
+    const T* rp = (const T*)a.X + row * a.ldx + g * C::V;
 #pragma unroll
     for (int q = 0; q < C::NQ; ++q) {
-      const int col = g * (DPAD / 4) + q * C::V;
-      if (FULLD || col < a.D) xr[p][q] = *(const u32x4*)(rp + q * C::V);
+      const int col = (4 * q + g) * C::V;
+      if (FULLD || col < a.D) xr[p][q] = *(const u32x4*)(rp + 4 * q * C::V);
       else xr[p][q] = u32x4{0u, 0u, 0u, 0u};
     }
   }

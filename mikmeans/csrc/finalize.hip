@@ -12,14 +12,15 @@
 
 namespace mk {
 
-// Packed layout (kernels.h): 16-centroid tiles, lane r+16g holds feature quarter g.
+// Packed layout (kernels.h): 16-centroid tiles; piece q of lane r+16g holds features
+// [(4q+g)V, (4q+g+1)V).
 template <typename T>
 __device__ __forceinline__ void store_pack(void* pack, int dpad, int k, int d, float v) {
   constexpr int V = Elem<T>::V;
   const int nq = dpad / (4 * V);
   const int t = k >> 4, r = k & 15;
-  const int g = d / (dpad / 4), e = d % (dpad / 4);
-  const int64_t off = ((int64_t)(t * nq + e / V) * 64 + r + 16 * g) * V + e % V;
+  const int g = (d / V) & 3, q = d / (4 * V);
+  const int64_t off = ((int64_t)(t * nq + q) * 64 + r + 16 * g) * V + d % V;
   ((T*)pack)[off] = Elem<T>::from_f32(v);
 }
 

@@ -21,8 +21,10 @@ constexpr int SLOT_STRIDE = 8;
 // centroids) and 16-byte piece q, the 64 lanes' MFMA A-operand fragments are stored
 // contiguously (1 KiB), so one LDS-DMA wave-instruction stages a piece and one
 // ds_read_b128 per lane fetches it conflict-free.
-//   element (k, d): t = k/16, r = k%16, g = d / (DPAD/4), e = d % (DPAD/4)
-//   offset = ((t*NQ + e/V)*64 + r + 16*g)*V + e%V,  V = 16/sizeof(T), NQ = DPAD/(4V)
+//   element (k, d): t = k/16, r = k%16, q = d / (4V), g = (d / V) % 4
+//   offset = ((t*NQ + q)*64 + r + 16*g)*V + d%V,  V = 16/sizeof(T), NQ = DPAD/(4V)
+// (piece q of lane group g holds features [(4q+g)V, +V): the four lane groups of a
+// point read 64 contiguous bytes of its row per fragment load, see assign16.hip)
 // The stored value is -2*c (exact in bf16/f32) and cn[k] = |c_q|^2 of the quantised
 // centroid, so the MFMA chain seeded with cn directly yields
 // score = |c|^2 - 2 x.c  (= |x-c|^2 - |x|^2).

@@ -57,23 +57,33 @@ static uint16_t f2bf(float f) {
 typedef hipError_t (*LaunchFn)(const mk::AssignArgs&, hipStream_t);
 struct Variant { const char* name; LaunchFn fn; };
 
-static hipError_t v_prod128(const mk::AssignArgs& a, hipStream_t s) { return mk::launch_assign16(mk::DT_BF16, 128, a, s); }
+static void* g_pack2 = nullptr;  // centres in the production layout (old copies read the old one)
+static hipError_t v_prod128(const mk::AssignArgs& a, hipStream_t s) {
+  mk::AssignArgs b = a; b.Cpack = g_pack2;
+  return mk::launch_assign16(mk::DT_BF16, 128, b, s);
+}
 static double* g_slots = nullptr;
 // the Lloyd engine's call: previous labels read (changed count), inertia/changed slots
 static hipError_t v_prod128_lloyd(const mk::AssignArgs& a, hipStream_t s) {
-  mk::AssignArgs b = a; b.track_changed = 1; b.slots = g_slots;
+  mk::AssignArgs b = a; b.Cpack = g_pack2; b.track_changed = 1; b.slots = g_slots;
   return mk::launch_assign16(mk::DT_BF16, 128, b, s);
 }
 static hipError_t v_prod128_lloyd_nomind(const mk::AssignArgs& a, hipStream_t s) {
-  mk::AssignArgs b = a; b.track_changed = 1; b.slots = g_slots; b.mind = nullptr;
+  mk::AssignArgs b = a; b.Cpack = g_pack2; b.track_changed = 1; b.slots = g_slots; b.mind = nullptr;
   return mk::launch_assign16(mk::DT_BF16, 128, b, s);
 }
 static hipError_t v_prod128_nomind(const mk::AssignArgs& a, hipStream_t s) {
-  mk::AssignArgs b = a; b.mind = nullptr;
+  mk::AssignArgs b = a; b.Cpack = g_pack2; b.mind = nullptr;
   return mk::launch_assign16(mk::DT_BF16, 128, b, s);
 }
-static hipError_t v_prod64(const mk::AssignArgs& a, hipStream_t s) { return mk::launch_assign16(mk::DT_BF16, 64, a, s); }
-static hipError_t v_prod256(const mk::AssignArgs& a, hipStream_t s) { return mk::launch_assign16(mk::DT_BF16, 256, a, s); }
+static hipError_t v_prod64(const mk::AssignArgs& a, hipStream_t s) {
+  mk::AssignArgs b = a; b.Cpack = g_pack2;
+  return mk::launch_assign16(mk::DT_BF16, 64, b, s);
+}
+static hipError_t v_prod256(const mk::AssignArgs& a, hipStream_t s) {
+  mk::AssignArgs b = a; b.Cpack = g_pack2;
+  return mk::launch_assign16(mk::DT_BF16, 256, b, s);
+}
 
 int main(int argc, char** argv) {
   const int64_t N = argc > 1 ? atoll(argv[1]) : 20000000;
@@ -120,7 +130,7 @@ int main(int argc, char** argv) {
   }
   // layout 16: offset = ((t*NQ + e/V)*64 + r + 16*g)*V + e%V, value -2c; cn = |c|^2 (f32)
   const int V = 8, NQ = D / 4 / V;
-  std::vector<uint16_t> hp((size_t)Kpad * D, 0);
+  std::vector<uint16_t> hp((size_t)Kpad * D, 0), hp2((size_t)Kpad * D, 0);
   std::vector<float> hcn(cnl, mk::PAD_SCORE);
   for (int k = 0; k < K; ++k) {
     double s = 0;
@@ -130,10 +140,15 @@ int main(int argc, char** argv) {
       const int t = k / 16, r = k % 16, g = d / (D / 4), e = d % (D / 4);
       const size_t off = ((size_t)(t * NQ + e / V) * 64 + r + 16 * g) * V + e % V;
       hp[off] = f2bf(-2.f * c);
+      // production layout: piece q of lane group g holds features [(4q+g)V, +V)
+      const int q2 = d / (4 * V), g2 = (d / V) & 3;
+      hp2[((size_t)(t * NQ + q2) * 64 + r + 16 * g2) * V + d % V] = f2bf(-2.f * c);
     }
     hcn[k] = (float)s;
   }
   CK(hipMemcpy(pack, hp.data(), hp.size() * 2, hipMemcpyHostToDevice));
+  CK(hipMalloc(&g_pack2, (size_t)Kpad * D * 2));
+  CK(hipMemcpy(g_pack2, hp2.data(), hp2.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(cn, hcn.data(), cnl * 4, hipMemcpyHostToDevice));
 
   mk::AssignArgs a{};
