@@ -98,6 +98,75 @@ __global__ __launch_bounds__(256) void blobs_x(uint16_t* X, int64_t i0, int64_t 
   for (int o = 1; o < TPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
   if (row_ok && t == 0) xn[il] = sq;
 }
+
+// XO: one Philox4x32-10 call per (row, lane chunk) seeds a xoshiro128++ state that
+// yields the chunk's words (4 per 8-value group); chunk c holds groups c, c+8, ...
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+__device__ __forceinline__ uint32_t xo_next(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
+  const uint32_t r = rotl32(s0 + s3, 7) + s0;
+  const uint32_t t = s1 << 9;
+  s2 ^= s0;
+  s3 ^= s1;
+  s1 ^= s2;
+  s0 ^= s3;
+  s2 ^= t;
+  s3 = rotl32(s3, 11);
+  return r;
+}
+template <int TPR>
+__global__ __launch_bounds__(256) void blobs_xo(uint16_t* X, int64_t i0, int64_t n, int D,
+                                                const float* __restrict__ centers, int n_centers,
+                                                float stddev, uint32_t k0, uint32_t k1, float* xn) {
+  constexpr int EL = 8;
+  const int G = D / EL;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t il = e / TPR;
+  const int t = (int)(e % TPR);
+  const bool row_ok = il < n;
+  const uint64_t gi = (uint64_t)(i0 + (row_ok ? il : 0));
+  int cid = 0;
+  if (t == 0) {
+    const U4 rc = philox_r<10>(U4{(uint32_t)gi, (uint32_t)(gi >> 32), mk::TAG_CID, 0u}, k0, k1);
+    cid = (int)__umulhi(rc.x, (uint32_t)n_centers);
+  }
+  cid = __shfl(cid, (int)(threadIdx.x & 63) & ~(TPR - 1), 64);
+  float sq = 0.f;
+  if (row_ok) {
+    const float* mu = centers + (int64_t)cid * D;
+    uint16_t* out = X + il * D;
+    const U4 sd = philox_r<10>(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)t, 0x584Fu}, k0, k1);
+    uint32_t s0 = sd.x, s1 = sd.y, s2 = sd.z, s3 = sd.w;
+    for (int g = t; g < G; g += TPR) {
+      f32x4 m[2];
+      m[0] = *(const f32x4*)(mu + EL * g);
+      m[1] = *(const f32x4*)(mu + EL * g + 4);
+      U4 r;
+      r.x = xo_next(s0, s1, s2, s3);
+      r.y = xo_next(s0, s1, s2, s3);
+      r.z = xo_next(s0, s1, s2, s3);
+      r.w = xo_next(s0, s1, s2, s3);
+      float z[EL], f[EL];
+      mk::box_muller<uint16_t>(r, z);
+#pragma unroll
+      for (int j = 0; j < EL; ++j) f[j] = __builtin_fmaf(stddev, z[j], m[j / 4][j % 4]);
+      uint32_t h[EL];
+#pragma unroll
+      for (int j = 0; j < EL; ++j) {
+        const uint32_t u = __float_as_uint(f[j]);
+        h[j] = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+        const float q = __uint_as_float(h[j] << 16);
+        sq = __builtin_fmaf(q, q, sq);
+      }
+      u32x4 wv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wv[j] = h[2 * j] | (h[2 * j + 1] << 16);
+      *(u32x4*)(out + EL * g) = wv;
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < TPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
+  if (row_ok && t == 0) xn[il] = sq;
+}
 }  // namespace bx
 
 struct Var { const char* name; int kind; };
@@ -123,10 +192,13 @@ int main(int argc, char** argv) {
       case 3: hipLaunchKernelGGL((bx::blobs_x<8, 10, 0>), dim3(nb), dim3(256), 0, 0, X, 0, N, D, C, NC, 1.f, k0, k1, xn); break;
       case 4: hipLaunchKernelGGL((bx::blobs_x<8, 0, 1>), dim3(nb), dim3(256), 0, 0, X, 0, N, D, C, NC, 1.f, k0, k1, xn); break;
       case 5: hipLaunchKernelGGL((bx::blobs_x<8, 0, 0>), dim3(nb), dim3(256), 0, 0, X, 0, N, D, C, NC, 1.f, k0, k1, xn); break;
+      case 6: hipLaunchKernelGGL((bx::blobs_xo<8>), dim3(nb), dim3(256), 0, 0, X, 0, N, D, C, NC, 1.f, k0, k1, xn); break;
+      case 7: hipLaunchKernelGGL((bx::blobs_xo<4>), dim3((unsigned)((N * 4 + 255) / 256)), dim3(256), 0, 0, X, 0, N, D, C, NC, 1.f, k0, k1, xn); break;
+      case 8: hipLaunchKernelGGL((bx::blobs_xo<2>), dim3((unsigned)((N * 2 + 255) / 256)), dim3(256), 0, 0, X, 0, N, D, C, NC, 1.f, k0, k1, xn); break;
     }
     return hipGetLastError();
   };
-  std::vector<Var> vs = {{"prod", 0}, {"copy_r10", 1}, {"r7", 2}, {"r10_noBM", 3}, {"r0_BM", 4}, {"r0_noBM(store)", 5}};
+  std::vector<Var> vs = {{"prod", 0}, {"copy_r10", 1}, {"r7", 2}, {"r10_noBM", 3}, {"r0_BM", 4}, {"r0_noBM(store)", 5}, {"xo_tpr8", 6}, {"xo_tpr4", 7}, {"xo_tpr2", 8}};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
