@@ -102,9 +102,14 @@ __device__ __forceinline__ long long fx_q(float v, float sc) {
 // (weighted fits only).  With an odd stride (LDc = SW/2 + 1) rows start on scattered
 // banks; where only LDc = SW/2 fits, the pair index is XOR-swizzled by label bits
 // instead (swz), which scatters the banks of one instruction the same way.
+// Within a label, lane lp's c-th pair (columns lp*V + 2c, +1) sits at index c*LPR + lp, so
+// the lanes of one row hit consecutive cells in each ds_add_u64 (ds_write_b64 banking: 16
+// contiguous lanes per LDS cycle, bank (a/4) mod 32); per-lane pairs (index lp*V/2 + c)
+// put a row's lanes 8 or 16 dwords apart, 2-way conflicts inside every row.
 struct UpdLayout {
   int K, LDc, np, ksh;
   bool swz;
+  int lpr, npl;  // lanes per row, pairs per lane (lpr * npl == np)
   __device__ unsigned long long* cells(char* m) const { return (unsigned long long*)m; }
   __device__ unsigned* nadd(char* m) const { return (unsigned*)(cells(m) + (size_t)(K + 1) * LDc); }
   __device__ int* flag(char* m) const { return (int*)(nadd(m) + K + 1); }
@@ -116,8 +121,13 @@ struct UpdLayout {
   __device__ unsigned short* hot(char* m, bool weighted) const {
     return (unsigned short*)(wcnt(m) + (weighted ? K + 1 : 0));
   }
-  // cell position of pair p of label k
-  __device__ int pos(int k, int p) const { return swz ? (p ^ ((k >> ksh) & (np - 1))) : p; }
+  // cell index of lane lp's pair c of label k
+  __device__ int at(int k, int lp, int c) const {
+    const int i = c * lpr + lp;
+    return swz ? (i ^ ((k >> ksh) & (np - 1))) : i;
+  }
+  // cell index of column pair p of label k
+  __device__ int pos(int k, int p) const { return at(k, p / npl, p % npl); }
 };
 
 // nadd[k]: adds since label k's last flush in bits 0..30; bit 31 = "k's slab row
@@ -235,7 +245,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   static_assert(V % 2 == 0 && UNR >= 1 && FX_LIM >= PERIOD, "update tiling");
   typedef typename LoadT<PB>::type LT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const UpdLayout L{a.K, LDC, NP, KSH, SWZ};
+  const UpdLayout L{a.K, LDC, NP, KSH, SWZ, LPR, V / 2};
   unsigned long long* cells = L.cells(smem);
   long long* wcnt = L.wcnt(smem);
   unsigned* nadd = L.nadd(smem);
@@ -348,18 +358,10 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
     unsigned run = 0;
     auto emit = [&]() {
       unsigned long long* dst = cells + cur * LDC;
-      if constexpr (SWZ) {
-        const int f = (cur >> KSH) & (NP - 1);
 #pragma unroll
-        for (int c = 0; c < V / 2; ++c)
-          __hip_atomic_fetch_add(dst + ((lp * (V / 2) + c) ^ f), acc[c], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-#pragma unroll
-        for (int c = 0; c < V / 2; ++c)
-          __hip_atomic_fetch_add(dst + lp * (V / 2) + c, acc[c], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
+      for (int c = 0; c < V / 2; ++c)
+        __hip_atomic_fetch_add(dst + L.at(cur, lp, c), acc[c], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
       if (counter) {
         const unsigned old = __hip_atomic_fetch_add(nadd + cur, run, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_WORKGROUP) & NADD_MASK;
@@ -462,17 +464,19 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
 //      bound every label's adds below FX_LIM.
 // The slab layout ([n_chunks][K][D] int64 + [n_chunks][K] counts) and the reduce are
 // shared with the slice kernel.
-template <typename T>
+// Cell q of a label holds column pair p = (q % LPR) * NPL + q / LPR (see update_ks_kernel).
+template <typename T, int LPR>
 __device__ void ks_flush(const UpdateArgs& a, char* m, int kq, int kn, int ldc, int npair, int k0,
                          int chunk, unsigned thresh) {
+  constexpr int NPL = 8 / (int)sizeof(T);           // cell pairs per lane
   unsigned long long* cells = (unsigned long long*)m;
   unsigned* nadd = (unsigned*)(cells + (size_t)kq * ldc);
   const int tot = kn * npair;
   for (int e = threadIdx.x; e < tot; e += blockDim.x) {
-    const int kl = e / npair, p = e % npair;
+    const int kl = e / npair, p = e % npair;        // p-major: the slab writes coalesce
     const unsigned na = nadd[kl];
     if ((na & NADD_MASK) < thresh) continue;
-    const int q = kl * ldc + p;
+    const int q = kl * ldc + (p % NPL) * LPR + p / NPL;
     const unsigned long long T_ = cells[q] - (unsigned long long)(na & NADD_MASK) * FX_MM;
     cells[q] = 0;
     const int lo = (int)(uint32_t)T_;
@@ -562,7 +566,12 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
   auto accumulate = [&](const u32x4& w, int kl) {
     float f[V];
     unpack16(colok ? w : u32x4{0u, 0u, 0u, 0u}, f, (T*)nullptr);
-    unsigned long long* dst = cells + kl * ldc + cc * NPL;
+    // lane cc's pair j sits in cell j*LPR + cc: the 16 lanes of one ds_add_u64 lane group
+    // (ds_write_b64 banking: 16 contiguous lanes, bank (a/4) mod 32) cover 32 consecutive
+    // dwords of one label, so every bank once.  Pairs stored per lane (cell cc*NPL + j) put
+    // lanes 32 B apart: 4-way conflicts, ~12 extra LDS cycles per instruction at the
+    // headline (profiles/r2_21_pmc_headline.md).
+    unsigned long long* dst = cells + kl * ldc + cc;
 #pragma unroll
     for (int e = 0; e < V; e += 2) {
       const float r0 = fx_raw<CLAMP>(f[e], sc[e]), r1 = fx_raw<CLAMP>(f[e + 1], sc[e + 1]);
@@ -572,7 +581,7 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
       }
       const unsigned long long v = (unsigned long long)fx_clamp<CLAMP>(r0) |
                                    ((unsigned long long)fx_clamp<CLAMP>(r1) << 32);
-      __hip_atomic_fetch_add(dst + e / 2, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(dst + (e / 2) * LPR, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (cc == 0) {
       const unsigned old = __hip_atomic_fetch_add(nadd + kl, 1u, __ATOMIC_RELAXED,
@@ -610,7 +619,7 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
     if (seen >= THRESH) *flag = 1;
     __syncthreads();
     if (*flag) {
-      ks_flush<T>(a, smem, kq, kn, ldc, NPAIR, k0, chunk, THRESH / 2);
+      ks_flush<T, LPR>(a, smem, kq, kn, ldc, NPAIR, k0, chunk, THRESH / 2);
       if (threadIdx.x == 0) *flag = 0;
       seen = 0;
       __syncthreads();
@@ -622,7 +631,7 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
     unsigned* t = lbuf0; lbuf0 = lbuf1; lbuf1 = t;
   }
   __syncthreads();
-  ks_flush<T>(a, smem, kq, kn, ldc, NPAIR, k0, chunk, 0u);
+  ks_flush<T, LPR>(a, smem, kq, kn, ldc, NPAIR, k0, chunk, 0u);
   if constexpr (CLAMP) {
     if (a.clamp_count) {
       const unsigned long long any = __ballot(!(rlo >= FX_MAGIC - FX_QMAX && rhi <= FX_MAGIC + FX_QMAX));
