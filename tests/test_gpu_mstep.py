@@ -179,3 +179,29 @@ def test_ksplit_clamp_count(native):
     C.update(X, lab, K, slab, cnt, nch, None, col_exp, 0, True, clamp_count=cc)
     assert int(cc.item()) == 0
     assert int(cnt.view(nch, K).sum()) == n
+
+
+@pytest.mark.parametrize("dtype,d,k", [(torch.bfloat16, 256, 1024), (torch.bfloat16, 96, 2048),
+                                       (torch.float32, 128, 2048), (torch.float32, 256, 1024)])
+def test_cluster_sums_ksplit_other_widths_vs_f64(native, dtype, d, k):
+    """K-split M-step at 32 / 64 lanes per row and a column-padded width (96 -> 128): each
+    lane's column pairs sit one cell per lane group (csrc/update.hip update_ks_kernel), so
+    a wrong pair <-> cell map would move sums between columns.  Means against f64."""
+    C = native
+    es = 2 if dtype == torch.bfloat16 else 4
+    dt = ops.dtype_code(dtype)
+    dp = ops.pad_columns(torch.zeros(1, d, dtype=dtype)).shape[1]
+    sw = C.update_slice_width(dt, k, dp, False)
+    if not (0 < sw < dp and sw * es < 128):
+        pytest.skip("shape not routed to the K-split kernel")
+    n = 200_000
+    g = torch.Generator().manual_seed(d * 7 + k)
+    X = (torch.randn(n, d, generator=g) * 2 + torch.arange(d) * 0.25).to(dtype)
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32)
+    sums, counts = ops.cluster_sums(X.to(DEV), lab.to(DEV), k)
+    s_ref, c_ref = _oracle_means(X, lab, k)
+    assert torch.equal(counts.cpu().double(), c_ref)
+    colmax = X.double().abs().amax(0)
+    m = c_ref > 0
+    err = ((sums.cpu().double()[m] - s_ref[m]) / c_ref[m][:, None]).abs() / colmax
+    assert err.max().item() <= 2.0**-19, err.max().item()
