@@ -374,6 +374,20 @@ class KMeans(_Serving):
         return km
 
 
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
+def _step_generator(seed: int, rank: int, step: int) -> torch.Generator:
+    """CPU generator for one mini-batch step (step -1: the init sample), keyed by
+    (seed, rank, step) so a resumed fit draws the rows the uninterrupted one would."""
+    key = _splitmix64(_splitmix64(_splitmix64(seed & 0xFFFFFFFFFFFFFFFF) ^ rank) ^ (step & 0xFFFFFFFFFFFFFFFF))
+    return torch.Generator(device="cpu").manual_seed(key & 0x7FFFFFFFFFFFFFFF)
+
+
 class MiniBatchKMeans(_Serving):
     """Mini-batch k-means (Sculley 2010) over tensors or device-generated streams."""
 
@@ -411,28 +425,50 @@ class MiniBatchKMeans(_Serving):
         return resolve_init(self.init, Xs, D, self.n_clusters, n_global, start, comm, self.seed,
                             None)[:, :D]
 
-    def fit(self, X):
-        """Fit on a tensor/array (random batches each step; ``max_iter`` epochs)."""
+    def fit(self, X, *, resume_from=None, checkpoint_every: int = 0, checkpoint_dir=None):
+        """Fit on a tensor/array (random batches each step; ``max_iter`` epochs).
+
+        The batch of step s on rank r is drawn from a generator keyed by (seed, r, s)
+        (:func:`_step_generator`), so the sampler's state is the step counter itself:
+        ``checkpoint_every`` saves centres, running counts, scales and the step, and
+        ``resume_from`` continues such a run with the same rows every later step draws --
+        bit for bit the uninterrupted fit on the same world size."""
+        from .utils import faults
+        from .utils.checkpoint import load_checkpoint
+
         comm = self.comm or get_comm()
         device = _default_device(self.device, X) if self.device is not None or comm.world == 1 else comm.device
         Xt, was_numpy = _to_tensor(X, device, self.dtype)
         self._numpy_io = was_numpy
         n, D = Xt.shape
         eng = self._engine(D, device)
-        g = torch.Generator(device="cpu").manual_seed(self.seed + 7919 * comm.rank)
-        init_n = min(n, self.init_size or max(3 * self.batch_size, 3 * self.n_clusters))
-        sample_idx = torch.randperm(n, generator=g)[:init_n].to(device)
-        eng.set_centers(self._init_centers(Xt[sample_idx]))
+        if resume_from is not None:
+            ck = load_checkpoint(resume_from, comm=comm)
+            if ck.get("kind") != "minibatch" or int(ck["n_features"]) != D:
+                raise ValueError(f"{resume_from} is not a mini-batch checkpoint for {D} features")
+            eng.load_state(ck["centers"], ck["tensors"], ck["iteration"], ck.get("rescales", 0))
+        else:
+            g = _step_generator(self.seed, comm.rank, -1)
+            init_n = min(n, self.init_size or max(3 * self.batch_size, 3 * self.n_clusters))
+            sample_idx = torch.randperm(n, generator=g)[:init_n].to(device)
+            eng.set_centers(self._init_centers(Xt[sample_idx]))
+            eng.steps = 0
         # the step count must be the same on every rank (each step is a collective): derive
         # it from the global row count, never from this rank's shard size
         n_global, _ = _shard_info(n, comm, device)
         steps = self.max_steps or max(1, math.ceil(self.max_iter * n_global / (self.batch_size * comm.world)))
-        for s in range(steps):
+        while eng.steps < steps:
+            s = eng.steps
             if n:
+                g = _step_generator(self.seed, comm.rank, s)
                 idx = torch.randint(0, n, (min(self.batch_size, n),), generator=g).to(device)
                 eng.partial_fit(Xt[idx])
             else:
                 eng.partial_fit(Xt[:0])       # empty shard: still joins the step's all-reduce
+            faults.maybe_fail(comm.rank, eng.steps)
+            if checkpoint_every and checkpoint_dir and eng.steps % checkpoint_every == 0:
+                self._finish(eng)
+                self._save(checkpoint_dir, comm)
             if self.tol > 0 and (s + 1) % 10 == 0:
                 if float(eng.shift.sum()) <= self.tol:
                     break
@@ -489,7 +525,11 @@ class MiniBatchKMeans(_Serving):
         cfg = {"n_clusters": self.n_clusters, "batch_size": self.batch_size, "max_iter": self.max_iter,
                "init": self.init if isinstance(self.init, str) else "array", "dtype": str(self.dtype),
                "seed": self.seed, "tol": self.tol}
-        extra = {"kind": "minibatch", "rescales": getattr(eng, "rescales", 0)}
+        extra = {"kind": "minibatch", "rescales": getattr(eng, "rescales", 0),
+                 # the samplers are counter-based: (seed, rank, step) is the whole RNG state
+                 "rng": {"scheme": "fit: torch CPU generator per step seeded splitmix64(seed, rank, step); "
+                                   "streams: Philox4x32-10 by global row (BlobStream)",
+                         "seed": self.seed, "step": int(eng.steps)}}
         if stream_pos is not None:
             extra["stream_pos"] = int(stream_pos)
         return save_checkpoint(path, eng.centers, eng.steps, cfg, comm=comm, extra=extra,

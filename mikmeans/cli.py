@@ -46,7 +46,6 @@ def cmd_fit(a) -> int:
     from . import KMeans, MiniBatchKMeans
     from .config import KMeansConfig, resolve_dtype
     from .utils.io import load_points
-    from .utils.jsjson import centroids_to_json
 
     cfg = KMeansConfig.from_args(a)
     device = cfg.device or ("cuda" if torch.cuda.is_available() else "cpu")
@@ -65,9 +64,11 @@ def cmd_fit(a) -> int:
     if cfg.batch_size > 0:
         km = MiniBatchKMeans(cfg.n_clusters, batch_size=cfg.batch_size, max_iter=cfg.max_iter, init=cfg.init,
                              dtype=dtype, device=comm.device, seed=cfg.seed, comm=comm)
-        if resume:
-            raise SystemExit("--resume applies to Lloyd fits and streams (MiniBatchKMeans.fit_stream)")
-        km.fit(X)
+        if resume and comm.rank == 0:
+            print(f"[mikmeans] resuming from {resume}", file=sys.stderr, flush=True)
+        # batch rows are drawn by (seed, rank, step): a restart on the same world size
+        # continues the interrupted fit exactly
+        km.fit(X, resume_from=resume, checkpoint_every=cfg.checkpoint_every, checkpoint_dir=cfg.checkpoint_dir)
     else:
         km = KMeans.from_config(cfg, comm=comm)
         km.device = comm.device
@@ -82,11 +83,7 @@ def cmd_fit(a) -> int:
                        metrics=km.metrics())
         print(json.dumps(rec, default=str))
     if out is not None:
-        if isinstance(km, KMeans):
-            km.save(out)
-        elif comm.rank == 0:
-            out.mkdir(parents=True, exist_ok=True)
-            (out / "centroids.json").write_text(centroids_to_json(km.cluster_centers_))
+        km.save(out)   # safetensors + state.json + flat centroids.json (mini-batch: + running counts)
         if a.save_labels and hasattr(km, "labels_"):
             lab = km.labels_
             lab = lab.cpu().numpy() if torch.is_tensor(lab) else lab

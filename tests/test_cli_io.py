@@ -122,7 +122,8 @@ def test_init_reset_and_unassigned_predict():
         km.predict(X)
 
 
-def test_launch_restarts_failed_job_from_checkpoint(tmp_path):
+@pytest.mark.parametrize("mode", ["lloyd", "minibatch"])
+def test_launch_restarts_failed_job_from_checkpoint(tmp_path, mode):
     """``mikmeans launch``: a 2-rank job whose rank 1 dies after iteration 5 is restarted
     as a fresh process tree, resumes from the iteration-4 checkpoint and ends with the
     centres of an uninterrupted run (the reference re-meshes after a
@@ -131,6 +132,9 @@ def test_launch_restarts_failed_job_from_checkpoint(tmp_path):
 
     common = ["--blobs", "6000,4,5", "--device", "cpu", "--n-clusters", "5", "--max-iter", "8", "--tol", "-1",
               "--checkpoint-every", "2", "--seed", "3"]
+    if mode == "minibatch":   # 2 epochs of 256-row batches per rank: 24 steps, checkpoint every 2
+        common = ["--blobs", "6000,4,5", "--device", "cpu", "--n-clusters", "5", "--max-iter", "2",
+                  "--batch-size", "256", "--checkpoint-every", "2", "--seed", "3"]
     env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)

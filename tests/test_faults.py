@@ -87,3 +87,46 @@ def test_minibatch_save_load_roundtrip(tmp_path):
     km.partial_fit(X[:512])
     km2.partial_fit(X[:512])
     assert torch.equal(km2.cluster_centers_, km.cluster_centers_)
+
+
+def _mb_fit(comm, ckdir, resume):
+    from mikmeans import MiniBatchKMeans
+    from mikmeans.data.blobs import make_blobs
+
+    X = make_blobs(6000, 5, 6, std=2.0, seed=4)
+    s, e = shard_range(6000, comm.rank, comm.world)
+    km = MiniBatchKMeans(6, batch_size=256, max_steps=12, seed=5, comm=comm, init="random", device="cpu")
+    km.fit(X[s:e], resume_from=ckdir if resume else None, checkpoint_every=3, checkpoint_dir=ckdir)
+    return {"C": km.cluster_centers_, "steps": km.n_steps_, "counts": km.counts_}
+
+
+def test_minibatch_fit_failure_then_resume(tmp_path, monkeypatch):
+    """MiniBatchKMeans.fit on tensors: batch rows are drawn from a generator keyed by
+    (seed, rank, step), so the checkpointed step is the whole sampler state and a job
+    killed mid-fit resumes to the uninterrupted fit's centres bit for bit."""
+    from mikmeans.utils.checkpoint import load_checkpoint
+
+    ref = spawn_local(_mb_fit, 2, str(tmp_path / "ref"), False)
+    ck = str(tmp_path / "ck")
+    monkeypatch.setenv("MIKMEANS_FAULT", "0:7")
+    with pytest.raises(Exception):
+        spawn_local(_mb_fit, 2, ck, False)
+    monkeypatch.delenv("MIKMEANS_FAULT")
+    st = load_checkpoint(ck)
+    assert st["iteration"] == 6 and st["rng"]["step"] == 6 and st["rng"]["seed"] == 5
+    res = spawn_local(_mb_fit, 2, ck, True)
+    for r in res:
+        assert r["steps"] == 12
+        assert torch.equal(r["C"], ref[0]["C"])
+        assert torch.equal(r["counts"], ref[0]["counts"])
+
+
+def test_minibatch_refit_runs_all_steps():
+    import mikmeans
+    from mikmeans.data.blobs import make_blobs
+
+    X = make_blobs(3000, 4, 3, seed=9)
+    km = mikmeans.MiniBatchKMeans(3, batch_size=128, max_steps=5, seed=1, device="cpu")
+    a = km.fit(X).cluster_centers_.clone()
+    assert km.n_steps_ == 5
+    assert torch.equal(km.fit(X).cluster_centers_, a) and km.n_steps_ == 5
