@@ -261,8 +261,12 @@ class KMeans(_Serving):
                 if self.checkpoint_every and self.checkpoint_dir and st.iteration % self.checkpoint_every == 0:
                     from .utils.checkpoint import save_checkpoint
 
+                    # Lloyd draws random numbers only while seeding (Philox / seeded NumPy keyed
+                    # by config.seed and the trial); a resumed run continues from the centres
                     save_checkpoint(self.checkpoint_dir, _eng.centers, st.iteration, self.get_config(),
-                                    history=_hist, comm=comm)
+                                    history=_hist, comm=comm,
+                                    extra={"rng": {"scheme": "seeding only, keyed by (seed, trial)",
+                                                   "seed": self.seed, "trial": trial}})
 
             if self.graph:
                 eng.capture()
