@@ -12,8 +12,9 @@ from mikmeans.parallel.launch import free_port
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_bench_json_line_on_cpu_ranks(world):
+    """The driver's 1/2/4/8-rank command lines (gloo ranks standing in for GPUs)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py",
            "--gpus", str(world), "--steps", "2", "--warmup", "1", "--device", "cpu", "--points", "6000"]

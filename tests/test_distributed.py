@@ -40,9 +40,10 @@ def _single(init, iters):
     return _lloyd(Comm.local(), init, iters)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("init", ["random", "k-means++"])
+@pytest.mark.parametrize("world,init", [(2, "random"), (2, "k-means++"), (3, "random"), (3, "k-means++"),
+                                        (4, "k-means++"), (8, "random"), (8, "k-means++")])
 def test_lloyd_dp_equals_single_rank(world, init):
+    """W = 2/3/4/8 gloo ranks (the 1/2/4/8-GPU job's code path, backend aside)."""
     ref = _single(init, 6)
     outs = spawn_local(_lloyd, world, init, 6)
     for o in outs:  # centroids are replicated bit-identically on every rank
