@@ -63,6 +63,17 @@ static hipError_t ksv(const mk::UpdateArgs& a, int, hipStream_t s) {
   return mku::launch_ks_t<uint16_t, LPR, GM, false>(b, kp, s);
 }
 
+// the production K-split kernel (pair x lanes cell layout) at other row-group depths
+template <int LPR, int GM, int KS>
+static hipError_t ksn(const mk::UpdateArgs& a, int, hipStream_t s) {
+  mk::plan::KsPlan kp{};
+  kp.ks = KS; kp.kq = (a.K + KS - 1) / KS; kp.lpr = LPR; kp.ldc = LPR * 8 / 2 + 1; kp.gm = GM;
+  if (mk::plan::ks_lds_bytes(kp.kq, kp.ldc) > mk::plan::UPD_LDS_MAX) return hipErrorInvalidValue;
+  mk::UpdateArgs b = a;
+  b.n_chunks = ((256 / KS + 7) / 8) * 8 > a.n_chunks ? ((256 / KS + 7) / 8) * 8 : a.n_chunks;
+  return mk::launch_ks_t<uint16_t, LPR, GM, false>(b, kp, s);
+}
+
 int main(int argc, char** argv) {
   const int64_t N = argc > 1 ? atoll(argv[1]) : 100000000;
   const int D = argc > 2 ? atoi(argv[2]) : 128;
@@ -104,11 +115,18 @@ int main(int argc, char** argv) {
     vs.push_back({"ks4_gm4", ksv<16, 4, 4>});
     vs.push_back({"ks8_gm3", ksv<16, 3, 8>});
     vs.push_back({"ks8_gm6", ksv<16, 6, 8>});
+    vs.push_back({"new_gm4", ksn<16, 4, 4>});
+    vs.push_back({"new_gm6", ksn<16, 6, 4>});
+    vs.push_back({"new_gm8", ksn<16, 8, 4>});
+    vs.push_back({"new_gm10", ksn<16, 10, 4>});
   }
   if (!f32 && D == 64 && K == 4096) {
     vs.push_back({"ks8_gm3", ksv<8, 3, 8>});
     vs.push_back({"ks8_gm2", ksv<8, 2, 8>});
     vs.push_back({"ks16_gm2", ksv<8, 2, 16>});
+    vs.push_back({"new_ks8_gm2", ksn<8, 2, 8>});
+    vs.push_back({"new_ks8_gm3", ksn<8, 3, 8>});
+    vs.push_back({"new_ks8_gm4", ksn<8, 4, 8>});
   }
   if (!f32 && sw == 64) vs.push_back({"slice_old", xv<0, 1024, 3, 512, 64>});
   if (!f32 && sw == 8) vs.push_back({"slice_old", xv<4, 1024, 6, 1024, 8>});
