@@ -235,10 +235,24 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       f32x4 acc[C::P];
 #pragma unroll
       for (int p = 0; p < C::P; ++p) acc[p] = ci;
+      // bf16: the wave issues its MFMAs at raised priority and drops back for the epilogue,
+      // so a SIMD's arbiter feeds the matrix core before another wave's argmin VALU work
+      // (-2.2 % at D=128 K=1024, -1.4 % at D=64 K=4096 in one-process A/B:
+      // profiles/r2_29_assign_setprio_ab.log)
+      if constexpr (!EXACT) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int q = 0; q < C::NQ; ++q) {
 #pragma unroll
         for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
+      }
+      if constexpr (!EXACT) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (EARLY) {
         if (tl_i + 1 < C::CT) load_a(tl_i + 1, awe, cie);

@@ -27,6 +27,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void assign_x_kernel(AssignArgs a) {
   constexpr bool STAMP = MODE & 8;   // per-workgroup (s_memtime, s_memrealtime) at start/end
   constexpr bool NOEPI = MODE & 16;
   constexpr bool EARLY = MODE & 32;
+  constexpr bool PRIO = MODE & 1024;  // s_setprio 1 while this wave issues its MFMAs, 0 for the epilogue
   // exact fp32 (value, index) compare, gated per tile: a tile's keyed update runs only for
   // point blocks where some lane's tile minimum is <= its threshold, seeded with the score
   // to the previous label's centre (VALU dot product + rounding margin)
@@ -200,10 +201,20 @@ __global__ __launch_bounds__(NW * 64, OCC) void assign_x_kernel(AssignArgs a) {
       f32x4 acc[P];
 #pragma unroll
       for (int p = 0; p < P; ++p) acc[p] = ci;
+      if constexpr (PRIO) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
 #pragma unroll
         for (int p = 0; p < P; ++p) acc[p] = Mfma16<uint16_t>::run(aw[q], xr[p][q], acc[p]);
+      }
+      if constexpr (PRIO) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (SKEW) {
         epilogue(accp, tprev);
@@ -317,10 +328,14 @@ static hipError_t launch_x(const AssignArgs& a, hipStream_t s) {
 
 template <typename VS>
 static void add_variants(int D, VS& vs) {
-  if (D == 64) vs.push_back({"x64_p8o3_m0", launch_x<64, 8, 3, 0>});
+  if (D == 64) {
+    vs.push_back({"x64_p8o3_m0", launch_x<64, 8, 3, 0>});
+    vs.push_back({"x64_p8o3_prio", launch_x<64, 8, 3, 1024>});
+  }
   if (D == 128) {
     vs.push_back({"x_p4o4_m0", launch_x<128, 4, 4, 0>});
     vs.push_back({"x_p4o4_st", launch_x<128, 4, 4, 8>});
+    vs.push_back({"x_p4o4_prio", launch_x<128, 4, 4, 1024>});
 
   }
   if (D == 256) {
