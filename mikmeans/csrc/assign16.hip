@@ -237,8 +237,9 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       for (int p = 0; p < C::P; ++p) acc[p] = ci;
       // bf16: the wave issues its MFMAs at raised priority and drops back for the epilogue,
       // so a SIMD's arbiter feeds the matrix core before another wave's argmin VALU work
-      // (-2.2 % at D=128 K=1024, -1.4 % at D=64 K=4096 in one-process A/B:
-      // profiles/r2_29_assign_setprio_ab.log)
+      // (profiles/r2_29_assign_setprio_ab.log, one process each: the harness copy -2.2 % at
+      // D=128 K=1024 and -1.4 % at D=64 K=4096; this kernel against that copy +0.8 % at D=128,
+      // +0.3 % at D=64, about +5 % at D=256 K=512)
       if constexpr (!EXACT) {
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
