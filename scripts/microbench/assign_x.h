@@ -27,7 +27,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void assign_x_kernel(AssignArgs a) {
   constexpr bool STAMP = MODE & 8;   // per-workgroup (s_memtime, s_memrealtime) at start/end
   constexpr bool NOEPI = MODE & 16;
   constexpr bool EARLY = MODE & 32;
-  constexpr bool PRIO = MODE & 1024;  // s_setprio 1 while this wave issues its MFMAs, 0 for the epilogue
+  constexpr bool PRIO = MODE & (1024 | 2048 | 4096);  // raised s_setprio while this wave issues its MFMAs
+  constexpr int PRIO_LV = (MODE & 2048) ? 3 : 1;       // 2048: level 3 instead of 1
+  constexpr bool PRIO_LD = MODE & 4096;                // 4096: raised already for the tile's LDS reads
   // exact fp32 (value, index) compare, gated per tile: a tile's keyed update runs only for
   // point blocks where some lane's tile minimum is <= its threshold, seeded with the score
   // to the previous label's centre (VALU dot product + rounding margin)
@@ -196,14 +198,19 @@ __global__ __launch_bounds__(NW * 64, OCC) void assign_x_kernel(AssignArgs a) {
         for (int q = 0; q < NQ; ++q) aw[q] = awe[q];
         ci = cie;
       } else {
+        if constexpr (PRIO_LD) {
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_setprio(1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
         load_a(tl_i, aw, ci);
       }
       f32x4 acc[P];
 #pragma unroll
       for (int p = 0; p < P; ++p) acc[p] = ci;
-      if constexpr (PRIO) {
+      if constexpr (PRIO && !PRIO_LD) {
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(PRIO_LV);
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
@@ -331,16 +338,22 @@ static void add_variants(int D, VS& vs) {
   if (D == 64) {
     vs.push_back({"x64_p8o3_m0", launch_x<64, 8, 3, 0>});
     vs.push_back({"x64_p8o3_prio", launch_x<64, 8, 3, 1024>});
+    vs.push_back({"x64_p8o3_prio_ld", launch_x<64, 8, 3, 4096>});
+    vs.push_back({"x64_p8o3_early_prio", launch_x<64, 8, 3, 1024 | 32>});
   }
   if (D == 128) {
     vs.push_back({"x_p4o4_m0", launch_x<128, 4, 4, 0>});
     vs.push_back({"x_p4o4_st", launch_x<128, 4, 4, 8>});
     vs.push_back({"x_p4o4_prio", launch_x<128, 4, 4, 1024>});
+    vs.push_back({"x_p4o4_prio3", launch_x<128, 4, 4, 2048>});
+    vs.push_back({"x_p4o4_prio_ld", launch_x<128, 4, 4, 4096>});
 
   }
   if (D == 256) {
     vs.push_back({"x256_p3o3_m0", launch_x<256, 3, 3, 0>});
     vs.push_back({"x256_p3o3_early", launch_x<256, 3, 3, 32>});
+    vs.push_back({"x256_p3o3_prio", launch_x<256, 3, 3, 1024>});
+    vs.push_back({"x256_p3o3_prio_ld", launch_x<256, 3, 3, 4096>});
   }
 }
 
