@@ -70,14 +70,14 @@ def _digest(paths, flags) -> str:
     return h.hexdigest()[:16]
 
 
-def _headers():
-    return sorted(CSRC.glob("*.h"))
+def _headers(csrc: Path = CSRC):
+    return sorted(csrc.glob("*.h"))
 
 
-def _compile(src: Path, flags, verbose: bool) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
-    tag = _digest([src, *_headers()], flags)
-    obj = BUILD / f"{src.stem}.{tag}.o"
+def _compile(src: Path, flags, verbose: bool, build_dir: Path = BUILD) -> Path:
+    build_dir.mkdir(parents=True, exist_ok=True)
+    tag = _digest([src, *_headers(src.parent)], flags)
+    obj = build_dir / f"{src.stem}.{tag}.o"
     if obj.exists():
         return obj
     cmd = [_hipcc(), *flags, "-c", str(src), "-o", str(obj) + ".tmp"]
@@ -87,39 +87,44 @@ def _compile(src: Path, flags, verbose: bool) -> Path:
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
     os.replace(str(obj) + ".tmp", obj)
-    for old in BUILD.glob(f"{src.stem}.*.o"):  # keep only the current object per source
+    for old in build_dir.glob(f"{src.stem}.*.o"):  # keep only the current object per source
         if old != obj:
             old.unlink(missing_ok=True)
     return obj
 
 
-def build(force: bool = False, verbose: bool = True, jobs: int | None = None) -> Path:
-    """Compile every HIP TU for gfx950 and link ``mikmeans/_C*.so``; return its path."""
+def build(force: bool = False, verbose: bool = True, jobs: int | None = None, *, csrc: Path = CSRC,
+          build_dir: Path = BUILD, out: Path | None = None, module: str = "_C") -> Path:
+    """Compile every HIP TU for gfx950 and link ``mikmeans/_C*.so``; return its path.
+
+    ``csrc`` / ``build_dir`` / ``out`` / ``module`` build another checkout of the kernel
+    sources into a separately named module (scripts/ab_ext.py: A/B against a git ref)."""
     inc, lib, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     binding_flags = [
         *DEVICE_FLAGS,
         "-x",
         "hip",
-        "-DTORCH_EXTENSION_NAME=_C",
+        f"-DTORCH_EXTENSION_NAME={module}",
         "-DTORCH_API_INCLUDE_EXTENSION_H",
         f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
         *[f"-I{p}" for p in inc],
         f"-I{py_inc}",
-        f"-I{CSRC}",
+        f"-I{csrc}",
         "-w",
     ]
-    if force and BUILD.exists():
-        for o in BUILD.glob("*.o"):
+    if force and build_dir.exists():
+        for o in build_dir.glob("*.o"):
             o.unlink()
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        futs = [ex.submit(_compile, CSRC / s, [*DEVICE_FLAGS, f"-I{CSRC}"], verbose) for s in HIP_SOURCES]
-        futs.append(ex.submit(_compile, CSRC / BINDING, binding_flags, verbose))
+        sources = [s for s in HIP_SOURCES if (csrc / s).exists()]
+        futs = [ex.submit(_compile, csrc / s, [*DEVICE_FLAGS, f"-I{csrc}"], verbose, build_dir) for s in sources]
+        futs.append(ex.submit(_compile, csrc / BINDING, binding_flags, verbose, build_dir))
         objs = [f.result() for f in futs]
-    out = ext_path()
-    link_tag = _digest(objs, ["link"])
-    stamp = BUILD / "link.stamp"
+    out = out or ext_path()
+    link_tag = _digest(objs, ["link", str(out)])
+    stamp = build_dir / "link.stamp"
     if not force and out.exists() and stamp.exists() and stamp.read_text() == link_tag:
         return out
     cmd = [

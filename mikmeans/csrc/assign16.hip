@@ -19,15 +19,19 @@
 // Argmin epilogue.
 //  * bf16: keys carry a 6-bit index in the low mantissa bits (tile-in-segment*4 + reg)
 //    so one v_min3 tree yields (min, index): 1.5 VALU per score.  The workgroup adds
-//    o = (1 + 2^-12) max |x|^2 over its 256 points to its LDS copy of |c|^2 once, which
-//    makes every key |x-c|^2 + (o - |x|^2) > 0: among equal keys the lower index then
-//    always wins (an OR of the index into a NEGATIVE float favours the higher one), and
-//    the key resolution is 2^-17 of the squared distance plus the spread of |x|^2 inside
-//    the workgroup, not 2^-17 of |x|^2 (coarse for data far from the origin).  A
-//    per-point offset would make the keys a function of the point alone, but its per-tile
-//    seed adds cost 17 % at the headline shape (one process A/B, round 2); workgroups
-//    are therefore aligned to the global 256-row grid by the callers (shard_range,
-//    streaming chunks), so near-tie resolution is the same on any world size.
+//    o = (1 + 2^-12) max |x|^2 over its 192-512 points to its LDS copy of |c|^2 once,
+//    which makes every key |x-c|^2 + (o - |x|^2) > 0: among equal keys the lower index
+//    then always wins (an OR of the index into a NEGATIVE float favours the higher one),
+//    and the key resolution is 2^-17 of the squared distance plus the spread of |x|^2
+//    inside the workgroup, not 2^-17 of |x|^2 (coarse for data far from the origin).
+//    Where that spread is large (max |x|^2 > 4 min |x|^2: an outlier row, data around the
+//    origin) the workgroup uses per-point offsets instead (added to the scores after each
+//    tile's MFMAs, a uniform branch the common path skips), so the resolution is never
+//    worse than 2^-17 (|x-c|^2 + 3|x|^2).  Per-point offsets everywhere would make the keys
+//    a function of the point alone, but cost 17 % at the headline shape (one process A/B,
+//    round 2); workgroups are therefore aligned to the global ROW_ALIGN = 1536-row grid by
+//    the callers (shard_range, streaming chunks), so near-tie resolution is the same on
+//    any world size.
 //  * f32: an exact (value, index) compare per score (v_cmp + 2 v_cndmask).  The f32
 //    MFMA is 16x slower per FLOP than bf16, so the epilogue is noise there and the
 //    labels carry full fp32 score resolution; strict < in ascending index order keeps
@@ -36,6 +40,8 @@
 // Layout "16" of the packed centroids (csrc/kernels.h):
 //   element (k, d): t = k/16, r = k%16, q = d / (4V), g = (d / V) % 4
 //   offset = ((t*NQ + q)*64 + r + 16*g)*V + d%V,  NQ = DPAD/(4V)
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 #include "plan.h"
@@ -58,6 +64,8 @@ struct Assign16Cfg {
   static constexpr int PIECES = CHUNK_BYTES / 1024;
   static constexpr int NPW = PIECES / NW;
   static constexpr int PTS = NW * P * 16;
+  static constexpr int PP = (P + 3) / 4 * 4;    // per-point offset slots per lane (LDS, f32x4 reads)
+  static constexpr int OPT_BYTES = NW * 16 * PP * 4;
   static constexpr int NBUF = NBUF_;
   static_assert(NBUF == 2 || NBUF == 3, "ring depth");
   static_assert(chunk_tiles16(sizeof(T), DPAD) % CT == 0, "chunk must divide the Kpad granule");
@@ -161,13 +169,16 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   // bf16 seed offset (see the header): o = (1 + 2^-12) max |x|^2 over the workgroup's
   // points, from the caller's row norms when given (loaded with the fragments) or from
   // the fragments themselves, folded into this workgroup's LDS copy of |c|^2 once.
+  // A workgroup whose max |x|^2 exceeds 4x its min (an outlier row, or data around the
+  // origin) takes per-point offsets o_p = (1 + 2^-12) |x_p|^2 instead, parked in LDS and
+  // added to each tile's seed (uniform branch): a shared offset would coarsen every
+  // neighbour's keys to 2^-17 of the outlier's norm.  Either way a key resolves
+  // 2^-17 (|x - c|^2 + 3 |x|^2) or better.
   float off = 0.f;
+  bool ppo = false;
+  float* opt = (float*)(bufs + C::NBUF * C::CHUNK_BYTES + 16 * C::NW);  // [NW][16][PP] offsets
   if constexpr (!EXACT) {
-    float m = 0.f;
-    if (a.xn) {
-#pragma unroll
-      for (int p = 0; p < C::P; ++p) m = fmaxf(m, xnr[p]);
-    } else {
+    if (!a.xn) {
 #pragma unroll
       for (int p = 0; p < C::P; ++p) {
         float s = 0.f;
@@ -175,19 +186,35 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         for (int q = 0; q < C::NQ; ++q) s += sq16(xr[p][q], (T*)nullptr);
         s += __shfl_xor(s, 16, 64);
         s += __shfl_xor(s, 32, 64);
-        m = fmaxf(m, s);
+        xnr[p] = s;
       }
     }
+    float m = 0.f, mn = 3.0e38f;
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    for (int p = 0; p < C::P; ++p) { m = fmaxf(m, xnr[p]); mn = fminf(mn, xnr[p]); }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      m = fmaxf(m, __shfl_xor(m, o, 64));
+      mn = fminf(mn, __shfl_xor(mn, o, 64));
+    }
     float* red = (float*)(bufs + C::NBUF * C::CHUNK_BYTES);
-    if (lane == 0) red[wid] = m;
+    if (lane == 0) { red[2 * wid] = m; red[2 * wid + 1] = mn; }
     __syncthreads();  // (every wave's cn / chunk-0 DMA has landed: vmcnt(0) above)
+    float mnw = 3.0e38f;
 #pragma unroll
-    for (int w = 0; w < C::NW; ++w) off = fmaxf(off, red[w]);
-    off = __builtin_fmaf(off, 2.44140625e-04f, off);  // * (1 + 2^-12)
-    off = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(off)));
-    for (int k = threadIdx.x; k < a.Kpad; k += C::NW * 64) ((float*)cn_lds)[k] += off;
+    for (int w = 0; w < C::NW; ++w) { off = fmaxf(off, red[2 * w]); mnw = fminf(mnw, red[2 * w + 1]); }
+    ppo = __builtin_amdgcn_readfirstlane((int)(off > 4.f * mnw)) != 0;
+    if (!ppo) {
+      off = __builtin_fmaf(off, 2.44140625e-04f, off);  // * (1 + 2^-12)
+      off = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(off)));
+      for (int k = threadIdx.x; k < a.Kpad; k += C::NW * 64) ((float*)cn_lds)[k] += off;
+    } else {
+      off = 0.f;
+      if (g == 0) {
+#pragma unroll
+        for (int p = 0; p < C::P; ++p) opt[(wid * 16 + r) * C::PP + p] = __builtin_fmaf(xnr[p], 2.44140625e-04f, xnr[p]);
+      }
+    }
     // (published by the main loop's first wait_lgkm0 + barrier)
   }
 
@@ -198,109 +225,130 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   const int ngrp = nch * C::CT;   // one past the last tile (global tile numbering)
   const unsigned kmask = key6_mask();
 
-  for (int c = 0; c < ncl; ++c) {
-    // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
-    if (C::NBUF == 3 && c + 1 < ncl) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
-    wait_lgkm0();
-    raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
-    if (c + C::NBUF - 1 < ncl) issue_chunk(c + C::NBUF - 1);
-    const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
-    // A fragments + |c|^2 of a tile from the LDS ring
-    auto load_a = [&](int tl_i, u32x4* aw_, f32x4& ci_) {
-      const int tile = (c0 + c) * C::CT + tl_i;
-      ci_ = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
-      const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
-#pragma unroll
-      for (int q = 0; q < C::NQ; ++q) aw_[q] = *(const u32x4*)(tl + q * 1024);
-    };
-    // EARLY (bf16 D=64): the next tile's fragments are read right after this tile's
-    // MFMAs are issued, so their LDS latency hides under the argmin epilogue (+2 % at D=64
-    // in one-process A/B, profiles/r2_08_assign_clock_study.md; no gain at D=128)
-    constexpr bool EARLY = !EXACT && DPAD == 64;
-    u32x4 awe[C::NQ];
-    f32x4 cie;
-    if constexpr (EARLY) load_a(0, awe, cie);
-#pragma unroll
-    for (int tl_i = 0; tl_i < C::CT; ++tl_i) {
-      const int tile = (c0 + c) * C::CT + tl_i;
-      u32x4 aw[C::NQ];
-      f32x4 ci;
-      if constexpr (EARLY) {
-#pragma unroll
-        for (int q = 0; q < C::NQ; ++q) aw[q] = awe[q];
-        ci = cie;
-      } else {
-        load_a(tl_i, aw, ci);
-      }
-      f32x4 acc[C::P];
-#pragma unroll
-      for (int p = 0; p < C::P; ++p) acc[p] = ci;
-      // bf16: the wave issues its MFMAs at raised priority and drops back for the epilogue,
-      // so a SIMD's arbiter feeds the matrix core before another wave's argmin VALU work
-      // (profiles/r2_29_assign_setprio_ab.log, one process each: the harness copy -2.2 % at
-      // D=128 K=1024 and -1.4 % at D=64 K=4096; this kernel against that copy +0.8 % at D=128,
-      // +0.3 % at D=64, about +5 % at D=256 K=512)
-      if constexpr (!EXACT) {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int q = 0; q < C::NQ; ++q) {
-#pragma unroll
-        for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
-      }
-      if constexpr (!EXACT) {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr (EARLY) {
-        if (tl_i + 1 < C::CT) load_a(tl_i + 1, awe, cie);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr (EXACT) {
-        // (tile*4 + reg) as wave-uniform values: the index select needs no VALU add
-        const int u = tile * 4;
-#pragma unroll
-        for (int p = 0; p < C::P; ++p) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bool lt = acc[p][e] < best[p];
-            best[p] = lt ? acc[p][e] : best[p];
-            bg[p] = lt ? u + e : bg[p];
+  // The chunk loop, instantiated twice: per-point offsets (PPO, outlier workgroups) add a
+  // tile's offsets to its scores after the MFMAs; the common instantiation has no such
+  // code at all -- a per-tile branch cost 1-3 % (one-process A/B against round 2).
+  auto chunk_loop = [&](auto ppo_tag) {
+    constexpr bool PPO = decltype(ppo_tag)::value;
+    for (int c = 0; c < ncl; ++c) {
+      // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
+      if (C::NBUF == 3 && c + 1 < ncl) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
+      wait_lgkm0();
+      raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
+      if (c + C::NBUF - 1 < ncl) issue_chunk(c + C::NBUF - 1);
+      const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
+      // A fragments + |c|^2 of a tile from the LDS ring
+      auto load_a = [&](int tl_i, u32x4* aw_, f32x4& ci_) {
+        const int tile = (c0 + c) * C::CT + tl_i;
+        ci_ = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
+        const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
+  #pragma unroll
+        for (int q = 0; q < C::NQ; ++q) aw_[q] = *(const u32x4*)(tl + q * 1024);
+      };
+      // EARLY (bf16 D=64): the next tile's fragments are read right after this tile's
+      // MFMAs are issued, so their LDS latency hides under the argmin epilogue (+2 % at D=64
+      // in one-process A/B, profiles/r2_08_assign_clock_study.md; no gain at D=128)
+      constexpr bool EARLY = !EXACT && DPAD == 64;
+      u32x4 awe[C::NQ];
+      f32x4 cie;
+      if constexpr (EARLY) load_a(0, awe, cie);
+  #pragma unroll
+      for (int tl_i = 0; tl_i < C::CT; ++tl_i) {
+        const int tile = (c0 + c) * C::CT + tl_i;
+        u32x4 aw[C::NQ];
+        f32x4 ci;
+        if constexpr (EARLY) {
+  #pragma unroll
+          for (int q = 0; q < C::NQ; ++q) aw[q] = awe[q];
+          ci = cie;
+        } else {
+          load_a(tl_i, aw, ci);
+        }
+        f32x4 acc[C::P];
+  #pragma unroll
+        for (int p = 0; p < C::P; ++p) acc[p] = ci;
+        // bf16: the wave issues its MFMAs at raised priority and drops back for the epilogue,
+        // so a SIMD's arbiter feeds the matrix core before another wave's argmin VALU work
+        // (profiles/r2_29_assign_setprio_ab.log, one process each: the harness copy -2.2 % at
+        // D=128 K=1024 and -1.4 % at D=64 K=4096; this kernel against that copy +0.8 % at D=128,
+        // +0.3 % at D=64, about +5 % at D=256 K=512)
+        if constexpr (!EXACT) {
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_setprio(1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+  #pragma unroll
+        for (int q = 0; q < C::NQ; ++q) {
+  #pragma unroll
+          for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
+        }
+        if constexpr (!EXACT) {
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_setprio(0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (EARLY) {
+          if (tl_i + 1 < C::CT) load_a(tl_i + 1, awe, cie);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (!EXACT) {
+          if (ppo) {  // per-point offsets, added to the scores in place (outlier workgroups only, see above; after the
+                      // MFMAs, so the common path seeds them with ci directly)
+            const float* o = opt + (wid * 16 + r) * C::PP;
+  #pragma unroll
+            for (int p4 = 0; p4 < C::P; p4 += 4) {
+              const f32x4 ov = *(const f32x4*)(o + p4);
+  #pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (p4 + j < C::P) acc[p4 + j] += ov[j];
+            }
           }
         }
-      } else {
-        // 6-bit keys over a segment of 16 tiles (tile-in-segment * 4 + reg): 4 key packs
-        // + 2 v_min3 per tile and point block; the running best is merged with its
-        // segment id once per segment.  The four indices as opaque SGPRs, so each key is
-        // one v_and_or_b32.
-        const unsigned tis = (unsigned)(tile & 15) << 2;
-        unsigned t0, t1, t2, t3;
-        asm volatile("s_mov_b32 %0, %4\n\ts_or_b32 %1, %4, 1\n\ts_or_b32 %2, %4, 2\n\ts_or_b32 %3, %4, 3"
-                     : "=s"(t0), "=s"(t1), "=s"(t2), "=s"(t3) : "s"(tis));
-#pragma unroll
-        for (int p = 0; p < C::P; ++p) {
-          const f32x4& sv = acc[p];
-          const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
-          const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
-          seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
-        }
-        if ((tile & 15) == 15 || tile == ngrp - 1) {
-#pragma unroll
+        if constexpr (EXACT) {
+          // (tile*4 + reg) as wave-uniform values: the index select needs no VALU add
+          const int u = tile * 4;
+  #pragma unroll
           for (int p = 0; p < C::P; ++p) {
-            // compare values only: on equal (truncated) values the earlier segment keeps
-            // the lower centroid index (all keys are >= 0, see the header)
-            const float sv = __uint_as_float(__float_as_uint(seg_best[p]) & ~63u);
-            const float bv = __uint_as_float(__float_as_uint(best[p]) & ~63u);
-            if (sv < bv) { best[p] = seg_best[p]; bg[p] = tile >> 4; }
-            seg_best[p] = 3.0e38f;
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const bool lt = acc[p][e] < best[p];
+              best[p] = lt ? acc[p][e] : best[p];
+              bg[p] = lt ? u + e : bg[p];
+            }
+          }
+        } else {
+          // 6-bit keys over a segment of 16 tiles (tile-in-segment * 4 + reg): 4 key packs
+          // + 2 v_min3 per tile and point block; the running best is merged with its
+          // segment id once per segment.  The four indices as opaque SGPRs, so each key is
+          // one v_and_or_b32.
+          const unsigned tis = (unsigned)(tile & 15) << 2;
+          unsigned t0, t1, t2, t3;
+          asm volatile("s_mov_b32 %0, %4\n\ts_or_b32 %1, %4, 1\n\ts_or_b32 %2, %4, 2\n\ts_or_b32 %3, %4, 3"
+                       : "=s"(t0), "=s"(t1), "=s"(t2), "=s"(t3) : "s"(tis));
+  #pragma unroll
+          for (int p = 0; p < C::P; ++p) {
+            const f32x4& sv = acc[p];
+            const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
+            const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
+            seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
+          }
+          if ((tile & 15) == 15 || tile == ngrp - 1) {
+  #pragma unroll
+            for (int p = 0; p < C::P; ++p) {
+              // compare values only: on equal (truncated) values the earlier segment keeps
+              // the lower centroid index (all keys are >= 0, see the header)
+              const float sv = __uint_as_float(__float_as_uint(seg_best[p]) & ~63u);
+              const float bv = __uint_as_float(__float_as_uint(best[p]) & ~63u);
+              if (sv < bv) { best[p] = seg_best[p]; bg[p] = tile >> 4; }
+              seg_best[p] = 3.0e38f;
+            }
           }
         }
       }
     }
-  }
+  };
+  if (ppo) chunk_loop(std::true_type{});
+  else chunk_loop(std::false_type{});
 
   float inert = 0.f;
   int changed = 0;
@@ -324,7 +372,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       if (vo < v || (vo == v && ko < k)) { v = vo; k = ko; }
     }
     // this point's seed offset (0 for f32)
-    const float offp = off;
+    const float offp = ppo ? opt[(wid * 16 + r) * C::PP + p] : off;
     if ((p & 3) == g) {
       const int64_t i = pbase + p * 16 + r;
       if (a.split_keys) {
@@ -412,7 +460,8 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   if (a.Kpad % (16 * C::CT) != 0) return hipErrorInvalidValue;
   const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
-  const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW;  // + offset / slot scratch
+  // + min/max / slot scratch + per-point offsets
+  const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW + C::OPT_BYTES;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {

@@ -300,17 +300,27 @@ void row_sqnorm(const Tensor& X, const Tensor& out) {
 }
 
 // out: int32 [D] zero-filled by the caller; receives max |x[:, d]| as float bit patterns.
-void col_absmax(const Tensor& X, const Tensor& out, const c10::optional<Tensor>& sumsq) {
+// Optional column statistics (all three or none): sumabs f64 [D] and nnz int64 [D]
+// zero-filled, lowbit int32 [D] filled with INT_MAX.
+void col_absmax(const Tensor& X, const Tensor& out, const c10::optional<Tensor>& sumabs,
+                const c10::optional<Tensor>& nnz, const c10::optional<Tensor>& lowbit) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   check_cuda(out, "out");
   TORCH_CHECK(out.scalar_type() == at::kInt && out.is_contiguous() && out.numel() == X.size(1),
               "mikmeans: col_absmax out must be int32 [D]");
   TORCH_CHECK(X.size(1) / vec_of(dt) <= 64, "mikmeans: col_absmax supports D <= 64 16-B pieces");
-  if (sumsq.has_value()) check_f64(*sumsq, "sumsq", X.size(1));
+  TORCH_CHECK(sumabs.has_value() == nnz.has_value() && sumabs.has_value() == lowbit.has_value(),
+              "mikmeans: col_absmax statistics come together (sumabs, nnz, lowbit)");
+  if (sumabs.has_value()) {
+    check_f64(*sumabs, "sumabs", X.size(1));
+    check_i64(*nnz, "nnz", X.size(1));
+    check_i32(*lowbit, "lowbit", X.size(1));
+  }
   hip_check(mk::launch_col_absmax(dt, X.data_ptr(), X.size(0), (int)X.size(1), ldx,
                                   reinterpret_cast<uint32_t*>(out.data_ptr<int32_t>()), stream(),
-                                  opt_ptr<double>(sumsq)),
+                                  opt_ptr<double>(sumabs), opt_ptr<unsigned long long>(nnz),
+                                  opt_ptr<int>(lowbit)),
             "col_absmax");
 }
 
@@ -454,8 +464,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("reduce_delta", &reduce_delta, "slab reduction into running totals + packed message");
   m.def("finalize", &finalize, "new centroids, shift, fragment re-pack (K4)");
   m.def("row_sqnorm", &row_sqnorm, "row squared norms (K1)");
-  m.def("col_absmax", &col_absmax, "per-column max |x| as f32 bit patterns (+ optional f64 sum |x|; fixed-point scales)",
-        py::arg("X"), py::arg("out"), py::arg("sumabs") = py::none());
+  m.def("col_absmax", &col_absmax,
+        "per-column max |x| as f32 bit patterns (+ optional sum |x|, nonzero count, lowest-bit exponent)",
+        py::arg("X"), py::arg("out"), py::arg("sumabs") = py::none(), py::arg("nnz") = py::none(),
+        py::arg("lowbit") = py::none());
   m.def("kpp_d2", &kpp_d2, "k-means++ D^2 update (K5; triangle-inequality pruned with owner/cc)",
         py::arg("X"), py::arg("c"), py::arg("first"), py::arg("d2"), py::arg("block_sums"),
         py::arg("rows_per_block"), py::arg("owner") = py::none(), py::arg("cc") = py::none(),

@@ -143,28 +143,48 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
 // per row (power of two >= the row's 16-byte pieces, <= 64), 256/L rows per pass, four
 // independent row loads in flight per lane; |x| compared as bit patterns (non-negative
 // floats order like unsigned integers, and a NaN's pattern exceeds +inf's, so NaN
-// propagates like torch.aminmax).  One global atomicMax per (block, column).  SQ: also
-// the per-column sum of |x| (f32 per lane, one f64 atomicAdd per (block, column)), from
-// which the engine flags wide-range columns (max >> mean |x|) for the residual pass.
-template <typename T, bool SQ>
+// propagates like torch.aminmax).  One global atomicMax per (block, column).  STATS: also,
+// per column, the sum of |x| (f32 per lane, one f64 atomicAdd per (block, column)), the
+// count of nonzero values and the exponent of the lowest set bit over all nonzero finite
+// values (x is an integer multiple of 2^lowbit).  From these the engine flags wide-range
+// columns for the residual M-step pass: a column whose values all sit on the hi pass's
+// grid (lowbit >= -col_exp: one-hot, small integers, coarse bf16) never needs it, and
+// otherwise the max is compared with the mean of the NONZERO |x| (sparse columns stay
+// single-pass).
+__device__ __forceinline__ int lowbit_exp(float f) {
+  const uint32_t b = __float_as_uint(f) & 0x7fffffffu;
+  const uint32_t e = b >> 23, m = b & 0x7fffffu;
+  if (b == 0u || e == 255u) return 1 << 30;            // zero / inf / NaN: no constraint
+  return e == 0u ? -149 + (int)__builtin_ctz(m) : (int)e - 150 + (int)__builtin_ctz(m | 0x800000u);
+}
+
+template <typename T, bool STATS>
 __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X, int64_t N, int NP,
                                                          int L, int64_t ldx, uint32_t* __restrict__ out,
-                                                         double* __restrict__ sumsq) {
+                                                         double* __restrict__ sumabs,
+                                                         unsigned long long* __restrict__ nnz,
+                                                         int* __restrict__ lowbit) {
   constexpr int V = Elem<T>::V;
   const int p = threadIdx.x & (L - 1);
   const int R = 256 / L;
   const int64_t step = (int64_t)gridDim.x * R;
   uint32_t m[V];
   float q[V];
+  uint32_t nz[V];
+  int lb[V];
 #pragma unroll
-  for (int e = 0; e < V; ++e) { m[e] = 0u; q[e] = 0.f; }
+  for (int e = 0; e < V; ++e) { m[e] = 0u; q[e] = 0.f; nz[e] = 0u; lb[e] = 1 << 30; }
   auto take = [&](const u32x4& w) {
     float f[V];
     unpack16(w, f, (T*)nullptr);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       m[e] = max(m[e], __float_as_uint(f[e]) & 0x7fffffffu);
-      if constexpr (SQ) q[e] += fabsf(f[e]);
+      if constexpr (STATS) {
+        q[e] += fabsf(f[e]);
+        nz[e] += f[e] != 0.f;
+        lb[e] = min(lb[e], lowbit_exp(f[e]));
+      }
     }
   };
   if (p < NP) {
@@ -183,7 +203,11 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       m[e] = max(m[e], (uint32_t)__shfl_xor((int)m[e], o, 64));
-      if constexpr (SQ) q[e] += __shfl_xor(q[e], o, 64);
+      if constexpr (STATS) {
+        q[e] += __shfl_xor(q[e], o, 64);
+        nz[e] += (uint32_t)__shfl_xor((int)nz[e], o, 64);
+        lb[e] = min(lb[e], __shfl_xor(lb[e], o, 64));
+      }
     }
   __shared__ uint32_t red[4][64 * V];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -195,7 +219,7 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
     const uint32_t v = max(max(red[0][j], red[1][j]), max(red[2][j], red[3][j]));
     if (v) atomicMax(out + j, v);
   }
-  if constexpr (SQ) {
+  if constexpr (STATS) {
     __syncthreads();
     float* rf = (float*)&red[0][0];
     if (lane < L)
@@ -204,16 +228,37 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
     __syncthreads();
     for (int j = threadIdx.x; j < NP * V; j += 256) {
       const double v = (double)rf[j] + rf[64 * V + j] + rf[128 * V + j] + rf[192 * V + j];
-      if (v != 0.0) atomicAdd(sumsq + j, v);
+      if (v != 0.0) atomicAdd(sumabs + j, v);
+    }
+    __syncthreads();
+    if (lane < L)
+#pragma unroll
+      for (int e = 0; e < V; ++e) red[wv][lane * V + e] = nz[e];
+    __syncthreads();
+    for (int j = threadIdx.x; j < NP * V; j += 256) {
+      const unsigned long long c = (unsigned long long)red[0][j] + red[1][j] + red[2][j] + red[3][j];
+      if (c) atomicAdd(nnz + j, c);
+    }
+    __syncthreads();
+    int* ri = (int*)&red[0][0];
+    if (lane < L)
+#pragma unroll
+      for (int e = 0; e < V; ++e) ri[wv * 64 * V + lane * V + e] = lb[e];
+    __syncthreads();
+    for (int j = threadIdx.x; j < NP * V; j += 256) {
+      const int v = min(min(ri[j], ri[64 * V + j]), min(ri[128 * V + j], ri[192 * V + j]));
+      if (v < (1 << 30)) atomicMin(lowbit + j, v);
     }
   }
 }
 
 hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
-                             hipStream_t s, double* sumsq) {
+                             hipStream_t s, double* sumabs, unsigned long long* nnz, int* lowbit) {
   const int V = dtype == DT_BF16 ? 8 : 4;
   const int NP = D / V;
   if (N <= 0 || D % V || NP > 64 || NP < 1) return N <= 0 ? hipSuccess : hipErrorInvalidValue;
+  if ((sumabs != nullptr) != (nnz != nullptr) || (sumabs != nullptr) != (lowbit != nullptr))
+    return hipErrorInvalidValue;  // the statistics come together
   int L = 1;
   while (L < NP) L *= 2;
   const int R = 256 / L;
@@ -221,11 +266,11 @@ hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t
   if (nb > 2048) nb = 2048;  // 8 per CU; each streams its rows with 4 loads in flight per lane
   const dim3 g((unsigned)nb), b(256);
   if (dtype == DT_BF16) {
-    if (sumsq) hipLaunchKernelGGL((col_absmax_kernel<uint16_t, true>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, sumsq);
-    else hipLaunchKernelGGL((col_absmax_kernel<uint16_t, false>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, sumsq);
+    if (sumabs) hipLaunchKernelGGL((col_absmax_kernel<uint16_t, true>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, sumabs, nnz, lowbit);
+    else hipLaunchKernelGGL((col_absmax_kernel<uint16_t, false>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, sumabs, nnz, lowbit);
   } else {
-    if (sumsq) hipLaunchKernelGGL((col_absmax_kernel<float, true>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, sumsq);
-    else hipLaunchKernelGGL((col_absmax_kernel<float, false>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, sumsq);
+    if (sumabs) hipLaunchKernelGGL((col_absmax_kernel<float, true>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, sumabs, nnz, lowbit);
+    else hipLaunchKernelGGL((col_absmax_kernel<float, false>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, sumabs, nnz, lowbit);
   }
   return hipGetLastError();
 }

@@ -114,8 +114,12 @@ struct FinalizeArgs {
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 
 // ---- row squared norms -------------------------------------------------------
+// Per-column max |x| (as f32 bit patterns, atomicMax into a zeroed out[D]); optionally, all
+// together, sum |x| (f64, zeroed), nonzero count (u64, zeroed) and the lowest set bit's
+// exponent over nonzero finite values (int, initialised to INT_MAX by the caller).
 hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
-                             hipStream_t s, double* sumsq = nullptr);
+                             hipStream_t s, double* sumabs = nullptr, unsigned long long* nnz = nullptr,
+                             int* lowbit = nullptr);
 hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t ldx, float* out,
                              hipStream_t s);
 

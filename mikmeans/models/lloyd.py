@@ -134,13 +134,18 @@ class LloydEngine:
         dev = self.device
         self.pk = CentroidPack(self.K, self.Dp, self.dtype, dev)
         self.slots = torch.zeros(C.NSLOT * C.SLOT_STRIDE, dtype=torch.float64, device=dev)
-        if self.segments > 1 and self.n >= 2 * self.segments:
-            # Overlapped M-step: segment s is scattered on a side stream while the
-            # matrix cores assign segment s+1.  Narrow slices keep the update's LDS
-            # small enough to share a CU with assign workgroups.
-            from ..parallel.shard import shard_range
+        from ..parallel.shard import shard_range
 
-            self.seg_ranges = [shard_range(self.n, s, self.segments) for s in range(self.segments)]
+        # Overlapped M-step: segment s is scattered on a side stream while the matrix
+        # cores assign segment s+1.  Narrow slices keep the update's LDS small enough to
+        # share a CU with assign workgroups.  Segments fall on the 1536-row grid, so a
+        # small shard leaves some empty: they are dropped (the reduce would otherwise sum
+        # their never-written slab chunks).
+        segs = [sr for sr in (shard_range(self.n, s, self.segments) for s in range(self.segments))
+                if sr[1] > sr[0]] if self.segments > 1 else []
+        if len(segs) > 1:
+            self.seg_ranges = segs
+            self.segments = len(segs)
             C.set_update_max_sw(self.overlap_sw)
             seg_rows = max(e - s for s, e in self.seg_ranges)
             self.seg_chunks = C.update_n_chunks(self.dt, self.K, self.Dp, seg_rows, self.weights is not None)

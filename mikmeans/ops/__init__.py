@@ -164,33 +164,72 @@ def _native_colstats_ok(X: torch.Tensor) -> bool:
 
 def col_max_abs(X: torch.Tensor) -> torch.Tensor:
     """Per-column max |x| as float64 ``[D]`` (no |X| temporary)."""
-    return col_stats(X, sumsq=False)[0]
+    return col_stats(X, stats=False).absmax
 
 
-def col_stats(X: torch.Tensor, sumsq: bool = True):
-    """``(max |x|, sum |x|)`` per column as float64 ``[D]`` tensors (the second is None
-    unless ``sumsq``): one streaming pass on the GPU (csrc/finalize.hip col_absmax)."""
+class ColStats:
+    """Per-column statistics of one streaming pass (csrc/finalize.hip col_absmax):
+    ``absmax`` (f64 [D]); with ``stats``: ``sumabs`` (f64), ``nnz`` (int64, nonzero
+    values) and ``lowbit`` (int32: every value is an integer multiple of 2^lowbit; a large
+    sentinel for an all-zero column)."""
+
+    LOWBIT_NONE = 2**31 - 1
+
+    def __init__(self, absmax, sumabs=None, nnz=None, lowbit=None):
+        self.absmax, self.sumabs, self.nnz, self.lowbit = absmax, sumabs, nnz, lowbit
+
+
+def _lowbit_torch(Xb: torch.Tensor) -> torch.Tensor:
+    """Exponent of the lowest set bit of each nonzero finite value (f32 semantics)."""
+    b = Xb.to(torch.float32).contiguous().view(torch.int32).long() & 0x7FFFFFFF
+    e = b >> 23
+    m = b & 0x7FFFFF
+    sig = torch.where(e == 0, m, m | 0x800000)
+    tz = ((sig & -sig).double().log2()).long()
+    lb = torch.where(e == 0, -149 + tz, e - 150 + tz)
+    return torch.where((b == 0) | (e == 255), torch.full_like(lb, ColStats.LOWBIT_NONE), lb)
+
+
+def col_stats(X: torch.Tensor, stats: bool = True) -> ColStats:
+    """One pass over ``X``: per-column max |x| and, with ``stats``, sum |x|, the nonzero
+    count and the lowest-bit exponent (native kernel on the GPU; torch elsewhere)."""
+    D = X.shape[1]
     if X.shape[0] == 0:
-        z = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
-        return z, (z.clone() if sumsq else None)
+        z = torch.zeros(D, dtype=torch.float64, device=X.device)
+        if not stats:
+            return ColStats(z)
+        return ColStats(z, z.clone(), torch.zeros(D, dtype=torch.int64, device=X.device),
+                        torch.full((D,), ColStats.LOWBIT_NONE, dtype=torch.int32, device=X.device))
     if _native_colstats_ok(X):
-        out = torch.zeros(X.shape[1], dtype=torch.int32, device=X.device)
-        ss = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device) if sumsq else None
-        require().col_absmax(X, out, ss)
-        return out.view(torch.float32).double(), ss
+        out = torch.zeros(D, dtype=torch.int32, device=X.device)
+        if not stats:
+            require().col_absmax(X, out)
+            return ColStats(out.view(torch.float32).double())
+        sa = torch.zeros(D, dtype=torch.float64, device=X.device)
+        nz = torch.zeros(D, dtype=torch.int64, device=X.device)
+        lb = torch.full((D,), ColStats.LOWBIT_NONE, dtype=torch.int32, device=X.device)
+        require().col_absmax(X, out, sa, nz, lb)
+        return ColStats(out.view(torch.float32).double(), sa, nz, lb)
     mn, mx = torch.aminmax(X, dim=0)
     m = torch.maximum(mn.double().abs(), mx.double().abs())
-    ss = None
-    if sumsq:
-        ss = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
-        for i in range(0, X.shape[0], 1 << 20):
-            ss += X[i : i + (1 << 20)].to(torch.float64).abs().sum(0)
-    return m, ss
+    if not stats:
+        return ColStats(m)
+    sa = torch.zeros(D, dtype=torch.float64, device=X.device)
+    nz = torch.zeros(D, dtype=torch.int64, device=X.device)
+    lb = torch.full((D,), ColStats.LOWBIT_NONE, dtype=torch.int64, device=X.device)
+    for i in range(0, X.shape[0], 1 << 18):
+        xb = X[i : i + (1 << 18)]
+        sa += xb.to(torch.float64).abs().sum(0)
+        nz += (xb != 0).sum(0)
+        lb = torch.minimum(lb, _lowbit_torch(xb).amin(0))
+    return ColStats(m, sa, nz, lb.to(torch.int32))
 
 
-# A column whose max |x| exceeds WIDE_RATIO x its mean |x| gets the residual (lo) M-step pass:
-# its contributions are then exact to 2^-41 (not 2^-21) of the column maximum, so one
-# outlier no longer coarsens every other point's contribution (csrc/update.hip UPD_RESID).
+# A column whose values do not all sit on the hi pass's grid (2^-col_exp) and whose max |x|
+# exceeds WIDE_RATIO x the mean of its NONZERO |x| gets the residual (lo) M-step pass: its
+# contributions are then exact to 2^-41 (not 2^-21) of the column maximum, so one outlier no
+# longer coarsens every other point's contribution (csrc/update.hip UPD_RESID).  Columns the
+# hi grid represents exactly (one-hot, small integers) and sparse columns never need it.
 WIDE_RATIO = 256.0
 
 
@@ -228,33 +267,50 @@ class MStepScales:
 
 
 def mstep_scales(X: torch.Tensor, weights: torch.Tensor | None = None, comm=None, bound=None,
-                 n_global: int | None = None, wide_ratio: float | None = None) -> MStepScales:
-    """Scales of the fixed-point M-step (global over ranks) and the wide-range columns."""
+                 n_global: int | None = None, wide_ratio: float | None = None,
+                 stats: ColStats | None = None) -> MStepScales:
+    """Scales of the fixed-point M-step (global over ranks) and the wide-range columns.
+    ``stats``: this rank's column statistics when already computed (streamed shards)."""
     C = require()
     ratio = WIDE_RATIO if wide_ratio is None else float(wide_ratio)
-    want_ss = bound is None and ratio > 0
+    want = bound is None and ratio > 0
+    st = None
     if bound is None:
-        m, ss = col_stats(X, sumsq=want_ss)
+        st = stats if stats is not None else col_stats(X, stats=want)
+        m = st.absmax.to(device=X.device, dtype=torch.float64).clone()
     else:
-        m, ss = bound.to(device=X.device, dtype=torch.float64), None
+        m = bound.to(device=X.device, dtype=torch.float64)
     wm = torch.zeros(1, dtype=torch.float64, device=X.device)
     if weights is not None and weights.numel():
         wm[0] = max_abs(weights)
+    want = want and st is not None and st.sumabs is not None
+    if want:
+        sa = st.sumabs.to(device=X.device, dtype=torch.float64).clone()
+        nz = st.nnz.to(device=X.device, dtype=torch.float64)
+        lb = st.lowbit.to(device=X.device, dtype=torch.float64)
     if comm is not None:
         comm.allreduce_max_(m)
         comm.allreduce_max_(wm)
-        if ss is not None:
-            comm.allreduce_(ss)
+        if want:
+            comm.allreduce_(sa)
+            comm.allreduce_(nz)
+            lb = -lb
+            comm.allreduce_max_(lb)        # global min of the lowest-bit exponents
+            lb = -lb
     w = float(wm.item()) if weights is not None else 1.0
     mh = m.cpu()
     exps = [C.fixed_exp(v * w) for v in mh.tolist()]
     col_exp = torch.tensor(exps, dtype=torch.int32, device=X.device)
     wide = []
-    if ss is not None:
-        n = n_global if n_global is not None else X.shape[0]
-        mean_abs = ss.cpu() / max(int(n), 1)
-        wide = [d for d in range(len(exps)) if mh[d] > 0 and mh[d] > ratio * mean_abs[d]
-                and exps[d] + 20 <= 126]  # the lo scale must stay a normal float
+    if want:
+        mean_nz = (sa / nz.clamp_min(1)).cpu()
+        lbh = lb.cpu()
+        for d in range(len(exps)):
+            # weighted contributions x*w are never assumed to sit on the grid
+            exact = weights is None and lbh[d] + exps[d] >= 0
+            if (mh[d] > 0 and not exact and mh[d] > ratio * mean_nz[d]
+                    and exps[d] + 20 <= 126):  # the lo scale must stay a normal float
+                wide.append(d)
     return MStepScales(col_exp, C.fixed_exp(w) if weights is not None else 0, wide, X.device)
 
 

@@ -59,7 +59,7 @@ def main():
     res["reduce"] = timed(lambda: C.reduce(eng.slab, eng.cnt_slab, eng.n_chunks, eng.K, eng.Dp, eng.slots,
                                            eng.packed, eng.col_exp, eng.cnt_exp), a.reps)
     from mikmeans.ops import col_stats
-    res["col_absmax"] = timed(lambda: col_stats(eng.X, sumsq=False), a.reps)   # streaming-read reference
+    res["col_absmax"] = timed(lambda: col_stats(eng.X, stats=False), a.reps)   # streaming-read reference
     if a.slice_probe and a.d == 128:
         # EXPERIMENT: the same bytes as contiguous 64-B "rows" (what a slice-blocked layout of
         # X would give the M-step): X viewed as [4n, 32], random labels

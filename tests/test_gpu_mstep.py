@@ -205,3 +205,51 @@ def test_cluster_sums_ksplit_other_widths_vs_f64(native, dtype, d, k):
     m = c_ref > 0
     err = ((sums.cpu().double()[m] - s_ref[m]) / c_ref[m][:, None]).abs() / colmax
     assert err.max().item() <= 2.0**-19, err.max().item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_col_stats_native_matches_torch(native, dtype):
+    """Native column statistics (max |x|, sum |x|, nonzero count, lowest-bit exponent)
+    against the torch reference path of the same pass, subnormals and zero columns too."""
+    n, d = 50_001, 64
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(n, d, generator=g) * torch.logspace(-3, 3, d)
+    X[:, 5] = 0.0                                           # all-zero column
+    X[:, 6] = (torch.rand(n, generator=g) < 0.01).float()  # one-hot-like
+    X[::7, 7] = 0.0
+    X[3, 8] = 1e-40                                         # f32 subnormal (bf16 keeps it too)
+    X = X.to(dtype)
+    st = ops.col_stats(X.to(DEV))
+    ref = ops.col_stats(X)                                  # CPU: the torch implementation
+    assert torch.equal(st.absmax.cpu(), ref.absmax)
+    assert torch.equal(st.nnz.cpu(), ref.nnz)
+    assert torch.equal(st.lowbit.cpu(), ref.lowbit)
+    torch.testing.assert_close(st.sumabs.cpu(), ref.sumabs, rtol=1e-5, atol=0)
+    assert int(st.nnz[5]) == 0 and int(st.lowbit[5]) == ops.ColStats.LOWBIT_NONE
+    assert int(st.lowbit[6]) == 0
+
+
+def test_sparse_and_grid_exact_columns_stay_single_pass(native):
+    """One-hot columns, sparse continuous columns and small-integer columns with a huge
+    value are exact on the hi grid or have a nonzero mean near their max: no residual
+    pass (and the incremental M-step stays on).  A dense column with one outlier still
+    gets it."""
+    from mikmeans.models.lloyd import LloydEngine
+
+    n, d, K = 200_000, 32, 8
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(n, d, generator=g)
+    hot = torch.randint(0, 1000, (n,), generator=g)
+    X[:, 0] = (hot == 0).float()                          # one-hot, 0.1 % nonzero
+    X[:, 1] = (hot == 1).float() * 3.0
+    sp = torch.rand(n, generator=g) < 0.002
+    X[:, 2] = torch.where(sp, torch.randn(n, generator=g) * 2.0, torch.zeros(n))  # sparse continuous
+    X[:, 3] = torch.randint(0, 4, (n,), generator=g).float()
+    X[17, 3] = 10_000.0                                   # small integers + one huge integer
+    X[99, 9] = 4.0e5                                      # dense N(0,1) column with an outlier
+    sc = ops.mstep_scales(X.to(DEV), n_global=n)
+    assert sc.wide_cols.cpu().tolist() == [9]
+    Xs = X.clone()
+    Xs[99, 9] = 0.5
+    eng = LloydEngine(Xs.to(DEV), K, incremental=True).set_centers(Xs[:K])
+    assert eng.scales.nw == 0 and eng.delta is not None
