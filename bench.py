@@ -49,6 +49,10 @@ def main(argv=None):
     ap.add_argument("--points", "--n", dest="n", type=int, default=None, help="override total points")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--batch", type=int, default=1 << 24, help="cfg5 rows per rank per step")
+    ap.add_argument("--resident", action="store_true",
+                    help="cfg5: batches drawn on the device from an HBM-resident shard of stored rows")
+    ap.add_argument("--shard-rows", type=int, default=None,
+                    help="cfg5 --resident: rows per rank (default N/8: the W=8 shard of N=1e9, 64 GB)")
     ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=False,
                     help="cfg5: generate the next batch on a side stream while the current one is fitted "
                          "(measured no faster: profiles/r1_18_blobstream_prefetch_ab.json)")
@@ -245,33 +249,92 @@ def _phase_breakdown(eng) -> dict:
 
 
 def _bench_minibatch(args, cfg, comm, dtype):
-    from mikmeans.data.blobs import BlobStream
+    """cfg5: mini-batch k-means, D=256, K=512, 2^24 rows per rank per step.
+
+    Default: every batch is a fresh slice of the N=1e9-row blob dataset generated on the
+    device (the stream covers distinct rows).  ``--resident``: every rank holds its shard of
+    a stored dataset in HBM (``--shard-rows``, default the W=8 shard of N=1e9: 1.25e8 rows,
+    64 GB -- at W<8 a rehearsal of one W=8 rank) and each step draws its batch on the device
+    (Philox keyed by (seed, rank, step), csrc/rows.hip).  Both report the whole step's
+    points/s and, split by device events inside the timed steps, ``gen_ms`` (generating /
+    gathering the batch) and ``kmeans_ms`` (assign + M-step + reduce + all-reduce + finalize)."""
+    from mikmeans.data.blobs import BlobStream, blob_centers, make_blobs
     from mikmeans.models.init import init_random
     from mikmeans.models.minibatch import MiniBatchEngine
+    from mikmeans.ops import col_stats, native
+    from mikmeans.parallel import memplan
 
     N, D, K = cfg["n"], cfg["d"], cfg["k"]
     b = args.batch
-    stream = BlobStream(N, D, K, b, seed=args.seed, dtype=dtype, device=comm.device, rank=comm.rank,
-                        world=comm.world, with_norms=True,  # row norms fused into the generator
-                        prefetch=args.prefetch)  # batch j+1 generated on a side stream during step j
-    # the generator's value bound fixes the fixed-point scales up front (no per-step clamp check)
-    eng = MiniBatchEngine(K, D, b, dtype=dtype, device=comm.device, comm=comm, value_bound=stream.value_bound)
-    first = next(stream)
+    dev = comm.device
+    extra = {"batch_per_rank": b}
+    if args.resident:
+        S = args.shard_rows or -(-N // 8)
+        plan = memplan.plan_minibatch(S, D, K, dtype, batch_rows=b, resident=True)
+        plan.budget = memplan.hbm_budget(dev)
+        extra["memory_plan"] = {"mode": plan.mode, "peak_GB": round(plan.peak / 1e9, 3),
+                                "budget_GB": round(plan.budget / 1e9, 3), "shard_rows": S}
+        if not plan.fits:
+            raise SystemExit(f"[bench] resident shard does not fit: {plan.summary()}")
+        centers = blob_centers(K, D, 10.0, args.seed, device=dev)
+        X = torch.empty((S, D), dtype=dtype, device=dev)
+        step_rows = 1 << 24
+        for i in range(0, S, step_rows):   # rank r holds global rows [r*S, (r+1)*S)
+            make_blobs(min(step_rows, S - i), D, K, seed=args.seed, i0=comm.rank * S + i, dtype=dtype,
+                       device=dev, centers=centers, out=X[i : i + step_rows])
+        C = native.require()
+        buf = torch.empty((b, D), dtype=dtype, device=dev)
+        xn = torch.empty(b, dtype=torch.float32, device=dev)
+        eng = MiniBatchEngine(K, D, b, dtype=dtype, device=dev, comm=comm)
+        eng.set_bound(col_stats(X, stats=False).absmax)
+        state = {"step": 0}
+
+        def gen():
+            C.sample_rows(X, buf, b, args.seed, comm.rank, state["step"], xn)
+            state["step"] += 1
+            return buf, xn
+        extra["data_bytes_per_rank"] = S * D * X.element_size()
+    else:
+        stream = BlobStream(N, D, K, b, seed=args.seed, dtype=dtype, device=dev, rank=comm.rank,
+                            world=comm.world, with_norms=True,  # row norms fused into the generator
+                            prefetch=args.prefetch)  # batch j+1 generated on a side stream during step j
+        # the generator's value bound fixes the fixed-point scales up front (no per-step clamp check)
+        eng = MiniBatchEngine(K, D, b, dtype=dtype, device=dev, comm=comm, value_bound=stream.value_bound)
+
+        def gen():
+            Xb = next(stream)
+            return Xb, stream.last_norms
+    first, _ = gen()
     eng.set_centers(init_random(first, D, K, b * comm.world, comm.rank * b, comm, args.seed))
     for _ in range(args.warmup):
-        eng.partial_fit(next(stream), stream.last_norms)
+        eng.partial_fit(*gen())
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.partial_fit(next(stream), stream.last_norms)  # includes on-device generation of the batch
+    for i in range(args.steps):
+        ev[i][0].record()
+        Xb, nb = gen()
+        ev[i][1].record()
+        eng.partial_fit(Xb, nb)
+        ev[i][2].record()
     torch.cuda.synchronize()
     comm.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=comm.device)
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     comm.allreduce_max_(el)
     elapsed = float(el.item())
+    gen_ms = sum(a.elapsed_time(m) for a, m, _ in ev) / args.steps
+    km_ms = sum(m.elapsed_time(z) for _, m, z in ev) / args.steps
+    t = torch.tensor([gen_ms, km_ms], dtype=torch.float64, device=dev)
+    comm.allreduce_max_(t)
+    gen_ms, km_ms = float(t[0]), float(t[1])
     pts = args.steps * b * comm.world
-    return pts / elapsed, elapsed * 1e3 / args.steps, {"batch_per_rank": b, "steps_cover_points": pts}
+    extra.update(mode="resident" if args.resident else "stream", steps_cover_points=pts,
+                 gen_ms=round(gen_ms, 4), kmeans_ms=round(km_ms, 4),
+                 kmeans_points_per_s=b * comm.world / (km_ms * 1e-3),
+                 batch_inertia=eng.last_batch_inertia())
+    return pts / elapsed, elapsed * 1e3 / args.steps, extra
 
 
 if __name__ == "__main__":

@@ -62,6 +62,47 @@ def _unit_rows(X: torch.Tensor, block: int = 1 << 22) -> torch.Tensor:
     return out
 
 
+def native_dpad(D: int, dtype) -> int:
+    """The MFMA kernels' padded width for D features (0: D > 256, PyTorch GEMM path)."""
+    from .ops import native
+
+    return native.dpad_for(pad_columns(torch.empty((0, D), dtype=dtype)).shape[1], dtype)
+
+
+def native_mod():
+    from .ops import native
+
+    return native.require()
+
+
+def _device_rows(X: torch.Tensor, device, dtype, gpu: bool, block_bytes: int = 1 << 28) -> torch.Tensor:
+    """``X`` on ``device`` in ``dtype`` -- column-padded to 16-byte rows for the GPU kernels --
+    built block by block, so no full-size temporary in another dtype ever exists on the
+    device (host blocks are converted on the host).  ``X`` itself when it already qualifies."""
+    if not gpu:
+        t = X.to(device=device)
+        return t if t.dtype == dtype else t.to(dtype)
+    if X.device == device and X.dtype == dtype:
+        P = pad_columns(X)
+        if P is X:
+            return X
+    n, D = X.shape
+    v = 8 if dtype == torch.bfloat16 else 4
+    Dp = -(-D // v) * v
+    out = torch.empty((n, Dp), dtype=dtype, device=device)
+    if Dp > D:
+        out[:, D:].zero_()
+    rows = max(1, block_bytes // max(1, D * max(X.element_size(), out.element_size())))
+    for i in range(0, n, rows):
+        out[i : i + rows, :D].copy_(X[i : i + rows])
+    return out
+
+
+def buf_empty(eng, device) -> torch.Tensor:
+    """A 0-row batch for a rank with an empty shard (it still joins every step's all-reduce)."""
+    return torch.zeros((0, eng.Dp), dtype=eng.dtype, device=device)
+
+
 def _shard_info(n_local: int, comm: Comm, device):
     sizes = comm.all_gather(torch.tensor([n_local], dtype=torch.int64, device=device)).reshape(-1).cpu()
     start = int(sizes[: comm.rank].sum())
@@ -91,11 +132,44 @@ class _Serving:
         return cached[2]
 
     def _inputs(self, X):
-        """X on the model's device and dtype; unit rows for the cosine metric."""
+        """X on the model's device and dtype; unit rows for the cosine metric (on the GPU by
+        the same kernel the fit normalised with)."""
         Xt, was_numpy = _to_tensor(X, self.cluster_centers_.device, self.dtype)
         if getattr(self, "metric", "euclidean") == "cosine":
-            Xt = _unit_rows(Xt)
+            if Xt.is_cuda and native_dpad(Xt.shape[1], Xt.dtype):
+                P = pad_columns(Xt)
+                if torch.is_tensor(X) and P.data_ptr() == X.data_ptr():
+                    P = P.clone()          # never normalise the caller's rows in place
+                native_mod().row_normalize(P)
+                Xt = P
+            else:
+                Xt = _unit_rows(Xt)
         return Xt, was_numpy
+
+    def _assign_rows(self, X, with_dist: bool):
+        """(labels, squared distances or None) of every row of X under the fitted centres.
+        Host rows bound for a GPU model go through in blocks of ~256 MB, so a shard larger
+        than HBM (a streamed fit's) is never copied to the device whole."""
+        from . import ops
+
+        dev = self.cluster_centers_.device
+        host = not (torch.is_tensor(X) and X.device == dev)
+        n = X.shape[0]
+        if dev.type != "cuda" or not host or n == 0:
+            Xt, was_numpy = self._inputs(X)
+            lab, mind = ops.assign(Xt, self.cluster_centers_, with_dist=with_dist, pack=self._serving_pack(Xt))
+            return lab, mind, was_numpy
+        was_numpy = not torch.is_tensor(X)
+        block = max(1, (1 << 28) // max(1, X.shape[1] * 4))
+        labels = torch.empty(n, dtype=torch.int32, device=dev)
+        mind = torch.empty(n, dtype=torch.float32, device=dev) if with_dist else None
+        for i in range(0, n, block):
+            Xt, _ = self._inputs(X[i : i + block])
+            lab, md = ops.assign(Xt, self.cluster_centers_, with_dist=with_dist, pack=self._serving_pack(Xt))
+            labels[i : i + block] = lab
+            if with_dist:
+                mind[i : i + block] = md
+        return labels, mind, was_numpy
 
     def transform(self, X):
         """Euclidean distances to every centre, ``[n, K]`` (float32; for the cosine
@@ -181,43 +255,119 @@ class KMeans(_Serving):
                             metric=self.metric)
 
     # ------------------------------------------------------------------- fit
+    def _memory_plan(self, X, comm, device, D, weighted):
+        """Resident or streamed (parallel/memplan.py), agreed by every rank: a rank whose
+        shard does not fit makes all of them stream (the init sample and its collectives
+        must match).  ``chunk_rows`` forces streaming with that chunk."""
+        from .parallel import memplan
+
+        n_local = int(X.shape[0])
+        es_src = X.element_size() if torch.is_tensor(X) else np.asarray(X).itemsize
+        x_dev = torch.is_tensor(X) and X.is_cuda
+        kw = dict(weighted=weighted, init=self.init, n_local_trials=self.n_local_trials,
+                  empty_policy=self.empty_cluster)
+        budget = memplan.hbm_budget(device)
+        if self.chunk_rows is not None and not x_dev:
+            plan = memplan.plan_streaming(n_local, D, self.n_clusters, self.dtype, chunk_rows=self.chunk_rows,
+                                          init_rows=self.init_size, src_itemsize=es_src, **kw)
+            plan.budget = budget
+        else:
+            try:
+                plan = memplan.plan_fit(n_local, D, self.n_clusters, self.dtype, budget=budget, x_on_device=x_dev,
+                                        incremental=self.incremental, init_rows=self.init_size,
+                                        src_itemsize=es_src, copy_x=not self._x_ready(X, device), **kw)
+                err = 0.0
+            except memplan.HBMCapacityError as e:
+                plan, err = e, 1.0
+            flags = torch.tensor([err, 1.0 if (err == 0.0 and plan.mode == "streaming") else 0.0],
+                                 dtype=torch.float64, device=comm.device)
+            comm.allreduce_max_(flags)
+            if flags[0].item() > 0:
+                raise plan if isinstance(plan, memplan.HBMCapacityError) else memplan.HBMCapacityError(
+                    "KMeans.fit: another rank's shard does not fit its HBM budget")
+            if flags[1].item() > 0 and plan.mode != "streaming":
+                if x_dev:
+                    raise memplan.HBMCapacityError("KMeans.fit: other ranks stream their shards; pass this "
+                                                   "rank's rows as a host tensor too")
+                plan = self._stream_plan(n_local, D, es_src, budget, kw)
+        if self.verbose and comm.rank == 0:
+            print(f"[mikmeans] memory plan: {plan.summary()}", flush=True)
+        return plan
+
+    def _stream_plan(self, n_local, D, es_src, budget, kw):
+        from .parallel import memplan
+
+        R = memplan.ROW_ALIGN
+        while R * 2 <= (1 << 24) and R < n_local:
+            R *= 2
+        while True:
+            pl = memplan.plan_streaming(n_local, D, self.n_clusters, self.dtype, chunk_rows=R,
+                                        init_rows=self.init_size, src_itemsize=es_src, **kw)
+            pl.budget = budget
+            if pl.fits or R <= memplan.ROW_ALIGN:
+                return pl
+            R //= 2
+
+    def _x_ready(self, X, device) -> bool:
+        """X is already the device tensor the resident engine computes on (no copy made)."""
+        if not (torch.is_tensor(X) and X.device == device and X.dtype == self.dtype) or self.metric == "cosine":
+            return False
+        return pad_columns(X[:0]).data_ptr() == X[:0].data_ptr() if X.shape[0] else True
+
     def fit(self, X, y=None, sample_weight=None, *, resume_from=None):
+        """Lloyd fit.  On a GPU the memory plan (``memory_plan_``) decides whether the shard
+        is copied into HBM or streamed from host memory chunk by chunk; both give the same
+        model from the same start (init 'random', an array, or a resumed checkpoint;
+        k-means++ seeds a streamed fit from an ``init_size``-row sample)."""
         comm = self.comm or get_comm()
         device = _default_device(self.device, X) if self.device is not None or comm.world == 1 else comm.device
-        streaming = self.chunk_rows is not None and device.type == "cuda"
-        Xt, was_numpy = _to_tensor(X, torch.device("cpu") if streaming else device, self.dtype)
-        self._numpy_io = was_numpy
-        if self.metric == "cosine":
-            if streaming:
-                raise NotImplementedError("metric='cosine' with chunk_rows (out-of-core) is not supported")
-            Xt = _unit_rows(Xt)
-        D = Xt.shape[1]
-        if Xt.is_cuda:
-            Xt = pad_columns(Xt)
-        n_global, start = _shard_info(Xt.shape[0], comm, device)
-        if n_global < self.n_clusters:
-            raise ValueError(f"n_samples={n_global} should be >= n_clusters={self.n_clusters}")
+        if not torch.is_tensor(X):
+            X = torch.from_numpy(np.ascontiguousarray(np.asarray(X, dtype=np.float32)
+                                                      if np.asarray(X).dtype not in (np.float32, np.float64)
+                                                      else np.asarray(X)))
+            self._numpy_io = True
+        else:
+            self._numpy_io = False
+        if X.dim() != 2:
+            raise ValueError(f"X must be 2-D [n_samples, n_features], got shape {tuple(X.shape)}")
+        D = int(X.shape[1])
         w = None
         if sample_weight is not None:
-            if streaming:
-                raise NotImplementedError("sample_weight with chunk_rows (out-of-core) is not supported")
             w = torch.as_tensor(np.asarray(sample_weight) if not torch.is_tensor(sample_weight)
-                                else sample_weight, dtype=torch.float32).to(device)
-        Xs = None
+                                else sample_weight, dtype=torch.float32)
+        gpu = device.type == "cuda" and native_dpad(D, self.dtype) != 0
+        self.memory_plan_ = None
+        streaming = False
+        if gpu:
+            plan = self._memory_plan(X, comm, device, D, w is not None)
+            self.memory_plan_ = plan.as_dict()
+            streaming = plan.mode == "streaming"
+        n_global, start = _shard_info(X.shape[0], comm, comm.device)
+        if n_global < self.n_clusters:
+            raise ValueError(f"n_samples={n_global} should be >= n_clusters={self.n_clusters}")
+        spherical = self.metric == "cosine"
         if streaming:
             from .models.streaming import StreamingLloydEngine
 
-            if self.empty_cluster != "keep":
-                raise NotImplementedError("chunk_rows (out-of-core) supports empty_cluster='keep' only")
-            sengine = StreamingLloydEngine(Xt, self.n_clusters, chunk_rows=self.chunk_rows, comm=comm,
-                                           device=device, frozen=self.frozen, n_features=D)
-            # init + tol scale on a device-resident sample of every rank's rows
-            m = self.init_size or max(20 * self.n_clusters, 1 << 16)
-            Xs = sengine.sample_rows(m, self.seed)
-            s_global, s_start = _shard_info(Xs.shape[0], comm, device)
-        tol_src = Xs if streaming else Xt
-        tol_abs = tol_to_abs(self.tol, tol_src[:, :D] if tol_src.shape[1] != D else tol_src, comm,
-                             s_global if streaming else n_global)
+            Xh = X if X.device.type == "cpu" else X.cpu()
+            sengine = StreamingLloydEngine(Xh, self.n_clusters, chunk_rows=plan.chunk_rows, comm=comm,
+                                           device=device, frozen=self.frozen, n_features=D, dtype=self.dtype,
+                                           sample_weight=w, empty_policy=self.empty_cluster, spherical=spherical)
+            tol_abs = tol_to_abs(self.tol, None, comm, n_global, D, stats=sengine.stats)
+            Xt = None
+        else:
+            Xt = _device_rows(X, device, self.dtype, gpu)
+            if spherical:
+                if gpu:
+                    if Xt is X:
+                        Xt = Xt.clone()
+                    from .ops import native as _nat
+
+                    _nat.require().row_normalize(Xt)
+                else:
+                    Xt = _unit_rows(Xt)
+            if w is not None:
+                w = w.to(device)
         best = None
         t0 = time.perf_counter()
         start_iter = 0
@@ -228,19 +378,19 @@ class KMeans(_Serving):
             else:
                 eng = LloydEngine(Xt, self.n_clusters, comm=comm, sample_weight=w, frozen=self.frozen,
                                   empty_policy=self.empty_cluster, n_features=D, incremental=self.incremental,
-                                  spherical=self.metric == "cosine")
+                                  spherical=spherical)
+                if trial == 0:
+                    stats = eng.stats if eng.gpu else None
+                    tol_abs = tol_to_abs(self.tol, Xt, comm, n_global, D, stats=stats)
             if resume_from is not None and trial == 0:
                 from .utils.checkpoint import load_checkpoint
 
                 ck = load_checkpoint(resume_from, comm=comm)
                 centers = ck["centers"].to(device)
                 start_iter = int(ck["iteration"])
-            elif streaming:
-                centers = resolve_init(self.init, Xs, D, self.n_clusters, s_global, s_start, comm,
-                                       self.seed + trial, self.n_local_trials)
             else:
-                centers = resolve_init(self.init, Xt, D, self.n_clusters, n_global, start, comm,
-                                       self.seed + trial, self.n_local_trials)
+                centers = self._init_centers(eng if streaming else Xt, streaming, D, n_global, start, comm,
+                                             trial)
             eng.set_centers(centers[:, :D])
             eng.iteration = start_iter
             hist = []
@@ -275,9 +425,15 @@ class KMeans(_Serving):
             if mlog is not None:
                 mlog.close()
             labels, mind = eng.assign(True)
-            wt = eng.weights.double() if eng.weights is not None else 1.0
-            inert = (mind.double() * wt).sum().reshape(1) if eng.n else torch.zeros(1, dtype=torch.float64,
-                                                                                    device=device)
+            inert = torch.zeros(1, dtype=torch.float64, device=comm.device)
+            if eng.n:
+                if eng.weights is not None and eng.gpu:
+                    native_mod().wdot(mind, eng.weights, inert)
+                elif eng.weights is not None:
+                    inert += (mind.double() * eng.weights.double()).sum().to(inert.device)
+                else:
+                    inert += mind.sum(dtype=torch.float64).to(inert.device)
+            del mind
             comm.allreduce_(inert)
             inertia = float(inert.item())
             if best is None or inertia < best[0]:
@@ -294,10 +450,33 @@ class KMeans(_Serving):
         self.history_ = hist
         self.n_features_in_ = D
         self.fit_time_s_ = time.perf_counter() - t0
-        cnt = torch.bincount(labels.long(), minlength=self.n_clusters).to(torch.float64)
+        cnt = torch.bincount(labels, minlength=self.n_clusters).to(torch.float64).to(comm.device)
         comm.allreduce_(cnt)
         self.counts_ = cnt.cpu()
         return self
+
+    def _init_centers(self, src, streaming: bool, D: int, n_global: int, start: int, comm, trial: int):
+        """Initial centres.  Streamed shards: 'random' draws its rows from the whole shard
+        (fetched from host memory, so the resident fit's rows), k-means++ runs on a
+        device-resident ``init_size``-row sample of every rank's rows."""
+        seed = self.seed + trial
+        if not streaming:
+            return resolve_init(self.init, src, D, self.n_clusters, n_global, start, comm, seed,
+                                self.n_local_trials)
+        name = self.init.lower().replace("_", "-") if isinstance(self.init, str) else None
+        if name == "random":
+            from .models.init import init_random
+
+            return init_random(None, D, self.n_clusters, n_global, start, comm, seed, fetch=src.fetch_rows,
+                               n_local=src.n)
+        if name is None:
+            return resolve_init(self.init, src.fetch_rows([]), D, self.n_clusters, n_global, start, comm,
+                                seed, self.n_local_trials)
+        m = self.init_size or max(20 * self.n_clusters, 1 << 16)
+        Xs = src.sample_rows(m, self.seed)
+        s_global, s_start = _shard_info(Xs.shape[0], comm, comm.device)
+        return resolve_init(self.init, Xs, D, self.n_clusters, s_global, s_start, comm, seed,
+                            self.n_local_trials)
 
     def fit_predict(self, X, y=None, sample_weight=None):
         return self.fit(X, sample_weight=sample_weight)._out(self.labels_)
@@ -321,26 +500,20 @@ class KMeans(_Serving):
         coordinates the label -1 ("unassigned", the reference's unassigned list,
         app.mjs:421-433); the M-step ignores such labels."""
         self._check_fitted()
-        from . import ops
-
-        Xt, was_numpy = self._inputs(X)
-        labels, _ = ops.assign(Xt, self.cluster_centers_, with_dist=False, pack=self._serving_pack(Xt))
+        labels, _, was_numpy = self._assign_rows(X, False)
         if unassign_nonfinite:
-            bad = ~torch.isfinite(Xt).all(dim=1)
+            Xt = torch.as_tensor(np.asarray(X) if not torch.is_tensor(X) else X)
+            bad = (~torch.isfinite(Xt).all(dim=1)).to(labels.device)
             labels = labels.masked_fill(bad, -1)
         return labels.cpu().numpy() if was_numpy else labels
 
     def score(self, X, sample_weight=None):
         """Negative inertia of ``X`` under the fitted centres."""
         self._check_fitted()
-        from . import ops
-
-        device = self.cluster_centers_.device
-        Xt, _ = self._inputs(X)
-        _, mind = ops.assign(Xt, self.cluster_centers_, with_dist=True, pack=self._serving_pack(Xt))
+        _, mind, _ = self._assign_rows(X, True)
         if sample_weight is not None:
-            mind = mind * torch.as_tensor(np.asarray(sample_weight), dtype=torch.float32, device=device)
-        return -float(mind.double().sum())
+            mind = mind * torch.as_tensor(np.asarray(sample_weight), dtype=torch.float32, device=mind.device)
+        return -float(mind.sum(dtype=torch.float64))
 
     # --------------------------------------------------------------- metrics
     def metrics(self) -> dict:
@@ -432,20 +605,67 @@ class MiniBatchKMeans(_Serving):
     def fit(self, X, *, resume_from=None, checkpoint_every: int = 0, checkpoint_dir=None):
         """Fit on a tensor/array (random batches each step; ``max_iter`` epochs).
 
-        The batch of step s on rank r is drawn from a generator keyed by (seed, r, s)
-        (:func:`_step_generator`), so the sampler's state is the step counter itself:
-        ``checkpoint_every`` saves centres, running counts, scales and the step, and
-        ``resume_from`` continues such a run with the same rows every later step draws --
-        bit for bit the uninterrupted fit on the same world size."""
+        Batch row j of step s on rank r is local row floor(u * n) for a Philox draw keyed by
+        (seed; j, s, r) (:mod:`mikmeans.data.sampler`), so the sampler's state is the step
+        counter itself: ``checkpoint_every`` saves centres, running counts, scales and the
+        step, and ``resume_from`` continues such a run with the rows every later step draws
+        -- bit for bit the uninterrupted fit on the same world size.
+
+        On a GPU the memory plan (``memory_plan_``, parallel/memplan.py) keeps the shard in
+        HBM when it fits and draws every batch on the device (csrc/rows.hip: one gather
+        kernel, no host work per step); a shard over the budget stays in host memory and its
+        batches (the same rows) are gathered on the host.  The fixed-point scales come from
+        the whole shard's column maxima, so no batch can saturate them and steps never
+        synchronise with the host (the ``tol`` check reads the shift every 10 steps)."""
+        from .data.sampler import sample_indices
+        from .ops import col_stats
+        from .parallel import memplan
         from .utils import faults
         from .utils.checkpoint import load_checkpoint
 
         comm = self.comm or get_comm()
         device = _default_device(self.device, X) if self.device is not None or comm.world == 1 else comm.device
-        Xt, was_numpy = _to_tensor(X, device, self.dtype)
-        self._numpy_io = was_numpy
-        n, D = Xt.shape
+        if not torch.is_tensor(X):
+            a = np.asarray(X)
+            X = torch.from_numpy(np.ascontiguousarray(a if a.dtype in (np.float32, np.float64)
+                                                      else a.astype(np.float32)))
+            self._numpy_io = True
+        else:
+            self._numpy_io = False
+        n, D = int(X.shape[0]), int(X.shape[1])
+        gpu = device.type == "cuda" and native_dpad(D, self.dtype) != 0
+        b = min(self.batch_size, n) if n else 0
+        self.memory_plan_ = None
+        resident = True
+        if gpu:
+            plan = memplan.plan_minibatch(n, D, self.n_clusters, self.dtype, batch_rows=self.batch_size,
+                                          resident=True, init_rows=self.init_size)
+            plan.budget = memplan.hbm_budget(device)
+            if not plan.fits and not X.is_cuda:
+                plan = memplan.plan_minibatch(n, D, self.n_clusters, self.dtype, batch_rows=self.batch_size,
+                                              resident=False, init_rows=self.init_size)
+                plan.budget = memplan.hbm_budget(device)
+                resident = False
+            if not plan.fits:
+                raise memplan.HBMCapacityError(f"MiniBatchKMeans.fit: {plan.summary()} does not fit; "
+                                               "use a smaller batch_size or more ranks")
+            self.memory_plan_ = plan.as_dict()
+        if not gpu or resident:
+            Xt = _device_rows(X, device, self.dtype, gpu)
+            Xh = None
+        else:
+            Xt, Xh = None, (X if X.device.type == "cpu" else X.cpu())
         eng = self._engine(D, device)
+        if eng.gpu:
+            # per-column bound of the whole shard (in the compute dtype): fixed scales, never exceeded
+            if Xt is not None:
+                bound = col_stats(Xt, stats=False).absmax
+            else:
+                bound = torch.zeros(D, dtype=torch.float64)
+                for i in range(0, n, 1 << 20):
+                    xb = Xh[i : i + (1 << 20)].to(self.dtype).float().abs()
+                    bound = torch.maximum(bound, xb.amax(0).double())
+            eng.set_bound(bound)
         if resume_from is not None:
             ck = load_checkpoint(resume_from, comm=comm)
             if ck.get("kind") != "minibatch" or int(ck["n_features"]) != D:
@@ -454,21 +674,36 @@ class MiniBatchKMeans(_Serving):
         else:
             g = _step_generator(self.seed, comm.rank, -1)
             init_n = min(n, self.init_size or max(3 * self.batch_size, 3 * self.n_clusters))
-            sample_idx = torch.randperm(n, generator=g)[:init_n].to(device)
-            eng.set_centers(self._init_centers(Xt[sample_idx]))
+            sample_idx = torch.randperm(n, generator=g)[:init_n]
+            sample = (Xt[sample_idx.to(Xt.device)] if Xt is not None
+                      else _device_rows(Xh[sample_idx], device, self.dtype, True))
+            eng.set_centers(self._init_centers(sample))
             eng.steps = 0
         # the step count must be the same on every rank (each step is a collective): derive
         # it from the global row count, never from this rank's shard size
-        n_global, _ = _shard_info(n, comm, device)
+        n_global, _ = _shard_info(n, comm, comm.device)
         steps = self.max_steps or max(1, math.ceil(self.max_iter * n_global / (self.batch_size * comm.world)))
+        buf = xn = None
+        if eng.gpu and b:
+            Dp = eng.Dp
+            buf = torch.zeros((b, Dp), dtype=self.dtype, device=device)
+            xn = torch.empty(b, dtype=torch.float32, device=device)
+        C = native_mod() if eng.gpu else None
         while eng.steps < steps:
             s = eng.steps
-            if n:
-                g = _step_generator(self.seed, comm.rank, s)
-                idx = torch.randint(0, n, (min(self.batch_size, n),), generator=g).to(device)
-                eng.partial_fit(Xt[idx])
+            if not n:
+                eng.partial_fit(X[:0].to(device) if not eng.gpu else buf_empty(eng, device))
+            elif eng.gpu and Xt is not None:
+                C.sample_rows(Xt, buf, b, self.seed, comm.rank, s, xn)       # on-device draw + gather
+                eng.partial_fit(buf, xn)
             else:
-                eng.partial_fit(Xt[:0])       # empty shard: still joins the step's all-reduce
+                idx = torch.from_numpy(sample_indices(n, b, self.seed, comm.rank, s))
+                if eng.gpu:
+                    buf[:, :D].copy_(Xh[idx].to(device, non_blocking=False))
+                    C.row_sqnorm(buf, xn)
+                    eng.partial_fit(buf, xn)
+                else:
+                    eng.partial_fit(Xt[idx])
             faults.maybe_fail(comm.rank, eng.steps)
             if checkpoint_every and checkpoint_dir and eng.steps % checkpoint_every == 0:
                 self._finish(eng)
@@ -477,7 +712,9 @@ class MiniBatchKMeans(_Serving):
                 if float(eng.shift.sum()) <= self.tol:
                     break
         self._finish(eng)
-        self.labels_ = self.predict(X)
+        self.labels_ = self.predict(Xt if Xt is not None else X)
+        if self._numpy_io and torch.is_tensor(self.labels_):
+            self.labels_ = self.labels_.cpu().numpy()
         return self
 
     def fit_stream(self, stream, steps: int, init_batch: torch.Tensor | None = None, *, resume_from=None,
@@ -489,7 +726,10 @@ class MiniBatchKMeans(_Serving):
         every that many steps, and ``resume_from`` continues such a run -- also on another
         world size: a stream with the same global batch (``batch * world``) then replays the
         same rows per step and the exact integer M-step gives the same centres (the
-        reference's export/import of the whole board, app.mjs:263-282).  A generic iterator
+        reference's export/import of the whole board, app.mjs:263-282).  Across world sizes
+        that holds up to near-ties of the bf16 assign: its key offset is shared by a
+        workgroup of rows, and which rows share one changes with the per-rank batch
+        (f32 data, and a resume on the same world size, are bitwise).  A generic iterator
         must itself be positioned at the checkpoint's ``stream_pos`` (BlobStream is seeked)."""
         from .utils import faults
         from .utils.checkpoint import load_checkpoint
@@ -508,8 +748,12 @@ class MiniBatchKMeans(_Serving):
             first = init_batch if init_batch is not None else next(iter(stream))
             eng = self._engine(first.shape[1], first.device)
             eng.set_centers(self._init_centers(first.to(self.dtype)))
-        if getattr(stream, "value_bound", None) is not None and eng.gpu and eng.col_exp is None:
-            eng.value_bound = float(stream.value_bound)   # bounded stream: no per-step clamp check
+        vb = getattr(stream, "value_bound", None)
+        if vb is not None and eng.gpu and (eng.col_exp is None or bool((eng.bound >= float(vb)).all())):
+            # bounded stream: no per-step clamp check (also after a resume, whose restored
+            # scales came from the same bound)
+            eng.value_bound = float(vb)
+            eng.bounded = True
         while eng.steps < steps:
             Xb = next(stream)
             eng.partial_fit(Xb, getattr(stream, "last_norms", None))
@@ -531,8 +775,8 @@ class MiniBatchKMeans(_Serving):
                "seed": self.seed, "tol": self.tol}
         extra = {"kind": "minibatch", "rescales": getattr(eng, "rescales", 0),
                  # the samplers are counter-based: (seed, rank, step) is the whole RNG state
-                 "rng": {"scheme": "fit: torch CPU generator per step seeded splitmix64(seed, rank, step); "
-                                   "streams: Philox4x32-10 by global row (BlobStream)",
+                 "rng": {"scheme": "fit: Philox4x32-10 row draws keyed by (seed; row, step, rank), "
+                                   "data/sampler.py; streams: Philox4x32-10 by global row (BlobStream)",
                          "seed": self.seed, "step": int(eng.steps)}}
         if stream_pos is not None:
             extra["stream_pos"] = int(stream_pos)
@@ -581,23 +825,17 @@ class MiniBatchKMeans(_Serving):
         self.counts_ = eng.vcount.clone()
 
     def predict(self, X):
-        from . import ops
-
         self._check_fitted()
-        Xt, was_numpy = _to_tensor(X, self.cluster_centers_.device, self.dtype)
-        labels, _ = ops.assign(Xt, self.cluster_centers_, with_dist=False, pack=self._serving_pack(Xt))
+        labels, _, was_numpy = self._assign_rows(X, False)
         return labels.cpu().numpy() if was_numpy else labels
 
     def fit_predict(self, X):
         return self.fit(X).predict(X)
 
     def score(self, X):
-        from . import ops
-
         self._check_fitted()
-        Xt, _ = _to_tensor(X, self.cluster_centers_.device, self.dtype)
-        _, mind = ops.assign(Xt, self.cluster_centers_, with_dist=True, pack=self._serving_pack(Xt))
-        return -float(mind.double().sum())
+        _, mind, _ = self._assign_rows(X, True)
+        return -float(mind.sum(dtype=torch.float64))
 
 
 # ------------------------------------------------------------------ functional

@@ -81,6 +81,9 @@ def cmd_fit(a) -> int:
         if hasattr(km, "inertia_"):
             rec.update(inertia=km.inertia_, n_iter=km.n_iter_, fit_time_s=round(km.fit_time_s_, 4),
                        metrics=km.metrics())
+        mp = getattr(km, "memory_plan_", None)
+        if mp:
+            rec["memory_plan"] = {k: mp[k] for k in ("mode", "peak", "budget", "chunk_rows", "batch_rows")}
         print(json.dumps(rec, default=str))
     if out is not None:
         km.save(out)   # safetensors + state.json + flat centroids.json (mini-batch: + running counts)
@@ -229,6 +232,41 @@ def cmd_bench(a, rest) -> int:
     return 0
 
 
+def cmd_plan(a) -> int:
+    """HBM plan of a fit (parallel/memplan.py) for N rows over W ranks: resident or
+    streamed, the chunk, every buffer's bytes.  Budget: --budget-gb, MIKMEANS_HBM_BYTES,
+    this GPU's free memory, or else an idle MI355X (98 % of 288 GB)."""
+    import os
+
+    from .parallel import memplan, shard_sizes
+
+    n_local = max(shard_sizes(a.n, a.world))
+    if a.budget_gb:
+        budget = int(a.budget_gb * 1e9)
+    elif os.environ.get("MIKMEANS_HBM_BYTES") or torch.cuda.is_available():
+        budget = memplan.hbm_budget()
+    else:
+        budget = int(memplan.HBM_BYTES * 0.98)
+    try:
+        if a.batch_size > 0:
+            pl = memplan.plan_minibatch(n_local, a.d, a.k, a.dtype, batch_rows=a.batch_size, resident=True)
+            pl.budget = budget
+            if not pl.fits:
+                pl = memplan.plan_minibatch(n_local, a.d, a.k, a.dtype, batch_rows=a.batch_size, resident=False)
+                pl.budget = budget
+        else:
+            pl = memplan.plan_fit(n_local, a.d, a.k, a.dtype, budget=budget, x_on_device=False,
+                                  incremental=not a.full_mstep, init=a.init)
+    except memplan.HBMCapacityError as e:
+        print(json.dumps({"error": str(e)}))
+        return 1
+    out = pl.as_dict()
+    out["summary"] = pl.summary()
+    out["world"] = a.world
+    print(json.dumps(out, indent=None if a.compact else 1))
+    return 0
+
+
 def cmd_info(a) -> int:
     from .ops import native
 
@@ -296,6 +334,17 @@ def build_parser():
     sub.add_parser("bench", help="headline benchmark (args forwarded to bench.py)", add_help=False)
     sub.add_parser("launch", help="N-rank job with restarts from the last checkpoint", add_help=False)
     sub.add_parser("info", help="environment / build info")
+    pl = sub.add_parser("plan", help="HBM plan of a fit: resident / streamed, chunk rows, buffer bytes")
+    pl.add_argument("--n", type=int, required=True, help="total rows (over all ranks)")
+    pl.add_argument("--d", type=int, required=True)
+    pl.add_argument("--k", type=int, required=True)
+    pl.add_argument("--world", type=int, default=1)
+    pl.add_argument("--dtype", default="bfloat16")
+    pl.add_argument("--init", default="k-means++")
+    pl.add_argument("--batch-size", type=int, default=0, help="> 0: plan a mini-batch fit")
+    pl.add_argument("--full-mstep", action="store_true", help="no incremental M-step buffers")
+    pl.add_argument("--budget-gb", type=float, default=None)
+    pl.add_argument("--compact", action="store_true")
     return ap
 
 
@@ -311,7 +360,7 @@ def main(argv=None) -> int:
         return cmd_launch(a, rest)
     a = build_parser().parse_args(argv)
     return {"fit": cmd_fit, "predict": cmd_predict, "blobs": cmd_blobs, "room": cmd_room,
-            "export": cmd_export, "import": cmd_import, "info": cmd_info}[a.cmd](a)
+            "export": cmd_export, "import": cmd_import, "info": cmd_info, "plan": cmd_plan}[a.cmd](a)
 
 
 if __name__ == "__main__":

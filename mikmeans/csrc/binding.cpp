@@ -300,9 +300,9 @@ void row_sqnorm(const Tensor& X, const Tensor& out) {
 }
 
 // out: int32 [D] zero-filled by the caller; receives max |x[:, d]| as float bit patterns.
-// Optional column statistics (all three or none): sumabs f64 [D] and nnz int64 [D]
-// zero-filled, lowbit int32 [D] filled with INT_MAX.
-void col_absmax(const Tensor& X, const Tensor& out, const c10::optional<Tensor>& sumabs,
+// Optional column statistics (all three or none): fstats f64 [3, D] (sum |x|, sum x,
+// sum x^2) and nnz int64 [D] zero-filled, lowbit int32 [D] filled with INT_MAX.
+void col_absmax(const Tensor& X, const Tensor& out, const c10::optional<Tensor>& fstats,
                 const c10::optional<Tensor>& nnz, const c10::optional<Tensor>& lowbit) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
@@ -310,18 +310,52 @@ void col_absmax(const Tensor& X, const Tensor& out, const c10::optional<Tensor>&
   TORCH_CHECK(out.scalar_type() == at::kInt && out.is_contiguous() && out.numel() == X.size(1),
               "mikmeans: col_absmax out must be int32 [D]");
   TORCH_CHECK(X.size(1) / vec_of(dt) <= 64, "mikmeans: col_absmax supports D <= 64 16-B pieces");
-  TORCH_CHECK(sumabs.has_value() == nnz.has_value() && sumabs.has_value() == lowbit.has_value(),
-              "mikmeans: col_absmax statistics come together (sumabs, nnz, lowbit)");
-  if (sumabs.has_value()) {
-    check_f64(*sumabs, "sumabs", X.size(1));
+  TORCH_CHECK(fstats.has_value() == nnz.has_value() && fstats.has_value() == lowbit.has_value(),
+              "mikmeans: col_absmax statistics come together (fstats, nnz, lowbit)");
+  if (fstats.has_value()) {
+    check_f64(*fstats, "fstats", 3 * X.size(1));
     check_i64(*nnz, "nnz", X.size(1));
     check_i32(*lowbit, "lowbit", X.size(1));
   }
   hip_check(mk::launch_col_absmax(dt, X.data_ptr(), X.size(0), (int)X.size(1), ldx,
                                   reinterpret_cast<uint32_t*>(out.data_ptr<int32_t>()), stream(),
-                                  opt_ptr<double>(sumabs), opt_ptr<unsigned long long>(nnz),
+                                  opt_ptr<double>(fstats), opt_ptr<unsigned long long>(nnz),
                                   opt_ptr<int>(lowbit)),
             "col_absmax");
+}
+
+// Mini-batch sampler (csrc/rows.hip): out[:b] = X[philox indices of (seed, rank, step)].
+void sample_rows(const Tensor& X, const Tensor& out, int64_t b, int64_t seed, int64_t rank, int64_t step,
+                 const c10::optional<Tensor>& xn, const c10::optional<Tensor>& idx_out) {
+  const int dt = dtype_of(X);
+  const int64_t ldx = check_points(X, dt);
+  const int64_t ldo = check_points(out, dt);
+  TORCH_CHECK(out.scalar_type() == X.scalar_type() && out.size(1) == X.size(1), "mikmeans: sample_rows out must match X");
+  TORCH_CHECK(b >= 0 && b <= out.size(0) && b < ((int64_t)1 << 32), "mikmeans: sample_rows batch out of range");
+  TORCH_CHECK(b == 0 || X.size(0) > 0, "mikmeans: sample_rows from an empty shard");
+  TORCH_CHECK(rank >= 0 && step >= 0 && step < ((int64_t)1 << 32), "mikmeans: sample_rows rank/step range");
+  if (xn.has_value()) check_f32(*xn, "xn", b);
+  if (idx_out.has_value()) check_i64(*idx_out, "idx_out", b);
+  hip_check(mk::launch_sample_rows(dt, X.data_ptr(), X.size(0), ldx, (int)X.size(1), out.data_ptr(), ldo, b,
+                                   (uint64_t)seed, (uint32_t)rank, (uint32_t)step, opt_ptr<float>(xn),
+                                   opt_ptr<int64_t>(idx_out), stream()),
+            "sample_rows");
+}
+
+void row_normalize(const Tensor& X, const c10::optional<Tensor>& xn) {
+  const int dt = dtype_of(X);
+  const int64_t ldx = check_points(X, dt);
+  if (xn.has_value()) check_f32(*xn, "xn", X.size(0));
+  hip_check(mk::launch_row_normalize(dt, X.data_ptr(), X.size(0), (int)X.size(1), ldx, opt_ptr<float>(xn), stream()),
+            "row_normalize");
+}
+
+void wdot(const Tensor& a, const Tensor& b, const Tensor& out) {
+  check_f32(a, "a");
+  check_f32(b, "b", a.numel());
+  check_f64(out, "out", 1);
+  hip_check(mk::launch_wdot(a.data_ptr<float>(), b.data_ptr<float>(), a.numel(), out.data_ptr<double>(), stream()),
+            "wdot");
 }
 
 void kpp_d2(const Tensor& X, const Tensor& c, bool first, const Tensor& d2, const Tensor& block_sums,
@@ -419,6 +453,21 @@ void blobs(const Tensor& X, int64_t i0, const Tensor& centers, double stddev, in
             "blobs");
 }
 
+// Page-lock a host tensor in place (out-of-core streaming: async H2D DMA straight from the
+// caller's rows, no pinned copy of a shard that may be hundreds of GB).  False when the
+// range was already registered / pinned.
+bool host_register(const Tensor& t) {
+  TORCH_CHECK(!t.is_cuda() && t.is_contiguous(), "mikmeans: host_register needs a contiguous CPU tensor");
+  if (t.nbytes() == 0) return false;
+  const hipError_t e = hipHostRegister(t.data_ptr(), t.nbytes(), hipHostRegisterDefault);
+  if (e == hipErrorHostMemoryAlreadyRegistered) { (void)hipGetLastError(); return false; }
+  hip_check(e, "hipHostRegister");
+  return true;
+}
+void host_unregister(const Tensor& t) {
+  hip_check(hipHostUnregister(t.data_ptr()), "hipHostUnregister");
+}
+
 std::string js_format(double v) {
   std::string s;
   mk::js_number(v, s);
@@ -466,8 +515,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("row_sqnorm", &row_sqnorm, "row squared norms (K1)");
   m.def("col_absmax", &col_absmax,
         "per-column max |x| as f32 bit patterns (+ optional sum |x|, nonzero count, lowest-bit exponent)",
-        py::arg("X"), py::arg("out"), py::arg("sumabs") = py::none(), py::arg("nnz") = py::none(),
+        py::arg("X"), py::arg("out"), py::arg("fstats") = py::none(), py::arg("nnz") = py::none(),
         py::arg("lowbit") = py::none());
+  m.def("sample_rows", &sample_rows, "mini-batch rows X[philox(seed; j, step, rank) * n] (+ norms, indices)",
+        py::arg("X"), py::arg("out"), py::arg("b"), py::arg("seed"), py::arg("rank"), py::arg("step"),
+        py::arg("xn") = py::none(), py::arg("idx_out") = py::none());
+  m.def("row_normalize", &row_normalize, "in-place unit rows (cosine metric)", py::arg("X"), py::arg("xn") = py::none());
+  m.def("wdot", &wdot, "out[0] += sum a*b in f64 (weighted inertia)");
   m.def("kpp_d2", &kpp_d2, "k-means++ D^2 update (K5; triangle-inequality pruned with owner/cc)",
         py::arg("X"), py::arg("c"), py::arg("first"), py::arg("d2"), py::arg("block_sums"),
         py::arg("rows_per_block"), py::arg("owner") = py::none(), py::arg("cc") = py::none(),
@@ -487,6 +541,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dtype"), py::arg("K"), py::arg("D"), py::arg("N"), py::arg("weighted") = false);
   m.def("fixed_exp", [](double maxabs) { return mk::fixed_exp(maxabs); },
         "fixed-point exponent e with maxabs * 2^e <= 2^30 (M-step accumulators)");
+  m.def("host_register", &host_register, "page-lock a CPU tensor in place (hipHostRegister)");
+  m.def("host_unregister", &host_unregister, "undo host_register");
   m.def("js_format", &js_format, "ECMAScript Number::toString of a double");
   m.def("js_array", &js_array, "JSON array of a CPU float tensor with JS number formatting");
   m.attr("NSLOT") = mk::NSLOT;

@@ -163,6 +163,29 @@ __device__ __forceinline__ unsigned key6_mask() {
   return m;
 }
 
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11): the counter-based generator of the synthetic
+// blobs (kpp.hip) and the mini-batch row sampler (rows.hip); NumPy mirror in
+// mikmeans/data/blobs.py.
+struct U4 { uint32_t x, y, z, w; };
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    // one 32x32->64 product per word: a single v_mad_u64_u32 (quarter rate) instead of a
+    // v_mul_lo_u32 + v_mul_hi_u32 pair
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+__device__ __forceinline__ float u01_open0(uint32_t v) { return ((v >> 8) + 1) * (1.0f / 16777216.0f); }
+__device__ __forceinline__ float u01(uint32_t v) { return (v >> 8) * (1.0f / 16777216.0f); }
+
 // Row index of accumulator register `reg` for lane half `h` in the 32x32 MFMA C/D map.
 __device__ __forceinline__ int mfma32_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 

@@ -144,8 +144,9 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
 // independent row loads in flight per lane; |x| compared as bit patterns (non-negative
 // floats order like unsigned integers, and a NaN's pattern exceeds +inf's, so NaN
 // propagates like torch.aminmax).  One global atomicMax per (block, column).  STATS: also,
-// per column, the sum of |x| (f32 per lane, one f64 atomicAdd per (block, column)), the
-// count of nonzero values and the exponent of the lowest set bit over all nonzero finite
+// per column, the sums of |x|, x and x^2 (f32 per lane, one f64 atomicAdd per (block,
+// column) each: fstats = [sum |x| | sum x | sum x^2], the last two give the tol scale's
+// variance without an f32 copy of X), the count of nonzero values and the exponent of the lowest set bit over all nonzero finite
 // values (x is an integer multiple of 2^lowbit).  From these the engine flags wide-range
 // columns for the residual M-step pass: a column whose values all sit on the hi pass's
 // grid (lowbit >= -col_exp: one-hot, small integers, coarse bf16) never needs it, and
@@ -161,7 +162,7 @@ __device__ __forceinline__ int lowbit_exp(float f) {
 template <typename T, bool STATS>
 __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X, int64_t N, int NP,
                                                          int L, int64_t ldx, uint32_t* __restrict__ out,
-                                                         double* __restrict__ sumabs,
+                                                         double* __restrict__ fstats,
                                                          unsigned long long* __restrict__ nnz,
                                                          int* __restrict__ lowbit) {
   constexpr int V = Elem<T>::V;
@@ -169,11 +170,11 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
   const int R = 256 / L;
   const int64_t step = (int64_t)gridDim.x * R;
   uint32_t m[V];
-  float q[V];
+  float q[V], sx[V], sxx[V];
   uint32_t nz[V];
   int lb[V];
 #pragma unroll
-  for (int e = 0; e < V; ++e) { m[e] = 0u; q[e] = 0.f; nz[e] = 0u; lb[e] = 1 << 30; }
+  for (int e = 0; e < V; ++e) { m[e] = 0u; q[e] = 0.f; sx[e] = 0.f; sxx[e] = 0.f; nz[e] = 0u; lb[e] = 1 << 30; }
   auto take = [&](const u32x4& w) {
     float f[V];
     unpack16(w, f, (T*)nullptr);
@@ -182,6 +183,8 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
       m[e] = max(m[e], __float_as_uint(f[e]) & 0x7fffffffu);
       if constexpr (STATS) {
         q[e] += fabsf(f[e]);
+        sx[e] += f[e];
+        sxx[e] = __builtin_fmaf(f[e], f[e], sxx[e]);
         nz[e] += f[e] != 0.f;
         lb[e] = min(lb[e], lowbit_exp(f[e]));
       }
@@ -205,6 +208,8 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
       m[e] = max(m[e], (uint32_t)__shfl_xor((int)m[e], o, 64));
       if constexpr (STATS) {
         q[e] += __shfl_xor(q[e], o, 64);
+        sx[e] += __shfl_xor(sx[e], o, 64);
+        sxx[e] += __shfl_xor(sxx[e], o, 64);
         nz[e] += (uint32_t)__shfl_xor((int)nz[e], o, 64);
         lb[e] = min(lb[e], __shfl_xor(lb[e], o, 64));
       }
@@ -220,15 +225,18 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
     if (v) atomicMax(out + j, v);
   }
   if constexpr (STATS) {
-    __syncthreads();
     float* rf = (float*)&red[0][0];
-    if (lane < L)
 #pragma unroll
-      for (int e = 0; e < V; ++e) rf[wv * 64 * V + lane * V + e] = q[e];
-    __syncthreads();
-    for (int j = threadIdx.x; j < NP * V; j += 256) {
-      const double v = (double)rf[j] + rf[64 * V + j] + rf[128 * V + j] + rf[192 * V + j];
-      if (v != 0.0) atomicAdd(sumabs + j, v);
+    for (int k = 0; k < 3; ++k) {
+      __syncthreads();
+      if (lane < L)
+#pragma unroll
+        for (int e = 0; e < V; ++e) rf[wv * 64 * V + lane * V + e] = k == 0 ? q[e] : k == 1 ? sx[e] : sxx[e];
+      __syncthreads();
+      for (int j = threadIdx.x; j < NP * V; j += 256) {
+        const double v = (double)rf[j] + rf[64 * V + j] + rf[128 * V + j] + rf[192 * V + j];
+        if (v != 0.0) atomicAdd(fstats + (int64_t)k * NP * V + j, v);
+      }
     }
     __syncthreads();
     if (lane < L)
@@ -253,11 +261,11 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
 }
 
 hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
-                             hipStream_t s, double* sumabs, unsigned long long* nnz, int* lowbit) {
+                             hipStream_t s, double* fstats, unsigned long long* nnz, int* lowbit) {
   const int V = dtype == DT_BF16 ? 8 : 4;
   const int NP = D / V;
   if (N <= 0 || D % V || NP > 64 || NP < 1) return N <= 0 ? hipSuccess : hipErrorInvalidValue;
-  if ((sumabs != nullptr) != (nnz != nullptr) || (sumabs != nullptr) != (lowbit != nullptr))
+  if ((fstats != nullptr) != (nnz != nullptr) || (fstats != nullptr) != (lowbit != nullptr))
     return hipErrorInvalidValue;  // the statistics come together
   int L = 1;
   while (L < NP) L *= 2;
@@ -266,11 +274,11 @@ hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t
   if (nb > 2048) nb = 2048;  // 8 per CU; each streams its rows with 4 loads in flight per lane
   const dim3 g((unsigned)nb), b(256);
   if (dtype == DT_BF16) {
-    if (sumabs) hipLaunchKernelGGL((col_absmax_kernel<uint16_t, true>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, sumabs, nnz, lowbit);
-    else hipLaunchKernelGGL((col_absmax_kernel<uint16_t, false>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, sumabs, nnz, lowbit);
+    if (fstats) hipLaunchKernelGGL((col_absmax_kernel<uint16_t, true>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, fstats, nnz, lowbit);
+    else hipLaunchKernelGGL((col_absmax_kernel<uint16_t, false>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, fstats, nnz, lowbit);
   } else {
-    if (sumabs) hipLaunchKernelGGL((col_absmax_kernel<float, true>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, sumabs, nnz, lowbit);
-    else hipLaunchKernelGGL((col_absmax_kernel<float, false>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, sumabs, nnz, lowbit);
+    if (fstats) hipLaunchKernelGGL((col_absmax_kernel<float, true>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, fstats, nnz, lowbit);
+    else hipLaunchKernelGGL((col_absmax_kernel<float, false>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, fstats, nnz, lowbit);
   }
   return hipGetLastError();
 }

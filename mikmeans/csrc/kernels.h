@@ -115,13 +115,25 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 
 // ---- row squared norms -------------------------------------------------------
 // Per-column max |x| (as f32 bit patterns, atomicMax into a zeroed out[D]); optionally, all
-// together, sum |x| (f64, zeroed), nonzero count (u64, zeroed) and the lowest set bit's
-// exponent over nonzero finite values (int, initialised to INT_MAX by the caller).
+// together, fstats = [sum |x| | sum x | sum x^2] (f64 [3][D], zeroed), the nonzero count
+// (u64 [D], zeroed) and the lowest set bit's exponent over nonzero finite values (int [D],
+// initialised to INT_MAX by the caller).
 hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
-                             hipStream_t s, double* sumabs = nullptr, unsigned long long* nnz = nullptr,
+                             hipStream_t s, double* fstats = nullptr, unsigned long long* nnz = nullptr,
                              int* lowbit = nullptr);
 hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t ldx, float* out,
                              hipStream_t s);
+
+// ---- rows (csrc/rows.hip) ----------------------------------------------------------
+// Mini-batch sampler: out[j] = X[idx_j] for j < b, idx_j = floor(u * n) from Philox keyed by
+// (seed; j, step, rank) (NumPy mirror: mikmeans/data/sampler.py); xn / idx_out optional.
+hipError_t launch_sample_rows(int dtype, const void* X, int64_t n, int64_t ldx, int D, void* out,
+                              int64_t ldo, int64_t b, uint64_t seed, uint32_t rank, uint32_t step,
+                              float* xn, int64_t* idx_out, hipStream_t s);
+// In place x <- x / max(|x|, 1e-30) per row (cosine metric); xn (optional) = |x_rounded|^2.
+hipError_t launch_row_normalize(int dtype, void* X, int64_t N, int D, int64_t ldx, float* xn, hipStream_t s);
+// out[0] += sum a[i] * b[i] (f64 accumulation).
+hipError_t launch_wdot(const float* a, const float* b, int64_t n, double* out, hipStream_t s);
 
 // ---- k-means++ ---------------------------------------------------------------
 // With owner[N] (int32: centre each d2 was measured against) and cc[k] (|c - c_j|^2, from

@@ -1,0 +1,178 @@
+// mikmeans — row-level helper kernels for gfx950: the device mini-batch sampler, in-place
+// row normalisation (cosine metric) and a weighted dot product (weighted inertia).
+//
+// sample_rows: batch row j of step s on rank r is source row
+//   idx = floor(u * n),  u = (philox(j, s, r, TAG_SMP; seed) as a 64-bit word >> 11) * 2^-53
+// (with replacement, clamped to n-1), a pure function of (seed, rank, step, j): the
+// sampler's whole state is the step counter, so a resumed fit draws the rows the
+// uninterrupted one would, and the host (NumPy, mikmeans/data/sampler.py) reproduces the
+// indices for shards that live in host memory.  The kernel gathers the rows (16-B
+// pieces, TPR lanes per row) and writes their squared norms (of the stored values) for
+// the assign kernel's inertia -- one read of each sampled row and one write of the batch,
+// the same bytes the blob generator writes for a streamed batch.
+//
+// Reference parity: the reference's "Shuffle unassigned" (app.mjs:159-166, Fisher-Yates
+// over the cards) is its only random selection of points; mini-batch sampling is the
+// numeric framework's use of it.
+#include "common.h"
+#include "kernels.h"
+
+namespace mk {
+
+constexpr uint32_t TAG_SMP = 0x53414D50u;  // "SAMP"
+
+__device__ __forceinline__ int64_t sample_index(int64_t j, uint32_t step, uint32_t rank, int64_t n,
+                                                uint32_t k0, uint32_t k1) {
+  const U4 r = philox(U4{(uint32_t)j, step, rank, TAG_SMP}, k0, k1);
+  const uint64_t w = ((uint64_t)r.y << 32) | r.x;
+  const double u = (double)(w >> 11) * 0x1p-53;
+  const int64_t i = (int64_t)(u * (double)n);
+  return i < n ? i : n - 1;
+}
+
+template <typename T, int TPR>
+__global__ __launch_bounds__(256) void sample_rows_kernel(const T* __restrict__ X, int64_t n, int64_t ldx,
+                                                          int NP, T* __restrict__ out, int64_t ldo,
+                                                          int64_t b, uint32_t k0, uint32_t k1,
+                                                          uint32_t rank, uint32_t step, float* xn,
+                                                          int64_t* idx_out) {
+  constexpr int V = Elem<T>::V;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t j = e / TPR;
+  const int t = (int)(e % TPR);
+  const bool ok = j < b;
+  int64_t src = 0;
+  if (t == 0 && ok) src = sample_index(j, step, rank, n, k0, k1);
+  // broadcast within the row's lanes (TPR divides 64)
+  const int leader = (int)(threadIdx.x & 63) & ~(TPR - 1);
+  src = ((int64_t)__shfl((int)(uint32_t)src, leader, 64) & 0xffffffffll) |
+        ((int64_t)__shfl((int)(src >> 32), leader, 64) << 32);
+  float sq = 0.f;
+  if (ok) {
+    if (idx_out && t == 0) idx_out[j] = src;
+    const T* rp = X + src * ldx;
+    T* op = out + j * ldo;
+    for (int p = t; p < NP; p += TPR) {
+      const u32x4 w = *(const u32x4*)(rp + p * V);
+      float f[V];
+      unpack16(w, f, (T*)nullptr);
+#pragma unroll
+      for (int q = 0; q < V; ++q) sq = __builtin_fmaf(f[q], f[q], sq);
+      *(u32x4*)(op + p * V) = w;
+    }
+  }
+  if (xn) {
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
+    if (ok && t == 0) xn[j] = sq;
+  }
+}
+
+hipError_t launch_sample_rows(int dtype, const void* X, int64_t n, int64_t ldx, int D, void* out,
+                              int64_t ldo, int64_t b, uint64_t seed, uint32_t rank, uint32_t step,
+                              float* xn, int64_t* idx_out, hipStream_t s) {
+  if (b <= 0) return hipSuccess;
+  if (n <= 0) return hipErrorInvalidValue;
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  if (D % V) return hipErrorInvalidValue;
+  const int NP = D / V;
+  int tpr = 1;
+  while (tpr < NP && tpr < 16) tpr *= 2;
+  const int64_t tot = b * tpr;
+  const dim3 g((unsigned)((tot + 255) / 256)), blk(256);
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#define MK_SMP(TT, TP)                                                                           \
+  hipLaunchKernelGGL((sample_rows_kernel<TT, TP>), g, blk, 0, s, (const TT*)X, n, ldx, NP, (TT*)out, \
+                     ldo, b, k0, k1, rank, step, xn, idx_out)
+#define MK_SMP_T(TT)                                                                             \
+  switch (tpr) {                                                                                 \
+    case 1: MK_SMP(TT, 1); break;                                                                \
+    case 2: MK_SMP(TT, 2); break;                                                                \
+    case 4: MK_SMP(TT, 4); break;                                                                \
+    case 8: MK_SMP(TT, 8); break;                                                                \
+    default: MK_SMP(TT, 16); break;                                                              \
+  }
+  if (dtype == DT_BF16) { MK_SMP_T(uint16_t) } else { MK_SMP_T(float) }
+#undef MK_SMP_T
+#undef MK_SMP
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// In-place unit rows: x <- x / max(|x|, 1e-30), f32 arithmetic (norm of the stored values,
+// IEEE sqrt and division), rounded back to the storage type; xn (optional) receives the
+// squared norm of the rounded row.  16 lanes per row.
+template <typename T>
+__global__ __launch_bounds__(256) void row_normalize_kernel(T* X, int64_t N, int NP, int64_t ldx, float* xn) {
+  constexpr int V = Elem<T>::V;
+  const int sub = threadIdx.x & 15;
+  const int64_t i = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const bool ok = i < N;
+  T* row = X + (ok ? i : 0) * ldx;
+  float s = 0.f;
+  if (ok)
+    for (int p = sub; p < NP; p += 16) {
+      float f[V];
+      unpack16(*(const u32x4*)(row + p * V), f, (T*)nullptr);
+#pragma unroll
+      for (int q = 0; q < V; ++q) s = __builtin_fmaf(f[q], f[q], s);
+    }
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+  const float nrm = fmaxf(sqrtf(s), 1e-30f);
+  float s2 = 0.f;
+  if (ok)
+    for (int p = sub; p < NP; p += 16) {
+      float f[V];
+      unpack16(*(const u32x4*)(row + p * V), f, (T*)nullptr);
+      T h[V];
+#pragma unroll
+      for (int q = 0; q < V; ++q) {
+        h[q] = Elem<T>::from_f32(f[q] / nrm);
+        const float r = Elem<T>::to_f32(h[q]);
+        s2 = __builtin_fmaf(r, r, s2);
+      }
+      *(u32x4*)(row + p * V) = *(const u32x4*)h;
+    }
+  if (xn) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) s2 += __shfl_xor(s2, o, 64);
+    if (ok && sub == 0) xn[i] = s2;
+  }
+}
+
+hipError_t launch_row_normalize(int dtype, void* X, int64_t N, int D, int64_t ldx, float* xn, hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  if (D % V) return hipErrorInvalidValue;
+  const dim3 g((unsigned)((N + 15) / 16)), b(256);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(row_normalize_kernel<uint16_t>, g, b, 0, s, (uint16_t*)X, N, D / V, ldx, xn);
+  else
+    hipLaunchKernelGGL(row_normalize_kernel<float>, g, b, 0, s, (float*)X, N, D / V, ldx, xn);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// out[0] += sum_i a[i] * b[i] in f64 (weighted inertia: a = squared distances, b = weights).
+__global__ __launch_bounds__(256) void wdot_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                   int64_t n, double* out) {
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    acc += (double)a[i] * (double)b[i];
+  acc = wave_sum(acc);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+hipError_t launch_wdot(const float* a, const float* b, int64_t n, double* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  int64_t nb = (n + 255) / 256;
+  if (nb > 1024) nb = 1024;
+  hipLaunchKernelGGL(wdot_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, b, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace mk

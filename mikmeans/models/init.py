@@ -43,24 +43,33 @@ def floyd_sample(n: int, k: int, rng: np.random.Generator) -> np.ndarray:
     return out
 
 
-def gather_rows(X: torch.Tensor, D: int, global_idx: np.ndarray, start: int, comm: Comm) -> torch.Tensor:
-    """Rows ``global_idx`` of the sharded dataset, replicated on every rank (f32 [k, D])."""
+def gather_rows(X: torch.Tensor | None, D: int, global_idx: np.ndarray, start: int, comm: Comm, *,
+                fetch=None, n_local: int | None = None) -> torch.Tensor:
+    """Rows ``global_idx`` of the sharded dataset, replicated on every rank (f32 [k, D]).
+    ``fetch(local_idx) -> [m, >=D]`` supplies local rows from elsewhere (a streamed shard's
+    host memory) when ``X`` is None; the sum all-reduce runs on the communicator's device."""
     k = len(global_idx)
-    out = torch.zeros((k, D), dtype=torch.float64, device=X.device)
-    n = X.shape[0]
+    dev = comm.device if X is None else X.device
+    out = torch.zeros((k, D), dtype=torch.float64, device=dev)
+    n = X.shape[0] if X is not None else int(n_local)
     loc = global_idx - start
     mine = np.nonzero((loc >= 0) & (loc < n))[0]
     if len(mine):
-        li = torch.as_tensor(loc[mine], device=X.device)
-        out[torch.as_tensor(mine, device=X.device)] = X[li][:, :D].to(torch.float64)
+        if X is not None:
+            li = torch.as_tensor(loc[mine], device=X.device)
+            rows = X[li][:, :D]
+        else:
+            rows = fetch(loc[mine])[:, :D]
+        out[torch.as_tensor(mine, device=dev)] = rows.to(device=dev, dtype=torch.float64)
     comm.allreduce_(out)
     return out.to(torch.float32)
 
 
-def init_random(X, D, K, n_global, start, comm: Comm, seed: int) -> torch.Tensor:
+def init_random(X, D, K, n_global, start, comm: Comm, seed: int, *, fetch=None,
+                n_local: int | None = None) -> torch.Tensor:
     rng = np.random.default_rng(seed)
     idx = floyd_sample(n_global, K, rng)
-    return gather_rows(X, D, idx, start, comm)
+    return gather_rows(X, D, idx, start, comm, fetch=fetch, n_local=n_local)
 
 
 def init_kmeanspp(X: torch.Tensor, D: int, K: int, n_global: int, start: int, comm: Comm, seed: int,

@@ -166,11 +166,12 @@ class LloydEngine:
         # fixed-point scale of the M-step accumulators (X is static for the fit)
         from ..ops import MStepScales, mstep_scales
 
-        # (global column maxima: every rank uses the same scale -> exact, world-size independent
-        # sums; columns whose max is far above their RMS also get a residual lo pass)
-        n_glob = torch.tensor([float(self.n)], dtype=torch.float64, device=dev)
-        self.comm.allreduce_(n_glob)
-        self.scales = mstep_scales(self.X, self.weights, comm=self.comm, n_global=int(n_glob.item()))
+        # (global column statistics: every rank uses the same scale -> exact, world-size independent
+        # sums; columns with inexact values far above their nonzero mean also get a residual lo pass)
+        from ..ops import col_stats
+
+        self.stats = col_stats(self.X)             # (also the tol scale's column sums: api.fit)
+        self.scales = mstep_scales(self.X, self.weights, comm=self.comm, stats=self.stats)
         if self.scales.nw and C.update_slice_width(self.dt, self.K, self.Dp, self.weights is not None) == 0:
             self.scales = MStepScales(self.scales.col_exp, self.scales.cnt_exp, [], dev)
         self.col_exp, self.cnt_exp = self.scales.col_exp, self.scales.cnt_exp
@@ -198,6 +199,33 @@ class LloydEngine:
                 }
                 if self.n == 0:
                     self.delta = None
+
+    def device_buffers(self) -> dict:
+        """Allocator bytes of every device buffer the engine holds, under the names
+        parallel/memplan.py plans them by (tests/test_memplan_gpu.py pins the two)."""
+        from ..parallel.memplan import _r
+
+        t = {"labels": self.labels, "xn": self.xn, "slab": self.slab, "cnt_slab": self.cnt_slab,
+             "packed": self.packed, "C": self.C, "Cnew": self.Cnew, "shift": self.shift,
+             "counts": self.counts, "pack": self.pk.pack, "cn": self.pk.cn, "slots": self.slots}
+        if self.weights is not None:
+            t["weights"] = self.weights
+        if self.mind is not None:
+            t["mind"] = self.mind
+        if self.pk._keys is not None:
+            t["split_keys"] = self.pk._keys
+        if self.delta is not None:
+            t.update(delta_prev=self.delta["prev"], delta_list=self.delta["list"],
+                     delta_count=self.delta["count"], delta_tot=self.delta["tot"])
+        out = {k: _r(v.numel() * v.element_size()) for k, v in t.items()}
+        for name in ("bufs", "stage"):          # streaming: two chunk / staging buffers
+            bl = getattr(self, name, None)
+            if bl:
+                out["chunk_bufs" if name == "bufs" else "staging"] = sum(
+                    _r(b.numel() * b.element_size()) for b in bl)
+        if getattr(self, "part", None) is not None:
+            out["packed"] += _r(self.part.numel() * 8)
+        return out
 
     def reset_labels(self):
         """Unassign every point (the reference's Restart, app.mjs:167-178); the next
@@ -283,7 +311,7 @@ class LloydEngine:
             C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
                      self.col_exp, self.cnt_exp)
             if self.weights is not None:
-                self.packed[KD + self.K] = (self.mind.double() * self.weights.double()).sum()
+                self._weighted_inertia()
         elif self.n:
             with _phase("mikmeans.assign"):
                 self.pk.assign(self.X, self.xn, self.labels, self.mind, self.slots, True)
@@ -302,7 +330,7 @@ class LloydEngine:
                     C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots,
                              self.packed, self.col_exp, self.cnt_exp)
             if self.weights is not None:
-                self.packed[KD + self.K] = (self.mind.double() * self.weights.double()).sum()
+                self._weighted_inertia()
         else:
             self.packed.zero_()
         sc = self.scales
@@ -320,6 +348,13 @@ class LloydEngine:
         with _phase("mikmeans.finalize"):
             self._relocate_empty()
             self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts)
+
+    def _weighted_inertia(self):
+        """packed[inertia] = sum_i w_i mind_i (f64, one pass, no n x 8-byte temporaries)."""
+        KD = self.K * self.Dp
+        slot = self.packed[KD + self.K : KD + self.K + 1]
+        slot.zero_()
+        self._C.wdot(self.mind, self.weights, slot)
 
     def _project_sphere(self):
         """Cnew <- Cnew / |Cnew| (empty / frozen rows are already unit or kept), then the
@@ -403,7 +438,7 @@ class LloydEngine:
         if kk:
             v, idx = torch.topk(local.double(), kk)
             vals[:kk] = v
-            rows[:kk] = self.X[idx.long()].double()
+            rows[:kk] = self._rows(idx)
         allv = self.comm.all_gather(vals).reshape(-1)
         allr = self.comm.all_gather(rows).reshape(-1, Dp)
         order = torch.argsort(allv, descending=True)[:m]
@@ -412,6 +447,10 @@ class LloydEngine:
                 continue
             self.packed[k * Dp : (k + 1) * Dp] = allr[order[j]]
             self.packed[KD + k] = 1.0
+
+    def _rows(self, idx: torch.Tensor) -> torch.Tensor:
+        """Local rows ``idx`` as float64 ``[m, Dp]`` (the streaming engine fetches them from host)."""
+        return self.X[idx.long()].double()
 
     def _assign_into(self, mind):
         labels = torch.empty_like(self.labels)
@@ -469,29 +508,37 @@ class LloydEngine:
         return float(t.item())
 
 
-def mean_variance(X: torch.Tensor, comm: Comm, n_global: int) -> float:
-    """Mean over features of the global per-feature variance (sklearn's tol scale)."""
-    if X.shape[0]:
-        s = X.sum(0, dtype=torch.float64)
-        ss = (X.to(torch.float32) ** 2).sum(0, dtype=torch.float64) if not X.is_cuda else None
-        if ss is None:
-            ss = torch.zeros_like(s)
-            step = 1 << 22
-            for i in range(0, X.shape[0], step):
-                xb = X[i : i + step].to(torch.float32)
-                ss += (xb * xb).sum(0, dtype=torch.float64)
-    else:
-        s = torch.zeros(X.shape[1], dtype=torch.float64, device=X.device)
+def mean_variance(X: torch.Tensor, comm: Comm, n_global: int, D: int | None = None, stats=None) -> float:
+    """Mean over the first ``D`` features of the global per-feature variance (sklearn's tol
+    scale).  GPU shards use the column-statistics pass (f64 sums of x and x^2, no f32 copy
+    of X); ``stats``: this rank's :class:`~mikmeans.ops.ColStats` when already computed."""
+    from ..ops import col_stats
+
+    d = int(D if D is not None else X.shape[1])
+    if stats is None and X.shape[0] and X.is_cuda:
+        stats = col_stats(X)
+    if stats is not None:
+        s = stats.sum[:d].to(device=comm.device, dtype=torch.float64)
+        ss = stats.sumsq[:d].to(device=comm.device, dtype=torch.float64)
+    elif X.shape[0]:
+        s = torch.zeros(d, dtype=torch.float64, device=X.device)
         ss = torch.zeros_like(s)
-    t = torch.cat([s, ss])
+        for i in range(0, X.shape[0], 1 << 16):
+            xb = X[i : i + (1 << 16), :d].to(torch.float64)
+            s += xb.sum(0)
+            ss += (xb * xb).sum(0)
+    else:
+        s = torch.zeros(d, dtype=torch.float64, device=comm.device)
+        ss = torch.zeros_like(s)
+    t = torch.cat([s, ss]).to(comm.device)
     comm.allreduce_(t)
-    d = X.shape[1]
     mean = t[:d] / max(n_global, 1)
     var = t[d:] / max(n_global, 1) - mean * mean
     return float(var.clamp_min(0).mean().item()) if d else 0.0
 
 
-def tol_to_abs(tol: float, X: torch.Tensor, comm: Comm, n_global: int) -> float:
+def tol_to_abs(tol: float, X: torch.Tensor, comm: Comm, n_global: int, D: int | None = None,
+               stats=None) -> float:
     if tol <= 0:
         return 0.0 if tol == 0 else -math.inf
-    return tol * mean_variance(X, comm, n_global)
+    return tol * mean_variance(X, comm, n_global, D, stats)

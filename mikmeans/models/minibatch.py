@@ -65,6 +65,7 @@ class MiniBatchEngine:
             self.bound = None    # per-column |x| bound [D] f64 the scales were made for
             self.rescales = 0    # batches redone with a wider scale
             self.value_bound = value_bound
+            self.bounded = value_bound is not None   # scales cover every value: no clamp, no sync
             self.clampc = torch.zeros(1, dtype=torch.int32, device=dev)
             self.labels = torch.empty(self.batch, dtype=torch.int32, device=dev)
             self.xn = torch.empty(self.batch, dtype=torch.float32, device=dev)
@@ -115,6 +116,23 @@ class MiniBatchEngine:
                                              None, comm=self.comm, bound=self.bound)
         return self
 
+    def set_bound(self, bound: torch.Tensor):
+        """Fix the fixed-point scales from a per-column bound on |x| over the WHOLE dataset
+        (f64 ``[D]`` or ``[Dp]``; all-reduced MAX over ranks): no batch can exceed it, so
+        the M-step runs unclamped and no step reads anything back to the host."""
+        from ..ops import fixed_exps
+
+        if not self.gpu:
+            return self
+        b = torch.zeros(self.Dp, dtype=torch.float64, device=self.device)
+        bd = bound.to(device=self.device, dtype=torch.float64).reshape(-1)
+        b[: bd.numel()] = bd[: self.Dp]
+        self.col_exp, _ = fixed_exps(torch.empty((0, self.Dp), dtype=self.dtype, device=self.device), None,
+                                     comm=self.comm, bound=b)
+        self.bound = b
+        self.bounded = True
+        return self
+
     def _set_bound(self, Xb, grow: bool = False):
         from ..ops import col_max_abs, fixed_exps
 
@@ -133,7 +151,7 @@ class MiniBatchEngine:
         KD = self.K * self.Dp
         if Xb.shape[0]:
             # a given value bound cannot be exceeded: no clamp, no count (the plain kernel)
-            bounded = self.value_bound is not None
+            bounded = self.bounded
             C.update(Xb, lab, self.K, self.slab, self.cnt_slab, self.n_chunks, None, self.col_exp, 0,
                      not bounded, clamp_count=None if bounded else self.clampc)
             C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
@@ -161,7 +179,7 @@ class MiniBatchEngine:
                 C.row_sqnorm(Xb, xn)
             self.pk.assign(Xb, xn, lab, None, self.slots, False)
         self._mstep(Xb, lab)
-        if self.value_bound is None:
+        if not self.bounded:
             # one host read per step: the all-reduced clamp count is the same on every rank,
             # so all ranks agree to redo this batch with scales grown from its maxima
             KD = self.K * self.Dp

@@ -169,14 +169,36 @@ def col_max_abs(X: torch.Tensor) -> torch.Tensor:
 
 class ColStats:
     """Per-column statistics of one streaming pass (csrc/finalize.hip col_absmax):
-    ``absmax`` (f64 [D]); with ``stats``: ``sumabs`` (f64), ``nnz`` (int64, nonzero
-    values) and ``lowbit`` (int32: every value is an integer multiple of 2^lowbit; a large
-    sentinel for an all-zero column)."""
+    ``absmax`` (f64 [D]); with ``stats``: ``sumabs``, ``sum``, ``sumsq`` (f64), ``nnz``
+    (int64, nonzero values) and ``lowbit`` (int32: every value is an integer multiple of
+    2^lowbit; LOWBIT_NONE for an all-zero column).  Statistics of row blocks merge with
+    :meth:`merge` (streamed shards)."""
 
     LOWBIT_NONE = 2**31 - 1
 
-    def __init__(self, absmax, sumabs=None, nnz=None, lowbit=None):
+    def __init__(self, absmax, sumabs=None, nnz=None, lowbit=None, sum=None, sumsq=None):
         self.absmax, self.sumabs, self.nnz, self.lowbit = absmax, sumabs, nnz, lowbit
+        self.sum, self.sumsq = sum, sumsq
+
+    @property
+    def full(self) -> bool:
+        return self.sumabs is not None
+
+    def merge(self, other: "ColStats") -> "ColStats":
+        if not (self.full and other.full):
+            return ColStats(torch.maximum(self.absmax, other.absmax))
+        return ColStats(torch.maximum(self.absmax, other.absmax), self.sumabs + other.sumabs,
+                        self.nnz + other.nnz, torch.minimum(self.lowbit, other.lowbit),
+                        self.sum + other.sum, self.sumsq + other.sumsq)
+
+    @staticmethod
+    def empty(D: int, device, full: bool = True) -> "ColStats":
+        z = torch.zeros(D, dtype=torch.float64, device=device)
+        if not full:
+            return ColStats(z)
+        return ColStats(z, z.clone(), torch.zeros(D, dtype=torch.int64, device=device),
+                        torch.full((D,), ColStats.LOWBIT_NONE, dtype=torch.int32, device=device),
+                        z.clone(), z.clone())
 
 
 def _lowbit_torch(Xb: torch.Tensor) -> torch.Tensor:
@@ -185,44 +207,43 @@ def _lowbit_torch(Xb: torch.Tensor) -> torch.Tensor:
     e = b >> 23
     m = b & 0x7FFFFF
     sig = torch.where(e == 0, m, m | 0x800000)
-    tz = ((sig & -sig).double().log2()).long()
+    tz = ((sig & -sig).clamp_min(1).double().log2()).long()
     lb = torch.where(e == 0, -149 + tz, e - 150 + tz)
     return torch.where((b == 0) | (e == 255), torch.full_like(lb, ColStats.LOWBIT_NONE), lb)
 
 
 def col_stats(X: torch.Tensor, stats: bool = True) -> ColStats:
-    """One pass over ``X``: per-column max |x| and, with ``stats``, sum |x|, the nonzero
-    count and the lowest-bit exponent (native kernel on the GPU; torch elsewhere)."""
+    """One pass over ``X``: per-column max |x| and, with ``stats``, sum |x|, sum x, sum x^2,
+    the nonzero count and the lowest-bit exponent (native kernel on the GPU; torch elsewhere)."""
     D = X.shape[1]
     if X.shape[0] == 0:
-        z = torch.zeros(D, dtype=torch.float64, device=X.device)
-        if not stats:
-            return ColStats(z)
-        return ColStats(z, z.clone(), torch.zeros(D, dtype=torch.int64, device=X.device),
-                        torch.full((D,), ColStats.LOWBIT_NONE, dtype=torch.int32, device=X.device))
+        return ColStats.empty(D, X.device, stats)
     if _native_colstats_ok(X):
         out = torch.zeros(D, dtype=torch.int32, device=X.device)
         if not stats:
             require().col_absmax(X, out)
             return ColStats(out.view(torch.float32).double())
-        sa = torch.zeros(D, dtype=torch.float64, device=X.device)
+        fs = torch.zeros((3, D), dtype=torch.float64, device=X.device)
         nz = torch.zeros(D, dtype=torch.int64, device=X.device)
         lb = torch.full((D,), ColStats.LOWBIT_NONE, dtype=torch.int32, device=X.device)
-        require().col_absmax(X, out, sa, nz, lb)
-        return ColStats(out.view(torch.float32).double(), sa, nz, lb)
+        require().col_absmax(X, out, fs, nz, lb)
+        return ColStats(out.view(torch.float32).double(), fs[0], nz, lb, fs[1], fs[2])
     mn, mx = torch.aminmax(X, dim=0)
     m = torch.maximum(mn.double().abs(), mx.double().abs())
     if not stats:
         return ColStats(m)
-    sa = torch.zeros(D, dtype=torch.float64, device=X.device)
-    nz = torch.zeros(D, dtype=torch.int64, device=X.device)
-    lb = torch.full((D,), ColStats.LOWBIT_NONE, dtype=torch.int64, device=X.device)
-    for i in range(0, X.shape[0], 1 << 18):
-        xb = X[i : i + (1 << 18)]
-        sa += xb.to(torch.float64).abs().sum(0)
-        nz += (xb != 0).sum(0)
-        lb = torch.minimum(lb, _lowbit_torch(xb).amin(0))
-    return ColStats(m, sa, nz, lb.to(torch.int32))
+    st = ColStats.empty(D, X.device)
+    st.absmax = m
+    lb = st.lowbit.long()
+    for i in range(0, X.shape[0], 1 << 16):
+        xb = X[i : i + (1 << 16)].to(torch.float64)
+        st.sumabs += xb.abs().sum(0)
+        st.sum += xb.sum(0)
+        st.sumsq += (xb * xb).sum(0)
+        st.nnz += (xb != 0).sum(0)
+        lb = torch.minimum(lb, _lowbit_torch(X[i : i + (1 << 16)]).amin(0))
+    st.lowbit = lb.to(torch.int32)
+    return st
 
 
 # A column whose values do not all sit on the hi pass's grid (2^-col_exp) and whose max |x|

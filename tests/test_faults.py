@@ -34,11 +34,13 @@ def test_rank_failure_then_resume_with_other_world(tmp_path, monkeypatch):
 
     assert load_checkpoint(ck)["iteration"] == 4          # last checkpoint before the fault
     res = spawn_local(_fit, 3, ck, True)
-    if ref["n_iter"] == ITERS:
-        for r in res:
-            assert r["n_iter"] == ITERS
-            assert torch.equal(r["C"], ref["C"])           # exact: integer-sum M-step, any world size
-            assert r["inertia"] == pytest.approx(ref["inertia"], rel=1e-12)
+    # the reference must run every iteration (labels still changing), so the resumed runs
+    # are compared over the same trajectory
+    assert ref["n_iter"] == ITERS
+    for r in res:
+        assert r["n_iter"] == ITERS
+        assert torch.equal(r["C"], ref["C"])           # exact: integer-sum M-step, any world size
+        assert r["inertia"] == pytest.approx(ref["inertia"], rel=1e-12)
 
 
 def _mb_stream(comm, ckdir, resume, batch_global, steps):

@@ -1,0 +1,105 @@
+"""HBM planning on the GPU: the plan equals the engines' real buffers, the fit's measured
+peak stays within the plan, and a small budget streams the fit with the resident result."""
+import pytest
+import torch
+
+import mikmeans
+from mikmeans.data import blobs as B
+from mikmeans.parallel import memplan as M
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("n,D,K,dtype,weighted,inc", [
+    (300_000, 128, 1024, torch.bfloat16, False, True),
+    (200_000, 64, 256, torch.float32, True, False),
+    (70_000, 30, 9, torch.bfloat16, False, False),
+])
+def test_memory_plan_matches_engine_buffers(native, n, D, K, dtype, weighted, inc):
+    from mikmeans.models.lloyd import LloydEngine
+    from mikmeans.ops import pad_columns
+
+    X = pad_columns(B.make_blobs(n, D, K, seed=1, dtype=dtype, device=DEV))
+    w = torch.rand(n, device=DEV) + 0.5 if weighted else None
+    eng = LloydEngine(X, K, sample_weight=w, incremental=inc, n_features=D).set_centers(X[:K, :D].float())
+    eng.step()
+    inv = eng.device_buffers()
+    plan = M.plan_resident(n, D, K, dtype, weighted=weighted, incremental=inc, copy_x=False)
+    assert set(plan.persistent) == set(inv), (set(plan.persistent) ^ set(inv))
+    assert plan.persistent == inv
+
+
+@pytest.mark.parametrize("n,D,K", [(4_000_000, 64, 256), (2_000_000, 128, 1024)])
+def test_fit_peak_memory_within_plan(native, n, D, K):
+    """A mid-size fit from host rows: torch's measured peak allocation within +-10 % of the
+    plan (X's device copy, engine buffers, k-means++ workspace, final E-step)."""
+    X = B.make_blobs(n, D, 64, seed=2, dtype=torch.float32, device="cpu")
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    km = mikmeans.KMeans(K, dtype="bfloat16", max_iter=4, device=DEV).fit(X)
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - base
+    plan = km.memory_plan_
+    assert plan["mode"] == "resident"
+    assert 0.9 * plan["peak"] <= peak <= 1.1 * plan["peak"], (peak, plan["peak"], plan)
+
+
+def test_small_budget_streams_with_the_resident_result(native, monkeypatch):
+    """MIKMEANS_HBM_BYTES below the resident need: KMeans.fit plans a streamed fit (a chunk
+    that fits the budget) and returns the resident fit's model bit for bit."""
+    n, D, K = 400_000, 64, 48
+    X = B.make_blobs(n, D, K, seed=3, dtype=torch.float32, device="cpu")
+    kw = dict(init="random", dtype="bfloat16", max_iter=10, seed=4, device=DEV)
+    ref = mikmeans.KMeans(K, **kw).fit(X)
+    assert ref.memory_plan_["mode"] == "resident"
+    budget = int(ref.memory_plan_["peak"] * 0.4)
+    monkeypatch.setenv("MIKMEANS_HBM_BYTES", str(budget))
+    st = mikmeans.KMeans(K, **kw).fit(X)
+    p = st.memory_plan_
+    assert p["mode"] == "streaming" and p["peak"] <= budget and p["chunk_rows"] < n
+    assert st.n_iter_ == ref.n_iter_
+    assert torch.equal(st.cluster_centers_, ref.cluster_centers_)
+    assert torch.equal(st.labels_, ref.labels_)
+    assert st.inertia_ == pytest.approx(ref.inertia_, rel=1e-9)
+    # a budget below even the streamed per-row state: a clear error up front
+    monkeypatch.setenv("MIKMEANS_HBM_BYTES", str(n * 4))
+    with pytest.raises(M.HBMCapacityError):
+        mikmeans.KMeans(K, **kw).fit(X)
+
+
+@pytest.mark.parametrize("case", ["weighted", "cosine", "farthest", "wide_column", "f32_rows_ragged"])
+def test_streaming_options_match_resident(native, case):
+    """Out-of-core fits with sample weights, the cosine metric, the 'farthest' empty-cluster
+    policy, a wide-range column (residual pass) and host rows needing conversion + column
+    padding on the device: the resident fit's centres and labels, bit for bit."""
+    n, D, K = 120_000, 48, 24
+    dtype = "bfloat16"
+    X = B.make_blobs(n, D, K, seed=7, dtype=torch.float32, device="cpu")
+    kw = dict(dtype=dtype, max_iter=6, tol=0, device=DEV)
+    C0 = X[:K].clone()
+    w = None
+    if case == "weighted":
+        w = torch.rand(n, generator=torch.Generator().manual_seed(1)) + 0.5
+    elif case == "cosine":
+        kw["metric"] = "cosine"
+    elif case == "farthest":
+        kw["empty_cluster"] = "farthest"
+        C0[5:9] = 1.0e4                       # far-away centres stay empty -> relocated
+    elif case == "wide_column":
+        X[777, 3] = 3.0e5
+    elif case == "f32_rows_ragged":
+        X = X[:, :45].contiguous()            # bf16 compute, 45 f32 columns -> padded to 48
+        C0 = C0[:, :45].contiguous()
+        kw["dtype"] = "bfloat16"
+    Xh = X if dtype != "bfloat16" or case == "f32_rows_ragged" else X.to(torch.bfloat16)
+    ref = mikmeans.KMeans(K, init=C0, **kw).fit(Xh.to(DEV), sample_weight=w)
+    st = mikmeans.KMeans(K, init=C0, chunk_rows=20_000, **kw).fit(Xh, sample_weight=w)
+    assert st.memory_plan_["mode"] == "streaming"
+    if case == "wide_column":
+        assert st._engine.scales.nw == 1 and ref._engine.scales.nw == 1
+    assert torch.equal(st.cluster_centers_, ref.cluster_centers_)
+    assert torch.equal(st.labels_, ref.labels_)
+    assert st.inertia_ == pytest.approx(ref.inertia_, rel=1e-6)

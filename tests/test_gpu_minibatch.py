@@ -1,0 +1,107 @@
+"""Mini-batch k-means on the device: the Philox row sampler (csrc/rows.hip) against its NumPy
+mirror, device-resident vs host-resident shards (same rows, same model), host syncs per
+step, and the helper kernels of the cosine / weighted paths."""
+import numpy as np
+import pytest
+import torch
+
+import mikmeans
+from mikmeans.data import blobs as B
+from mikmeans.data.sampler import sample_indices
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("dtype,D", [(torch.bfloat16, 256), (torch.float32, 20), (torch.bfloat16, 40)])
+def test_sample_rows_matches_numpy_mirror(native, dtype, D):
+    from mikmeans.ops import pad_columns
+
+    n, b = 123_457, 50_001
+    X = pad_columns(B.make_blobs(n, D, 16, seed=3, dtype=dtype, device=DEV))
+    out = torch.empty((b, X.shape[1]), dtype=dtype, device=DEV)
+    xn = torch.empty(b, dtype=torch.float32, device=DEV)
+    idx = torch.empty(b, dtype=torch.int64, device=DEV)
+    for step, rank in ((0, 0), (7, 3), (2**31 + 5, 1)):
+        native.sample_rows(X, out, b, 99, rank, step, xn, idx)
+        exp = torch.from_numpy(sample_indices(n, b, 99, rank, step))
+        assert torch.equal(idx.cpu(), exp)
+        assert torch.equal(out, X[exp.to(DEV)])
+        torch.testing.assert_close(xn, X[exp.to(DEV)].float().pow(2).sum(1), rtol=1e-5, atol=1e-4)
+    # uniform draws: every row about b/n times over many steps
+    cnt = np.bincount(np.concatenate([sample_indices(1000, 10_000, 5, 0, s) for s in range(20)]), minlength=1000)
+    assert cnt.min() > 120 and cnt.max() < 290
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_row_normalize_and_wdot(native, dtype):
+    from mikmeans.ops import pad_columns
+
+    X = pad_columns((torch.randn(5000, 40, device=DEV) * 3).to(dtype))
+    X[7] = 0
+    ref = X.float() / X.float().norm(dim=1, keepdim=True).clamp_min(1e-30)
+    Y = X.clone()
+    xn = torch.empty(5000, device=DEV)
+    native.row_normalize(Y, xn)
+    tol = 1e-6 if dtype == torch.float32 else 2 ** -8
+    torch.testing.assert_close(Y.float(), ref, rtol=tol, atol=tol)
+    assert torch.equal(Y[7], X[7])
+    torch.testing.assert_close(xn, Y.float().pow(2).sum(1), rtol=1e-5, atol=1e-6)
+    a, w = torch.rand(100_001, device=DEV), torch.rand(100_001, device=DEV)
+    out = torch.zeros(1, dtype=torch.float64, device=DEV)
+    native.wdot(a, w, out)
+    assert float(out) == pytest.approx(float((a.double() * w.double()).sum()), rel=1e-12)
+
+
+def test_minibatch_fit_device_vs_host_shard(native, monkeypatch):
+    """The same Philox rows on both placements: a device-resident shard (batches drawn by
+    the gather kernel) and a host shard over the HBM budget (rows gathered on the host)
+    give the same centres bit for bit; the CPU fit draws the same rows too."""
+    n, D, K = 200_000, 32, 16
+    X = B.make_blobs(n, D, K, seed=8, dtype=torch.float32, device="cpu")
+    kw = dict(batch_size=4096, max_steps=25, init="random", seed=3, dtype="bfloat16", device=DEV)
+    a = mikmeans.MiniBatchKMeans(K, **kw).fit(X)
+    assert a.memory_plan_["mode"] == "minibatch-resident"
+    monkeypatch.setenv("MIKMEANS_HBM_BYTES", str(int(a.memory_plan_["peak"] * 0.5)))
+    b = mikmeans.MiniBatchKMeans(K, **kw).fit(X)
+    assert b.memory_plan_["mode"] == "minibatch-host"
+    assert torch.equal(a.cluster_centers_, b.cluster_centers_)
+    assert torch.equal(a.counts_, b.counts_)
+    monkeypatch.delenv("MIKMEANS_HBM_BYTES")
+    c = mikmeans.MiniBatchKMeans(K, **dict(kw, dtype="float32")).fit(X.to(DEV))
+    d = mikmeans.MiniBatchKMeans(K, **dict(kw, dtype="float32", device="cpu")).fit(X)
+    torch.testing.assert_close(c.cluster_centers_.cpu(), d.cluster_centers_, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(c.counts_.cpu(), d.counts_)
+
+
+def test_minibatch_fit_steps_do_not_sync(native):
+    """Bounded scales from the whole shard: no step reads back to the host (one tol check
+    per 10 steps at most) -- counted with a hooked .item()/.tolist() on device tensors."""
+    n, D, K = 100_000, 64, 32
+    X = B.make_blobs(n, D, K, seed=2, dtype=torch.bfloat16, device=DEV)
+    km = mikmeans.MiniBatchKMeans(K, batch_size=2048, max_steps=40, init="random", seed=1,
+                                  dtype="bfloat16", device=DEV, tol=1e-12)
+    calls = {"n": 0}
+    orig_item, orig_float = torch.Tensor.item, torch.Tensor.__float__
+
+    def item(t):
+        if t.is_cuda:
+            calls["n"] += 1
+        return orig_item(t)
+
+    def flt(t):
+        if t.is_cuda:
+            calls["n"] += 1
+        return orig_float(t)
+    km._engine(D, torch.device(DEV))
+    torch.Tensor.item, torch.Tensor.__float__ = item, flt
+    try:
+        eng = km._eng
+        before = calls["n"]
+        km.fit(X)
+        per_step = (calls["n"] - before) / 40
+    finally:
+        torch.Tensor.item, torch.Tensor.__float__ = orig_item, orig_float
+    assert eng.rescales == 0 and km.n_steps_ == 40
+    # setup (bound, shard sizes, init) costs a few reads; the loop at most 1 per 10 steps
+    assert per_step <= 0.1 + 12 / 40, per_step
