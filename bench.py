@@ -127,6 +127,22 @@ def main(argv=None):
             C0 = init_random(X, D, K, N, s, comm, args.seed)
         sync()
         extra["init_s"] = round(time.perf_counter() - t0, 3)
+        if args.config == "cfg4" and world == 1 and comm.grouped and dev.type == "cuda":
+            # the multi-rank owner path (all-gather of the potentials + owner sampling +
+            # all-reduce of the drawn row per step) on the 1-rank RCCL group: its collective
+            # overhead against the local path above, same centres
+            t0 = time.perf_counter()
+            C1 = init_kmeanspp(X, D, K, N, s, comm, args.seed, owner_path=True)
+            sync()
+            extra["init_owner_path_s"] = round(time.perf_counter() - t0, 3)
+            extra["init_owner_path_same_centres"] = bool(torch.equal(C0, C1))
+        from mikmeans.parallel import memplan
+
+        mp = memplan.plan_resident(e - s, D, K, dtype, incremental=args.incremental,
+                                   init="k-means++" if args.config == "cfg4" else "random")
+        extra["memory_plan"] = {"mode": mp.mode, "peak_GB": round(mp.peak / 1e9, 3),
+                                "HBM_GB": round(torch.cuda.get_device_properties(dev).total_memory / 1e9, 1)
+                                if dev.type == "cuda" else None}
         eng = LloydEngine(X, K, comm=comm, incremental=args.incremental).set_centers(C0)
         use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
         extra["graph"] = _capture(eng, use_graph)

@@ -131,7 +131,6 @@ def _kpp_gpu(X, centers, K, comm: Comm, u, L, prune: bool = True, multi: bool = 
     bs = torch.zeros(nb, dtype=torch.float64, device=dev)
     d2c = torch.empty_like(d2) if L > 1 else None
     bsc = torch.zeros_like(bs) if L > 1 else None
-    crow = torch.empty(D, dtype=torch.float32, device=dev)
     cand = torch.empty((L, D), dtype=torch.float32, device=dev)
     # Triangle-inequality pruning of the D^2 passes (csrc/kpp.hip, KPP_PRUNE): owner[i] is
     # the centre d2[i] belongs to, cc the new centre's squared distances to the previous
@@ -148,25 +147,26 @@ def _kpp_gpu(X, centers, K, comm: Comm, u, L, prune: bool = True, multi: bool = 
 
     if n:
         C.kpp_d2(X, centers[0], True, d2, bs, rpb)
+    # Per seeding step: L == 1 -- [all-gather of the W potentials] + sample + [all-reduce of
+    # the drawn row, straight into centers[k]]; greedy (L > 1) -- ONE all-gather (the L
+    # trials draw from the same D^2), L samples into cand, ONE all-reduce of cand [L, D],
+    # L potential passes, ONE all-reduce of the L potentials.  No host synchronisation.
     for k in range(1, K):
+        allt = None
+        if multi:
+            tot = bs.sum().reshape(1) if n else torch.zeros(1, dtype=torch.float64, device=dev)
+            allt = comm.all_gather(tot).reshape(-1)
         for t in range(L):
             uk = u[(k - 1) * L + t: (k - 1) * L + t + 1]
-            # the sampled row lands straight in centers[k] on one rank (L == 1)
-            row = centers[k] if (L == 1 and not multi) else crow
+            row = centers[k] if L == 1 else cand[t]
             if not multi:
                 C.kpp_sample(bs, d2, rpb, uk, X, row, None, 1, None, 0)  # target = u * total, on device
+            elif n:
+                C.kpp_sample(bs, d2, rpb, uk, X, row, None, 2, allt, comm.rank)  # owner's row, else zeros
             else:
-                tot = bs.sum().reshape(1) if n else torch.zeros(1, dtype=torch.float64, device=dev)
-                allt = comm.all_gather(tot).reshape(-1).contiguous()
-                if n:
-                    C.kpp_sample(bs, d2, rpb, uk, X, row, None, 2, allt, comm.rank)
-                else:
-                    row.zero_()
-                comm.allreduce_(row)
-            if L > 1:
-                cand[t] = row
-            elif row is not centers[k]:
-                centers[k] = row
+                row.zero_()
+        if multi:
+            comm.allreduce_(centers[k] if L == 1 else cand)
         if L == 1:
             if n:
                 d2_pass(centers[k], k, d2, bs, True)
@@ -195,22 +195,21 @@ def _kpp_cpu(X, centers, K, comm: Comm, u, L):
 
     d2 = dist_to(centers[0]) if n else torch.zeros(0)
     for k in range(1, K):
+        # one all-gather of the rank potentials and one all-reduce of the L drawn rows per
+        # step (the trials draw from the same D^2), as on the GPU
+        allt = comm.all_gather(d2.double().sum().reshape(1)).reshape(-1)
         cand = torch.zeros((L, D), dtype=torch.float32)
+        cs = torch.cumsum(d2.double(), 0) if n else None
         for t in range(L):
-            tot = d2.double().sum().reshape(1)
-            allt = comm.all_gather(tot).reshape(-1)
             target, _ = _local_target(allt, u[(k - 1) * L + t], comm.rank)
-            row = torch.zeros(D, dtype=torch.float32)
             tv = float(target.item())
             if tv >= 0 and n:
-                cs = torch.cumsum(d2.double(), 0)
                 i = int(torch.searchsorted(cs, torch.tensor([tv], dtype=torch.float64), right=True).item())
                 if i >= n or d2[min(i, n - 1)] <= 0:
                     pos = torch.nonzero(d2 > 0).flatten()
                     i = int(pos[-1].item()) if pos.numel() else 0
-                row = Xf[i].clone()
-            comm.allreduce_(row)
-            cand[t] = row
+                cand[t] = Xf[i]
+        comm.allreduce_(cand)
         if L == 1:
             centers[k] = cand[0]
         else:

@@ -154,3 +154,25 @@ def test_minibatch_fit_uneven_shards_same_step_count():
     assert len({o["steps"] for o in outs}) == 1
     for o in outs:
         assert torch.equal(o["C"], outs[0]["C"])
+
+
+def _kpp(comm, trials):
+    from mikmeans.models.init import init_kmeanspp
+
+    X = _data()
+    s, e = shard_range(N, comm.rank, comm.world)
+    return init_kmeanspp(X[s:e], D, K, N, s, comm, seed=9, n_local_trials=trials)
+
+
+@pytest.mark.parametrize("trials", [1, 3])
+def test_kmeanspp_world_size_invariant(trials):
+    """k-means++ (plain and greedy, one all-gather + one all-reduce of all L candidate rows
+    per step) gives the 1-rank centres bit for bit on W = 2/4/8 gloo ranks, empty shards
+    included (N=6000 covers 4 units of the 1536-row grid)."""
+    from mikmeans.parallel import Comm
+
+    ref = _kpp(Comm.local(), trials)
+    for world in (2, 4, 8):
+        outs = spawn_local(_kpp, world, trials)
+        for o in outs:
+            assert torch.equal(o, ref), (world, trials)
