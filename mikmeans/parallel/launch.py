@@ -50,7 +50,8 @@ def torchrun_cmd(nproc: int, script_argv: list[str], port: int | None = None) ->
             "--master-addr", "127.0.0.1", "--master-port", str(port or free_port()), *script_argv]
 
 
-def launch_self(nproc: int, script_argv: list[str], max_restarts: int = 0, env: dict | None = None) -> int:
+def launch_self(nproc: int, script_argv: list[str], max_restarts: int = 0, env: dict | None = None,
+                dmabuf_ipc: bool = False) -> int:
     """Start ``script_argv`` (a script path plus its arguments) as an ``nproc``-rank job and
     return its exit code -- the MI355X analogue of the reference meshing every tab on page
     load (app.mjs:70-118, called at :583).
@@ -61,7 +62,11 @@ def launch_self(nproc: int, script_argv: list[str], max_restarts: int = 0, env: 
     (``mikmeans fit --resume auto``), so a lost rank costs at most the work since it.
     """
     env = dict(os.environ if env is None else env)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    if dmabuf_ipc or os.environ.get("MIKMEANS_DMABUF_IPC", "0") not in ("", "0"):
+        # Opt-in: hosts whose amdgpu driver only supports dmabuf IPC need the HSA runtime's
+        # legacy IPC mode off, or RCCL's peer mappings fail with "hipIpcGetMemHandle: invalid
+        # argument".  Other hosts keep whatever the caller's environment says.
+        env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
     rc = 1
     for attempt in range(max_restarts + 1):
         cmd = torchrun_cmd(nproc, script_argv)
