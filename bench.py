@@ -299,16 +299,15 @@ def _bench_minibatch(args, cfg, comm, dtype):
             make_blobs(min(step_rows, S - i), D, K, seed=args.seed, i0=comm.rank * S + i, dtype=dtype,
                        device=dev, centers=centers, out=X[i : i + step_rows])
         C = native.require()
-        buf = torch.empty((b, D), dtype=dtype, device=dev)
-        xn = torch.empty(b, dtype=torch.float32, device=dev)
+        rows = torch.empty(b, dtype=torch.int64, device=dev)
         eng = MiniBatchEngine(K, D, b, dtype=dtype, device=dev, comm=comm)
         eng.set_bound(col_stats(X, stats=False).absmax)
         state = {"step": 0}
 
-        def gen():
-            C.sample_rows(X, buf, b, args.seed, comm.rank, state["step"], xn)
+        def gen():   # the step's Philox row draws; the assign / M-step read X[rows] in place
+            C.sample_index(S, b, args.seed, comm.rank, state["step"], rows)
             state["step"] += 1
-            return buf, xn
+            return X, rows
         extra["data_bytes_per_rank"] = S * D * X.element_size()
     else:
         stream = BlobStream(N, D, K, b, seed=args.seed, dtype=dtype, device=dev, rank=comm.rank,
@@ -320,10 +319,13 @@ def _bench_minibatch(args, cfg, comm, dtype):
         def gen():
             Xb = next(stream)
             return Xb, stream.last_norms
-    first, _ = gen()
+    step = eng.partial_fit_rows if args.resident else eng.partial_fit
+    first, r0 = gen()
+    first = first[r0] if args.resident else first
     eng.set_centers(init_random(first, D, K, b * comm.world, comm.rank * b, comm, args.seed))
+    del first
     for _ in range(args.warmup):
-        eng.partial_fit(*gen())
+        step(*gen())
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     comm.barrier()
@@ -333,7 +335,7 @@ def _bench_minibatch(args, cfg, comm, dtype):
         ev[i][0].record()
         Xb, nb = gen()
         ev[i][1].record()
-        eng.partial_fit(Xb, nb)
+        step(Xb, nb)
         ev[i][2].record()
     torch.cuda.synchronize()
     comm.barrier()

@@ -683,25 +683,25 @@ class MiniBatchKMeans(_Serving):
         # it from the global row count, never from this rank's shard size
         n_global, _ = _shard_info(n, comm, comm.device)
         steps = self.max_steps or max(1, math.ceil(self.max_iter * n_global / (self.batch_size * comm.world)))
-        buf = xn = None
+        buf = rows = None
         if eng.gpu and b:
-            Dp = eng.Dp
-            buf = torch.zeros((b, Dp), dtype=self.dtype, device=device)
-            xn = torch.empty(b, dtype=torch.float32, device=device)
+            if Xt is not None:    # device shard: the step reads X[rows] in place, nothing gathered
+                rows = torch.empty(b, dtype=torch.int64, device=device)
+            else:                 # host shard: the batch's rows are gathered on the host
+                buf = torch.zeros((b, eng.Dp), dtype=self.dtype, device=device)
         C = native_mod() if eng.gpu else None
         while eng.steps < steps:
             s = eng.steps
             if not n:
                 eng.partial_fit(X[:0].to(device) if not eng.gpu else buf_empty(eng, device))
-            elif eng.gpu and Xt is not None:
-                C.sample_rows(Xt, buf, b, self.seed, comm.rank, s, xn)       # on-device draw + gather
-                eng.partial_fit(buf, xn)
+            elif rows is not None:
+                C.sample_index(n, b, self.seed, comm.rank, s, rows)           # Philox draws on device
+                eng.partial_fit_rows(Xt, rows)
             else:
                 idx = torch.from_numpy(sample_indices(n, b, self.seed, comm.rank, s))
                 if eng.gpu:
                     buf[:, :D].copy_(Xh[idx].to(device, non_blocking=False))
-                    C.row_sqnorm(buf, xn)
-                    eng.partial_fit(buf, xn)
+                    eng.partial_fit(buf)
                 else:
                     eng.partial_fit(Xt[idx])
             faults.maybe_fail(comm.rank, eng.steps)

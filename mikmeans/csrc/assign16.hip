@@ -65,7 +65,7 @@ struct Assign16Cfg {
   static constexpr int NPW = PIECES / NW;
   static constexpr int PTS = NW * P * 16;
   static constexpr int PP = (P + 3) / 4 * 4;    // per-point offset slots per lane (LDS, f32x4 reads)
-  static constexpr int OPT_BYTES = NW * 16 * PP * 4;
+  static constexpr int OPT_BYTES = 2 * NW * 16 * PP * 4;   // offsets + gathered |x|^2
   static constexpr int NBUF = NBUF_;
   static_assert(NBUF == 2 || NBUF == 3, "ring depth");
   static_assert(chunk_tiles16(sizeof(T), DPAD) % CT == 0, "chunk must divide the Kpad granule");
@@ -177,18 +177,23 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   float off = 0.f;
   bool ppo = false;
   float* opt = (float*)(bufs + C::NBUF * C::CHUNK_BYTES + 16 * C::NW);  // [NW][16][PP] offsets
-  if constexpr (!EXACT) {
-    if (!a.xn) {
+  float* xnl = opt + C::NW * 16 * C::PP;                                 // [NW][16][PP] |x|^2
+  if (!a.xn && (!EXACT || a.slots)) {
 #pragma unroll
-      for (int p = 0; p < C::P; ++p) {
-        float s = 0.f;
+    for (int p = 0; p < C::P; ++p) {
+      float s = 0.f;
 #pragma unroll
-        for (int q = 0; q < C::NQ; ++q) s += sq16(xr[p][q], (T*)nullptr);
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        xnr[p] = s;
-      }
+      for (int q = 0; q < C::NQ; ++q) s += sq16(xr[p][q], (T*)nullptr);
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      xnr[p] = s;
     }
+    if (a.slots && g == 0) {   // no caller norms: the epilogue's inertia reads them back
+#pragma unroll
+      for (int p = 0; p < C::P; ++p) xnl[(wid * 16 + r) * C::PP + p] = xnr[p];
+    }
+  }
+  if constexpr (!EXACT) {
     float m = 0.f, mn = 3.0e38f;
 #pragma unroll
     for (int p = 0; p < C::P; ++p) { m = fmaxf(m, xnr[p]); mn = fminf(mn, xnr[p]); }
@@ -373,6 +378,8 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     }
     // this point's seed offset (0 for f32)
     const float offp = ppo ? opt[(wid * 16 + r) * C::PP + p] : off;
+    // inertia without caller norms: the prologue parked |x|^2 of the fragments in LDS
+    const float xv = (a.slots && !a.xn) ? xnl[(wid * 16 + r) * C::PP + p] : 0.f;
     if ((p & 3) == g) {
       const int64_t i = pbase + p * 16 + r;
       if (a.split_keys) {
@@ -386,8 +393,8 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         v -= offp;   // back to |c|^2 - 2 x.c
         if (a.track_changed) changed += (a.labels[i] != k);
         a.labels[i] = k;
-        if (a.xn) {
-          const float d = fmaxf(a.xn[i] + v, 0.f);
+        if (a.xn || a.slots) {
+          const float d = fmaxf((a.xn ? a.xn[i] : xv) + v, 0.f);
           inert += d;
           if (a.mind) a.mind[i] = d;
         }

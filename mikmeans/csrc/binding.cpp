@@ -73,10 +73,18 @@ void check_i64(const Tensor& t, const char* name, int64_t numel_min);
 void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::optional<Tensor>& xn,
             const Tensor& labels, const c10::optional<Tensor>& mind,
             const c10::optional<Tensor>& slots, int64_t Kpad, int64_t dpad, bool track_changed,
-            const c10::optional<Tensor>& keys) {
+            const c10::optional<Tensor>& keys, const c10::optional<Tensor>& rows) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
-  const int64_t N = X.size(0);
+  // gathered batch: N logical rows, row i = X[rows[i]] (indices from sample_index: in range
+  // by construction -- the binding cannot check them without a device sync)
+  const bool gathered = rows.has_value() && rows->defined();
+  if (gathered) {
+    check_i64(*rows, "rows", 0);
+    TORCH_CHECK(X.size(0) > 0 || rows->numel() == 0, "mikmeans: gathered rows from an empty X");
+    TORCH_CHECK(!(keys.has_value() && keys->defined()), "mikmeans: gathered rows take the one-pass grid");
+  }
+  const int64_t N = gathered ? rows->numel() : X.size(0);
   const int D = (int)X.size(1);
   TORCH_CHECK(D <= dpad, "mikmeans: D exceeds dpad");
   TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, (int)Kpad) == Kpad, "mikmeans: bad Kpad ", Kpad, " for dpad ",
@@ -106,6 +114,7 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
     TORCH_CHECK(!xn.has_value() || mind.has_value(), "mikmeans: split assign with xn needs mind");
     a.split_keys = (unsigned long long*)keys->data_ptr<int64_t>();
   }
+  if (gathered) a.rows = rows->data_ptr<int64_t>();
   hip_check(mk::launch_assign16(dt, (int)dpad, a, stream()), "assign");
 }
 
@@ -119,10 +128,18 @@ void check_i64(const Tensor& t, const char* name, int64_t numel_min) {
 void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab,
             const Tensor& cnt_slab, int64_t n_chunks, const c10::optional<Tensor>& weights,
             const Tensor& col_exp, int64_t cnt_exp, bool clamp,
-            const c10::optional<Tensor>& clamp_count, const c10::optional<Tensor>& col_exp2) {
+            const c10::optional<Tensor>& clamp_count, const c10::optional<Tensor>& col_exp2,
+            const c10::optional<Tensor>& rows) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
-  const int64_t N = X.size(0);
+  const bool gathered = rows.has_value() && rows->defined();
+  if (gathered) {
+    check_i64(*rows, "rows", 0);
+    TORCH_CHECK(!clamp && !(col_exp2.has_value() && col_exp2->defined()),
+                "mikmeans: gathered rows take plain (bounded) M-step passes");
+    TORCH_CHECK(X.size(0) > 0 || rows->numel() == 0, "mikmeans: gathered rows from an empty X");
+  }
+  const int64_t N = gathered ? rows->numel() : X.size(0);
   const int D = (int)X.size(1);
   TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kInt && labels.numel() >= N,
               "mikmeans: labels must be int32 [N]");
@@ -151,6 +168,7 @@ void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab
     check_i32(*col_exp2, "col_exp2", D);
     a.col_exp2 = col_exp2->data_ptr<int32_t>();
   }
+  if (gathered) a.rows = rows->data_ptr<int64_t>();
   hip_check(mk::launch_update(dt, a, stream()), "update");
 }
 
@@ -342,6 +360,16 @@ void sample_rows(const Tensor& X, const Tensor& out, int64_t b, int64_t seed, in
             "sample_rows");
 }
 
+void sample_index(int64_t n, int64_t b, int64_t seed, int64_t rank, int64_t step, const Tensor& idx) {
+  check_i64(idx, "idx", b);
+  TORCH_CHECK(b >= 0 && b < ((int64_t)1 << 32) && rank >= 0 && step >= 0 && step < ((int64_t)1 << 32),
+              "mikmeans: sample_index range");
+  TORCH_CHECK(b == 0 || n > 0, "mikmeans: sample_index from an empty shard");
+  hip_check(mk::launch_sample_index(n, b, (uint64_t)seed, (uint32_t)rank, (uint32_t)step,
+                                    idx.data_ptr<int64_t>(), stream()),
+            "sample_index");
+}
+
 void row_normalize(const Tensor& X, const c10::optional<Tensor>& xn) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
@@ -501,11 +529,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mikmeans native ops (gfx950 HIP kernels + host helpers)";
   m.def("assign", &assign, "fused MFMA distance + argmin (K2)", py::arg("X"), py::arg("pack"), py::arg("cn"),
         py::arg("xn"), py::arg("labels"), py::arg("mind"), py::arg("slots"), py::arg("Kpad"), py::arg("dpad"),
-        py::arg("track_changed"), py::arg("keys") = py::none());
+        py::arg("track_changed"), py::arg("keys") = py::none(), py::arg("rows") = py::none());
   m.def("update", &update, "LDS-privatised per-cluster sums/counts (K3)", py::arg("X"), py::arg("labels"),
         py::arg("K"), py::arg("slab"), py::arg("cnt_slab"), py::arg("n_chunks"), py::arg("weights"),
         py::arg("col_exp"), py::arg("cnt_exp"), py::arg("clamp"), py::arg("clamp_count") = py::none(),
-        py::arg("col_exp2") = py::none());
+        py::arg("col_exp2") = py::none(), py::arg("rows") = py::none());
   m.def("reduce_cols", &reduce_cols, "lo sums of the wide-range columns (residual pass)");
   m.def("reduce", &reduce, "slab reduction into the packed f64 all-reduce message");
   m.def("label_delta", &label_delta, "changed-row list for the incremental M-step");
@@ -520,6 +548,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample_rows", &sample_rows, "mini-batch rows X[philox(seed; j, step, rank) * n] (+ norms, indices)",
         py::arg("X"), py::arg("out"), py::arg("b"), py::arg("seed"), py::arg("rank"), py::arg("step"),
         py::arg("xn") = py::none(), py::arg("idx_out") = py::none());
+  m.def("sample_index", &sample_index, "the mini-batch sampler's source rows of one step (int64 [b])");
   m.def("row_normalize", &row_normalize, "in-place unit rows (cosine metric)", py::arg("X"), py::arg("xn") = py::none());
   m.def("wdot", &wdot, "out[0] += sum a*b in f64 (weighted inertia)");
   m.def("kpp_d2", &kpp_d2, "k-means++ D^2 update (K5; triangle-inequality pruned with owner/cc)",

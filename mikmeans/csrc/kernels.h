@@ -43,6 +43,9 @@ struct AssignArgs {
   // optional u64 [N] all-ones scratch; small N then splits the centre range over
   // grid.y (split_finish_kernel writes labels and restores the all-ones)
   unsigned long long* split_keys = nullptr;
+  // optional gathered batch: logical row i is X row rows[i] (labels / mind / xn stay
+  // logical; without xn the inertia uses |x|^2 of the gathered fragments)
+  const int64_t* rows = nullptr;
 };
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 
@@ -74,6 +77,9 @@ struct UpdateArgs {
   const int2* dlist = nullptr;
   const int* dcount = nullptr;
   int dcap = 0;
+  // Gathered batch (optional, plain passes only): logical row i is X row rows[i], so a
+  // mini-batch drawn from an HBM-resident shard is never copied (labels / weights logical).
+  const int64_t* rows = nullptr;
 };
 int update_slice_width(int dtype, int K, int D, bool weighted = false);  // 0 = global fallback
 int update_n_chunks(int dtype, int K, int D, int64_t N, bool weighted = false);
@@ -130,6 +136,9 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
 hipError_t launch_sample_rows(int dtype, const void* X, int64_t n, int64_t ldx, int D, void* out,
                               int64_t ldo, int64_t b, uint64_t seed, uint32_t rank, uint32_t step,
                               float* xn, int64_t* idx_out, hipStream_t s);
+// idx[j] = the sampler's source row of batch row j (the same draws as launch_sample_rows).
+hipError_t launch_sample_index(int64_t n, int64_t b, uint64_t seed, uint32_t rank, uint32_t step, int64_t* idx,
+                               hipStream_t s);
 // In place x <- x / max(|x|, 1e-30) per row (cosine metric); xn (optional) = |x_rounded|^2.
 hipError_t launch_row_normalize(int dtype, void* X, int64_t N, int D, int64_t ldx, float* xn, hipStream_t s);
 // out[0] += sum a[i] * b[i] (f64 accumulation).

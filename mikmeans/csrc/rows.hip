@@ -98,6 +98,21 @@ hipError_t launch_sample_rows(int dtype, const void* X, int64_t n, int64_t ldx, 
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void sample_index_kernel(int64_t n, int64_t b, uint32_t k0, uint32_t k1,
+                                                           uint32_t rank, uint32_t step, int64_t* idx) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < b) idx[j] = sample_index(j, step, rank, n, k0, k1);
+}
+
+hipError_t launch_sample_index(int64_t n, int64_t b, uint64_t seed, uint32_t rank, uint32_t step, int64_t* idx,
+                               hipStream_t s) {
+  if (b <= 0) return hipSuccess;
+  if (n <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sample_index_kernel, dim3((unsigned)((b + 255) / 256)), dim3(256), 0, s, n, b,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), rank, step, idx);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // In-place unit rows: x <- x / max(|x|, 1e-30), f32 arithmetic (norm of the stored values,
 // IEEE sqrt and division), rounded back to the storage type; xn (optional) receives the

@@ -217,7 +217,7 @@ __device__ void upd_flush_all(const UpdateArgs& a, const UpdLayout& L, char* m, 
   }
 }
 
-enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8, UPD_RESID = 32 };
+enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8, UPD_RESID = 32, UPD_GATHER = 64 };
 
 constexpr int upd_ksh(int np) { return np >= 32 ? 0 : np == 16 ? 1 : np == 8 ? 2 : np == 4 ? 3 : np == 2 ? 4 : 5; }
 using plan::upd_lds_bytes;
@@ -231,6 +231,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   constexpr bool W = MODE & (UPD_WEIGHTED | UPD_DELTA);  // per-row signed weights
   constexpr bool SWZ = MODE & UPD_SWZ;
   constexpr bool RESID = MODE & UPD_RESID;               // lo pass of the wide-range columns
+  constexpr bool GATHER = MODE & UPD_GATHER;             // logical row i is X row a.rows[i]
   constexpr int ES = sizeof(T);
   constexpr int PB = (SW * ES >= 16) ? 16 : SW * ES;  // bytes per lane load
   constexpr int V = PB / ES;                           // elements per lane load (even)
@@ -330,7 +331,10 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
         lab_[u] = ((unsigned)l < (unsigned)a.K) ? l : a.K;
         if constexpr (DELTA) wt_[u] = wrow ? wrow[off + u] : 1.f;
         else if constexpr (W) wt_[u] = wrow[off + u];
-        w_[u] = *(const LT*)(p + u * a.ldx);
+        if constexpr (GATHER)
+          w_[u] = *(const LT*)((const T*)a.X + a.rows[base + (int64_t)lr * UNR + u] * a.ldx + colc);
+        else
+          w_[u] = *(const LT*)(p + u * a.ldx);
       }
     } else {                                           // clamp rows past the chunk -> sink row K
 #pragma unroll
@@ -341,7 +345,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
         lab_[u] = (i0 < row1 && (unsigned)l < (unsigned)a.K) ? l : a.K;
         if constexpr (DELTA) wt_[u] = a.weights ? a.weights[i] : 1.f;
         else if constexpr (W) wt_[u] = a.weights[i];
-        w_[u] = *(const LT*)((const T*)a.X + i * a.ldx + colc);
+        w_[u] = *(const LT*)((const T*)a.X + (GATHER ? a.rows[i] : i) * a.ldx + colc);
       }
     }
     if (!all_cols && !colok) {
@@ -498,7 +502,7 @@ __device__ void ks_flush(const UpdateArgs& a, char* m, int kq, int kn, int ldc, 
   __syncthreads();
 }
 
-template <typename T, int LPR, int GM, bool CLAMP>
+template <typename T, int LPR, int GM, bool CLAMP, bool GATHER = false>
 __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, int ks, int kq, int ldc,
                                                                 int64_t rows_per_chunk) {
   constexpr int NT = plan::KS_NT;
@@ -559,7 +563,7 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
       const bool v = e < cnt;
       const unsigned ent = lst[v ? e : 0];
       const int64_t row = v ? wbase + (int64_t)(ent & 63u) : rsafe;
-      xb[j] = *(const u32x4*)(xcol + row * a.ldx);
+      xb[j] = *(const u32x4*)(xcol + (GATHER ? a.rows[row] : row) * a.ldx);
       lb[j] = v ? (int)(ent >> 6) : -1;
     }
   };
@@ -612,7 +616,8 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
       const int e = g0 + rr;
       if (e < cnt) {
         const unsigned ent = lbuf0[e];
-        const u32x4 w = *(const u32x4*)(xcol + (base + wid * 64 + (int64_t)(ent & 63u)) * a.ldx);
+        const int64_t row = base + wid * 64 + (int64_t)(ent & 63u);
+        const u32x4 w = *(const u32x4*)(xcol + (GATHER ? a.rows[row] : row) * a.ldx);
         accumulate(w, (int)(ent >> 6));
       }
     }
@@ -650,7 +655,7 @@ __global__ __launch_bounds__(256) void update_global_kernel(UpdateArgs a) {
   const int k = a.labels[i];
   if ((unsigned)k >= (unsigned)a.K) return;
   const float wt = a.weights ? a.weights[i] : 1.f;
-  const T* xr = (const T*)a.X + i * a.ldx;
+  const T* xr = (const T*)a.X + (a.rows ? a.rows[i] : i) * a.ldx;
   for (int d = lane; d < a.D; d += 64)
     atomicAdd((unsigned long long*)(a.slab + (int64_t)k * a.D + d),
               (unsigned long long)fx_q(Elem<T>::to_f32(xr[d]), ldexpf(1.f, a.col_exp[d]) * wt));
@@ -752,12 +757,21 @@ static hipError_t launch_clamp(const UpdateArgs& a, int ldc, hipStream_t s) {
   const int mode = (a.clamp ? UPD_CLAMP : 0) | (a.weights ? UPD_WEIGHTED : 0) |
                    (ldc == SW / 2 ? UPD_SWZ : 0);
   if (a.col_exp2) {  // residual (lo) pass of the wide-range columns: never clamped / incremental
-    if (a.clamp || a.dlist) return hipErrorInvalidValue;
+    if (a.clamp || a.dlist || a.rows) return hipErrorInvalidValue;
     switch (mode) {
       case 0: return launch_sw<T, SW, UPD_RESID>(a, ldc, s);
       case 2: return launch_sw<T, SW, UPD_RESID | UPD_WEIGHTED>(a, ldc, s);
       case 4: return launch_sw<T, SW, UPD_RESID | UPD_SWZ>(a, ldc, s);
       default: return launch_sw<T, SW, UPD_RESID | UPD_WEIGHTED | UPD_SWZ>(a, ldc, s);
+    }
+  }
+  if (a.rows) {  // gathered mini-batch rows: plain (bounded, unclamped) passes only
+    if (a.clamp || a.dlist) return hipErrorInvalidValue;
+    switch (mode) {
+      case 0: return launch_sw<T, SW, UPD_GATHER>(a, ldc, s);
+      case 2: return launch_sw<T, SW, UPD_GATHER | UPD_WEIGHTED>(a, ldc, s);
+      case 4: return launch_sw<T, SW, UPD_GATHER | UPD_SWZ>(a, ldc, s);
+      default: return launch_sw<T, SW, UPD_GATHER | UPD_WEIGHTED | UPD_SWZ>(a, ldc, s);
     }
   }
   if (a.dlist) {  // incremental M-step (Lloyd: never clamped; weights read at run time)
@@ -795,16 +809,16 @@ static hipError_t launch_update_t(const UpdateArgs& a, hipStream_t s, int sw, in
   return hipErrorInvalidValue;
 }
 
-template <typename T, int LPR, int GM, bool CLAMP>
+template <typename T, int LPR, int GM, bool CLAMP, bool GATHER = false>
 static hipError_t launch_ks_t(const UpdateArgs& a, const plan::KsPlan& kp, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)update_ks_kernel<T, LPR, GM, CLAMP>,
+    (void)hipFuncSetAttribute((const void*)update_ks_kernel<T, LPR, GM, CLAMP, GATHER>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)UPD_LDS_MAX);
     attr = true;
   }
   const int64_t rows_per_chunk = (a.N + a.n_chunks - 1) / a.n_chunks;
-  hipLaunchKernelGGL((update_ks_kernel<T, LPR, GM, CLAMP>), dim3((unsigned)(a.n_chunks * kp.ks)),
+  hipLaunchKernelGGL((update_ks_kernel<T, LPR, GM, CLAMP, GATHER>), dim3((unsigned)(a.n_chunks * kp.ks)),
                      dim3(plan::KS_NT), plan::ks_lds_bytes(kp.kq, kp.ldc), s, a, kp.ks, kp.kq, kp.ldc,
                      rows_per_chunk);
   return hipGetLastError();
@@ -812,6 +826,12 @@ static hipError_t launch_ks_t(const UpdateArgs& a, const plan::KsPlan& kp, hipSt
 
 template <typename T, int LPR>
 static hipError_t launch_ks_l(const UpdateArgs& a, const plan::KsPlan& kp, hipStream_t s) {
+  if (a.rows) {  // gathered mini-batch rows (bounded scales: never clamped)
+    if (a.clamp) return hipErrorInvalidValue;
+    if (kp.gm == 6) return launch_ks_t<T, LPR, 6, false, true>(a, kp, s);
+    if (kp.gm == 3) return launch_ks_t<T, LPR, 3, false, true>(a, kp, s);
+    return launch_ks_t<T, LPR, 2, false, true>(a, kp, s);
+  }
   if (kp.gm == 6) return a.clamp ? launch_ks_t<T, LPR, 6, true>(a, kp, s) : launch_ks_t<T, LPR, 6, false>(a, kp, s);
   if (kp.gm == 3) return a.clamp ? launch_ks_t<T, LPR, 3, true>(a, kp, s) : launch_ks_t<T, LPR, 3, false>(a, kp, s);
   return a.clamp ? launch_ks_t<T, LPR, 2, true>(a, kp, s) : launch_ks_t<T, LPR, 2, false>(a, kp, s);

@@ -84,9 +84,9 @@ class MiniBatchEngine:
         return self.C[:, : self.D]
 
     def partial_fit(self, Xb: torch.Tensor, norms: torch.Tensor | None = None):
-        """One mini-batch step on this rank's batch ``Xb`` (may be empty).  ``norms``:
-        precomputed squared row norms (e.g. fused into the blob generator); the GPU
-        path otherwise runs a row-norm pass for the batch inertia."""
+        """One mini-batch step on this rank's batch ``Xb`` (may be empty).  ``norms`` is
+        accepted for API compatibility and unused: the GPU assign takes |x|^2 from the row
+        fragments it loads anyway (key offsets and the batch inertia)."""
         if self.gpu:
             self._step_gpu(Xb, norms)
         else:
@@ -146,14 +146,14 @@ class MiniBatchEngine:
         self.col_exp, _ = fixed_exps(Xb, None, comm=self.comm, bound=bound)   # bound all-reduced (MAX)
         self.bound = bound
 
-    def _mstep(self, Xb, lab):
+    def _mstep(self, Xb, lab, rows=None):
         C = self._C
         KD = self.K * self.Dp
-        if Xb.shape[0]:
+        if (rows.numel() if rows is not None else Xb.shape[0]):
             # a given value bound cannot be exceeded: no clamp, no count (the plain kernel)
             bounded = self.bounded
             C.update(Xb, lab, self.K, self.slab, self.cnt_slab, self.n_chunks, None, self.col_exp, 0,
-                     not bounded, clamp_count=None if bounded else self.clampc)
+                     not bounded, clamp_count=None if bounded else self.clampc, rows=rows)
             C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots, self.packed,
                      self.col_exp, 0)
             self.packed[KD + self.K + 2] = self.clampc[0].double()
@@ -161,6 +161,28 @@ class MiniBatchEngine:
         else:
             self.packed.zero_()
         self.comm.allreduce_(self.packed)
+
+    def partial_fit_rows(self, X: torch.Tensor, rows: torch.Tensor):
+        """One step on the batch ``X[rows]`` without materialising it: the assign and the
+        M-step read the sampled rows of the (device-resident, column-padded) shard through
+        the index list (csrc/assign16.hip, csrc/update.hip ``rows``).  Needs fixed scales
+        (:meth:`set_bound`); the same centres as :meth:`partial_fit` on the gathered batch."""
+        if not self.gpu:
+            self.partial_fit(X[rows.to(X.device)] if rows.numel() else X[:0])
+            return
+        if not self.bounded:
+            raise RuntimeError("partial_fit_rows needs fixed scales: call set_bound() first")
+        b = rows.numel()
+        if b > self.batch:
+            raise ValueError(f"batch of {b} rows exceeds the engine's batch_size {self.batch}")
+        Xp = pad_columns(X, self.dtype)
+        lab = self.labels[:b]
+        if b:
+            self.pk.assign(Xp, None, lab, None, self.slots, False, rows=rows)
+        self._mstep(Xp, lab, rows)
+        self.pk.finalize(2, self.packed, self.C, self.Cnew, self.frozen, self.vcount, self.shift, self.counts)
+        self.C, self.Cnew = self.Cnew, self.C
+        self.steps += 1
 
     def _step_gpu(self, Xb, norms=None):
         C = self._C
@@ -172,12 +194,9 @@ class MiniBatchEngine:
             self._set_bound(Xb)
         lab = self.labels[:b]
         if b:
-            if norms is not None and norms.shape[0] >= b and norms.dtype == torch.float32 and norms.is_cuda:
-                xn = norms[:b].contiguous()
-            else:
-                xn = self.xn[:b]
-                C.row_sqnorm(Xb, xn)
-            self.pk.assign(Xb, xn, lab, None, self.slots, False)
+            # key offsets and the inertia from the row fragments (no caller norms): the
+            # gathered-row path (partial_fit_rows) computes them the same way, bit for bit
+            self.pk.assign(Xb, None, lab, None, self.slots, False)
         self._mstep(Xb, lab)
         if not self.bounded:
             # one host read per step: the all-reduced clamp count is the same on every rank,

@@ -96,8 +96,13 @@ class CentroidPack:
         self._C.finalize(mode, packed, Cold, Cnew, frozen, mb_counts, self.pack, self.cn, shift, counts,
                          self.dpad, self.Kpad)
 
-    def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False):
-        """K2 on these centres (``X`` column-padded, 16-B rows)."""
+    def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False, rows=None):
+        """K2 on these centres (``X`` column-padded, 16-B rows).  ``rows`` (int64, device):
+        assign the gathered batch X[rows] without materialising it (labels etc. logical)."""
+        if rows is not None:
+            self._C.assign(X, self.pack, self.cn, xn, labels, mind, slots, self.Kpad, self.dpad,
+                           track_changed, None, rows)
+            return
         keys = None
         if 0 < X.shape[0] <= SPLIT_MAX_ROWS:
             # small batches split the centre range across workgroups (assign16 grid.y);

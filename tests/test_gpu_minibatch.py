@@ -105,3 +105,31 @@ def test_minibatch_fit_steps_do_not_sync(native):
     assert eng.rescales == 0 and km.n_steps_ == 40
     # setup (bound, shard sizes, init) costs a few reads; the loop at most 1 per 10 steps
     assert per_step <= 0.1 + 12 / 40, per_step
+
+
+@pytest.mark.parametrize("D,K,dtype", [(256, 512, torch.bfloat16), (128, 1024, torch.bfloat16),
+                                       (64, 4096, torch.bfloat16), (128, 256, torch.float32),
+                                       (40, 70000, torch.float32)])
+def test_gathered_rows_step_equals_materialised_batch(native, D, K, dtype):
+    """partial_fit_rows (assign + M-step reading X[rows] through the index list: slice,
+    K-split and global-atomic M-step kernels) equals partial_fit on the gathered copy."""
+    from mikmeans.models.minibatch import MiniBatchEngine
+    from mikmeans.ops import col_stats, pad_columns
+
+    n, b = 300_000, 40_000
+    X = pad_columns(B.make_blobs(n, D, 64, seed=D, dtype=dtype, device=DEV))
+    rows = torch.empty(b, dtype=torch.int64, device=DEV)
+    bound = col_stats(X, stats=False).absmax
+    ea = MiniBatchEngine(K, D, b, dtype=dtype, device=DEV).set_bound(bound)
+    eb = MiniBatchEngine(K, D, b, dtype=dtype, device=DEV).set_bound(bound)
+    C0 = X[torch.randperm(n, generator=torch.Generator().manual_seed(0))[:K].to(DEV), :D].float()
+    ea.set_centers(C0)
+    eb.set_centers(C0)
+    for s in range(3):
+        native.sample_index(n, b, 7, 0, s, rows)
+        ea.partial_fit_rows(X, rows)
+        eb.partial_fit(X[rows])
+        torch.cuda.synchronize()
+        assert torch.equal(ea.labels[:b], eb.labels[:b]), s
+        assert torch.equal(ea.C, eb.C) and torch.equal(ea.vcount, eb.vcount), s
+    assert ea.last_batch_inertia() == pytest.approx(eb.last_batch_inertia(), rel=1e-9)
