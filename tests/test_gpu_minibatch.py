@@ -116,7 +116,7 @@ def test_gathered_rows_step_equals_materialised_batch(native, D, K, dtype):
     from mikmeans.models.minibatch import MiniBatchEngine
     from mikmeans.ops import col_stats, pad_columns
 
-    n, b = 300_000, 40_000
+    n, b = 600_000, 270_000     # b > SPLIT_MAX_ROWS: both paths take the one-pass assign grid
     X = pad_columns(B.make_blobs(n, D, 64, seed=D, dtype=dtype, device=DEV))
     rows = torch.empty(b, dtype=torch.int64, device=DEV)
     bound = col_stats(X, stats=False).absmax
