@@ -428,7 +428,9 @@ class KMeans(_Serving):
             inert = torch.zeros(1, dtype=torch.float64, device=comm.device)
             if eng.n:
                 if eng.weights is not None and eng.gpu:
-                    native_mod().wdot(mind, eng.weights, inert)
+                    C_ = native_mod()
+                    C_.wdot(mind, eng.weights, inert,
+                            torch.empty(C_.WDOT_SCRATCH, dtype=torch.float64, device=mind.device))
                 elif eng.weights is not None:
                     inert += (mind.double() * eng.weights.double()).sum().to(inert.device)
                 else:

@@ -378,11 +378,13 @@ void row_normalize(const Tensor& X, const c10::optional<Tensor>& xn) {
             "row_normalize");
 }
 
-void wdot(const Tensor& a, const Tensor& b, const Tensor& out) {
+void wdot(const Tensor& a, const Tensor& b, const Tensor& out, const Tensor& scratch) {
   check_f32(a, "a");
   check_f32(b, "b", a.numel());
   check_f64(out, "out", 1);
-  hip_check(mk::launch_wdot(a.data_ptr<float>(), b.data_ptr<float>(), a.numel(), out.data_ptr<double>(), stream()),
+  check_f64(scratch, "scratch", mk::wdot_scratch_len());
+  hip_check(mk::launch_wdot(a.data_ptr<float>(), b.data_ptr<float>(), a.numel(), out.data_ptr<double>(),
+                            scratch.data_ptr<double>(), stream()),
             "wdot");
 }
 
@@ -550,7 +552,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("xn") = py::none(), py::arg("idx_out") = py::none());
   m.def("sample_index", &sample_index, "the mini-batch sampler's source rows of one step (int64 [b])");
   m.def("row_normalize", &row_normalize, "in-place unit rows (cosine metric)", py::arg("X"), py::arg("xn") = py::none());
-  m.def("wdot", &wdot, "out[0] += sum a*b in f64 (weighted inertia)");
+  m.def("wdot", &wdot, "out[0] += sum a*b in f64, fixed order (weighted inertia)");
+  m.attr("WDOT_SCRATCH") = mk::wdot_scratch_len();
   m.def("kpp_d2", &kpp_d2, "k-means++ D^2 update (K5; triangle-inequality pruned with owner/cc)",
         py::arg("X"), py::arg("c"), py::arg("first"), py::arg("d2"), py::arg("block_sums"),
         py::arg("rows_per_block"), py::arg("owner") = py::none(), py::arg("cc") = py::none(),

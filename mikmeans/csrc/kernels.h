@@ -141,8 +141,9 @@ hipError_t launch_sample_index(int64_t n, int64_t b, uint64_t seed, uint32_t ran
                                hipStream_t s);
 // In place x <- x / max(|x|, 1e-30) per row (cosine metric); xn (optional) = |x_rounded|^2.
 hipError_t launch_row_normalize(int dtype, void* X, int64_t N, int D, int64_t ldx, float* xn, hipStream_t s);
-// out[0] += sum a[i] * b[i] (f64 accumulation).
-hipError_t launch_wdot(const float* a, const float* b, int64_t n, double* out, hipStream_t s);
+// out[0] += sum a[i] * b[i] (f64 accumulation, deterministic order; scratch: wdot_scratch_len() f64).
+int wdot_scratch_len();
+hipError_t launch_wdot(const float* a, const float* b, int64_t n, double* out, double* scratch, hipStream_t s);
 
 // ---- k-means++ ---------------------------------------------------------------
 // With owner[N] (int32: centre each d2 was measured against) and cc[k] (|c - c_j|^2, from

@@ -170,8 +170,13 @@ hipError_t launch_row_normalize(int dtype, void* X, int64_t N, int D, int64_t ld
 
 // ---------------------------------------------------------------------------
 // out[0] += sum_i a[i] * b[i] in f64 (weighted inertia: a = squared distances, b = weights).
-__global__ __launch_bounds__(256) void wdot_kernel(const float* __restrict__ a, const float* __restrict__ b,
-                                                   int64_t n, double* out) {
+// Deterministic: a fixed grid of WDOT_BLOCKS blocks writes per-block partials (each summed
+// in a fixed order), and one block adds them in index order -- the same bits on every run,
+// so a hipGraph replay reproduces the eager step exactly.
+constexpr int WDOT_BLOCKS = 1024;
+
+__global__ __launch_bounds__(256) void wdot_partial_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                           int64_t n, double* __restrict__ part) {
   double acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     acc += (double)a[i] * (double)b[i];
@@ -179,14 +184,27 @@ __global__ __launch_bounds__(256) void wdot_kernel(const float* __restrict__ a, 
   __shared__ double red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-hipError_t launch_wdot(const float* a, const float* b, int64_t n, double* out, hipStream_t s) {
+__global__ __launch_bounds__(256) void wdot_final_kernel(const double* __restrict__ part, int nb, double* out) {
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) acc += part[i];
+  acc = wave_sum(acc);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] += (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+int wdot_scratch_len() { return WDOT_BLOCKS; }
+
+hipError_t launch_wdot(const float* a, const float* b, int64_t n, double* out, double* scratch, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   int64_t nb = (n + 255) / 256;
-  if (nb > 1024) nb = 1024;
-  hipLaunchKernelGGL(wdot_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, b, n, out);
+  if (nb > WDOT_BLOCKS) nb = WDOT_BLOCKS;
+  hipLaunchKernelGGL(wdot_partial_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, b, n, scratch);
+  hipLaunchKernelGGL(wdot_final_kernel, dim3(1), dim3(256), 0, s, scratch, (int)nb, out);
   return hipGetLastError();
 }
 

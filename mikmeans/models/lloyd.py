@@ -181,6 +181,7 @@ class LloydEngine:
                                       dtype=torch.float64, device=dev)
         if self.weights is not None:
             self.mind = torch.empty(self.n, dtype=torch.float32, device=dev)
+            self._wscratch = torch.empty(C.WDOT_SCRATCH, dtype=torch.float64, device=dev)
         self.delta = None
         if self.incremental:
             if self.scales.nw:
@@ -210,6 +211,7 @@ class LloydEngine:
              "counts": self.counts, "pack": self.pk.pack, "cn": self.pk.cn, "slots": self.slots}
         if self.weights is not None:
             t["weights"] = self.weights
+            t["wdot_scratch"] = self._wscratch
         if self.mind is not None:
             t["mind"] = self.mind
         if self.pk._keys is not None:
@@ -354,7 +356,9 @@ class LloydEngine:
         KD = self.K * self.Dp
         slot = self.packed[KD + self.K : KD + self.K + 1]
         slot.zero_()
-        self._C.wdot(self.mind, self.weights, slot)
+        if getattr(self, "_wscratch", None) is None:
+            self._wscratch = torch.empty(self._C.WDOT_SCRATCH, dtype=torch.float64, device=self.device)
+        self._C.wdot(self.mind, self.weights, slot, self._wscratch)
 
     def _project_sphere(self):
         """Cnew <- Cnew / |Cnew| (empty / frozen rows are already unit or kept), then the

@@ -79,6 +79,7 @@ class StreamingLloydEngine(LloydEngine):
         self.weights = None
         if sample_weight is not None:
             self.weights = sample_weight.to(device=dev, dtype=torch.float32).contiguous()
+            self._wscratch = torch.empty(C.WDOT_SCRATCH, dtype=torch.float64, device=dev)
         # chunks start on the 1536-row grid of the resident fit (csrc/assign16.hip seed offset)
         self.R = stream_chunk_rows(chunk_rows, self.n)
         self.ranges = [(r, min(r + self.R, self.n)) for r in range(0, self.n, self.R)]

@@ -33,6 +33,7 @@ GRANULE = 512                    # torch caching allocator rounding of every blo
 ROW_ALIGN = 1536                 # parallel/shard.py: shard / chunk row grid
 SPLIT_MAX_ROWS = 1 << 18         # ops.SPLIT_MAX_ROWS: small batches keep u64 split keys
 NSLOT, SLOT_STRIDE = 256, 8      # csrc/kernels.h
+WDOT_SCRATCH = 1024              # csrc/rows.hip WDOT_BLOCKS (weighted-inertia partials)
 UPD_LDS_MAX = 160 * 1024         # csrc/plan.h
 KS_NT = 1024
 KS_LIST_BYTES = 2 * (KS_NT // 64) * 64 * 4
@@ -177,8 +178,7 @@ def kpp_workspace(n: int, Dp: int, K: int, trials: int = 1, prune: bool = True) 
     rpb = max(256, _cdiv(n, 2048)) if n else 256
     nb = max(1, _cdiv(n, rpb))
     it = {"kpp_centers": _r(K * Dp * 4), "kpp_u": _r(max(0, K - 1) * trials * 8),
-          "kpp_d2": _r(max(n, 1) * 4), "kpp_block_sums": _r(nb * 8), "kpp_crow": _r(Dp * 4),
-          "kpp_cand": _r(trials * Dp * 4)}
+          "kpp_d2": _r(max(n, 1) * 4), "kpp_block_sums": _r(nb * 8), "kpp_cand": _r(trials * Dp * 4)}
     if prune:
         it["kpp_owner"] = _r(max(n, 1) * 4)
         it["kpp_cc"] = _r(K * 4)
@@ -261,6 +261,7 @@ def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = 
     p["xn"] = _r(n * 4)
     if weighted:
         p["mind"] = _r(n * 4)
+        p["wdot_scratch"] = _r(WDOT_SCRATCH * 8)
     nch = update_n_chunks(es, K, Dp, max(n, 1), wted or incremental)
     p["slab"] = _r(nch * K * Dp * 8)
     p["cnt_slab"] = _r(nch * K * 8)
@@ -291,6 +292,7 @@ def plan_streaming(n: int, D: int, K: int, dtype="bfloat16", *, chunk_rows: int,
     p = {"labels": _r(n * 4), "xn": _r(n * 4)}
     if weighted:
         p["weights"] = _r(n * 4)
+        p["wdot_scratch"] = _r(WDOT_SCRATCH * 8)
     if weighted or empty_policy == "farthest":
         p["mind"] = _r(n * 4)
     p["chunk_bufs"] = 2 * _r(R * Dp * es)

@@ -49,8 +49,12 @@ def test_row_normalize_and_wdot(native, dtype):
     torch.testing.assert_close(xn, Y.float().pow(2).sum(1), rtol=1e-5, atol=1e-6)
     a, w = torch.rand(100_001, device=DEV), torch.rand(100_001, device=DEV)
     out = torch.zeros(1, dtype=torch.float64, device=DEV)
-    native.wdot(a, w, out)
+    scratch = torch.empty(native.WDOT_SCRATCH, dtype=torch.float64, device=DEV)
+    native.wdot(a, w, out, scratch)
     assert float(out) == pytest.approx(float((a.double() * w.double()).sum()), rel=1e-12)
+    again = torch.zeros(1, dtype=torch.float64, device=DEV)
+    native.wdot(a, w, again, scratch)
+    assert float(again) == float(out)                  # fixed summation order
 
 
 def test_minibatch_fit_device_vs_host_shard(native, monkeypatch):

@@ -32,6 +32,7 @@ def test_plan_h_mirror_matches_native():
     for kp in (16, 256, 1024, 4352):
         assert M.assign_cn_len(kp) == C.assign_cn_len(kp)
     assert (M.NSLOT, M.SLOT_STRIDE) == (C.NSLOT, C.SLOT_STRIDE)
+    assert M.WDOT_SCRATCH == C.WDOT_SCRATCH
 
 
 def test_resident_inventory_fixed_shapes():
