@@ -425,7 +425,7 @@ class KMeans(_Serving):
             if mlog is not None:
                 mlog.close()
             labels, mind = eng.assign(True)
-            inert = torch.zeros(1, dtype=torch.float64, device=comm.device)
+            inert = torch.zeros(1, dtype=torch.float64, device=eng.device)
             if eng.n:
                 if eng.weights is not None and eng.gpu:
                     C_ = native_mod()
@@ -436,6 +436,7 @@ class KMeans(_Serving):
                 else:
                     inert += mind.sum(dtype=torch.float64).to(inert.device)
             del mind
+            inert = inert.to(comm.device)
             comm.allreduce_(inert)
             inertia = float(inert.item())
             if best is None or inertia < best[0]:

@@ -155,7 +155,8 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     int64_t row = pbase + p * 16 + r;
     row = row < a.N ? row : (a.N - 1);
     xnr[p] = (!EXACT && a.xn) ? a.xn[row] : 0.f;
-    const T* rp = (const T*)a.X + row * a.ldx + g * C::V;
+    const int64_t src = a.rows ? a.rows[row] : row;   // gathered batch: logical row -> X row
+    const T* rp = (const T*)a.X + src * a.ldx + g * C::V;
 #pragma unroll
     for (int q = 0; q < C::NQ; ++q) {
       const int col = (4 * q + g) * C::V;

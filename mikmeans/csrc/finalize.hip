@@ -170,11 +170,11 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
   const int R = 256 / L;
   const int64_t step = (int64_t)gridDim.x * R;
   uint32_t m[V];
-  float q[V], sx[V], sxx[V];
+  double q[V], sx[V], sxx[V];   // f64 per lane: chunked / sharded passes agree to ~1e-16
   uint32_t nz[V];
   int lb[V];
 #pragma unroll
-  for (int e = 0; e < V; ++e) { m[e] = 0u; q[e] = 0.f; sx[e] = 0.f; sxx[e] = 0.f; nz[e] = 0u; lb[e] = 1 << 30; }
+  for (int e = 0; e < V; ++e) { m[e] = 0u; q[e] = 0.0; sx[e] = 0.0; sxx[e] = 0.0; nz[e] = 0u; lb[e] = 1 << 30; }
   auto take = [&](const u32x4& w) {
     float f[V];
     unpack16(w, f, (T*)nullptr);
@@ -182,9 +182,10 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
     for (int e = 0; e < V; ++e) {
       m[e] = max(m[e], __float_as_uint(f[e]) & 0x7fffffffu);
       if constexpr (STATS) {
-        q[e] += fabsf(f[e]);
-        sx[e] += f[e];
-        sxx[e] = __builtin_fmaf(f[e], f[e], sxx[e]);
+        const double d = (double)f[e];
+        q[e] += fabs(d);
+        sx[e] += d;
+        sxx[e] = __builtin_fma(d, d, sxx[e]);
         nz[e] += f[e] != 0.f;
         lb[e] = min(lb[e], lowbit_exp(f[e]));
       }
@@ -225,16 +226,16 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
     if (v) atomicMax(out + j, v);
   }
   if constexpr (STATS) {
-    float* rf = (float*)&red[0][0];
+    __shared__ double rd[4][64 * 8];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       __syncthreads();
       if (lane < L)
 #pragma unroll
-        for (int e = 0; e < V; ++e) rf[wv * 64 * V + lane * V + e] = k == 0 ? q[e] : k == 1 ? sx[e] : sxx[e];
+        for (int e = 0; e < V; ++e) rd[wv][lane * V + e] = k == 0 ? q[e] : k == 1 ? sx[e] : sxx[e];
       __syncthreads();
       for (int j = threadIdx.x; j < NP * V; j += 256) {
-        const double v = (double)rf[j] + rf[64 * V + j] + rf[128 * V + j] + rf[192 * V + j];
+        const double v = (rd[0][j] + rd[1][j]) + (rd[2][j] + rd[3][j]);
         if (v != 0.0) atomicAdd(fstats + (int64_t)k * NP * V + j, v);
       }
     }
