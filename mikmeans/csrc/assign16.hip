@@ -172,7 +172,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   // the fragments themselves, folded into this workgroup's LDS copy of |c|^2 once.
   // A workgroup whose max |x|^2 exceeds 4x its min (an outlier row, or data around the
   // origin) takes per-point offsets o_p = (1 + 2^-12) |x_p|^2 instead, parked in LDS and
-  // added to each tile's seed (uniform branch): a shared offset would coarsen every
+  // added to each tile's seed (second chunk-loop instantiation): a shared offset would coarsen every
   // neighbour's keys to 2^-17 of the outlier's norm.  Either way a key resolves
   // 2^-17 (|x - c|^2 + 3 |x|^2) or better.
   float off = 0.f;
@@ -231,8 +231,8 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   const int ngrp = nch * C::CT;   // one past the last tile (global tile numbering)
   const unsigned kmask = key6_mask();
 
-  // The chunk loop, instantiated twice: per-point offsets (PPO, outlier workgroups) add a
-  // tile's offsets to its scores after the MFMAs; the common instantiation has no such
+  // The chunk loop, instantiated twice: per-point offsets (PPO, outlier workgroups) seed a
+  // tile's accumulators with its points' offsets; the common instantiation has no such
   // code at all -- a per-tile branch cost 1-3 % (one-process A/B against round 2).
   auto chunk_loop = [&](auto ppo_tag) {
     constexpr bool PPO = decltype(ppo_tag)::value;
@@ -273,6 +273,20 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         f32x4 acc[C::P];
   #pragma unroll
         for (int p = 0; p < C::P; ++p) acc[p] = ci;
+        if constexpr (PPO) {  // per-point offsets seed the accumulators (one LDS read per tile)
+          // (added BEFORE the MFMAs: VALU writes the MFMA then reads as src C.  Adding them
+          // to the MFMA results instead raced the matrix pipe: a v_pk_add_f32 read the
+          // result registers early when the LDS read ahead of it returned fast, a rare,
+          // nondeterministic wrong label, tests/test_gpu_kernels.py split-batch test)
+          const float* o = opt + (wid * 16 + r) * C::PP;
+  #pragma unroll
+          for (int p4 = 0; p4 < C::P; p4 += 4) {
+            const f32x4 ov = *(const f32x4*)(o + p4);
+  #pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (p4 + j < C::P) acc[p4 + j] += ov[j];
+          }
+        }
         // bf16: the wave issues its MFMAs at raised priority and drops back for the epilogue,
         // so a SIMD's arbiter feeds the matrix core before another wave's argmin VALU work
         // (profiles/r2_29_assign_setprio_ab.log, one process each: the harness copy -2.2 % at
@@ -296,19 +310,6 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         if constexpr (EARLY) {
           if (tl_i + 1 < C::CT) load_a(tl_i + 1, awe, cie);
           __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (!EXACT) {
-          if (ppo) {  // per-point offsets, added to the scores in place (outlier workgroups only, see above; after the
-                      // MFMAs, so the common path seeds them with ci directly)
-            const float* o = opt + (wid * 16 + r) * C::PP;
-  #pragma unroll
-            for (int p4 = 0; p4 < C::P; p4 += 4) {
-              const f32x4 ov = *(const f32x4*)(o + p4);
-  #pragma unroll
-              for (int j = 0; j < 4; ++j)
-                if (p4 + j < C::P) acc[p4 + j] += ov[j];
-            }
-          }
         }
         if constexpr (EXACT) {
           // (tile*4 + reg) as wave-uniform values: the index select needs no VALU add
