@@ -331,7 +331,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
           const unsigned tis = (unsigned)(tile & 15) << 2;
           unsigned t0, t1, t2, t3;
           asm volatile("s_mov_b32 %0, %4\n\ts_or_b32 %1, %4, 1\n\ts_or_b32 %2, %4, 2\n\ts_or_b32 %3, %4, 3"
-                       : "=s"(t0), "=s"(t1), "=s"(t2), "=s"(t3) : "s"(tis));
+                       : "=s"(t0), "=s"(t1), "=s"(t2), "=s"(t3) : "s"(tis) : "scc");  // s_or_b32 writes SCC
   #pragma unroll
           for (int p = 0; p < C::P; ++p) {
             const f32x4& sv = acc[p];
