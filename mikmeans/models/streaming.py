@@ -166,6 +166,11 @@ class StreamingLloydEngine(LloydEngine):
 
         if not self.ranges:
             return
+        # the copy stream starts behind everything the caller's stream has queued: the chunk
+        # buffers' zero fill at construction (a copy racing ahead of it was overwritten by
+        # zeros: wrong row norms / column statistics for chunk 0, a load-dependent race) and
+        # whatever last touched them
+        cp.wait_stream(main)
         issue(0)
         for c, (r0, r1) in enumerate(self.ranges):
             if c + 1 < len(self.ranges):

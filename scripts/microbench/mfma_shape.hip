@@ -50,7 +50,7 @@ __global__ void fill(uint16_t* p, int64_t n, int zero, uint32_t seed) {
   p[i] = (uint16_t)(__float_as_uint(f) >> 16);
 }
 
-template <int S, int D, bool EPI>
+template <int S, int D, int EPI>
 __global__ __launch_bounds__(NT) void kern(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Cg,
                                            float* __restrict__ out, unsigned long long* __restrict__ stamps,
                                            int sweeps) {
@@ -74,6 +74,9 @@ __global__ __launch_bounds__(NT) void kern(const uint16_t* __restrict__ X, const
   float m = 3.0e38f;
   float km = 3.0e38f;
   const unsigned kmask = key6_mask();
+  uint32_t vb[NB], tb[NB];   // EPI=2: value-only running min per block + the tile that set it
+#pragma unroll
+  for (int b = 0; b < NB; ++b) { vb[b] = 0x7f7fffffu; tb[b] = 0u; }
   f32x4 p16[NB];
   f32x16 p32[NB];
 #pragma unroll
@@ -97,7 +100,19 @@ __global__ __launch_bounds__(NT) void kern(const uint16_t* __restrict__ X, const
 #pragma unroll
           for (int b = 0; b < NB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cf, xf[b][s], acc[b], 0, 0, 0);
         }
-        if constexpr (EPI) {
+        if constexpr (EPI == 2) {
+          // value-only argmin: 2 v_min3_u32 (non-negative scores order as their bits) fold
+          // the tile's 4 scores into the running min, v_cmp + v_cndmask record the tile:
+          // 4 VALU per 4 scores (the row inside the tile is recovered once at the end)
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            const uint32_t u0 = __float_as_uint(acc[b][0]), u1 = __float_as_uint(acc[b][1]);
+            const uint32_t u2 = __float_as_uint(acc[b][2]), u3 = __float_as_uint(acc[b][3]);
+            const uint32_t nb = min(min(u0, u1), min(u2, min(u3, vb[b])));
+            tb[b] = nb != vb[b] ? (uint32_t)t : tb[b];
+            vb[b] = nb;
+          }
+        } else if constexpr (EPI == 1) {
 #pragma unroll
           for (int b = 0; b < NB; ++b) {
             // production skeleton: 4 v_and_or_b32 key packs (indices in SGPRs) + 2 v_min3
@@ -125,7 +140,7 @@ __global__ __launch_bounds__(NT) void kern(const uint16_t* __restrict__ X, const
 #pragma unroll
           for (int b = 0; b < NB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf, xf[b][s], acc[b], 0, 0, 0);
         }
-        if constexpr (EPI) {
+        if constexpr (EPI != 0) {
 #pragma unroll
           for (int b = 0; b < NB; ++b)
 #pragma unroll
@@ -144,6 +159,10 @@ __global__ __launch_bounds__(NT) void kern(const uint16_t* __restrict__ X, const
         }
       }
     }
+  }
+  if constexpr (EPI == 2) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) km = fminf(km, __uint_as_float(vb[b] ^ tb[b]));
   }
   if constexpr (!EPI) {
 #pragma unroll
@@ -167,7 +186,7 @@ __global__ __launch_bounds__(NT) void kern(const uint16_t* __restrict__ X, const
   }
 }
 
-template <int S, int D, bool EPI>
+template <int S, int D, int EPI>
 int run(const char* name, const uint16_t* X, const uint16_t* C, float* out, unsigned long long* st, int grid,
         int sweeps, const char* data) {
   hipEvent_t a, b;
@@ -204,7 +223,7 @@ int run(const char* name, const uint16_t* X, const uint16_t* C, float* out, unsi
   // pipe utilisation at the measured clock: 1024 SIMDs x 1024 FLOP/cycle (bf16 dense)
   const double util = tf * 1e12 / (1024.0 * 1024.0 * mhz * 1e6);
   printf("%-10s D=%-3d %-6s epi=%d  %8.3f ms  %7.1f TF/s  clock %6.0f MHz (p10 %4.0f p90 %4.0f)  MFMA util %5.1f %%\n",
-         name, D, data, (int)EPI, ms, tf, mhz, clk[grid / 10], clk[grid * 9 / 10], util * 100.0);
+         name, D, data, EPI, ms, tf, mhz, clk[grid / 10], clk[grid * 9 / 10], util * 100.0);
   fflush(stdout);
   CK(hipEventDestroy(a));
   CK(hipEventDestroy(b));
@@ -236,7 +255,11 @@ int main(int argc, char** argv) {
         if (run<32, 128, true>("32x32x16", X, C, out, st, grid, sweeps, data)) return 1;
         if (!zero && run<16, 64, true>("16x16x32", X, C, out, st, grid, 2 * sweeps, data)) return 1;
         if (!zero && run<32, 64, true>("32x32x16", X, C, out, st, grid, 2 * sweeps, data)) return 1;
+        if (!zero && run<16, 64, 2>("16x16x32", X, C, out, st, grid, 2 * sweeps, data)) return 1;
+        if (!zero && run<16, 128, 2>("16x16x32", X, C, out, st, grid, sweeps, data)) return 1;
       } else {
+        if (!zero && run<16, 128, 2>("16x16x32", X, C, out, st, grid, sweeps, data)) return 1;
+        if (!zero && run<16, 64, 2>("16x16x32", X, C, out, st, grid, 2 * sweeps, data)) return 1;
         if (!zero && run<32, 64, true>("32x32x16", X, C, out, st, grid, 2 * sweeps, data)) return 1;
         if (!zero && run<16, 64, true>("16x16x32", X, C, out, st, grid, 2 * sweeps, data)) return 1;
         if (run<32, 128, true>("32x32x16", X, C, out, st, grid, sweeps, data)) return 1;

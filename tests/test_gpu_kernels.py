@@ -549,6 +549,23 @@ def test_streaming_fit_matches_resident(native, dtype):
     torch.testing.assert_close(st.predict(X), ref.predict(X))
 
 
+def test_streaming_copy_stream_waits_for_buffer_init(native):
+    """The chunk copies run on a side stream: they must start behind the caller's queued
+    work, including the chunk buffers' own zero fill.  With the caller's stream busy (a
+    spin kernel), a copy that raced ahead was overwritten by that fill, and chunk 0's row
+    norms and column statistics came out as zeros."""
+    from mikmeans.models.streaming import StreamingLloydEngine
+
+    X = B.make_blobs(40_000, 32, 16, seed=5, dtype=torch.bfloat16, device="cpu")
+    torch.cuda._sleep(200_000_000)          # ~0.1 s of queued work on the current stream
+    eng = StreamingLloydEngine(X, 16, chunk_rows=1 << 13, device=DEV, dtype=torch.bfloat16)
+    Xd = X.to(DEV).float()
+    torch.testing.assert_close(eng.xn, Xd.pow(2).sum(1), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(eng.stats.sum[:32], Xd.double().sum(0), rtol=1e-9, atol=1e-6)
+    torch.testing.assert_close(eng.stats.sumsq[:32], Xd.double().pow(2).sum(0), rtol=1e-9, atol=1e-6)
+    eng.close()
+
+
 def test_streaming_fit_kmeanspp_sample_init(native):
     # k-means++ runs on a device-resident sample of init_size rows (seeded, sorted draw);
     # the resident fit started from the same seeding must give the same model
