@@ -32,6 +32,13 @@
 //    round 2); workgroups are therefore aligned to the global ROW_ALIGN = 1536-row grid by
 //    the callers (shard_range, streaming chunks), so near-tie resolution is the same on
 //    any world size.
+//  * bf16 D <= 64 with many centres (VARG): the keys' 1.5 VALU per score bound the body
+//    (1-2 MFMAs per tile and block), so the main loop keeps only the running minimum value
+//    (2 v_min3_u32 per tile and block: the positive scores order as their bits) and the
+//    tile that lowered it (v_cmp + v_cndmask): 1.0 VALU per score.  After the loop the
+//    winning tile's 4 candidate rows of every point are recomputed on the matrix cores,
+//    bitwise the main loop's scores, and the first equal to the minimum is the label
+//    (full fp32 resolution; 64/K extra matrix work, so K >= 2048 at D=64, >= 1024 at D=32).
 //  * f32: an exact (value, index) compare per score (v_cmp + 2 v_cndmask).  The f32
 //    MFMA is 16x slower per FLOP than bf16, so the epilogue is noise there and the
 //    labels carry full fp32 score resolution; strict < in ascending index order keeps
@@ -40,6 +47,7 @@
 // Layout "16" of the packed centroids (csrc/kernels.h):
 //   element (k, d): t = k/16, r = k%16, q = d / (4V), g = (d / V) % 4
 //   offset = ((t*NQ + q)*64 + r + 16*g)*V + d%V,  NQ = DPAD/(4V)
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -110,10 +118,17 @@ __device__ __forceinline__ float sq16(const u32x4& w, float*) {
 // OCC: minimum waves per SIMD the register allocation must allow (launch bounds).
 // FULLD: D == DPAD, so no fragment piece needs a column check.  The per-piece check costs
 // 7 % at D=256 K=512 even when every piece passes it (profiles/r2_08_assign_clock_study.md).
-template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false>
+// VARG (bf16): value-only argmin in the main loop -- 2 v_min3_u32 fold a tile's 4 scores
+// into the running minimum and v_cmp + v_cndmask record the tile that lowered it (1.0 VALU
+// per score instead of the packed keys' 1.5); the row inside the winning tile is recovered
+// once per point after the loop by recomputing the winning tile's candidates on the
+// matrix cores (bitwise the main loop's scores), see recover_rows below.
+template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false,
+          bool VARG = false>
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
+  static_assert(!(VARG && EXACT), "value-only argmin is the bf16 epilogue");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -226,8 +241,12 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
 
   float best[C::P], seg_best[C::P];
   int bg[C::P];
+  uint32_t vb[C::P], tb[C::P];   // VARG: running minimum (bits of a positive float), its tile
 #pragma unroll
-  for (int p = 0; p < C::P; ++p) { best[p] = 3.0e38f; seg_best[p] = 3.0e38f; bg[p] = 0; }
+  for (int p = 0; p < C::P; ++p) {
+    best[p] = 3.0e38f; seg_best[p] = 3.0e38f; bg[p] = 0;
+    vb[p] = 0x7f7fffffu; tb[p] = 0u;
+  }
   const int ngrp = nch * C::CT;   // one past the last tile (global tile numbering)
   const unsigned kmask = key6_mask();
 
@@ -323,6 +342,17 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
               bg[p] = lt ? u + e : bg[p];
             }
           }
+        } else if constexpr (VARG) {
+          // scores are positive (seed offset, see the header), so they order as their bits;
+          // a tie with the running minimum keeps the earlier tile (the lower index)
+  #pragma unroll
+          for (int p = 0; p < C::P; ++p) {
+            const uint32_t u0 = __float_as_uint(acc[p][0]), u1 = __float_as_uint(acc[p][1]);
+            const uint32_t u2 = __float_as_uint(acc[p][2]), u3 = __float_as_uint(acc[p][3]);
+            const uint32_t nb = min(min(u0, u1), min(u2, min(u3, vb[p])));
+            tb[p] = nb != vb[p] ? (uint32_t)tile : tb[p];
+            vb[p] = nb;
+          }
         } else {
           // 6-bit keys over a segment of 16 tiles (tile-in-segment * 4 + reg): 4 key packs
           // + 2 v_min3 per tile and point block; the running best is merged with its
@@ -357,26 +387,96 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   if (ppo) chunk_loop(std::true_type{});
   else chunk_loop(std::false_type{});
 
+  // VARG: merge the 4 lane groups of each point on (value, tile, group) -- the centre index
+  // 16 t + 4 g + e orders like that triple -- then recover e: for the points 4m..4m+3 the
+  // 16 A rows carry the 4 candidates of each (row 4g'+e = candidate e of point 4m+g'), so
+  // lane (r = 4m+g, g) receives its own point's 4 candidate scores, computed exactly as in
+  // the main loop (same packed -2c, same seed from the LDS |c|^2 copy, same k-step order),
+  // and takes the first that equals the minimum.  4 MFMA groups per point block: 64/K of
+  // the main loop's matrix work.
+  uint32_t kv[C::P];
+  if constexpr (VARG) {
+#pragma unroll
+    for (int p = 0; p < C::P; ++p) {
+      uint32_t v = vb[p], tg = tb[p] * 4u + (uint32_t)g;
+#pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) {
+        const uint32_t vo = (uint32_t)__shfl_xor((int)v, o, 64), to = (uint32_t)__shfl_xor((int)tg, o, 64);
+        if (vo < v || (vo == v && to < tg)) { v = vo; tg = to; }
+      }
+      vb[p] = v;
+      tb[p] = tg;
+    }
+    const T* pack = (const T*)a.Cpack;
+    int efound[C::P];
+#pragma unroll
+    for (int p = 0; p < C::P; ++p) efound[p] = 0;
+#pragma unroll
+    for (int p = 0; p < C::P; ++p) {
+      u32x4 aw[4][C::NQ];
+      f32x4 acc[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const uint32_t tga = (uint32_t)__shfl((int)tb[p], 4 * m + (r >> 2), 64);
+        const int ca = (int)(tga >> 2) * 16 + (int)(tga & 3u) * 4 + (r & 3);   // A row r's centre
+        const T* src = pack + ((int64_t)(ca >> 4) * C::NQ * 64 + (ca & 15) + 16 * g) * C::V;
+#pragma unroll
+        for (int q = 0; q < C::NQ; ++q) aw[m][q] = *(const u32x4*)(src + (int64_t)q * 64 * C::V);
+        const uint32_t tgs = (uint32_t)__shfl((int)tb[p], 4 * m + g, 64);     // output rows' point
+        acc[m] = *(const f32x4*)(cn_lds + ((int)(tgs >> 2) * 16 + (int)(tgs & 3u) * 4) * 4);
+        if (ppo) {
+          const float o = opt[(wid * 16 + r) * C::PP + p];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[m][e] += o;
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int q = 0; q < C::NQ; ++q) acc[m] = Mfma16<T>::run(aw[m][q], xr[p][q], acc[m]);
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        if (r == 4 * m + g) {
+          int e = 3;
+#pragma unroll
+          for (int j = 2; j >= 0; --j) e = __float_as_uint(acc[m][j]) == vb[p] ? j : e;
+          efound[p] = e;
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < C::P; ++p) {
+      const int e = __shfl(efound[p], r + 16 * (r & 3), 64);
+      kv[p] = (tb[p] >> 2) * 16u + (tb[p] & 3u) * 4u + (uint32_t)e;
+    }
+  }
+
   float inert = 0.f;
   int changed = 0;
 #pragma unroll
   for (int p = 0; p < C::P; ++p) {
     int k;
     float v;
-    if constexpr (EXACT) {  // bg = tile * 4 + reg of the first strict minimum
-      k = (bg[p] >> 2) * 16 + 4 * g + (bg[p] & 3);
-      v = best[p];
-    } else {               // bg = segment of 16 tiles, 6-bit key; undo the seed offset
-      const unsigned bits = __float_as_uint(best[p]);
-      const int idx = (int)(bits & 63u);
-      k = (bg[p] * 16 + (idx >> 2)) * 16 + 4 * g + (idx & 3);
-      v = __uint_as_float(bits & ~63u);
-    }
+    if constexpr (VARG) {  // merged and recovered above
+      k = (int)kv[p];
+      v = __uint_as_float(vb[p]);
+    } else {
+      if constexpr (EXACT) {  // bg = tile * 4 + reg of the first strict minimum
+        k = (bg[p] >> 2) * 16 + 4 * g + (bg[p] & 3);
+        v = best[p];
+      } else {               // bg = segment of 16 tiles, 6-bit key; undo the seed offset
+        const unsigned bits = __float_as_uint(best[p]);
+        const int idx = (int)(bits & 63u);
+        k = (bg[p] * 16 + (idx >> 2)) * 16 + 4 * g + (idx & 3);
+        v = __uint_as_float(bits & ~63u);
+      }
 #pragma unroll
-    for (int o = 16; o <= 32; o <<= 1) {
-      const float vo = __shfl_xor(v, o, 64);
-      const int ko = __shfl_xor(k, o, 64);
-      if (vo < v || (vo == v && ko < k)) { v = vo; k = ko; }
+      for (int o = 16; o <= 32; o <<= 1) {
+        const float vo = __shfl_xor(v, o, 64);
+        const int ko = __shfl_xor(k, o, 64);
+        if (vo < v || (vo == v && ko < k)) { v = vo; k = ko; }
+      }
     }
     // this point's seed offset (0 for f32)
     const float offp = ppo ? opt[(wid * 16 + r) * C::PP + p] : off;
@@ -464,6 +564,37 @@ static int assign16_splits(int64_t nblk, int nch) {
   return (nch + cps - 1) / cps;  // no empty split (the kernel's chunk range must be non-empty)
 }
 
+// Value-only argmin (VARG) where it pays: the D<=64 bf16 bodies are VALU-bound on the packed
+// keys (2 MFMAs per tile and block at D=64, 1 at D=32, against 6 epilogue VALU), and the
+// recovery pass costs 64/K of the matrix work, so it is taken for K >= 2048 at D=64 and
+// K >= 1024 at D=32 (scripts/varg_ab.py, profiles/r3_08_varg_ab.log: cfg4 shape +8.2 %,
+// D=64 K=2048 +8.5 %, K=1024 -3.7 %; D=32 K=1024 +5.6 %, K=512 -8.8 %).
+// MIKMEANS_ASSIGN_VARG=0/1 forces it off / on (A/B, tests).
+static int varg_env() {   // read per launch (tests switch it inside one process)
+  const char* e = getenv("MIKMEANS_ASSIGN_VARG");
+  return (e && *e) ? atoi(e) : -1;
+}
+
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG>
+static void set_lds_attr() {
+  static bool done = false;
+  if (done) return;
+  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  done = true;
+}
+
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG>
+static void launch16_k(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
+  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG>();
+  if (b.D == DPAD)
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG>), grid, dim3(NW_ * 64), lds, s, b);
+  else
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG>), grid, dim3(NW_ * 64), lds, s, b);
+}
+
 template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4>
 static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
@@ -472,25 +603,24 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   // + min/max / slot scratch + per-point offsets
   const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW + C::OPT_BYTES;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
   if (nblk <= 0) return hipSuccess;
   const int splits = a.split_keys ? assign16_splits(nblk, a.Kpad / (16 * C::CT)) : 1;
   AssignArgs b = a;
   if (splits == 1) b.split_keys = nullptr;
-  if (a.D == DPAD)
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true>),
-                       dim3((unsigned)nblk, (unsigned)splits), dim3(C::NW * 64), lds, s, b);
-  else
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false>),
-                       dim3((unsigned)nblk, (unsigned)splits), dim3(C::NW * 64), lds, s, b);
+  const dim3 grid((unsigned)nblk, (unsigned)splits);
+  bool varg = false;
+  constexpr bool VARG_OK = sizeof(T) == 2 && DPAD <= 64;
+  if constexpr (VARG_OK) {
+    const int e = varg_env();
+    varg = e >= 0 ? e != 0 : a.Kpad >= (DPAD == 64 ? 2048 : 1024);
+  }
+  if constexpr (VARG_OK) {
+    if (varg) launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, true>(b, grid, lds, s);
+    else launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, false>(b, grid, lds, s);
+  } else {
+    launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, false>(b, grid, lds, s);
+  }
   if (splits > 1)
     hipLaunchKernelGGL(split_finish_kernel, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, s, b);
   return hipGetLastError();

@@ -696,6 +696,43 @@ def test_assign_bf16_key_resolution_distance_relative(native):
     assert int(bad.sum()) == 0, f"{int(bad.sum())} wrong labels of {int(ok.sum())} resolvable rows"
 
 
+@pytest.mark.parametrize("n,outlier,d,k", [(20_000, False, 64, 4096), (300_000, False, 64, 4096),
+                                           (300_000, True, 64, 4096), (40_000, True, 64, 4096),
+                                           (300_000, False, 32, 1024), (30_000, True, 32, 1024)])
+def test_assign_value_argmin_d64(native, monkeypatch, n, outlier, d, k):
+    """The value-only argmin (bf16 D=64 K >= 2048, D=32 K >= 1024: running minimum + tile in the main loop,
+    the row inside the winning tile recovered on the matrix cores afterwards) gives the f64
+    argmin on every row resolvable at fp32 resolution of the seeded score, on the split and
+    one-pass grids and in per-point-offset workgroups, and distances of the same accuracy;
+    where the packed keys resolve a row, both epilogues agree."""
+    wg = 512 if d == 64 else 256           # workgroup points (csrc/assign16.hip launch16_d)
+    g = torch.Generator().manual_seed(11 + n + d)
+    X = torch.randn(n, d, generator=g)
+    C = torch.randn(k, d, generator=g) * 0.8
+    if outlier:
+        X[7] *= 300.0
+    Xb = X.to(torch.bfloat16)
+    monkeypatch.setenv("MIKMEANS_ASSIGN_VARG", "1")
+    lv, dv = ops.assign(Xb.to(DEV), C.to(DEV), with_dist=True)
+    monkeypatch.setenv("MIKMEANS_ASSIGN_VARG", "0")
+    lk, _ = ops.assign(Xb.to(DEV), C.to(DEV), with_dist=False)
+    xx, Cq, dist = _bf16_dist(Xb, C)
+    exp = _first_argmin(dist)
+    srt = dist.sort(1).values
+    pad = (-n) % wg
+    xw = torch.cat([xx, xx[-1:].expand(pad)]).view(-1, wg).max(1, keepdim=True).values.expand(-1, wg)
+    off = xw.reshape(-1)[:n] * (1 + 2**-12)          # the workgroup's seed offset scale
+    scale = srt[:, 0].clamp_min(0) + off + (Cq * Cq).sum(1).max()
+    ok = (srt[:, 1] - srt[:, 0]) > 2.0**-20 * scale
+    assert ok.float().mean() > 0.9
+    bad = (lv.cpu().long() != exp) & ok
+    assert int(bad.sum()) == 0, f"{int(bad.sum())} wrong labels of {int(ok.sum())} resolvable rows"
+    torch.testing.assert_close(dv.cpu().double(), srt[:, 0].clamp_min(0), rtol=0,
+                               atol=float(2.0**-19 * scale.max()))
+    okk = (srt[:, 1] - srt[:, 0]) > 2.0**-15 * scale    # resolvable by the 2^-17 keys too
+    assert torch.equal(lv.cpu()[okk], lk.cpu()[okk])
+
+
 @pytest.mark.parametrize("n,segments", [(3000, 4), (5000, 4), (60_000, 3)])
 def test_overlapped_segments_match_plain_step(native, n, segments):
     """The overlapped M-step (assign of segment s+1 on the main stream while segment s is
