@@ -34,6 +34,8 @@
 // are exactly those per-centroid counts.
 #include <math.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 #include "plan.h"
@@ -692,6 +694,11 @@ static int esize(int dtype);
 static bool use_ks(int dtype, int K, int D, bool weighted, plan::KsPlan* kp) {
   if (weighted) return false;
   const int sw = update_slice_width(dtype, K, D, false);
+  // A/B override (0 = slice kernel, 1 = K-split); the memory planner assumes the default.
+  // cfg5 (D=256 K=512, 128-B slices): K-split 6.58 vs slice 6.03 ms per resident step
+  // (profiles/r3_09_update_ks_cfg5_ab.log), so the rule below stands.
+  const char* ov = getenv("MIKMEANS_UPDATE_KS");
+  if (ov && *ov) return atoi(ov) != 0 && sw > 0 && sw < D && plan::choose_ks(esize(dtype), K, D, kp);
   return sw > 0 && sw < D && sw * esize(dtype) < 128 && plan::choose_ks(esize(dtype), K, D, kp);
 }
 
