@@ -25,8 +25,8 @@
 //    and the key resolution is 2^-17 of the squared distance plus the spread of |x|^2
 //    inside the workgroup, not 2^-17 of |x|^2 (coarse for data far from the origin).
 //    Where that spread is large (max |x|^2 > 4 min |x|^2: an outlier row, data around the
-//    origin) the workgroup uses per-point offsets instead (added to the scores after each
-//    tile's MFMAs, a uniform branch the common path skips), so the resolution is never
+//    origin) the workgroup uses per-point offsets instead (they seed each tile's
+//    accumulators, in a second instantiation of the chunk loop), so the resolution is never
 //    worse than 2^-17 (|x-c|^2 + 3|x|^2).  Per-point offsets everywhere would make the keys
 //    a function of the point alone, but cost 17 % at the headline shape (one process A/B,
 //    round 2); workgroups are therefore aligned to the global ROW_ALIGN = 1536-row grid by
@@ -122,7 +122,7 @@ __device__ __forceinline__ float sq16(const u32x4& w, float*) {
 // into the running minimum and v_cmp + v_cndmask record the tile that lowered it (1.0 VALU
 // per score instead of the packed keys' 1.5); the row inside the winning tile is recovered
 // once per point after the loop by recomputing the winning tile's candidates on the
-// matrix cores (bitwise the main loop's scores), see recover_rows below.
+// matrix cores (bitwise the main loop's scores), right after the chunk loop.
 template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false,
           bool VARG = false>
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
@@ -636,7 +636,9 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   //  * bf16 D=128: 4 point blocks per wave at <= 128 VGPRs (4 waves/SIMD) -- 3 / 5 blocks,
   //    3 waves/SIMD, 8/16 waves per ring, 4/8 KiB chunks x 3 slots and next-tile fragment
   //    loads under the MFMAs are all slower;
-  //  * bf16 D=64: 8 point blocks at 3 waves/SIMD, -5 % against 4 blocks at 4;
+  //  * bf16 D=64: 8 point blocks at 3 waves/SIMD, -5 % against 4 blocks at 4; with the
+  //    value-only argmin (K >= 2048) 4 blocks at 4 waves are 4-9 % slower and 12 blocks at
+  //    2 waves 1-10 % slower (profiles/r3_10_assign_p64_ab.log);
   //  * bf16 D=256: 3 point blocks at 3 waves/SIMD, -4 % against 2 at 4;
   //  * f32: the register file sets 4 (D <= 64) or 2 blocks at one wave per SIMD minimum.
   constexpr int P = sizeof(T) == 2 ? (DPAD == 64 ? 8 : DPAD == 256 ? 3 : 4) : (NQ >= 8 ? 2 : 4);

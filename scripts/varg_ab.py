@@ -1,5 +1,5 @@
-"""A/B of the assign kernel's value-only argmin (MIKMEANS_ASSIGN_VARG=1) against the packed
-6-bit keys (=0) in one process, interleaved rounds, on Gaussian blobs at the cfg4 shape
+"""A/B of assign-kernel variants selected by an environment switch (default: the value-only
+argmin MIKMEANS_ASSIGN_VARG=1 against the packed 6-bit keys =0) in one process, interleaved rounds, on Gaussian blobs at the cfg4 shape
 (N=1e7, D=64, K=4096 bf16) and optionally others: median ms, TF/s and label agreement."""
 import argparse
 import json
@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--shapes", default="10000000,64,4096;2000000,64,2048;2000000,64,1024;4000000,32,1024;4000000,32,512;4000000,32,256")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--env", default="MIKMEANS_ASSIGN_VARG", help="variable switched between the arms")
+    ap.add_argument("--values", default="0,1", help="its values, one arm each (first = baseline)")
     args = ap.parse_args()
     for sh in args.shapes.split(";"):
         n, d, k = (int(v) for v in sh.split(","))
@@ -26,12 +28,13 @@ def main():
         C = X[torch.randperm(n, generator=torch.Generator().manual_seed(1))[:k].cuda()].float()
         pack = ops.pack_centers(C, d, torch.bfloat16, "cuda")
         xn = ops.row_sqnorm(X)
-        labels = {v: torch.empty(n, dtype=torch.int32, device="cuda") for v in ("0", "1")}
-        times = {"0": [], "1": []}
+        vals = args.values.split(",")
+        labels = {v: torch.empty(n, dtype=torch.int32, device="cuda") for v in vals}
+        times = {v: [] for v in vals}
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for rd in range(args.rounds):
-            for v in (("0", "1") if rd % 2 == 0 else ("1", "0")):
-                os.environ["MIKMEANS_ASSIGN_VARG"] = v
+            for v in (vals if rd % 2 == 0 else vals[::-1]):
+                os.environ[args.env] = v
                 pack.assign(X, xn, labels[v])            # warm
                 ev[0].record()
                 for _ in range(args.reps):
@@ -40,15 +43,15 @@ def main():
                 torch.cuda.synchronize()
                 times[v].append(ev[0].elapsed_time(ev[1]) / args.reps)
         flop = 2.0 * n * k * d
-        out = {"n": n, "d": d, "k": k}
-        for v, name in (("0", "keys"), ("1", "value_argmin")):
+        out = {"n": n, "d": d, "k": k, "env": args.env}
+        base = statistics.median(times[vals[0]])
+        for v in vals:
             ms = statistics.median(times[v])
-            out[name] = {"median_ms": round(ms, 4), "min_ms": round(min(times[v]), 4),
-                         "tflops": round(flop / ms / 1e9, 1)}
-        out["speedup"] = round(out["keys"]["median_ms"] / out["value_argmin"]["median_ms"], 4)
-        out["label_mismatch"] = int((labels["0"] != labels["1"]).sum())
+            out[v] = {"median_ms": round(ms, 4), "min_ms": round(min(times[v]), 4),
+                      "tflops": round(flop / ms / 1e9, 1), "speedup": round(base / ms, 4),
+                      "label_mismatch": int((labels[vals[0]] != labels[v]).sum())}
         print(json.dumps(out), flush=True)
-    os.environ.pop("MIKMEANS_ASSIGN_VARG", None)
+    os.environ.pop(args.env, None)
 
 
 if __name__ == "__main__":
