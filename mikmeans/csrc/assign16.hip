@@ -413,35 +413,41 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     for (int p = 0; p < C::P; ++p) efound[p] = 0;
 #pragma unroll
     for (int p = 0; p < C::P; ++p) {
-      u32x4 aw[4][C::NQ];
-      f32x4 acc[4];
+      // MG candidate groups in flight at once (registers: MG * NQ fragments)
+      constexpr int MG = C::NQ <= 2 ? 4 : 1;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const uint32_t tga = (uint32_t)__shfl((int)tb[p], 4 * m + (r >> 2), 64);
-        const int ca = (int)(tga >> 2) * 16 + (int)(tga & 3u) * 4 + (r & 3);   // A row r's centre
-        const T* src = pack + ((int64_t)(ca >> 4) * C::NQ * 64 + (ca & 15) + 16 * g) * C::V;
+      for (int m0 = 0; m0 < 4; m0 += MG) {
+        u32x4 aw[MG][C::NQ];
+        f32x4 acc[MG];
 #pragma unroll
-        for (int q = 0; q < C::NQ; ++q) aw[m][q] = *(const u32x4*)(src + (int64_t)q * 64 * C::V);
-        const uint32_t tgs = (uint32_t)__shfl((int)tb[p], 4 * m + g, 64);     // output rows' point
-        acc[m] = *(const f32x4*)(cn_lds + ((int)(tgs >> 2) * 16 + (int)(tgs & 3u) * 4) * 4);
-        if (ppo) {
-          const float o = opt[(wid * 16 + r) * C::PP + p];
+        for (int mi = 0; mi < MG; ++mi) {
+          const int m = m0 + mi;
+          const uint32_t tga = (uint32_t)__shfl((int)tb[p], 4 * m + (r >> 2), 64);
+          const int ca = (int)(tga >> 2) * 16 + (int)(tga & 3u) * 4 + (r & 3);   // A row r's centre
+          const T* src = pack + ((int64_t)(ca >> 4) * C::NQ * 64 + (ca & 15) + 16 * g) * C::V;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[m][e] += o;
+          for (int q = 0; q < C::NQ; ++q) aw[mi][q] = *(const u32x4*)(src + (int64_t)q * 64 * C::V);
+          const uint32_t tgs = (uint32_t)__shfl((int)tb[p], 4 * m + g, 64);     // output rows' point
+          acc[mi] = *(const f32x4*)(cn_lds + ((int)(tgs >> 2) * 16 + (int)(tgs & 3u) * 4) * 4);
+          if (ppo) {
+            const float o = opt[(wid * 16 + r) * C::PP + p];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[mi][e] += o;
+          }
         }
-      }
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
+        for (int mi = 0; mi < MG; ++mi) {
 #pragma unroll
-        for (int q = 0; q < C::NQ; ++q) acc[m] = Mfma16<T>::run(aw[m][q], xr[p][q], acc[m]);
-      }
+          for (int q = 0; q < C::NQ; ++q) acc[mi] = Mfma16<T>::run(aw[mi][q], xr[p][q], acc[mi]);
+        }
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        if (r == 4 * m + g) {
-          int e = 3;
+        for (int mi = 0; mi < MG; ++mi) {
+          if (r == 4 * (m0 + mi) + g) {
+            int e = 3;
 #pragma unroll
-          for (int j = 2; j >= 0; --j) e = __float_as_uint(acc[m][j]) == vb[p] ? j : e;
-          efound[p] = e;
+            for (int j = 2; j >= 0; --j) e = __float_as_uint(acc[mi][j]) == vb[p] ? j : e;
+            efound[p] = e;
+          }
         }
       }
     }
@@ -610,7 +616,7 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if (splits == 1) b.split_keys = nullptr;
   const dim3 grid((unsigned)nblk, (unsigned)splits);
   bool varg = false;
-  constexpr bool VARG_OK = sizeof(T) == 2 && DPAD <= 64;
+  constexpr bool VARG_OK = sizeof(T) == 2 && DPAD <= 64;   // D=128: -12 % at K=1024, -4 % at 2048 (r3_11)
   if constexpr (VARG_OK) {
     const int e = varg_env();
     varg = e >= 0 ? e != 0 : a.Kpad >= (DPAD == 64 ? 2048 : 1024);
