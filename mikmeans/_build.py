@@ -40,6 +40,12 @@ DEVICE_FLAGS = [
 ]
 
 
+# Per-source extras.  assign16.hip: no SLP vectorizer, so the MFMA seed adds stay scalar
+# v_add_f32 (packed v_pk_add_f32 seeds intermittently corrupted a point block's scores on
+# gfx950; see seed_add in the source).
+SOURCE_FLAGS = {"assign16.hip": ["-fno-slp-vectorize"]}
+
+
 def ext_path() -> Path:
     return PKG / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
 
@@ -119,7 +125,8 @@ def build(force: bool = False, verbose: bool = True, jobs: int | None = None, *,
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         sources = [s for s in HIP_SOURCES if (csrc / s).exists()]
-        futs = [ex.submit(_compile, csrc / s, [*DEVICE_FLAGS, f"-I{csrc}"], verbose, build_dir) for s in sources]
+        futs = [ex.submit(_compile, csrc / s, [*DEVICE_FLAGS, *SOURCE_FLAGS.get(s, []), f"-I{csrc}"], verbose,
+                          build_dir) for s in sources]
         futs.append(ex.submit(_compile, csrc / BINDING, binding_flags, verbose, build_dir))
         objs = [f.result() for f in futs]
     out = out or ext_path()

@@ -81,6 +81,18 @@ struct Assign16Cfg {
   static_assert(PIECES % NW == 0, "chunk pieces must split evenly over waves");
 };
 
+// An MFMA seed plus a per-point offset, as four scalar v_add_f32.  Never a packed
+// v_pk_add_f32: seeds built that way (op_sel broadcasts of the offset) intermittently
+// reached the next MFMA wrong on gfx950 -- one point block of a per-point-offset
+// workgroup got labels from a corrupted seed in 5 of 12 launches
+// (scripts/debug/keys_d32_repro.py, profiles/r3_15_ppo_seed_race.md).  The file is built
+// with -fno-slp-vectorize (mikmeans/_build.py), so these stay scalar.
+__device__ __forceinline__ void seed_add(f32x4& acc, float o) {
+  float a0 = acc[0], a1 = acc[1], a2 = acc[2], a3 = acc[3];
+  a0 += o; a1 += o; a2 += o; a3 += o;
+  acc = f32x4{a0, a1, a2, a3};
+}
+
 template <typename T> struct Mfma16;
 template <> struct Mfma16<uint16_t> {
   __device__ static __forceinline__ f32x4 run(const u32x4& a, const u32x4& b, const f32x4& c) {
@@ -124,7 +136,7 @@ __device__ __forceinline__ float sq16(const u32x4& w, float*) {
 // once per point after the loop by recomputing the winning tile's candidates on the
 // matrix cores (bitwise the main loop's scores), right after the chunk loop.
 template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false,
-          bool VARG = false>
+          bool VARG = false, bool PMAJ = false>
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
@@ -149,8 +161,6 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   const uint32_t loff = (uint32_t)lane * 16u;
   const __amdgpu_buffer_rsrc_t rC = make_rsrc(a.Cpack, (uint32_t)a.Kpad * DPAD * sizeof(T));
   const __amdgpu_buffer_rsrc_t rN = make_rsrc(a.cn, (uint32_t)a.Kpad * 4u);
-  for (int p = wid; p < cn_bytes / 1024; p += C::NW)
-    blds16(rN, (MK_LDS void*)(cn_lds + p * 1024), loff, (uint32_t)p * 1024u);
   auto issue_chunk = [&](int c) {  // c: chunk index within this split (ring slot c % NBUF)
     const uint32_t src = (uint32_t)(c0 + c) * C::CHUNK_BYTES;
     char* dst = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
@@ -160,17 +170,19 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       blds16(rC, (MK_LDS void*)(dst + pc * 1024), loff, src + (uint32_t)pc * 1024u);
     }
   };
-  issue_chunk(0);
 
   const int64_t pbase = (int64_t)blockIdx.x * C::PTS + (int64_t)wid * (C::P * 16);
   u32x4 xr[C::P][C::NQ];
   float xnr[C::P];
-#pragma unroll
-  for (int p = 0; p < C::P; ++p) {
-    int64_t row = pbase + p * 16 + r;
-    row = row < a.N ? row : (a.N - 1);
-    xnr[p] = (!EXACT && a.xn) ? a.xn[row] : 0.f;
-    const int64_t src = a.rows ? a.rows[row] : row;   // gathered batch: logical row -> X row
+  // The P blocks' fragment loads go out back to back: one memory round trip (two for a
+  // gathered batch: the row indices first).  vmcnt retires in order, so a block whose
+  // address waited on a load issued after the previous block's fragments (the row index,
+  // or a row norm under a data-dependent branch) serialised the P round trips.
+  auto row_of = [&](int p) -> int64_t {
+    const int64_t row = pbase + p * 16 + r;
+    return row < a.N ? row : (a.N - 1);
+  };
+  auto load_frags = [&](int p, int64_t src) {
     const T* rp = (const T*)a.X + src * a.ldx + g * C::V;
 #pragma unroll
     for (int q = 0; q < C::NQ; ++q) {
@@ -178,7 +190,31 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       if (FULLD || col < a.D) xr[p][q] = *(const u32x4*)(rp + 4 * q * C::V);
       else xr[p][q] = u32x4{0u, 0u, 0u, 0u};
     }
+  };
+  if (a.rows) {   // gathered batch: logical row -> X row
+    int64_t src[C::P];
+#pragma unroll
+    for (int p = 0; p < C::P; ++p) src[p] = a.rows[row_of(p)];
+    __builtin_amdgcn_sched_barrier(0);   // all index loads in flight before the first use
+#pragma unroll
+    for (int p = 0; p < C::P; ++p) load_frags(p, src[p]);
+  } else {
+#pragma unroll
+    for (int p = 0; p < C::P; ++p) load_frags(p, row_of(p));
   }
+  if (!EXACT && a.xn) {
+#pragma unroll
+    for (int p = 0; p < C::P; ++p) xnr[p] = a.xn[row_of(p)];
+  } else {
+#pragma unroll
+    for (int p = 0; p < C::P; ++p) xnr[p] = 0.f;
+  }
+  // |c|^2 and the first centre chunk by LDS-DMA, issued after the fragments so no wait for a
+  // fragment address (the gathered row indices) also waits for them
+  __builtin_amdgcn_sched_barrier(0);
+  for (int p = wid; p < cn_bytes / 1024; p += C::NW)
+    blds16(rN, (MK_LDS void*)(cn_lds + p * 1024), loff, (uint32_t)p * 1024u);
+  issue_chunk(0);
   wait_vmcnt<0>();  // retire the fragments before the LDS-DMA loop (its vmcnt waits count chunks)
   if (C::NBUF == 3 && ncl > 1) issue_chunk(1);
 
@@ -303,7 +339,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
             const f32x4 ov = *(const f32x4*)(o + p4);
   #pragma unroll
             for (int j = 0; j < 4; ++j)
-              if (p4 + j < C::P) acc[p4 + j] += ov[j];
+              if (p4 + j < C::P) seed_add(acc[p4 + j], ov[j]);
           }
         }
         // bf16: the wave issues its MFMAs at raised priority and drops back for the epilogue,
@@ -316,10 +352,23 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
           __builtin_amdgcn_s_setprio(1);
           __builtin_amdgcn_sched_barrier(0);
         }
+        if constexpr (PMAJ) {
+          // point-block-major issue: each accumulator's NQ MFMAs back to back (srcC = the
+          // previous vDst), pinned in this order
   #pragma unroll
-        for (int q = 0; q < C::NQ; ++q) {
+          for (int p = 0; p < C::P; ++p) {
   #pragma unroll
-          for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
+            for (int q = 0; q < C::NQ; ++q) {
+              acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        } else {
+  #pragma unroll
+          for (int q = 0; q < C::NQ; ++q) {
+  #pragma unroll
+            for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
+          }
         }
         if constexpr (!EXACT) {
           __builtin_amdgcn_sched_barrier(0);
@@ -430,9 +479,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
           const uint32_t tgs = (uint32_t)__shfl((int)tb[p], 4 * m + g, 64);     // output rows' point
           acc[mi] = *(const f32x4*)(cn_lds + ((int)(tgs >> 2) * 16 + (int)(tgs & 3u) * 4) * 4);
           if (ppo) {
-            const float o = opt[(wid * 16 + r) * C::PP + p];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[mi][e] += o;
+            seed_add(acc[mi], opt[(wid * 16 + r) * C::PP + p]);
           }
         }
 #pragma unroll
@@ -581,24 +628,39 @@ static int varg_env() {   // read per launch (tests switch it inside one process
   return (e && *e) ? atoi(e) : -1;
 }
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, bool PMAJ>
 static void set_lds_attr() {
   static bool done = false;
   if (done) return;
-  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG>,
+  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG>,
+  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   done = true;
 }
 
+// Point-block-major MFMA issue (PMAJ); MIKMEANS_ASSIGN_PMAJ=0/1 forces it off / on.
+static int pmaj_env() {   // read per launch (A/B harnesses switch it inside one process)
+  const char* e = getenv("MIKMEANS_ASSIGN_PMAJ");
+  return (e && *e) ? atoi(e) : -1;
+}
+
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, bool PMAJ>
+static void launch16_kp(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
+  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ>();
+  if (b.D == DPAD)
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ>), grid, dim3(NW_ * 64), lds, s, b);
+  else
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ>), grid, dim3(NW_ * 64), lds, s, b);
+}
+
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG>
 static void launch16_k(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG>();
-  if (b.D == DPAD)
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG>), grid, dim3(NW_ * 64), lds, s, b);
-  else
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG>), grid, dim3(NW_ * 64), lds, s, b);
+  {
+    const int e = pmaj_env();
+    if (e >= 0 ? e != 0 : (sizeof(T) == 2 && DPAD >= 128)) return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, true>(b, grid, lds, s);
+  }
+  launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, false>(b, grid, lds, s);
 }
 
 template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4>
@@ -650,6 +712,13 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   constexpr int P = sizeof(T) == 2 ? (DPAD == 64 ? 8 : DPAD == 256 ? 3 : 4) : (NQ >= 8 ? 2 : 4);
   constexpr int OCC = sizeof(T) == 2 ? ((DPAD == 64 || DPAD == 256) ? 3 : 4) : 1;
   static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
+  if constexpr (sizeof(T) == 2 && DPAD == 256) {
+    // A/B switch MIKMEANS_ASSIGN_GEOM: 1 = 3-slot ring, 2 = 4 point blocks at 2 waves/SIMD
+    const char* e = getenv("MIKMEANS_ASSIGN_GEOM");
+    const int gm = (e && *e) ? atoi(e) : 0;
+    if (gm == 1) return launch16_t<T, DPAD, P, CT, 3, OCC>(a, s);
+    if (gm == 2) return launch16_t<T, DPAD, 4, CT, 2, 2>(a, s);
+  }
   return launch16_t<T, DPAD, P, CT, 2, OCC>(a, s);
 }
 

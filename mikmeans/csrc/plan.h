@@ -90,6 +90,7 @@ struct KsPlan {
 };
 constexpr int KS_NT = 1024;                         // threads per workgroup
 constexpr size_t KS_LIST_BYTES = 2 * (KS_NT / 64) * 64 * 4;  // per-wave match lists, 2 periods
+constexpr size_t KS_GLIST_BYTES = 2 * (KS_NT / 64) * 64 * 8 + 8;  // gathered batches: their X rows (+ 8-B alignment)
 MK_HD inline size_t ks_lds_bytes(int kq, int ldc) {
   return (size_t)kq * (size_t)ldc * 8 + (size_t)kq * 4 + 16 + KS_LIST_BYTES;
 }

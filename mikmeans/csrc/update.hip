@@ -519,6 +519,12 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
   unsigned* nadd = (unsigned*)(cells + (size_t)kq * ldc);
   int* flag = (int*)(nadd + kq);
   unsigned* lists = (unsigned*)(flag + 4);          // [2 periods][NT/64 waves][64]
+  // GATHER: the X row of every listed row, [2 periods][NT/64 waves][64], written by the
+  // compaction from indices loaded with the labels two periods ahead, so no X load waits on
+  // an index load issued after older X loads (vmcnt retires in order: it serialised the
+  // row groups in flight)
+  const size_t goff = ((size_t)((char*)(lists + 2 * (NT / 64) * 64) - smem) + 7) & ~(size_t)7;
+  long long* glists = (long long*)(smem + goff);
 
   const int b = blockIdx.x, jb = b >> 3;
   const int ksi = jb % ks;
@@ -547,25 +553,33 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
   const int64_t rsafe = row0 < row1 ? row0 : 0;    // a valid row for masked lanes
 
   auto label_at = [&](int64_t i) -> int { return i < row1 ? a.labels[i] : -1; };
-  // rows [base + wid*64, +64) of this wave: compact the owned ones into lst, return the count
-  auto compact = [&](int lab, unsigned* lst) -> int {
+  auto xrow_at = [&](int64_t i) -> long long { return GATHER ? (i < row1 ? a.rows[i] : a.rows[rsafe]) : 0; };
+  // rows [base + wid*64, +64) of this wave: compact the owned ones into lst (and, gathered,
+  // their X rows into gl), return the count
+  auto compact = [&](int lab, long long xrow, unsigned* lst, long long* gl) -> int {
     const unsigned rel = (unsigned)(lab - k0);
     const bool m = rel < (unsigned)kn;
     const unsigned long long bal = __ballot(m);
     const int pos = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-    if (m) lst[pos] = (unsigned)lane | (rel << 6);
+    if (m) {
+      lst[pos] = (unsigned)lane | (rel << 6);
+      if constexpr (GATHER) gl[pos] = xrow;
+    }
     return (int)__popcll(bal);
   };
   // one row group per instruction: entries [g0 + j*RG, +RG) of lst; label -1 = no row
-  auto issue = [&](const unsigned* lst, int cnt, int64_t wbase, int g0, u32x4* xb, int* lb) {
+  auto issue = [&](const unsigned* lst, const long long* gl, int cnt, int64_t wbase, int g0, u32x4* xb,
+                   int* lb) {
 #pragma unroll
     for (int j = 0; j < GM; ++j) {
       const int e = g0 + j * RG + rr;
       const bool v = e < cnt;
       const unsigned ent = lst[v ? e : 0];
-      const int64_t row = v ? wbase + (int64_t)(ent & 63u) : rsafe;
-      xb[j] = *(const u32x4*)(xcol + (GATHER ? a.rows[row] : row) * a.ldx);
+      int64_t row;
+      if constexpr (GATHER) row = v ? (int64_t)gl[e] : (int64_t)gl[0];
+      else row = v ? wbase + (int64_t)(ent & 63u) : rsafe;
+      xb[j] = *(const u32x4*)(xcol + row * a.ldx);
       lb[j] = v ? (int)(ent >> 6) : -1;
     }
   };
@@ -598,18 +612,22 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
 
   unsigned* lbuf0 = lists + wid * 64;
   unsigned* lbuf1 = lists + (NT / 64) * 64 + wid * 64;
+  long long* gbuf0 = glists + wid * 64;
+  long long* gbuf1 = glists + (NT / 64) * 64 + wid * 64;
   // prologue: period 0 compacted and its first groups in flight, period 1's labels loaded
   int lab_next = label_at(row0 + NT + threadIdx.x);
-  int cnt = compact(label_at(row0 + threadIdx.x), lbuf0);
+  long long xr_next = xrow_at(row0 + NT + threadIdx.x);
+  int cnt = compact(label_at(row0 + threadIdx.x), xrow_at(row0 + threadIdx.x), lbuf0, gbuf0);
   u32x4 xa[GM];
   int la[GM];
-  issue(lbuf0, cnt, row0 + wid * 64, 0, xa, la);
+  issue(lbuf0, gbuf0, cnt, row0 + wid * 64, 0, xa, la);
   for (int64_t base = row0; base < row1; base += NT) {
     const int lab_nn = label_at(base + 2 * NT + threadIdx.x);
-    const int cnt_n = compact(lab_next, lbuf1);
+    const long long xr_nn = xrow_at(base + 2 * NT + threadIdx.x);
+    const int cnt_n = compact(lab_next, xr_next, lbuf1, gbuf1);
     u32x4 xb[GM];
     int lb[GM];
-    issue(lbuf1, cnt_n, base + NT + wid * 64, 0, xb, lb);
+    issue(lbuf1, gbuf1, cnt_n, base + NT + wid * 64, 0, xb, lb);
 #pragma unroll
     for (int j = 0; j < GM; ++j)
       if (la[j] >= 0) accumulate(xa[j], la[j]);
@@ -618,8 +636,8 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
       const int e = g0 + rr;
       if (e < cnt) {
         const unsigned ent = lbuf0[e];
-        const int64_t row = base + wid * 64 + (int64_t)(ent & 63u);
-        const u32x4 w = *(const u32x4*)(xcol + (GATHER ? a.rows[row] : row) * a.ldx);
+        const int64_t row = GATHER ? (int64_t)gbuf0[e] : base + wid * 64 + (int64_t)(ent & 63u);
+        const u32x4 w = *(const u32x4*)(xcol + row * a.ldx);
         accumulate(w, (int)(ent >> 6));
       }
     }
@@ -635,7 +653,9 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
     for (int j = 0; j < GM; ++j) { xa[j] = xb[j]; la[j] = lb[j]; }
     cnt = cnt_n;
     lab_next = lab_nn;
+    xr_next = xr_nn;
     unsigned* t = lbuf0; lbuf0 = lbuf1; lbuf1 = t;
+    long long* tg = gbuf0; gbuf0 = gbuf1; gbuf1 = tg;
   }
   __syncthreads();
   ks_flush<T, LPR>(a, smem, kq, kn, ldc, NPAIR, k0, chunk, 0u);
@@ -825,9 +845,10 @@ static hipError_t launch_ks_t(const UpdateArgs& a, const plan::KsPlan& kp, hipSt
     attr = true;
   }
   const int64_t rows_per_chunk = (a.N + a.n_chunks - 1) / a.n_chunks;
+  const size_t lds = plan::ks_lds_bytes(kp.kq, kp.ldc) + (GATHER ? plan::KS_GLIST_BYTES : 0);
+  if (lds > UPD_LDS_MAX) return hipErrorInvalidValue;
   hipLaunchKernelGGL((update_ks_kernel<T, LPR, GM, CLAMP, GATHER>), dim3((unsigned)(a.n_chunks * kp.ks)),
-                     dim3(plan::KS_NT), plan::ks_lds_bytes(kp.kq, kp.ldc), s, a, kp.ks, kp.kq, kp.ldc,
-                     rows_per_chunk);
+                     dim3(plan::KS_NT), lds, s, a, kp.ks, kp.kq, kp.ldc, rows_per_chunk);
   return hipGetLastError();
 }
 

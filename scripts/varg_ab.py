@@ -21,12 +21,14 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--env", default="MIKMEANS_ASSIGN_VARG", help="variable switched between the arms")
     ap.add_argument("--values", default="0,1", help="its values, one arm each (first = baseline)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     args = ap.parse_args()
     for sh in args.shapes.split(";"):
         n, d, k = (int(v) for v in sh.split(","))
-        X = B.make_blobs(n, d, 256, seed=d, dtype=torch.bfloat16, device="cuda")
+        dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+        X = B.make_blobs(n, d, 256, seed=d, dtype=dt, device="cuda")
         C = X[torch.randperm(n, generator=torch.Generator().manual_seed(1))[:k].cuda()].float()
-        pack = ops.pack_centers(C, d, torch.bfloat16, "cuda")
+        pack = ops.pack_centers(C, d, dt, "cuda")
         xn = ops.row_sqnorm(X)
         vals = args.values.split(",")
         labels = {v: torch.empty(n, dtype=torch.int32, device="cuda") for v in vals}
@@ -43,7 +45,7 @@ def main():
                 torch.cuda.synchronize()
                 times[v].append(ev[0].elapsed_time(ev[1]) / args.reps)
         flop = 2.0 * n * k * d
-        out = {"n": n, "d": d, "k": k, "env": args.env}
+        out = {"n": n, "d": d, "k": k, "dtype": args.dtype, "env": args.env}
         base = statistics.median(times[vals[0]])
         for v in vals:
             ms = statistics.median(times[v])

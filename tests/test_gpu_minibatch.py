@@ -111,14 +111,18 @@ def test_minibatch_fit_steps_do_not_sync(native):
     assert per_step <= 0.1 + 12 / 40, per_step
 
 
-@pytest.mark.parametrize("D,K,dtype", [(256, 512, torch.bfloat16), (128, 1024, torch.bfloat16),
-                                       (64, 4096, torch.bfloat16), (128, 256, torch.float32),
-                                       (40, 20000, torch.float32)])
-def test_gathered_rows_step_equals_materialised_batch(native, D, K, dtype):
+@pytest.mark.parametrize("D,K,dtype,force_ks", [(256, 512, torch.bfloat16, None), (128, 1024, torch.bfloat16, None),
+                                                (64, 4096, torch.bfloat16, None), (128, 256, torch.float32, None),
+                                                (40, 20000, torch.float32, None), (256, 512, torch.bfloat16, "1")])
+def test_gathered_rows_step_equals_materialised_batch(native, monkeypatch, D, K, dtype, force_ks):
     """partial_fit_rows (assign + M-step reading X[rows] through the index list: slice,
-    K-split and global-atomic M-step kernels) equals partial_fit on the gathered copy."""
+    K-split and global-atomic M-step kernels; force_ks: the K-split kernel where the slice
+    kernel is the default) equals partial_fit on the gathered copy."""
     from mikmeans.models.minibatch import MiniBatchEngine
     from mikmeans.ops import col_stats, pad_columns
+
+    if force_ks is not None:
+        monkeypatch.setenv("MIKMEANS_UPDATE_KS", force_ks)
 
     n, b = 600_000, 270_000     # b > SPLIT_MAX_ROWS: both paths take the one-pass assign grid
     X = pad_columns(B.make_blobs(n, D, 64, seed=D, dtype=dtype, device=DEV))
