@@ -639,7 +639,14 @@ static void set_lds_attr() {
   done = true;
 }
 
-// Point-block-major MFMA issue (PMAJ); MIKMEANS_ASSIGN_PMAJ=0/1 forces it off / on.
+// Point-block-major MFMA issue (PMAJ), the bf16 default: each accumulator's NQ MFMAs back to
+// back instead of one A fragment against the P blocks in turn.  One-process A/B, bitwise the
+// same labels (profiles/r3_15_ab_pmaj*.log): D=128 K=1024 +2.8 %, K=2048 +3.8 %; D=256 K=512
+// +3.3 %; D=64 K=4096 (value-only argmin) +4.0 %, K=1024 +3.9 %; D=32 +1 %; f32 -0.5..-1 %
+// (its 16x16x4 MFMAs already chain 4 deep).  Same MFMAs, same registers: the gain is in the
+// clock the power-bound chip holds, presumably because a chained srcC is forwarded inside the
+// matrix core instead of being read from the register file.
+// MIKMEANS_ASSIGN_PMAJ=0/1 forces it off / on.
 static int pmaj_env() {   // read per launch (A/B harnesses switch it inside one process)
   const char* e = getenv("MIKMEANS_ASSIGN_PMAJ");
   return (e && *e) ? atoi(e) : -1;
@@ -658,7 +665,7 @@ template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, boo
 static void launch16_k(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
   {
     const int e = pmaj_env();
-    if (e >= 0 ? e != 0 : (sizeof(T) == 2 && DPAD >= 128)) return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, true>(b, grid, lds, s);
+    if (e >= 0 ? e != 0 : sizeof(T) == 2) return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, true>(b, grid, lds, s);
   }
   launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, false>(b, grid, lds, s);
 }

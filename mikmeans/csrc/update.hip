@@ -577,7 +577,7 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
       const bool v = e < cnt;
       const unsigned ent = lst[v ? e : 0];
       int64_t row;
-      if constexpr (GATHER) row = v ? (int64_t)gl[e] : (int64_t)gl[0];
+      if constexpr (GATHER) row = v ? (int64_t)gl[e] : 0;   // (masked lanes: X row 0; gl[0] may be stale)
       else row = v ? wbase + (int64_t)(ent & 63u) : rsafe;
       xb[j] = *(const u32x4*)(xcol + row * a.ldx);
       lb[j] = v ? (int)(ent >> 6) : -1;
@@ -879,7 +879,10 @@ static hipError_t launch_ks(const UpdateArgs& a, const plan::KsPlan& kp, hipStre
 hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s) {
   if (a.N <= 0) return hipSuccess;
   plan::KsPlan kp;
-  if (!a.dlist && !a.col_exp2 && use_ks(dtype, a.K, a.D, a.weights != nullptr, &kp)) {
+  // (gathered batches stage their X rows in LDS too; where that does not fit, the slice
+  // kernel takes the pass -- any chunk count that is a multiple of 8 serves it)
+  if (!a.dlist && !a.col_exp2 && use_ks(dtype, a.K, a.D, a.weights != nullptr, &kp) &&
+      (!a.rows || plan::ks_lds_bytes(kp.kq, kp.ldc) + plan::KS_GLIST_BYTES <= UPD_LDS_MAX)) {
     if (a.n_chunks % 8) return hipErrorInvalidValue;
     return dtype == DT_BF16 ? launch_ks<uint16_t>(a, kp, s) : launch_ks<float>(a, kp, s);
   }
