@@ -643,9 +643,12 @@ static void set_lds_attr() {
 // back instead of one A fragment against the P blocks in turn.  One-process A/B, bitwise the
 // same labels (profiles/r3_15_ab_pmaj*.log): D=128 K=1024 +2.8 %, K=2048 +3.8 %; D=256 K=512
 // +3.3 %; D=64 K=4096 (value-only argmin) +4.0 %, K=1024 +3.9 %; D=32 +1 %; f32 -0.5..-1 %
-// (its 16x16x4 MFMAs already chain 4 deep).  Same MFMAs, same registers: the gain is in the
-// clock the power-bound chip holds, presumably because a chained srcC is forwarded inside the
-// matrix core instead of being read from the register file.
+// (its 16x16x4 MFMAs already chain 4 deep).  Same MFMAs, same registers; the gain is MFMA
+// pipe utilisation, not clock: block 0's scores are final 12 MFMAs before the last issue
+// instead of 3, so the epilogue's first reads no longer wait on the matrix pipe
+// (scripts/microbench/mfma_shape.hip mode 1, profiles/r3_17_mfma_issue_order.log: with the
+// key epilogue 84.4 -> 91.6 % at 1780 -> 1762 MHz, +7.5 % TF/s; 32x32x16 gains 3.6 % the
+// same way and stays 12 % behind).
 // MIKMEANS_ASSIGN_PMAJ=0/1 forces it off / on.
 static int pmaj_env() {   // read per launch (A/B harnesses switch it inside one process)
   const char* e = getenv("MIKMEANS_ASSIGN_PMAJ");

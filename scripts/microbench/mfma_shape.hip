@@ -50,7 +50,7 @@ __global__ void fill(uint16_t* p, int64_t n, int zero, uint32_t seed) {
   p[i] = (uint16_t)(__float_as_uint(f) >> 16);
 }
 
-template <int S, int D, int EPI>
+template <int S, int D, int EPI, int ORD = 0>
 __global__ __launch_bounds__(NT) void kern(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Cg,
                                            float* __restrict__ out, unsigned long long* __restrict__ stamps,
                                            int sweeps) {
@@ -94,11 +94,24 @@ __global__ __launch_bounds__(NT) void kern(const uint16_t* __restrict__ X, const
         f32x4 acc[NB];
 #pragma unroll
         for (int b = 0; b < NB; ++b) acc[b] = EPI ? f32x4{0.f, 0.f, 0.f, 0.f} : p16[b];
+        if constexpr (ORD) {   // point-block-major: each accumulator's k-steps back to back
+          short8 cf[KS];
+#pragma unroll
+          for (int s = 0; s < KS; ++s) cf[s] = *(const short8*)(cl + ((t * KS + s) * 64 + lane) * 8);
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+              acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cf[s], xf[b][s], acc[b], 0, 0, 0);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
           const short8 cf = *(const short8*)(cl + ((t * KS + s) * 64 + lane) * 8);  // fragment-packed: 1 KB per (tile, k-step)
 #pragma unroll
           for (int b = 0; b < NB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cf, xf[b][s], acc[b], 0, 0, 0);
+        }
         }
         if constexpr (EPI == 2) {
           // value-only argmin: 2 v_min3_u32 (non-negative scores order as their bits) fold
@@ -134,11 +147,24 @@ __global__ __launch_bounds__(NT) void kern(const uint16_t* __restrict__ X, const
         for (int b = 0; b < NB; ++b)
 #pragma unroll
           for (int j = 0; j < 16; ++j) acc[b][j] = EPI ? 0.f : p32[b][j];
+        if constexpr (ORD) {
+          short8 cf[KS];
+#pragma unroll
+          for (int s = 0; s < KS; ++s) cf[s] = *(const short8*)(cl + ((t * KS + s) * 64 + lane) * 8);
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+              acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf[s], xf[b][s], acc[b], 0, 0, 0);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
           const short8 cf = *(const short8*)(cl + ((t * KS + s) * 64 + lane) * 8);  // fragment-packed: 1 KB per (tile, k-step)
 #pragma unroll
           for (int b = 0; b < NB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf, xf[b][s], acc[b], 0, 0, 0);
+        }
         }
         if constexpr (EPI != 0) {
 #pragma unroll
@@ -186,7 +212,7 @@ __global__ __launch_bounds__(NT) void kern(const uint16_t* __restrict__ X, const
   }
 }
 
-template <int S, int D, int EPI>
+template <int S, int D, int EPI, int ORD = 0>
 int run(const char* name, const uint16_t* X, const uint16_t* C, float* out, unsigned long long* st, int grid,
         int sweeps, const char* data) {
   hipEvent_t a, b;
@@ -196,7 +222,7 @@ int run(const char* name, const uint16_t* X, const uint16_t* C, float* out, unsi
   float warm = 0.f;
   while (warm < 2000.f) {
     CK(hipEventRecord(a));
-    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((kern<S, D, EPI>), dim3(grid), dim3(NT), 0, 0, X, C, out, st, sweeps);
+    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((kern<S, D, EPI, ORD>), dim3(grid), dim3(NT), 0, 0, X, C, out, st, sweeps);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
@@ -205,7 +231,7 @@ int run(const char* name, const uint16_t* X, const uint16_t* C, float* out, unsi
   }
   const int reps = 20;
   CK(hipEventRecord(a));
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((kern<S, D, EPI>), dim3(grid), dim3(NT), 0, 0, X, C, out, st, sweeps);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((kern<S, D, EPI, ORD>), dim3(grid), dim3(NT), 0, 0, X, C, out, st, sweeps);
   CK(hipEventRecord(b));
   CK(hipEventSynchronize(b));
   CK(hipGetLastError());
@@ -222,8 +248,8 @@ int run(const char* name, const uint16_t* X, const uint16_t* C, float* out, unsi
   const double mhz = clk[grid / 2];
   // pipe utilisation at the measured clock: 1024 SIMDs x 1024 FLOP/cycle (bf16 dense)
   const double util = tf * 1e12 / (1024.0 * 1024.0 * mhz * 1e6);
-  printf("%-10s D=%-3d %-6s epi=%d  %8.3f ms  %7.1f TF/s  clock %6.0f MHz (p10 %4.0f p90 %4.0f)  MFMA util %5.1f %%\n",
-         name, D, data, EPI, ms, tf, mhz, clk[grid / 10], clk[grid * 9 / 10], util * 100.0);
+  printf("%-10s ord=%d D=%-3d %-6s epi=%d  %8.3f ms  %7.1f TF/s  clock %6.0f MHz (p10 %4.0f p90 %4.0f)  MFMA util %5.1f %%\n",
+         name, ORD, D, data, EPI, ms, tf, mhz, clk[grid / 10], clk[grid * 9 / 10], util * 100.0);
   fflush(stdout);
   CK(hipEventDestroy(a));
   CK(hipEventDestroy(b));
@@ -241,6 +267,20 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&C, (size_t)KC * DMAX * 2));
   CK(hipMalloc(&out, (size_t)grid * NT * 4));
   CK(hipMalloc(&st, (size_t)grid * 16));
+  if (argc > 3 && atoi(argv[3]) == 1) {   // issue-order study: q-major vs point-block-major
+    hipLaunchKernelGGL(fill, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, 0, X, nx, 0, 1u);
+    hipLaunchKernelGGL(fill, dim3((KC * DMAX + 255) / 256), dim3(256), 0, 0, C, (int64_t)KC * DMAX, 0, 7u);
+    CK(hipDeviceSynchronize());
+    for (int round = 0; round < 2; ++round) {
+      if (run<16, 128, true, 0>("16x16x32", X, C, out, st, grid, sweeps, "random")) return 1;
+      if (run<16, 128, true, 1>("16x16x32", X, C, out, st, grid, sweeps, "random")) return 1;
+      if (run<32, 128, true, 0>("32x32x16", X, C, out, st, grid, sweeps, "random")) return 1;
+      if (run<32, 128, true, 1>("32x32x16", X, C, out, st, grid, sweeps, "random")) return 1;
+      if (run<16, 128, false, 1>("16x16x32", X, C, out, st, grid, sweeps, "random")) return 1;
+      if (run<32, 128, false, 1>("32x32x16", X, C, out, st, grid, sweeps, "random")) return 1;
+    }
+    return 0;
+  }
   for (int zero = 0; zero < 2; ++zero) {
     const char* data = zero ? "zeros" : "random";
     hipLaunchKernelGGL(fill, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, 0, X, nx, zero, 1u);
