@@ -219,7 +219,19 @@ __device__ void upd_flush_all(const UpdateArgs& a, const UpdLayout& L, char* m, 
   }
 }
 
-enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8, UPD_RESID = 32, UPD_GATHER = 64 };
+enum : int { UPD_CLAMP = 1, UPD_WEIGHTED = 2, UPD_SWZ = 4, UPD_DELTA = 8, UPD_RESID = 32, UPD_GATHER = 64,
+             UPD_GSTAGE = 128 };
+
+// Rows per period of the column-slice kernel (host and device agree on it: the gathered
+// index staging sizes its LDS ring from it).
+template <typename T, int SW, int NT, int PER>
+constexpr int upd_period() {
+  constexpr int PB = (SW * (int)sizeof(T) >= 16) ? 16 : SW * (int)sizeof(T);
+  constexpr int V = PB / (int)sizeof(T);
+  constexpr int RPP = NT / (SW / V);
+  constexpr int UNR = (PER / RPP) < 8 ? (PER / RPP) : 8;
+  return RPP * UNR;
+}
 
 constexpr int upd_ksh(int np) { return np >= 32 ? 0 : np == 16 ? 1 : np == 8 ? 2 : np == 4 ? 3 : np == 2 ? 4 : 5; }
 using plan::upd_lds_bytes;
@@ -234,6 +246,10 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   constexpr bool SWZ = MODE & UPD_SWZ;
   constexpr bool RESID = MODE & UPD_RESID;               // lo pass of the wide-range columns
   constexpr bool GATHER = MODE & UPD_GATHER;             // logical row i is X row a.rows[i]
+  // GSTAGE (gathered): the X rows of a period are staged in an LDS ring NBF periods ahead,
+  // so no X load's address waits on an index load issued after older X loads (vmcnt retires
+  // in order: the unstaged path drained the whole prefetch ring every period)
+  constexpr bool GSTAGE = GATHER && (MODE & UPD_GSTAGE) && !DELTA;
   constexpr int ES = sizeof(T);
   constexpr int PB = (SW * ES >= 16) ? 16 : SW * ES;  // bytes per lane load
   constexpr int V = PB / ES;                           // elements per lane load (even)
@@ -246,6 +262,8 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   constexpr int LDC = SWZ ? NP : NP + 1;                // unpadded + swizzle, or odd stride
   constexpr int KSH = upd_ksh(NP);
   static_assert(V % 2 == 0 && UNR >= 1 && FX_LIM >= PERIOD, "update tiling");
+  static_assert(PERIOD == upd_period<T, SW, NT, PER>(), "host period");
+  constexpr int GI = (PERIOD + NT - 1) / NT;            // GSTAGE: staged indices per thread
   typedef typename LoadT<PB>::type LT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const UpdLayout L{a.K, LDC, NP, KSH, SWZ, LPR, V / 2};
@@ -288,7 +306,6 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   const int lr = threadIdx.x / LPR, lp = threadIdx.x % LPR;
   const int col = slice * SW + lp * V;
   const bool colok = col < a.D;
-  const bool all_cols = (a.D % SW) == 0;               // kernel-uniform
   const int colc = colok ? col : 0;
   const bool counter = lp == 0;
   const bool wcounter = W && counter && slice == 0;
@@ -310,9 +327,21 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   const T* xrow = (const T*)a.X + (row0 + (int64_t)lr * UNR) * a.ldx + colc;
   const int* lrow = a.labels + row0 + lr * UNR;
   const float* wrow = a.weights ? a.weights + row0 + lr * UNR : nullptr;
-  auto load = [&](int64_t base, LT* w_, int* lab_, float* wt_) {
+  long long* gidx = (long long*)(smem + upd_lds_bytes(a.K, LDC, W));   // GSTAGE: [NBF][PERIOD]
+  auto load = [&](int64_t base, LT* w_, int* lab_, float* wt_, int slot) {
+    const long long* gs = gidx + slot * PERIOD + lr * UNR;
     const int64_t off = base - row0;
-    if (DELTA && !full) {                              // gather the listed rows
+    if constexpr (GSTAGE) {
+      // one straight-line form for every period (rows past the chunk clamp to its last row;
+      // accumulate sends them to the sink): a branch between differently shaped load
+      // sequences made the wait counter at the join fall back to vmcnt(0), draining the ring
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int64_t i0 = base + (int64_t)lr * UNR + u;
+        lab_[u] = a.labels[i0 < row1 ? i0 : row1 - 1];
+        w_[u] = *(const LT*)((const T*)a.X + gs[u] * a.ldx + colc);
+      }
+    } else if (DELTA && !full) {                       // gather the listed rows
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const int64_t j0 = base + (int64_t)lr * UNR + u;
@@ -333,7 +362,9 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
         lab_[u] = ((unsigned)l < (unsigned)a.K) ? l : a.K;
         if constexpr (DELTA) wt_[u] = wrow ? wrow[off + u] : 1.f;
         else if constexpr (W) wt_[u] = wrow[off + u];
-        if constexpr (GATHER)
+        if constexpr (GSTAGE)
+          w_[u] = *(const LT*)((const T*)a.X + gs[u] * a.ldx + colc);
+        else if constexpr (GATHER)
           w_[u] = *(const LT*)((const T*)a.X + a.rows[base + (int64_t)lr * UNR + u] * a.ldx + colc);
         else
           w_[u] = *(const LT*)(p + u * a.ldx);
@@ -347,17 +378,31 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
         lab_[u] = (i0 < row1 && (unsigned)l < (unsigned)a.K) ? l : a.K;
         if constexpr (DELTA) wt_[u] = a.weights ? a.weights[i] : 1.f;
         else if constexpr (W) wt_[u] = a.weights[i];
-        w_[u] = *(const LT*)((const T*)a.X + (GATHER ? a.rows[i] : i) * a.ldx + colc);
+        if constexpr (GSTAGE) w_[u] = *(const LT*)((const T*)a.X + gs[u] * a.ldx + colc);   // staged rows[min(i0, row1-1)]
+        else w_[u] = *(const LT*)((const T*)a.X + (GATHER ? a.rows[i] : i) * a.ldx + colc);
       }
     }
-    if (!all_cols && !colok) {
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) w_[u] = LT{};
-    }
+    // (lanes past the last column read column 0 of the row and add fma(x, 0, MAGIC) = +0:
+    // their scales are 0.  Zeroing the loaded registers here instead waited for every load
+    // of the period right after issuing it, in every build of the kernel.)
   };
 
   // Accumulate one period; sets the flush flag when a label's add count nears FX_LIM.
-  auto accumulate = [&](const LT* w_, const int* lab_, const float* wt_) {
+  // (GSTAGE: load leaves the raw labels and accumulate sends rows past the chunk and
+  // out-of-range labels -- unassigned rows -- to the sink row K; clamping them in load made
+  // each period's labels wait for their load right after it was issued, draining the ring.
+  // The other builds clamp in load, which measured 2 % faster for the f32 64-column kernel.)
+  auto accumulate = [&](int64_t base, const LT* w_, const int* labr_, const float* wt_, auto&& pre_barrier) {
+    int lab_[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if constexpr (GSTAGE) {
+        const bool in = base + (int64_t)lr * UNR + u < row1;
+        lab_[u] = (in && (unsigned)labr_[u] < (unsigned)a.K) ? labr_[u] : a.K;
+      } else {
+        lab_[u] = labr_[u];
+      }
+    }
     unsigned seen = 0;
     unsigned long long acc[V / 2];
     int cur = lab_[0];
@@ -418,9 +463,31 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
     }
     emit();
     if (seen >= THRESH) *L.flag(smem) = 1;
+    pre_barrier();
     // LDS-only barrier: the prefetched global loads stay in flight
     wait_lgkm0();
     raw_barrier();
+  };
+  // GSTAGE: thread t < PERIOD stages rows[pbase + t] (clamped to the chunk's last row, as
+  // the unstaged tail clamps); the load is issued before the step's X loads, the LDS store
+  // happens before the step's closing barrier
+  auto idx_load = [&](int64_t pbase, long long* v) {
+#pragma unroll
+    for (int q = 0; q < GI; ++q) {
+      const int t = (int)threadIdx.x + q * NT;
+      const int64_t i = pbase + t;
+      v[q] = (GSTAGE && t < PERIOD && pbase < row1) ? a.rows[i < row1 ? i : row1 - 1] : 0;
+    }
+  };
+  auto idx_store = [&](int slot, const long long* v) {
+#pragma unroll
+    for (int q = 0; q < GI; ++q) {
+      const int t = (int)threadIdx.x + q * NT;
+      // consumed on every lane: the index load's wait then sits here, not at the next
+      // step's reuse of the register (which waited for every X load in flight)
+      if constexpr (GSTAGE) asm volatile("" ::"v"(v[q]));
+      if (GSTAGE && t < PERIOD) gidx[slot * PERIOD + t] = v[q];
+    }
   };
 
   // NB-deep ring of period buffers: NB-1 periods of loads in flight while one accumulates
@@ -428,9 +495,17 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   LT wb[NB][UNR];
   int lb[NB][UNR];
   float tb[NB][UNR];
+  if constexpr (GSTAGE) {   // the rows of periods 0..NB-1, slot j % NB for period j
+    long long g[NB][GI];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) idx_load(row0 + (int64_t)q * PERIOD, g[q]);
+#pragma unroll
+    for (int q = 0; q < NB; ++q) idx_store(q, g[q]);
+    __syncthreads();
+  }
 #pragma unroll
   for (int s = 0; s < NB - 1; ++s)
-    if (row0 + (int64_t)s * PERIOD < row1) load(row0 + (int64_t)s * PERIOD, wb[s], lb[s], tb[s]);
+    if (row0 + (int64_t)s * PERIOD < row1) load(row0 + (int64_t)s * PERIOD, wb[s], lb[s], tb[s], s);
   __syncthreads();
   for (int64_t base = row0; base < row1; base += (int64_t)NB * PERIOD) {
 #pragma unroll
@@ -439,8 +514,19 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
       if (pb < row1) {
         const int64_t nb = pb + (int64_t)(NB - 1) * PERIOD;
         const int ns = (s + NB - 1) % NB;  // static after unrolling
-        if (nb < row1) load(nb, wb[ns], lb[ns], tb[ns]);
-        accumulate(wb[s], lb[s], tb[s]);
+        if constexpr (GSTAGE) {
+          // period j = s (mod NB): X of period j+NB-1 from slot ns; rows of period j+NB into
+          // slot s (period j's, read NB-1 steps ago).  The X loads go out unconditionally
+          // (past the chunk they clamp to its last row) so every step issues the same loads
+          // and the staging store waits only for its own index load.
+          long long gv[GI];
+          idx_load(pb + (int64_t)NB * PERIOD, gv);
+          load(nb, wb[ns], lb[ns], tb[ns], ns);
+          accumulate(pb, wb[s], lb[s], tb[s], [&] { idx_store(s, gv); });
+        } else {
+          if (nb < row1) load(nb, wb[ns], lb[ns], tb[ns], ns);
+          accumulate(pb, wb[s], lb[s], tb[s], [] {});
+        }
         if (*L.flag(smem)) upd_flush_hot<SW>(a, L, smem, slice, chunk, THRESH / 2);  // batch near-hot labels too
       }
     }
@@ -618,25 +704,29 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
   int lab_next = label_at(row0 + NT + threadIdx.x);
   long long xr_next = xrow_at(row0 + NT + threadIdx.x);
   int cnt = compact(label_at(row0 + threadIdx.x), xrow_at(row0 + threadIdx.x), lbuf0, gbuf0);
-  u32x4 xa[GM];
-  int la[GM];
+  u32x4 xa[GM], xb[GM];
+  int la[GM], lb[GM];
+  int cnt_b = 0;
   issue(lbuf0, gbuf0, cnt, row0 + wid * 64, 0, xa, la);
-  for (int64_t base = row0; base < row1; base += NT) {
+  // One period: compact and issue the NEXT period's row groups into (xn, ln), then
+  // accumulate this period's (xc, lc).  Called twice per loop trip with the two register
+  // sets swapped (ping-pong, no copies): a rolled loop copied xb into xa at the latch, which
+  // waited for every next-period load before the next labels were even read.
+  auto period = [&](int64_t base, u32x4* xc, int* lc, int cc_, const unsigned* lcur, const long long* gcur,
+                    u32x4* xn, int* ln, int& cn_, unsigned* lnxt, long long* gnxt) {
     const int lab_nn = label_at(base + 2 * NT + threadIdx.x);
     const long long xr_nn = xrow_at(base + 2 * NT + threadIdx.x);
-    const int cnt_n = compact(lab_next, xr_next, lbuf1, gbuf1);
-    u32x4 xb[GM];
-    int lb[GM];
-    issue(lbuf1, gbuf1, cnt_n, base + NT + wid * 64, 0, xb, lb);
+    cn_ = compact(lab_next, xr_next, lnxt, gnxt);
+    issue(lnxt, gnxt, cn_, base + NT + wid * 64, 0, xn, ln);
 #pragma unroll
     for (int j = 0; j < GM; ++j)
-      if (la[j] >= 0) accumulate(xa[j], la[j]);
+      if (lc[j] >= 0) accumulate(xc[j], lc[j]);
     // rare: more owned rows than GM groups hold -- the rest synchronously
-    for (int g0 = GM * RG; g0 < cnt; g0 += RG) {
+    for (int g0 = GM * RG; g0 < cc_; g0 += RG) {
       const int e = g0 + rr;
-      if (e < cnt) {
-        const unsigned ent = lbuf0[e];
-        const int64_t row = GATHER ? (int64_t)gbuf0[e] : base + wid * 64 + (int64_t)(ent & 63u);
+      if (e < cc_) {
+        const unsigned ent = lcur[e];
+        const int64_t row = GATHER ? (int64_t)gcur[e] : base + wid * 64 + (int64_t)(ent & 63u);
         const u32x4 w = *(const u32x4*)(xcol + row * a.ldx);
         accumulate(w, (int)(ent >> 6));
       }
@@ -649,13 +739,13 @@ __global__ __launch_bounds__(plan::KS_NT) void update_ks_kernel(UpdateArgs a, in
       seen = 0;
       __syncthreads();
     }
-#pragma unroll
-    for (int j = 0; j < GM; ++j) { xa[j] = xb[j]; la[j] = lb[j]; }
-    cnt = cnt_n;
     lab_next = lab_nn;
     xr_next = xr_nn;
-    unsigned* t = lbuf0; lbuf0 = lbuf1; lbuf1 = t;
-    long long* tg = gbuf0; gbuf0 = gbuf1; gbuf1 = tg;
+  };
+  for (int64_t base = row0; base < row1; base += 2 * NT) {
+    period(base, xa, la, cnt, lbuf0, gbuf0, xb, lb, cnt_b, lbuf1, gbuf1);
+    if (base + NT >= row1) break;   // (uniform)
+    period(base + NT, xb, lb, cnt_b, lbuf1, gbuf1, xa, la, cnt, lbuf0, gbuf0);
   }
   __syncthreads();
   ks_flush<T, LPR>(a, smem, kq, kn, ldc, NPAIR, k0, chunk, 0u);
@@ -740,9 +830,10 @@ static hipError_t launch_nt(const UpdateArgs& a, int ldc, hipStream_t s) {
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)UPD_LDS_MAX);
     attr = true;
   }
-  hipLaunchKernelGGL((update_kernel<T, SW, MODE, NT, NBF, PER>), dim3(a.n_chunks * n_slices), dim3(NT),
-                     upd_lds_bytes(a.K, ldc, (MODE & (UPD_WEIGHTED | UPD_DELTA)) != 0), s, a, n_slices,
-                     rows_per_chunk);
+  size_t lds = upd_lds_bytes(a.K, ldc, (MODE & (UPD_WEIGHTED | UPD_DELTA)) != 0);
+  if constexpr ((MODE & UPD_GSTAGE) != 0) lds += (size_t)NBF * upd_period<T, SW, NT, PER>() * 8;
+  hipLaunchKernelGGL((update_kernel<T, SW, MODE, NT, NBF, PER>), dim3(a.n_chunks * n_slices), dim3(NT), lds, s, a,
+                     n_slices, rows_per_chunk);
   return hipGetLastError();
 }
 
@@ -775,6 +866,12 @@ static hipError_t launch_sw(const UpdateArgs& a, int ldc, hipStream_t s) {
   constexpr int V = ((SW * ES >= 16) ? 16 : SW * ES) / ES;
   constexpr int RPP = NT / (SW / V);
   constexpr int PER = RPP > 512 ? RPP : 512;
+  if constexpr ((MODE & UPD_GSTAGE) != 0) {   // the staged-index ring must fit beside the cells
+    constexpr int NBF = NT == 1024 ? upd_ring_1024<T, SW, MODE>() : UPD_NBUF;
+    constexpr int P = NT == 1024 ? upd_period<T, SW, NT, PER>() : upd_period<T, SW, NT, UPD_MAX_PERIOD>();
+    if (upd_lds_bytes(a.K, ldc, false) + (size_t)NBF * P * 8 > UPD_LDS_MAX)
+      return launch_sw<T, SW, (MODE & ~UPD_GSTAGE)>(a, ldc, s);
+  }
   if constexpr (NT == 1024) return launch_nt<T, SW, MODE, 1024, upd_ring_1024<T, SW, MODE>(), PER>(a, ldc, s);
   else return launch_nt<T, SW, MODE, NT>(a, ldc, s);
 }
@@ -795,9 +892,9 @@ static hipError_t launch_clamp(const UpdateArgs& a, int ldc, hipStream_t s) {
   if (a.rows) {  // gathered mini-batch rows: plain (bounded, unclamped) passes only
     if (a.clamp || a.dlist) return hipErrorInvalidValue;
     switch (mode) {
-      case 0: return launch_sw<T, SW, UPD_GATHER>(a, ldc, s);
+      case 0: return launch_sw<T, SW, UPD_GATHER | UPD_GSTAGE>(a, ldc, s);
       case 2: return launch_sw<T, SW, UPD_GATHER | UPD_WEIGHTED>(a, ldc, s);
-      case 4: return launch_sw<T, SW, UPD_GATHER | UPD_SWZ>(a, ldc, s);
+      case 4: return launch_sw<T, SW, UPD_GATHER | UPD_SWZ | UPD_GSTAGE>(a, ldc, s);
       default: return launch_sw<T, SW, UPD_GATHER | UPD_WEIGHTED | UPD_SWZ>(a, ldc, s);
     }
   }

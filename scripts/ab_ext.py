@@ -114,20 +114,35 @@ def cmd_run(a) -> int:
         t["m"].assign(eng.X, t["pack"], t["cn"], eng.xn, t["lab"], t["mind"], t["slots"], t["kpad"], dpad, True,
                       None)
 
+    def run_update(t):   # the full M-step pass on the engine's labels into each module's own slab
+        m = t["m"]
+        if "slab" not in t:
+            t["nch"] = m.update_n_chunks(code, a.k, eng.Dp, a.n, False)
+            t["slab"] = torch.empty(t["nch"] * a.k * eng.Dp, dtype=torch.int64, device=dev)
+            t["cnt"] = torch.empty(t["nch"] * a.k, dtype=torch.int64, device=dev)
+        m.update(eng.X, eng.labels, a.k, t["slab"], t["cnt"], t["nch"], None, eng.col_exp, eng.cnt_exp, False)
+
+    fn = run_update if a.what == "update" else run_assign
     for t in per.values():          # warm-up (kernel attributes, code objects)
-        run_assign(t)
+        fn(t)
     torch.cuda.synchronize()
     for _ in range(a.rounds):
         for t in per.values():
-            t["ts"] += _timed(lambda t=t: run_assign(t), a.reps)
+            t["ts"] += _timed(lambda t=t: fn(t), a.reps)
     base = per["head"]
-    out = {"n": a.n, "d": a.d, "k": a.k, "dtype": a.dtype, "what": "assign", "variants": {}}
+    if a.what == "update":          # the same integer sums from every module
+        red = {tag: (t["slab"].view(t["nch"], -1).sum(0), t["cnt"].view(t["nch"], -1).sum(0)) for tag, t in per.items()}
+        for tag, t in per.items():
+            t["same"] = bool(torch.equal(red[tag][0], red["head"][0]) and torch.equal(red[tag][1], red["head"][1]))
+    out = {"n": a.n, "d": a.d, "k": a.k, "dtype": a.dtype, "what": a.what, "variants": {}}
     for tag, t in per.items():
         med = statistics.median(t["ts"])
         out["variants"][tag] = {
             "median_ms": round(med, 4), "min_ms": round(min(t["ts"]), 4),
             "tflops": round(2.0 * a.n * a.k * a.d / (med * 1e-3) / 1e12, 1),
-            "label_mismatch_vs_head": int((t["lab"] != base["lab"]).sum()),
+            "x_TBps": round(a.n * a.d * (2 if a.dtype == "bf16" else 4) / (med * 1e-3) / 1e12, 2),
+            "label_mismatch_vs_head": int((t["lab"] != base["lab"]).sum()) if a.what == "assign" else None,
+            "sums_equal_head": t.get("same"),
             "vs_head": round(statistics.median(base["ts"]) / med, 4),
         }
     print(json.dumps(out), flush=True)
@@ -147,6 +162,7 @@ def main(argv=None) -> int:
     r.add_argument("--dtype", default="bf16")
     r.add_argument("--rounds", type=int, default=5)
     r.add_argument("--reps", type=int, default=5)
+    r.add_argument("--what", default="assign", choices=["assign", "update"])
     a = ap.parse_args(argv)
     if a.cmd == "build":
         cmd_build(a.ref)

@@ -696,6 +696,39 @@ def test_assign_bf16_key_resolution_distance_relative(native):
     assert int(bad.sum()) == 0, f"{int(bad.sum())} wrong labels of {int(ok.sum())} resolvable rows"
 
 
+@pytest.mark.parametrize("pmaj", ["0", "1"])
+@pytest.mark.parametrize("varg", ["0", "1"])
+def test_assign_per_point_offset_seeds_repeatable(native, monkeypatch, pmaj, varg):
+    """Per-point-offset workgroups (N(0,1) rows at D=32: most workgroups) under both MFMA
+    issue orders and both epilogues, launched repeatedly with other kernels in between (they
+    leave their own data in LDS and registers): every launch gives the same labels, and no
+    row with a clear f64 gap (> 1e-3) takes another label.  Packed v_pk_add_f32 seeds got one
+    point block wrong in 5 of 12 launches here (profiles/r3_15_ppo_seed_race.md)."""
+    n, d, k = 300_000, 32, 1024
+    g = torch.Generator().manual_seed(11 + n + d)
+    X = torch.randn(n, d, generator=g)
+    C = torch.randn(k, d, generator=g) * 0.8
+    Xb = X.to(torch.bfloat16)
+    xx, Cq, dist = _bf16_dist(Xb, C)
+    exp = _first_argmin(dist)
+    srt = dist.sort(1).values
+    clear = (srt[:, 1] - srt[:, 0]) > 1e-3
+    monkeypatch.setenv("MIKMEANS_ASSIGN_PMAJ", pmaj)
+    monkeypatch.setenv("MIKMEANS_ASSIGN_VARG", varg)
+    Xd, Cd = Xb.to(DEV), C.to(DEV)
+    first = None
+    for r in range(6):
+        if r % 2:   # another kernel's LDS / register history before the next launch
+            Y = torch.randn(200_000, 256, device=DEV, dtype=torch.bfloat16) * 100
+            ops.assign(Y, torch.randn(512, 256, device=DEV) * 50, with_dist=True)
+        lab = ops.assign(Xd, Cd, with_dist=False)[0].cpu().long()
+        bad = (lab != exp) & clear
+        assert int(bad.sum()) == 0, f"launch {r}: {int(bad.sum())} rows off the f64 argmin"
+        if first is None:
+            first = lab
+        assert torch.equal(lab, first), f"launch {r} differs from launch 0"
+
+
 @pytest.mark.parametrize("n,outlier,d,k", [(20_000, False, 64, 4096), (300_000, False, 64, 4096),
                                            (300_000, True, 64, 4096), (40_000, True, 64, 4096),
                                            (300_000, False, 32, 1024), (30_000, True, 32, 1024)])
