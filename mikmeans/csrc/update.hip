@@ -250,6 +250,11 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   // so no X load's address waits on an index load issued after older X loads (vmcnt retires
   // in order: the unstaged path drained the whole prefetch ring every period)
   constexpr bool GSTAGE = GATHER && (MODE & UPD_GSTAGE) && !DELTA;
+  // FLAT (the staged builds): one straight-line load form for every period and unconditional
+  // ring loads (labels clamped in accumulate), so the wait counter stays exact across the
+  // period loop.  For plain passes the same form measured 3.5 % faster at D=256 bf16 but 29 %
+  // slower for the f32 64-column kernel (profiles/r3_20_abu_*_flat*.log), so they keep theirs.
+  constexpr bool FLAT = GSTAGE;
   constexpr int ES = sizeof(T);
   constexpr int PB = (SW * ES >= 16) ? 16 : SW * ES;  // bytes per lane load
   constexpr int V = PB / ES;                           // elements per lane load (even)
@@ -306,6 +311,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   const int lr = threadIdx.x / LPR, lp = threadIdx.x % LPR;
   const int col = slice * SW + lp * V;
   const bool colok = col < a.D;
+  const bool all_cols = (a.D % SW) == 0;               // kernel-uniform
   const int colc = colok ? col : 0;
   const bool counter = lp == 0;
   const bool wcounter = W && counter && slice == 0;
@@ -331,15 +337,18 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
   auto load = [&](int64_t base, LT* w_, int* lab_, float* wt_, int slot) {
     const long long* gs = gidx + slot * PERIOD + lr * UNR;
     const int64_t off = base - row0;
-    if constexpr (GSTAGE) {
+    if constexpr (FLAT) {
       // one straight-line form for every period (rows past the chunk clamp to its last row;
       // accumulate sends them to the sink): a branch between differently shaped load
       // sequences made the wait counter at the join fall back to vmcnt(0), draining the ring
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const int64_t i0 = base + (int64_t)lr * UNR + u;
-        lab_[u] = a.labels[i0 < row1 ? i0 : row1 - 1];
-        w_[u] = *(const LT*)((const T*)a.X + gs[u] * a.ldx + colc);
+        const int64_t i = i0 < row1 ? i0 : row1 - 1;
+        lab_[u] = a.labels[i];
+        if constexpr (W) wt_[u] = a.weights[i];
+        if constexpr (GSTAGE) w_[u] = *(const LT*)((const T*)a.X + gs[u] * a.ldx + colc);
+        else w_[u] = *(const LT*)((const T*)a.X + i * a.ldx + colc);
       }
     } else if (DELTA && !full) {                       // gather the listed rows
 #pragma unroll
@@ -382,9 +391,16 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
         else w_[u] = *(const LT*)((const T*)a.X + (GATHER ? a.rows[i] : i) * a.ldx + colc);
       }
     }
-    // (lanes past the last column read column 0 of the row and add fma(x, 0, MAGIC) = +0:
-    // their scales are 0.  Zeroing the loaded registers here instead waited for every load
-    // of the period right after issuing it, in every build of the kernel.)
+    // (staged builds: lanes past the last column read column 0 of the row and add
+    // fma(x, 0, MAGIC) = +0 -- their scales are 0; zeroing the loaded registers here waited
+    // for every load of the period right after issuing it.  The other builds keep the zeroing:
+    // without it the f32 64-column kernel measured 2 % slower.)
+    if constexpr (!FLAT) {
+      if (!all_cols && !colok) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) w_[u] = LT{};
+      }
+    }
   };
 
   // Accumulate one period; sets the flush flag when a label's add count nears FX_LIM.
@@ -396,7 +412,7 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
     int lab_[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      if constexpr (GSTAGE) {
+      if constexpr (FLAT) {
         const bool in = base + (int64_t)lr * UNR + u < row1;
         lab_[u] = (in && (unsigned)labr_[u] < (unsigned)a.K) ? labr_[u] : a.K;
       } else {
@@ -514,13 +530,13 @@ __global__ __launch_bounds__(NT) void update_kernel(UpdateArgs a, int n_slices,
       if (pb < row1) {
         const int64_t nb = pb + (int64_t)(NB - 1) * PERIOD;
         const int ns = (s + NB - 1) % NB;  // static after unrolling
-        if constexpr (GSTAGE) {
+        if constexpr (FLAT) {
           // period j = s (mod NB): X of period j+NB-1 from slot ns; rows of period j+NB into
           // slot s (period j's, read NB-1 steps ago).  The X loads go out unconditionally
           // (past the chunk they clamp to its last row) so every step issues the same loads
           // and the staging store waits only for its own index load.
           long long gv[GI];
-          idx_load(pb + (int64_t)NB * PERIOD, gv);
+          idx_load(pb + (int64_t)NB * PERIOD, gv);   // (no-op unless GSTAGE)
           load(nb, wb[ns], lb[ns], tb[ns], ns);
           accumulate(pb, wb[s], lb[s], tb[s], [&] { idx_store(s, gv); });
         } else {
