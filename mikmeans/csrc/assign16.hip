@@ -76,7 +76,8 @@ struct Assign16Cfg {
   static constexpr int OPT_BYTES = 2 * NW * 16 * PP * 4;   // offsets + gathered |x|^2
   static constexpr int NBUF = NBUF_;
   static_assert(NBUF == 2 || NBUF == 3, "ring depth");
-  static_assert(chunk_tiles16(sizeof(T), DPAD) % CT == 0, "chunk must divide the Kpad granule");
+  static_assert(chunk_tiles16(sizeof(T), DPAD) % CT == 0 || CT % chunk_tiles16(sizeof(T), DPAD) == 0,
+                "chunk and the Kpad granule must nest (a wider chunk runs only where Kpad is a multiple of it)");
   static_assert(NQ >= 1, "DPAD too small for the 16x16 layout");
   static_assert(PIECES % NW == 0, "chunk pieces must split evenly over waves");
 };
@@ -722,12 +723,15 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   constexpr int P = sizeof(T) == 2 ? (DPAD == 64 ? 8 : DPAD == 256 ? 3 : 4) : (NQ >= 8 ? 2 : 4);
   constexpr int OCC = sizeof(T) == 2 ? ((DPAD == 64 || DPAD == 256) ? 3 : 4) : 1;
   static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
-  if constexpr (sizeof(T) == 2 && DPAD == 256) {
-    // A/B switch MIKMEANS_ASSIGN_GEOM: 1 = 3-slot ring, 2 = 4 point blocks at 2 waves/SIMD
+  if constexpr (sizeof(T) == 2 && DPAD == 128) {
+    // A/B switch MIKMEANS_ASSIGN_GEOM: 1 = 8 waves share a ring of 32 KiB chunks (a barrier
+    // every 8 tiles instead of 4), 2 = 8 waves share the 16 KiB ring.  K=1024: -0.4 % / +0.1 %;
+    // K=2048: +4.9 % / +4.4 % (profiles/r3_21_ab_geom128.log), near-tie labels move with
+    // the workgroup's seed offset; the headline's K=1024 keeps 4 waves.
     const char* e = getenv("MIKMEANS_ASSIGN_GEOM");
     const int gm = (e && *e) ? atoi(e) : 0;
-    if (gm == 1) return launch16_t<T, DPAD, P, CT, 3, OCC>(a, s);
-    if (gm == 2) return launch16_t<T, DPAD, 4, CT, 2, 2>(a, s);
+    if (gm == 1 && a.Kpad % (16 * 8) == 0) return launch16_t<T, DPAD, P, 8, 2, OCC, 8>(a, s);
+    if (gm == 2) return launch16_t<T, DPAD, P, CT, 2, OCC, 8>(a, s);
   }
   return launch16_t<T, DPAD, P, CT, 2, OCC>(a, s);
 }
