@@ -723,6 +723,14 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   constexpr int P = sizeof(T) == 2 ? (DPAD == 64 ? 8 : DPAD == 256 ? 3 : 4) : (NQ >= 8 ? 2 : 4);
   constexpr int OCC = sizeof(T) == 2 ? ((DPAD == 64 || DPAD == 256) ? 3 : 4) : 1;
   static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
+  if constexpr (sizeof(T) == 2 && DPAD == 256) {
+    // A/B switch MIKMEANS_ASSIGN_GEOM: 8 waves per ring (half the per-point centre stream and
+    // per-workgroup start-up): 1 = 3 point blocks at 2 waves/SIMD, 2 = 2 blocks at 4
+    const char* e = getenv("MIKMEANS_ASSIGN_GEOM");
+    const int gm = (e && *e) ? atoi(e) : 0;
+    if (gm == 1) return launch16_t<T, DPAD, 3, CT, 2, 2, 8>(a, s);
+    if (gm == 2) return launch16_t<T, DPAD, 2, CT, 2, 4, 8>(a, s);
+  }
   if constexpr (sizeof(T) == 2 && DPAD == 128) {
     // A/B switch MIKMEANS_ASSIGN_GEOM: 1 = 8 waves share a ring of 32 KiB chunks (a barrier
     // every 8 tiles instead of 4), 2 = 8 waves share the 16 KiB ring.  K=1024: -0.4 % / +0.1 %;

@@ -113,11 +113,13 @@ def test_minibatch_fit_steps_do_not_sync(native):
 
 @pytest.mark.parametrize("D,K,dtype,force_ks", [(256, 512, torch.bfloat16, None), (128, 1024, torch.bfloat16, None),
                                                 (64, 4096, torch.bfloat16, None), (128, 256, torch.float32, None),
-                                                (40, 20000, torch.float32, None), (256, 512, torch.bfloat16, "1")])
+                                                (40, 20000, torch.float32, None), (256, 512, torch.bfloat16, "1"),
+                                                (256, 600, torch.bfloat16, None)])
 def test_gathered_rows_step_equals_materialised_batch(native, monkeypatch, D, K, dtype, force_ks):
     """partial_fit_rows (assign + M-step reading X[rows] through the index list: slice,
     K-split and global-atomic M-step kernels; force_ks: the K-split kernel where the slice
-    kernel is the default) equals partial_fit on the gathered copy."""
+    kernel is the default; K=600 at D=256: the slice kernel without its LDS index staging,
+    which no longer fits beside the cells) equals partial_fit on the gathered copy."""
     from mikmeans.models.minibatch import MiniBatchEngine
     from mikmeans.ops import col_stats, pad_columns
 
