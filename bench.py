@@ -242,26 +242,33 @@ def _timed_steps(eng, comm, warmup: int, steps: int, sync) -> float:
     return float(el.item())
 
 
-def _phase_breakdown(eng) -> dict:
-    """Per-phase device time of one Lloyd iteration (rank-local; after the timed region)."""
+def _phase_breakdown(eng, reps: int = 3) -> dict:
+    """Per-phase device time of a Lloyd iteration (rank-local; after the timed region): the
+    median of ``reps`` event-instrumented eager iterations, each phase bracketed alone."""
+    import statistics
+
     C = eng._C
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-    ev[0].record()
-    eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True)
-    ev[1].record()
-    C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks, eng.weights, eng.col_exp,
-             eng.cnt_exp, False)
-    ev[2].record()
-    C.reduce(eng.slab, eng.cnt_slab, eng.n_chunks, eng.K, eng.Dp, eng.slots, eng.packed, eng.col_exp,
-             eng.cnt_exp)
-    ev[3].record()
-    eng.comm.allreduce_(eng.packed)
-    ev[4].record()
-    eng.pk.finalize(1, eng.packed, eng.C, eng.Cnew, eng.frozen, None, eng.shift, eng.counts)
-    ev[5].record()
-    torch.cuda.synchronize()
     names = ["assign", "update", "reduce", "allreduce", "finalize"]
-    return {n: round(ev[i].elapsed_time(ev[i + 1]), 4) for i, n in enumerate(names)}
+    runs = {n: [] for n in names}
+    for _ in range(reps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        ev[0].record()
+        eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True)
+        ev[1].record()
+        C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks, eng.weights, eng.col_exp,
+                 eng.cnt_exp, False)
+        ev[2].record()
+        C.reduce(eng.slab, eng.cnt_slab, eng.n_chunks, eng.K, eng.Dp, eng.slots, eng.packed, eng.col_exp,
+                 eng.cnt_exp)
+        ev[3].record()
+        eng.comm.allreduce_(eng.packed)
+        ev[4].record()
+        eng.pk.finalize(1, eng.packed, eng.C, eng.Cnew, eng.frozen, None, eng.shift, eng.counts)
+        ev[5].record()
+        torch.cuda.synchronize()
+        for i, n in enumerate(names):
+            runs[n].append(ev[i].elapsed_time(ev[i + 1]))
+    return {n: round(statistics.median(v), 4) for n, v in runs.items()}
 
 
 def _bench_minibatch(args, cfg, comm, dtype):
