@@ -137,7 +137,7 @@ __device__ __forceinline__ float sq16(const u32x4& w, float*) {
 // once per point after the loop by recomputing the winning tile's candidates on the
 // matrix cores (bitwise the main loop's scores), right after the chunk loop.
 template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false,
-          bool VARG = false, bool PMAJ = false>
+          bool VARG = false, int PMAJ = 0>
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
@@ -353,21 +353,53 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
           __builtin_amdgcn_s_setprio(1);
           __builtin_amdgcn_sched_barrier(0);
         }
-        if constexpr (PMAJ) {
-          // point-block-major issue: each accumulator's NQ MFMAs back to back (srcC = the
-          // previous vDst), pinned in this order
-  #pragma unroll
-          for (int p = 0; p < C::P; ++p) {
-  #pragma unroll
-            for (int q = 0; q < C::NQ; ++q) {
-              acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
-              __builtin_amdgcn_sched_barrier(0);
-            }
+        // per-block argmin epilogue (bf16): packed 6-bit keys or the value-only running minimum
+        unsigned t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+        if constexpr (!EXACT && !VARG) {
+          // 6-bit keys over a segment of 16 tiles (tile-in-segment * 4 + reg): 4 key packs
+          // + 2 v_min3 per tile and point block; the running best is merged with its
+          // segment id once per segment.  The four indices as opaque SGPRs, so each key is
+          // one v_and_or_b32.
+          const unsigned tis = (unsigned)(tile & 15) << 2;
+          asm volatile("s_mov_b32 %0, %4\n\ts_or_b32 %1, %4, 1\n\ts_or_b32 %2, %4, 2\n\ts_or_b32 %3, %4, 3"
+                       : "=s"(t0), "=s"(t1), "=s"(t2), "=s"(t3) : "s"(tis) : "scc");  // s_or_b32 writes SCC
+        }
+        auto epi = [&](int p) {
+          if constexpr (VARG) {
+            // scores are positive (seed offset, see the header), so they order as their bits;
+            // a tie with the running minimum keeps the earlier tile (the lower index)
+            const uint32_t u0 = __float_as_uint(acc[p][0]), u1 = __float_as_uint(acc[p][1]);
+            const uint32_t u2 = __float_as_uint(acc[p][2]), u3 = __float_as_uint(acc[p][3]);
+            const uint32_t nb = min(min(u0, u1), min(u2, min(u3, vb[p])));
+            tb[p] = nb != vb[p] ? (uint32_t)tile : tb[p];
+            vb[p] = nb;
+          } else {
+            const f32x4& sv = acc[p];
+            const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
+            const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
+            seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
           }
-        } else {
+        };
+        auto chain = [&](int p) {   // block p's NQ MFMAs back to back (srcC = the previous vDst)
   #pragma unroll
           for (int q = 0; q < C::NQ; ++q) {
-  #pragma unroll
+            acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        };
+        if constexpr (!EXACT) {
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_setprio(1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (PMAJ) {
+          // point-block-major issue, pinned in this order
+#pragma unroll
+          for (int p = 0; p < C::P; ++p) chain(p);
+        } else {
+#pragma unroll
+          for (int q = 0; q < C::NQ; ++q) {
+#pragma unroll
             for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
           }
         }
@@ -383,42 +415,20 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         if constexpr (EXACT) {
           // (tile*4 + reg) as wave-uniform values: the index select needs no VALU add
           const int u = tile * 4;
-  #pragma unroll
+#pragma unroll
           for (int p = 0; p < C::P; ++p) {
-  #pragma unroll
+#pragma unroll
             for (int e = 0; e < 4; ++e) {
               const bool lt = acc[p][e] < best[p];
               best[p] = lt ? acc[p][e] : best[p];
               bg[p] = lt ? u + e : bg[p];
             }
           }
-        } else if constexpr (VARG) {
-          // scores are positive (seed offset, see the header), so they order as their bits;
-          // a tie with the running minimum keeps the earlier tile (the lower index)
-  #pragma unroll
-          for (int p = 0; p < C::P; ++p) {
-            const uint32_t u0 = __float_as_uint(acc[p][0]), u1 = __float_as_uint(acc[p][1]);
-            const uint32_t u2 = __float_as_uint(acc[p][2]), u3 = __float_as_uint(acc[p][3]);
-            const uint32_t nb = min(min(u0, u1), min(u2, min(u3, vb[p])));
-            tb[p] = nb != vb[p] ? (uint32_t)tile : tb[p];
-            vb[p] = nb;
-          }
         } else {
-          // 6-bit keys over a segment of 16 tiles (tile-in-segment * 4 + reg): 4 key packs
-          // + 2 v_min3 per tile and point block; the running best is merged with its
-          // segment id once per segment.  The four indices as opaque SGPRs, so each key is
-          // one v_and_or_b32.
-          const unsigned tis = (unsigned)(tile & 15) << 2;
-          unsigned t0, t1, t2, t3;
-          asm volatile("s_mov_b32 %0, %4\n\ts_or_b32 %1, %4, 1\n\ts_or_b32 %2, %4, 2\n\ts_or_b32 %3, %4, 3"
-                       : "=s"(t0), "=s"(t1), "=s"(t2), "=s"(t3) : "s"(tis) : "scc");  // s_or_b32 writes SCC
-  #pragma unroll
-          for (int p = 0; p < C::P; ++p) {
-            const f32x4& sv = acc[p];
-            const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
-            const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
-            seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
-          }
+#pragma unroll
+          for (int p = 0; p < C::P; ++p) epi(p);
+        }
+        if constexpr (!EXACT && !VARG) {
           if ((tile & 15) == 15 || tile == ngrp - 1) {
   #pragma unroll
             for (int p = 0; p < C::P; ++p) {
@@ -629,7 +639,7 @@ static int varg_env() {   // read per launch (tests switch it inside one process
   return (e && *e) ? atoi(e) : -1;
 }
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, bool PMAJ>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ>
 static void set_lds_attr() {
   static bool done = false;
   if (done) return;
@@ -650,13 +660,15 @@ static void set_lds_attr() {
 // (scripts/microbench/mfma_shape.hip mode 1, profiles/r3_17_mfma_issue_order.log: with the
 // key epilogue 84.4 -> 91.6 % at 1780 -> 1762 MHz, +7.5 % TF/s; 32x32x16 gains 3.6 % the
 // same way and stays 12 % behind).
-// MIKMEANS_ASSIGN_PMAJ=0/1 forces it off / on.
+// MIKMEANS_ASSIGN_PMAJ=0/1 forces it off / on.  Issuing each block's epilogue between the next
+// blocks' MFMA chains instead measured -1.1 % at D=128, -3.8 % at D=64 K=4096, +2.2 % at D=64
+// K=1024 (profiles/r3_23_ab_pmaj_interleaved.log) and is not built.
 static int pmaj_env() {   // read per launch (A/B harnesses switch it inside one process)
   const char* e = getenv("MIKMEANS_ASSIGN_PMAJ");
   return (e && *e) ? atoi(e) : -1;
 }
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, bool PMAJ>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ>
 static void launch16_kp(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
   set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ>();
   if (b.D == DPAD)
@@ -667,11 +679,10 @@ static void launch16_kp(const AssignArgs& b, const dim3& grid, size_t lds, hipSt
 
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG>
 static void launch16_k(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  {
-    const int e = pmaj_env();
-    if (e >= 0 ? e != 0 : sizeof(T) == 2) return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, true>(b, grid, lds, s);
-  }
-  launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, false>(b, grid, lds, s);
+  const int e = pmaj_env();
+  const int pm = e >= 0 ? e : (sizeof(T) == 2 ? 1 : 0);
+  if (pm != 0) return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 1>(b, grid, lds, s);
+  launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 0>(b, grid, lds, s);
 }
 
 template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4>
@@ -740,6 +751,7 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
     const int gm = (e && *e) ? atoi(e) : 0;
     if (gm == 1 && a.Kpad % (16 * 8) == 0) return launch16_t<T, DPAD, P, 8, 2, OCC, 8>(a, s);
     if (gm == 2) return launch16_t<T, DPAD, P, CT, 2, OCC, 8>(a, s);
+    if (gm == 3) return launch16_t<T, DPAD, 6, CT, 2, 3>(a, s);   // 6 point blocks at 3 waves/SIMD
   }
   return launch16_t<T, DPAD, P, CT, 2, OCC>(a, s);
 }
