@@ -14,6 +14,7 @@ run ab_head_d64 200 python -u scripts/ab_ext.py run $AB --n 10000000 --d 64 --k 
 MIKMEANS_ASSIGN_PMAJ=0 run ab_head_d128_nopmaj 200 python -u scripts/ab_ext.py run $AB --n 20000000 --d 128 --k 1024 || exit 1
 MIKMEANS_ASSIGN_PMAJ=0 run ab_head_d256_nopmaj 200 python -u scripts/ab_ext.py run $AB --n 16777216 --d 256 --k 512 || exit 1
 run bench 300 python -u bench.py || exit 1
+run bench4 300 python -u bench.py --config cfg4 || exit 1
 run bench5r 300 python -u bench.py --config cfg5 --resident || exit 1
 MIKMEANS_UPDATE_KS=1 run bench5r_ks 300 python -u bench.py --config cfg5 --resident || exit 1
 exit 0
