@@ -387,11 +387,6 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
             __builtin_amdgcn_sched_barrier(0);
           }
         };
-        if constexpr (!EXACT) {
-          __builtin_amdgcn_sched_barrier(0);
-          __builtin_amdgcn_s_setprio(1);
-          __builtin_amdgcn_sched_barrier(0);
-        }
         if constexpr (PMAJ) {
           // point-block-major issue, pinned in this order
 #pragma unroll
