@@ -297,6 +297,9 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       if (C::NBUF == 3 && c + 1 < ncl) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
       wait_lgkm0();
       raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
+      // (the next chunk's pieces all go out right after the barrier: spreading them one group
+      // per tile after that tile's epilogue measured -2.5 % at D=128, -5 % at D=256 and far
+      // slower at D=64, profiles/r3_28_ab_spread_dma.log)
       if (c + C::NBUF - 1 < ncl) issue_chunk(c + C::NBUF - 1);
       const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
       // A fragments + |c|^2 of a tile from the LDS ring
