@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 session S (final check of this session's tree): smoke, the whole GPU suite, the
+# Round-3 session S (check of this session's tree): smoke, the whole GPU suite, the
 # driver's bench command, the three configs, and rocprofv3 kernel stats of the headline.
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
