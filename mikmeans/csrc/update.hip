@@ -997,6 +997,12 @@ hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s) {
   if (!a.dlist && !a.col_exp2 && use_ks(dtype, a.K, a.D, a.weights != nullptr, &kp) &&
       (!a.rows || plan::ks_lds_bytes(kp.kq, kp.ldc) + plan::KS_GLIST_BYTES <= UPD_LDS_MAX)) {
     if (a.n_chunks % 8) return hipErrorInvalidValue;
+    {   // A/B override of the row groups in flight (2, 3 or 6).  With the ping-pong periods the
+        // plan's choice still wins: cfg4 2 > 3 > 6, headline 6 > 3 > 2 (profiles/r3_30_ks_gm_ab.log)
+      const char* g = getenv("MIKMEANS_UPDATE_KS_GM");
+      const int gm = (g && *g) ? atoi(g) : 0;
+      if (gm == 2 || gm == 3 || gm == 6) kp.gm = gm;
+    }
     return dtype == DT_BF16 ? launch_ks<uint16_t>(a, kp, s) : launch_ks<float>(a, kp, s);
   }
   int ldc = 0;
