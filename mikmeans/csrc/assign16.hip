@@ -745,6 +745,8 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
     // every 8 tiles instead of 4), 2 = 8 waves share the 16 KiB ring.  K=1024: -0.4 % / +0.1 %;
     // K=2048: +4.9 % / +4.4 % (profiles/r3_21_ab_geom128.log), near-tie labels move with
     // the workgroup's seed offset; the headline's K=1024 keeps 4 waves.
+    // A K sweep keeps 4 waves as the default: 8-wave rings measured +5.0 % at K=2048 but
+    // -5.3 % at 3072 and -5.5 % at 4096 (profiles/r3_33_ab_geom128_ksweep.log).
     const char* e = getenv("MIKMEANS_ASSIGN_GEOM");
     const int gm = (e && *e) ? atoi(e) : 0;
     if (gm == 1 && a.Kpad % (16 * 8) == 0) return launch16_t<T, DPAD, P, 8, 2, OCC, 8>(a, s);

@@ -58,7 +58,8 @@ def _first_argmin(sc):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("n,d,k", [(5000, 64, 1300), (3000, 128, 1024), (2000, 32, 300)])
+@pytest.mark.parametrize("n,d,k", [(5000, 64, 1300), (3000, 128, 1024), (2000, 32, 300), (4000, 128, 2048),
+                                   (60_000, 128, 4096)])
 def test_assign_exact_ties_lowest_index(native, dtype, n, d, k):
     """Integer data: every score is exact in f32, so labels must equal the f64 argmin with
     the LOWEST index on exact ties -- every row, ties included (duplicated centres, negative
