@@ -73,7 +73,13 @@ def main(argv=None):
                          "all-reduce, one launch; eager fallback if capture fails).  auto: on for one rank "
                          "(cfg2's 0.7 ms steps gain ~1 %%); off for N > 1, where the host already runs "
                          "far ahead of ~3 ms steps")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="host: host-staged gloo collectives, rank r on GPU r %% device_count -- a "
+                         "rehearsal of the N-rank job on fewer GPUs (N ranks may share one GPU; the "
+                         "value then measures ranks, not GPUs).  rccl (default): RCCL, one rank per GPU")
     args = ap.parse_args(argv)
+    if args.comm == "host":
+        os.environ["MIKMEANS_COMM"] = "host"      # children of the self-launch inherit it
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # Self-launch: this parent has not touched the GPU (no HIP call yet); it starts
@@ -198,7 +204,10 @@ def main(argv=None):
                 "parallelism": f"dp{world}",
                 **({"mstep": "incremental"} if args.incremental else {}),
             },
-            "comm": {"backend": comm.backend, "world_size": comm.world, "process_group": comm.grouped},
+            "comm": {"backend": comm.backend, "world_size": comm.world, "process_group": comm.grouped,
+                     **({"host_staged": True,
+                         "physical_gpus": min(world, torch.cuda.device_count()) if dev.type == "cuda" else 0}
+                        if comm.staged else {})},
             **extra,
         }
         print(json.dumps(out), flush=True)
@@ -206,22 +215,19 @@ def main(argv=None):
     return 0
 
 
-def _capture(eng, want: bool) -> bool:
-    """hipGraph-capture one Lloyd iteration (bitwise the eager step: tests/test_gpu_rccl.py);
-    every rank decides together, so either all replay graphs or none does."""
-    ok = torch.tensor([1.0 if (want and eng.gpu) else 0.0], dtype=torch.float64, device=eng.device)
-    if ok.item():
-        try:
-            eng.capture()
-            ok[0] = 1.0 if getattr(eng, "_graphs", None) is not None else 0.0
-        except Exception as e:  # noqa: BLE001 -- fall back to eager launches
-            print(f"[bench] graph capture failed ({e!r}); eager steps", file=sys.stderr, flush=True)
-            eng._graphs = None
-            ok[0] = 0.0
-    eng.comm.allreduce_(ok)                 # SUM over ranks: all must have captured
-    if ok.item() < eng.comm.world:
-        eng._graphs = None
+def _capture(eng, want: bool):
+    """hipGraph-capture the device work of a Lloyd iteration (bitwise the eager step:
+    tests/test_gpu_rccl.py).  The collective stays eager between the graphs, so a rank
+    may replay while another runs eagerly; a failed capture leaves the engine eager
+    (``capture_error``) and is reported, never fatal."""
+    if not (want and eng.gpu):
         return False
+    eng.capture()
+    if getattr(eng, "_graphs", None) is None:
+        err = getattr(eng, "capture_error", None)
+        if err:
+            print(f"[bench] graph capture failed ({err}); eager steps", file=sys.stderr, flush=True)
+        return {"captured": False, "error": err} if err else False
     return True
 
 

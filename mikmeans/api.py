@@ -673,7 +673,13 @@ class MiniBatchKMeans(_Serving):
             ck = load_checkpoint(resume_from, comm=comm)
             if ck.get("kind") != "minibatch" or int(ck["n_features"]) != D:
                 raise ValueError(f"{resume_from} is not a mini-batch checkpoint for {D} features")
+            shard_bound = eng.bound.clone() if (eng.gpu and eng.bound is not None) else None
             eng.load_state(ck["centers"], ck["tensors"], ck["iteration"], ck.get("rescales", 0))
+            if shard_bound is not None and eng.bound is not None:
+                # the restored scales must still cover this shard (the fit's M-step runs
+                # unclamped): a checkpoint written with a smaller bound (fit_stream's, or an
+                # earlier fit's first-batch bound) is widened to the shard's (all-reduced MAX)
+                eng.set_bound(torch.maximum(eng.bound.to(shard_bound.device), shard_bound))
         else:
             g = _step_generator(self.seed, comm.rank, -1)
             init_n = min(n, self.init_size or max(3 * self.batch_size, 3 * self.n_clusters))

@@ -179,8 +179,11 @@ class LloydEngine:
             # message tail: the wide columns' lo sums [K, nw], added onto the hi sums after the all-reduce
             self.packed = torch.zeros(self.K * self.Dp + self.K + 2 + self.K * self.scales.nw,
                                       dtype=torch.float64, device=dev)
-        if self.weights is not None:
+        if self.weights is not None or self.empty_policy == "farthest":
+            # per-row distances written by every step's assign: the weighted inertia and the
+            # 'farthest' relocation read them (no second assign pass for either)
             self.mind = torch.empty(self.n, dtype=torch.float32, device=dev)
+        if self.weights is not None:
             self._wscratch = torch.empty(C.WDOT_SCRATCH, dtype=torch.float64, device=dev)
         self.delta = None
         if self.incremental:
@@ -256,12 +259,16 @@ class LloydEngine:
         """One Lloyd iteration (E-step on the current centres, M-step, all-reduce, finalize)."""
         graphs = getattr(self, "_graphs", None)
         if graphs is not None:
-            graphs[self._gphase].replay()   # one hipGraph launch for the whole iteration
+            # two graph launches around the (eager) collective: everything up to the packed
+            # message, then everything after it for this centre-buffer parity
+            graphs[0].replay()
+            self._collective()
+            if self.empty_policy == "farthest":
+                self._relocate_empty()
+            graphs[1 + self._gphase].replay()
             self._gphase ^= 1
         elif self.gpu:
             self._step_gpu()
-            if self.spherical:
-                self._project_sphere()
         else:
             self._step_cpu()
             if self.spherical:
@@ -270,42 +277,104 @@ class LloydEngine:
         self.iteration += 1
 
     def capture(self):
-        """Record one Lloyd iteration as a hipGraph (two, one per centre-buffer parity) so
-        each later :meth:`step` is a single graph launch instead of ~6 kernel launches and
-        the RCCL call.  Needs the sync-free path: GPU, empty policy 'keep', no segment
-        overlap.  The graphs replay exactly the kernels :meth:`step` would launch."""
-        if not self.gpu or self.empty_policy != "keep" or self.segments > 1 or not self.n:
+        """Record a Lloyd iteration as hipGraphs so each later :meth:`step` is two graph
+        launches instead of ~6-12 kernel launches.  The graphs hold the device work on
+        either side of the iteration's collective -- the packed message (assign, M-step,
+        reduce) and the finalize (one graph per centre-buffer parity); the all-reduce and the
+        'farthest' empty-cluster relocation (host reads) run eagerly between them.  So no
+        RCCL call is ever recorded, and a host-staged communicator works too.
+
+        A capture that fails (a capture-illegal call in a kernel launcher, an allocator
+        refusal) is torn down before any further device work: the graphs are discarded, the
+        pre-capture state is restored and the engine keeps stepping eagerly
+        (``capture_error`` holds the reason).  The replay is bitwise the eager step
+        (tests/test_gpu_rccl.py)."""
+        self.capture_error = None
+        if not self.gpu or not self.n or getattr(self, "_graphs", None) is not None:
             return self
-        if getattr(self, "_graphs", None) is not None:
-            return self
-        # eager warm-up on a side stream: kernel attributes, RCCL communicator, allocator
-        side = torch.cuda.Stream(device=self.device)
-        side.wait_stream(torch.cuda.current_stream(self.device))
-        C0 = self.C.clone()
+        dev = self.device
+        main = torch.cuda.current_stream(dev)
+        C0, Cn0 = self.C.clone(), self.Cnew.clone()
         lab0 = self.labels.clone()
-        with torch.cuda.stream(side):
-            self._step_gpu()
-        torch.cuda.current_stream(self.device).wait_stream(side)
-        graphs = []
-        for _ in range(2):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=side):
-                self._step_gpu()
-                if self.spherical:
-                    self._project_sphere()
-            graphs.append(g)
-            self.C, self.Cnew = self.Cnew, self.C
-        # the warm-up changed labels / slots: restore the pre-capture state
+        state0 = self._capture_state()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(main)
+        try:
+            # eager warm-up on the side stream: kernel attributes, workspaces, allocator
+            with torch.cuda.stream(side):
+                self._pre_collective()
+                self._post_collective(relocate=False)
+            torch.cuda.synchronize(dev)
+            graphs = []
+            for part in ("pre", "post", "post"):
+                g = torch.cuda.CUDAGraph()
+                # thread_local: other threads (the RCCL watchdog polling earlier collectives)
+                # may keep making calls that are illegal while a stream captures
+                with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+                    if getattr(self, "_inject_capture_fault", False):
+                        self.packed[:1].sum().item()    # tests: a capture-illegal host read
+                    if part == "pre":
+                        self._pre_collective()
+                    else:
+                        self._post_collective(relocate=False)
+                graphs.append(g)
+                if part == "post":   # the second finalize graph: the other centre-buffer parity
+                    self.C, self.Cnew = self.Cnew, self.C
+        except Exception as e:  # noqa: BLE001 -- any capture failure: eager from here on
+            self.capture_error = f"{type(e).__name__}: {e}".splitlines()[0]
+            native.warn_once(f"hipGraph capture failed ({self.capture_error}); eager steps")
+            graphs = None
+            torch.cuda.synchronize(dev)   # (a capture error is not sticky; a device fault would raise here)
+        # the warm-up changed labels / slots / running totals: restore the pre-capture state
+        main.wait_stream(side)
         self.C.copy_(C0)
+        self.Cnew.copy_(Cn0)
         self.labels.copy_(lab0)
+        self._restore_capture_state(state0)
         self.pk.finalize(0, None, self.C)
-        if self.slots is not None:
-            self.slots.zero_()
+        torch.cuda.synchronize(dev)
         self._graphs = graphs
         self._gphase = 0
         return self
 
+    def _capture_state(self) -> dict:
+        """Device state a warm-up / captured step mutates besides C, Cnew and labels."""
+        st = {"slots": self.slots.clone()}
+        if self.delta is not None:
+            st.update({k: v.clone() for k, v in self.delta.items()})
+        return st
+
+    def _restore_capture_state(self, st: dict):
+        self.slots.copy_(st["slots"])
+        if self.delta is not None:
+            for k, v in self.delta.items():
+                v.copy_(st[k])
+
     def _step_gpu(self):
+        self._pre_collective()
+        self._collective()
+        self._post_collective()
+
+    def _collective(self):
+        with _phase("mikmeans.allreduce"):
+            self.comm.allreduce_(self.packed)
+
+    def _post_collective(self, relocate: bool = True):
+        """Device work after the all-reduce: wide-column lo sums, (relocation,) finalize,
+        and the sphere projection of the cosine metric."""
+        if self.scales.nw:
+            from ..ops import add_wide_lo
+
+            add_wide_lo(self.packed, self.K, self.Dp, self.scales)
+        with _phase("mikmeans.finalize"):
+            if relocate:
+                self._relocate_empty()
+            self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts)
+        if self.spherical:
+            self._project_sphere()
+
+    def _pre_collective(self):
+        """Device work up to the packed message: assign, M-step, slab reduce."""
         C = self._C
         KD = self.K * self.Dp
         if self.n and self.segments > 1:
@@ -341,15 +410,6 @@ class LloydEngine:
                      self.col_exp, self.cnt_exp, False, col_exp2=sc.col_exp2)
             C.reduce_cols(self.slab, self.n_chunks, self.K, self.Dp, sc.wide_cols, sc.wide_exps,
                           self.packed[KD + self.K + 2:])
-        with _phase("mikmeans.allreduce"):
-            self.comm.allreduce_(self.packed)
-        if sc.nw:
-            from ..ops import add_wide_lo
-
-            add_wide_lo(self.packed, self.K, self.Dp, sc)
-        with _phase("mikmeans.finalize"):
-            self._relocate_empty()
-            self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts)
 
     def _weighted_inertia(self):
         """packed[inertia] = sum_i w_i mind_i (f64, one pass, no n x 8-byte temporaries)."""
@@ -429,7 +489,9 @@ class LloydEngine:
         empty = torch.nonzero(cnt <= 0).flatten().tolist()
         if not empty:
             return
-        if self.mind is None or (self.gpu and self.weights is None):
+        if self.mind is None:
+            # (GPU engines with this policy allocate mind up front and every step's assign
+            # writes it under the step's centres, graph replays included: nothing to redo)
             self.mind = torch.empty(self.n, dtype=torch.float32, device=self.device)
             if self.gpu:
                 self._assign_into(self.mind)

@@ -180,7 +180,9 @@ class StreamingLloydEngine(LloydEngine):
             yield self.bufs[s][: r1 - r0], r0, r1
             self.free[s].record(main)
 
-    def _step_gpu(self):
+    def _pre_collective(self):
+        """The chunk loop: assign + M-step + reduce of every chunk into one message (the
+        collective, wide-column lo sums, relocation and finalize are the resident engine's)."""
         C = self._C
         KD = self.K * self.Dp
         sc = self.scales
@@ -202,16 +204,10 @@ class StreamingLloydEngine(LloydEngine):
             self.packed += self.part
         if self.weights is not None and self.n:
             self._weighted_inertia()
-        self.comm.allreduce_(self.packed)
-        if sc.nw:
-            from ..ops import add_wide_lo
-
-            add_wide_lo(self.packed, self.K, self.Dp, sc)
-        self._relocate_empty()
-        self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts)
 
     def capture(self):
-        return self  # a host-driven chunk loop: nothing to capture as one graph
+        self.capture_error = "streamed fit: a host-driven chunk loop (not captured)"
+        return self
 
     def _assign_into(self, mind):
         for Xc, r0, r1 in self._chunks():

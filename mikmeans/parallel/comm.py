@@ -10,6 +10,15 @@ reference's WebTorrent trackers (app.mjs:39-45); the run id plays the room code
 (app.mjs:15-19).
 
 The same code runs on CPU with the gloo backend (world_size > 1 in tests).
+
+Host-staged mode (``staged=True``, or ``MIKMEANS_COMM=host`` in the environment): the
+ranks compute on GPUs but the group is gloo, and every collective on a device tensor
+goes device -> host -> gloo -> host -> device.  RCCL refuses two ranks on one GPU, so
+this is how 2-4 processes share one MI355X and run the real HIP kernels through every
+multi-rank code path (k-means++ owner selection, memory-plan agreement, per-rank
+samplers, empty-cluster relocation) -- tests/test_gpu_multirank.py.  It is a correctness
+rehearsal, not a production transport: each collective synchronises the stream, and a
+host-staged step cannot be captured into a hipGraph (``capturable`` is False).
 """
 from __future__ import annotations
 
@@ -29,6 +38,7 @@ class Comm:
     backend: str | None = None
     device: torch.device = torch.device("cpu")
     owns_group: bool = False
+    staged: bool = False      # device tensors cross a gloo group through host memory
 
     # ---------------------------------------------------------------- setup
     @staticmethod
@@ -37,20 +47,31 @@ class Comm:
         return Comm(device=dev)
 
     @staticmethod
-    def from_env(device: str | None = None, timeout_s: float = 600.0) -> "Comm":
+    def from_env(device: str | None = None, timeout_s: float = 600.0, staged: bool | None = None) -> "Comm":
         """Join (or create) the default process group described by torchrun's env vars.
 
         ``device`` "cuda" binds LOCAL_RANK's GPU and uses RCCL; "cpu" uses gloo.
         Without WORLD_SIZE>1 in the environment this returns a single-rank Comm without a
         process group, unless ``MIKMEANS_FORCE_PG=1``: then even one rank joins a real group
         and every collective below is issued (a one-GPU rehearsal of the RCCL path).
+        ``staged`` (default: ``MIKMEANS_COMM=host``): GPU ranks over a host-staged gloo group,
+        rank r on GPU ``r % device_count`` -- several ranks may share one GPU.
         """
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
-        if device.startswith("cuda"):
+        if staged is None:
+            staged = os.environ.get("MIKMEANS_COMM", "").lower() == "host"
+        staged = bool(staged) and device.startswith("cuda")
+        if staged:
+            # (device_count does not initialise HIP on this image)
+            idx = local_rank % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(idx)
+            dev = torch.device("cuda", idx)
+            backend = "gloo"
+        elif device.startswith("cuda"):
             torch.cuda.set_device(local_rank)
             dev = torch.device("cuda", local_rank)
             backend = "nccl"
@@ -74,6 +95,7 @@ class Comm:
             backend=dist.get_backend(),
             device=dev,
             owns_group=owns,
+            staged=staged,
         )
 
     def close(self):
@@ -89,7 +111,8 @@ class Comm:
         if self.device.type == "cuda" and torch.cuda.is_available():
             dev = f"{dev} ({torch.cuda.get_device_name(self.device)})"
         return {"host": socket.gethostname(), "pid": os.getpid(), "rank": self.rank, "world": self.world,
-                "local_rank": self.local_rank, "backend": self.backend, "device": dev}
+                "local_rank": self.local_rank, "backend": self.backend, "device": dev,
+                "staged": self.staged}
 
     @property
     def distributed(self) -> bool:
@@ -100,29 +123,51 @@ class Comm:
         """A process group exists: collectives are issued (also on a forced 1-rank group)."""
         return self.backend is not None and dist.is_initialized()
 
+    @property
+    def capturable(self) -> bool:
+        """Collectives may be recorded into a hipGraph (device-side RCCL, or none at all).
+        A host-staged collective copies through host memory: never capturable."""
+        return not (self.staged and self.grouped)
+
     # ---------------------------------------------------------- collectives
+    def _run(self, t: torch.Tensor, op) -> torch.Tensor:
+        """``op(buffer)`` in place on ``t``: directly, or through a host copy when staged."""
+        if self.staged and t.is_cuda:
+            h = t.detach().to("cpu").contiguous()
+            op(h)
+            t.copy_(h)
+        else:
+            op(t)
+        return t
+
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
         """In-place SUM across ranks (no-op on one rank without a group)."""
         if self.grouped:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            self._run(t, lambda b: dist.all_reduce(b, op=dist.ReduceOp.SUM))
         return t
 
     def allreduce_max_(self, t: torch.Tensor) -> torch.Tensor:
         if self.grouped:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            self._run(t, lambda b: dist.all_reduce(b, op=dist.ReduceOp.MAX))
         return t
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.grouped:
-            dist.broadcast(t, src=src)
+            self._run(t, lambda b: dist.broadcast(b, src=src))
         return t
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """Stack ``t`` from every rank: shape ``[world, *t.shape]``."""
         if not self.grouped:
             return t.unsqueeze(0).clone()
-        flat = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(flat, t.contiguous().reshape(-1))  # gloo wants flat buffers
+        src = t.contiguous().reshape(-1)
+        host = self.staged and t.is_cuda
+        if host:
+            src = src.to("cpu")
+        flat = torch.empty(self.world * t.numel(), dtype=t.dtype, device=src.device)
+        dist.all_gather_into_tensor(flat, src)  # gloo wants flat buffers
+        if host:
+            flat = flat.to(t.device)
         return flat.view(self.world, *t.shape)
 
     def all_gather_object(self, obj):

@@ -26,16 +26,29 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, fn, args, outdir):
+def _to_cpu(obj):
+    """Results leave the rank as host tensors (the parent may not share the rank's GPU)."""
+    if torch.is_tensor(obj):
+        return obj.detach().cpu()
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_cpu(v) for v in obj)
+    return obj
+
+
+def _worker(rank, world, port, fn, args, outdir, device="cpu"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
     from .comm import Comm, set_comm
 
-    comm = Comm.from_env("cpu")
+    comm = Comm.from_env(device, staged=device == "cuda")
     set_comm(comm)
     try:
-        res = fn(comm, *args)
+        res = _to_cpu(fn(comm, *args))
+        if device == "cuda":
+            torch.cuda.synchronize()
         torch.save({"ok": True, "res": res}, os.path.join(outdir, f"r{rank}.pt"))
     except BaseException:  # report, never hang the others silently
         torch.save({"ok": False, "err": traceback.format_exc()}, os.path.join(outdir, f"r{rank}.pt"))
@@ -79,11 +92,15 @@ def launch_self(nproc: int, script_argv: list[str], max_restarts: int = 0, env: 
     return rc
 
 
-def spawn_local(fn, world: int, *args, timeout: float = 300.0):
-    """Run ``fn(comm, *args)`` on ``world`` gloo ranks; return the list of per-rank results."""
+def spawn_local(fn, world: int, *args, timeout: float = 300.0, device: str = "cpu"):
+    """Run ``fn(comm, *args)`` on ``world`` gloo ranks; return the list of per-rank results.
+
+    ``device="cuda"``: GPU ranks over a host-staged gloo group (:class:`~.comm.Comm`
+    ``staged``), rank r on GPU ``r % device_count`` -- on a one-GPU box all ranks share it
+    and run the real HIP kernels."""
     port = free_port()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, port, fn, args, d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, port, fn, args, d, device), nprocs=world, join=True)
         out = []
         for r in range(world):
             rec = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True)

@@ -259,8 +259,9 @@ def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = 
         p["weights"] = _r(n * 4)
     p["labels"] = _r(n * 4)
     p["xn"] = _r(n * 4)
+    if weighted or empty_policy == "farthest":
+        p["mind"] = _r(n * 4)          # written by every step's assign (relocation reads it)
     if weighted:
-        p["mind"] = _r(n * 4)
         p["wdot_scratch"] = _r(WDOT_SCRATCH * 8)
     nch = update_n_chunks(es, K, Dp, max(n, 1), wted or incremental)
     p["slab"] = _r(nch * K * Dp * 8)
@@ -275,8 +276,6 @@ def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = 
                  delta_tot=_r((K * Dp + K) * 8))
     tr = {"init": _init_items(init, n, Dp, D, K, n_local_trials or 0),
           "final_assign": {"labels_out": _r(n * 4), "mind_out": _r(n * 4)}}
-    if empty_policy == "farthest" and not weighted:
-        tr["relocate"] = {"mind": _r(n * 4), "labels_tmp": _r(n * 4)}
     return MemoryPlan("resident", n, D, Dp, K, "bfloat16" if es == 2 else "float32", p, tr)
 
 
@@ -306,9 +305,14 @@ def plan_streaming(n: int, D: int, K: int, dtype="bfloat16", *, chunk_rows: int,
     p.update(_centroid_items(K, Dp, es))
     if 0 < R <= SPLIT_MAX_ROWS:
         p["split_keys"] = _r(R * 8)
-    m = min(n, init_rows or max(20 * K, 1 << 16))
-    tr = {"init": {"sample": _r(m * Dp * es), **_init_items(init, m, Dp, D, K, n_local_trials or 0)},
-          "final_assign": {"labels_out": _r(n * 4), "mind_out": _r(n * 4)}}
+    name = init.lower().replace("_", "-") if isinstance(init, str) else "array"
+    if name in ("random", "array"):
+        # (api.KMeans._init_centers: rows fetched from the host shard, no device sample)
+        init_tr = _init_items(init, n, Dp, D, K, 0)
+    else:   # k-means++ seeds on a device-resident init_size-row sample
+        m = min(n, init_rows or max(20 * K, 1 << 16))
+        init_tr = {"sample": _r(m * Dp * es), **_init_items(init, m, Dp, D, K, n_local_trials or 0)}
+    tr = {"init": init_tr, "final_assign": {"labels_out": _r(n * 4), "mind_out": _r(n * 4)}}
     pl = MemoryPlan("streaming", n, D, Dp, K, "bfloat16" if es == 2 else "float32", p, tr)
     pl.chunk_rows = R
     return pl

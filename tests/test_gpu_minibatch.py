@@ -78,6 +78,37 @@ def test_minibatch_fit_device_vs_host_shard(native, monkeypatch):
     torch.testing.assert_close(c.counts_.cpu(), d.counts_)
 
 
+def test_minibatch_fit_resume_widens_a_smaller_checkpoint_bound(native, tmp_path):
+    """A mini-batch checkpoint whose col_bound is below the shard's maximum (fit_stream's,
+    or a first-batch bound) resumed by fit(): the scales are widened to the shard's, so the
+    unclamped M-step never saturates -- the centres equal an uninterrupted fit that started
+    from the checkpoint's state with the shard's own bound (api.py:676)."""
+    from mikmeans.utils.checkpoint import load_checkpoint
+
+    n, D, K = 60_000, 32, 12
+    X = B.make_blobs(n, D, K, seed=5, dtype=torch.float32, device=DEV)
+    X[123, 7] = 900.0                   # one large value: far above any small-batch bound
+    kw = dict(batch_size=2048, init="random", seed=3, dtype="float32", device=DEV)
+    a = mikmeans.MiniBatchKMeans(K, max_steps=3, **kw).fit(X)
+    ck = tmp_path / "mb"
+    a.save(str(ck))
+    st = load_checkpoint(str(ck))
+    small = st["tensors"]["col_bound"].clone()
+    small[:] = 1.0                      # a bound the shard's column 7 (900) exceeds
+    from mikmeans.utils.checkpoint import save_checkpoint
+
+    ck2 = tmp_path / "mb_small"
+    save_checkpoint(str(ck2), st["centers"], st["iteration"], st["config"],
+                    extra={"kind": "minibatch", "rescales": 0},
+                    tensors={"vcount": st["tensors"]["vcount"], "col_bound": small})
+    b = mikmeans.MiniBatchKMeans(K, max_steps=10, **kw).fit(X, resume_from=str(ck2))
+    assert bool((b._eng.bound[:D].cpu() >= X.abs().amax(0).double().cpu()).all())
+    c = mikmeans.MiniBatchKMeans(K, max_steps=10, **kw).fit(X, resume_from=str(ck))
+    assert torch.equal(b.cluster_centers_, c.cluster_centers_)
+    assert torch.equal(b.counts_, c.counts_)
+    assert torch.isfinite(b.cluster_centers_).all()
+
+
 def test_minibatch_fit_steps_do_not_sync(native):
     """Bounded scales from the whole shard: no step reads back to the host (one tol check
     per 10 steps at most) -- counted with a hooked .item()/.tolist() on device tensors."""
