@@ -498,6 +498,24 @@ void host_unregister(const Tensor& t) {
   hip_check(hipHostUnregister(t.data_ptr()), "hipHostUnregister");
 }
 
+// Tear down a stream capture that an error left open.  When a capture is invalidated,
+// hipStreamEndCapture inside torch's capture_end can fail and leave the stream in the
+// capturing state; every later launch on the legacy stream then fails with "operation
+// failed due to a previous error during capture".  Ends it (discarding any partial graph)
+// and clears the error state.  Returns the capture status found (0 = none).
+int capture_teardown(int64_t stream_ptr) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream_ptr);
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) { (void)hipGetLastError(); return -1; }
+  if (st != hipStreamCaptureStatusNone) {
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture(s, &g);
+    if (g) (void)hipGraphDestroy(g);
+  }
+  (void)hipGetLastError();
+  return (int)st;
+}
+
 std::string js_format(double v) {
   std::string s;
   mk::js_number(v, s);
@@ -575,6 +593,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "fixed-point exponent e with maxabs * 2^e <= 2^30 (M-step accumulators)");
   m.def("host_register", &host_register, "page-lock a CPU tensor in place (hipHostRegister)");
   m.def("host_unregister", &host_unregister, "undo host_register");
+  m.def("capture_teardown", &capture_teardown, "end a stream capture an error left open (status found)");
   m.def("js_format", &js_format, "ECMAScript Number::toString of a double");
   m.def("js_array", &js_array, "JSON array of a CPU float tensor with JS number formatting");
   m.attr("NSLOT") = mk::NSLOT;

@@ -324,6 +324,14 @@ class LloydEngine:
             self.capture_error = f"{type(e).__name__}: {e}".splitlines()[0]
             native.warn_once(f"hipGraph capture failed ({self.capture_error}); eager steps")
             graphs = None
+            # torch's graph context restores the caller's stream only after a successful
+            # capture_end: a failed one leaves the (invalidated) capture stream current, and
+            # every later launch on it fails "due to a previous error during capture".  End
+            # any capture still open, make the caller's stream current again and never
+            # touch the capture stream after this.
+            self._C.capture_teardown(side.cuda_stream)
+            torch.cuda.set_stream(main)
+            side = torch.cuda.Stream(device=dev)
             torch.cuda.synchronize(dev)   # (a capture error is not sticky; a device fault would raise here)
         # the warm-up changed labels / slots / running totals: restore the pre-capture state
         main.wait_stream(side)
