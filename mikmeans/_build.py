@@ -46,6 +46,11 @@ DEVICE_FLAGS = [
 SOURCE_FLAGS = {"assign16.hip": ["-fno-slp-vectorize"]}
 
 
+def source_flags(name: str, csrc: Path = CSRC) -> list[str]:
+    """hipcc flags of one HIP translation unit (tests/test_isa_guard.py rebuilds with them)."""
+    return [*DEVICE_FLAGS, *SOURCE_FLAGS.get(name, []), f"-I{csrc}"]
+
+
 def ext_path() -> Path:
     return PKG / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
 
@@ -125,8 +130,7 @@ def build(force: bool = False, verbose: bool = True, jobs: int | None = None, *,
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         sources = [s for s in HIP_SOURCES if (csrc / s).exists()]
-        futs = [ex.submit(_compile, csrc / s, [*DEVICE_FLAGS, *SOURCE_FLAGS.get(s, []), f"-I{csrc}"], verbose,
-                          build_dir) for s in sources]
+        futs = [ex.submit(_compile, csrc / s, source_flags(s, csrc), verbose, build_dir) for s in sources]
         futs.append(ex.submit(_compile, csrc / BINDING, binding_flags, verbose, build_dir))
         objs = [f.result() for f in futs]
     out = out or ext_path()

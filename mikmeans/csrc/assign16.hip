@@ -631,11 +631,7 @@ static int assign16_splits(int64_t nblk, int nch) {
 // recovery pass costs 64/K of the matrix work, so it is taken for K >= 2048 at D=64 and
 // K >= 1024 at D=32 (scripts/varg_ab.py, profiles/r3_08_varg_ab.log: cfg4 shape +8.2 %,
 // D=64 K=2048 +8.5 %, K=1024 -3.7 %; D=32 K=1024 +5.6 %, K=512 -8.8 %).
-// MIKMEANS_ASSIGN_VARG=0/1 forces it off / on (A/B, tests).
-static int varg_env() {   // read per launch (tests switch it inside one process)
-  const char* e = getenv("MIKMEANS_ASSIGN_VARG");
-  return (e && *e) ? atoi(e) : -1;
-}
+// Variant V_ASSIGN_VARG = 0/1 forces it off / on (A/B, tests).
 
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ>
 static void set_lds_attr() {
@@ -658,13 +654,9 @@ static void set_lds_attr() {
 // (scripts/microbench/mfma_shape.hip mode 1, profiles/r3_17_mfma_issue_order.log: with the
 // key epilogue 84.4 -> 91.6 % at 1780 -> 1762 MHz, +7.5 % TF/s; 32x32x16 gains 3.6 % the
 // same way and stays 12 % behind).
-// MIKMEANS_ASSIGN_PMAJ=0/1 forces it off / on.  Issuing each block's epilogue between the next
+// Variant V_ASSIGN_PMAJ = 0/1 forces it off / on.  Issuing each block's epilogue between the next
 // blocks' MFMA chains instead measured -1.1 % at D=128, -3.8 % at D=64 K=4096, +2.2 % at D=64
 // K=1024 (profiles/r3_23_ab_pmaj_interleaved.log) and is not built.
-static int pmaj_env() {   // read per launch (A/B harnesses switch it inside one process)
-  const char* e = getenv("MIKMEANS_ASSIGN_PMAJ");
-  return (e && *e) ? atoi(e) : -1;
-}
 
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ>
 static void launch16_kp(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
@@ -677,7 +669,7 @@ static void launch16_kp(const AssignArgs& b, const dim3& grid, size_t lds, hipSt
 
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG>
 static void launch16_k(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  const int e = pmaj_env();
+  const int e = variant(V_ASSIGN_PMAJ);
   const int pm = e >= 0 ? e : (sizeof(T) == 2 ? 1 : 0);
   if (pm != 0) return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 1>(b, grid, lds, s);
   launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 0>(b, grid, lds, s);
@@ -700,7 +692,7 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   bool varg = false;
   constexpr bool VARG_OK = sizeof(T) == 2 && DPAD <= 64;   // D=128: -12 % at K=1024, -4 % at 2048 (r3_11)
   if constexpr (VARG_OK) {
-    const int e = varg_env();
+    const int e = variant(V_ASSIGN_VARG);
     varg = e >= 0 ? e != 0 : a.Kpad >= (DPAD == 64 ? 2048 : 1024);
   }
   if constexpr (VARG_OK) {
@@ -733,22 +725,20 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   constexpr int OCC = sizeof(T) == 2 ? ((DPAD == 64 || DPAD == 256) ? 3 : 4) : 1;
   static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
   if constexpr (sizeof(T) == 2 && DPAD == 256) {
-    // A/B switch MIKMEANS_ASSIGN_GEOM: 8 waves per ring (half the per-point centre stream and
+    // A/B switch V_ASSIGN_GEOM: 8 waves per ring (half the per-point centre stream and
     // per-workgroup start-up): 1 = 3 point blocks at 2 waves/SIMD, 2 = 2 blocks at 4
-    const char* e = getenv("MIKMEANS_ASSIGN_GEOM");
-    const int gm = (e && *e) ? atoi(e) : 0;
+    const int gm = variant(V_ASSIGN_GEOM);
     if (gm == 1) return launch16_t<T, DPAD, 3, CT, 2, 2, 8>(a, s);
     if (gm == 2) return launch16_t<T, DPAD, 2, CT, 2, 4, 8>(a, s);
   }
   if constexpr (sizeof(T) == 2 && DPAD == 128) {
-    // A/B switch MIKMEANS_ASSIGN_GEOM: 1 = 8 waves share a ring of 32 KiB chunks (a barrier
+    // A/B switch V_ASSIGN_GEOM: 1 = 8 waves share a ring of 32 KiB chunks (a barrier
     // every 8 tiles instead of 4), 2 = 8 waves share the 16 KiB ring.  K=1024: -0.4 % / +0.1 %;
     // K=2048: +4.9 % / +4.4 % (profiles/r3_21_ab_geom128.log), near-tie labels move with
     // the workgroup's seed offset; the headline's K=1024 keeps 4 waves.
     // A K sweep keeps 4 waves as the default: 8-wave rings measured +5.0 % at K=2048 but
     // -5.3 % at 3072 and -5.5 % at 4096 (profiles/r3_33_ab_geom128_ksweep.log).
-    const char* e = getenv("MIKMEANS_ASSIGN_GEOM");
-    const int gm = (e && *e) ? atoi(e) : 0;
+    const int gm = variant(V_ASSIGN_GEOM);
     if (gm == 1 && a.Kpad % (16 * 8) == 0) return launch16_t<T, DPAD, P, 8, 2, OCC, 8>(a, s);
     if (gm == 2) return launch16_t<T, DPAD, P, CT, 2, OCC, 8>(a, s);
     if (gm == 3) return launch16_t<T, DPAD, 6, CT, 2, 3>(a, s);   // 6 point blocks at 3 waves/SIMD

@@ -8,7 +8,9 @@
 #include <c10/hip/HIPStream.h>
 #include <charconv>
 #include <cmath>
+#include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "jsnum.h"
 #include "kernels.h"
@@ -498,6 +500,31 @@ void host_unregister(const Tensor& t) {
   hip_check(hipHostUnregister(t.data_ptr()), "hipHostUnregister");
 }
 
+}  // namespace
+
+namespace mk {
+// The A/B switch registry (kernels.h): environment read once at load, then set_variant only.
+static const char* const kVariantEnv[V_COUNT] = {"MIKMEANS_ASSIGN_VARG", "MIKMEANS_ASSIGN_PMAJ",
+                                                 "MIKMEANS_ASSIGN_GEOM", "MIKMEANS_UPDATE_KS",
+                                                 "MIKMEANS_UPDATE_KS_GM", "MIKMEANS_BLOBS_TPR"};
+static int* variant_table() {
+  static int t[V_COUNT] = {};
+  static const bool init = [] {
+    for (int i = 0; i < V_COUNT; ++i) {
+      const char* e = getenv(kVariantEnv[i]);
+      t[i] = (e && *e) ? atoi(e) : -1;
+    }
+    return true;
+  }();
+  (void)init;
+  return t;
+}
+int variant(Variant v) { return variant_table()[v]; }
+void set_variant(Variant v, int value) { variant_table()[v] = value; }
+}  // namespace mk
+
+namespace {
+
 // Tear down a stream capture that an error left open.  When a capture is invalidated,
 // hipStreamEndCapture inside torch's capture_end can fail and leave the stream in the
 // capturing state; every later launch on the legacy stream then fails with "operation
@@ -593,6 +620,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "fixed-point exponent e with maxabs * 2^e <= 2^30 (M-step accumulators)");
   m.def("host_register", &host_register, "page-lock a CPU tensor in place (hipHostRegister)");
   m.def("host_unregister", &host_unregister, "undo host_register");
+  m.def("variant_names", []() {
+    std::vector<std::string> n;
+    for (int i = 0; i < mk::V_COUNT; ++i) n.emplace_back(mk::kVariantEnv[i] + 9);   // strip "MIKMEANS_"
+    return n;
+  }, "A/B switch names (lower-cased by mikmeans.ops.native)");
+  m.def("get_variant", [](int64_t i) { return mk::variant((mk::Variant)i); });
+  m.def("set_variant", [](int64_t i, int64_t v) { mk::set_variant((mk::Variant)i, (int)v); },
+        "set an A/B switch (-1 = built-in rule); launchers never read the environment");
+  (void)mk::variant(mk::V_ASSIGN_VARG);   // snapshot the environment now, at load
   m.def("capture_teardown", &capture_teardown, "end a stream capture an error left open (status found)");
   m.def("js_format", &js_format, "ECMAScript Number::toString of a double");
   m.def("js_array", &js_array, "JSON array of a CPU float tensor with JS number formatting");

@@ -28,6 +28,14 @@ constexpr int SLOT_STRIDE = 8;
 // The stored value is -2*c (exact in bf16/f32) and cn[k] = |c_q|^2 of the quantised
 // centroid, so the MFMA chain seeded with cn directly yields
 // score = |c|^2 - 2 x.c  (= |x-c|^2 - |x|^2).
+// A/B experiment switches (scripts/ab_ext.py, A/B harnesses, tests).  No launcher reads the
+// environment: the values are taken from MIKMEANS_<NAME> once when the extension loads and
+// changed only through set_variant (mikmeans.ops.native.variant); -1 = the built-in rule.
+// A captured hipGraph keeps the geometry that was in force when it was recorded.
+enum Variant { V_ASSIGN_VARG = 0, V_ASSIGN_PMAJ, V_ASSIGN_GEOM, V_UPDATE_KS, V_UPDATE_KS_GM, V_BLOBS_TPR, V_COUNT };
+int variant(Variant v);
+void set_variant(Variant v, int value);
+
 int assign16_chunk_tiles(int dtype, int dpad);  // centroid tiles per LDS chunk (0 = unsupported)
 int assign_kpad(int dtype, int dpad, int K);     // K rounded to a chunk multiple
 int assign_cn_len(int kpad);                     // cn array length (multiple of 256 floats)

@@ -532,13 +532,10 @@ hipError_t launch_blobs(int dtype, void* X, int64_t i0, int64_t n, int D, int64_
   // Lanes per row: the row's blob-id Philox runs once per wave whatever the number of
   // active lanes, so fewer lanes per row (more rows per wave) amortise it over more
   // groups (8 lanes x 16 B still store whole 128-B lines; profiles/r1_18_blobs_tpr_ab.json:
-  // 2.91 -> 2.69 ms per 16.8M x 256 bf16 batch).  MIKMEANS_BLOBS_TPR (1..16) overrides the
+  // 2.91 -> 2.69 ms per 16.8M x 256 bf16 batch).  Variant V_BLOBS_TPR (1..16) overrides the
   // cap for A/B runs.  The rows do not depend on it; the fused norms' f32 summation order does.
-  static const int tpr_cap = [] {
-    const char* e = getenv("MIKMEANS_BLOBS_TPR");
-    const int v = e ? atoi(e) : 8;
-    return v >= 1 && v <= 16 ? v : 16;
-  }();
+  const int tv = variant(V_BLOBS_TPR);
+  const int tpr_cap = tv < 0 ? 8 : (tv >= 1 && tv <= 16 ? tv : 16);
   while (tpr < G && tpr * 2 <= tpr_cap) tpr *= 2;
   const int64_t tot = n * tpr;
   const unsigned nb = (unsigned)((tot + 255) / 256);

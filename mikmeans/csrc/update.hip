@@ -823,8 +823,8 @@ static bool use_ks(int dtype, int K, int D, bool weighted, plan::KsPlan* kp) {
   // A/B override (0 = slice kernel, 1 = K-split); the memory planner assumes the default.
   // cfg5 (D=256 K=512, 128-B slices): K-split 6.58 vs slice 6.03 ms per resident step
   // (profiles/r3_09_update_ks_cfg5_ab.log), so the rule below stands.
-  const char* ov = getenv("MIKMEANS_UPDATE_KS");
-  if (ov && *ov) return atoi(ov) != 0 && sw > 0 && sw < D && plan::choose_ks(esize(dtype), K, D, kp);
+  const int ov = variant(V_UPDATE_KS);
+  if (ov >= 0) return ov != 0 && sw > 0 && sw < D && plan::choose_ks(esize(dtype), K, D, kp);
   return sw > 0 && sw < D && sw * esize(dtype) < 128 && plan::choose_ks(esize(dtype), K, D, kp);
 }
 
@@ -999,8 +999,7 @@ hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s) {
     if (a.n_chunks % 8) return hipErrorInvalidValue;
     {   // A/B override of the row groups in flight (2, 3 or 6).  With the ping-pong periods the
         // plan's choice still wins: cfg4 2 > 3 > 6, headline 6 > 3 > 2 (profiles/r3_30_ks_gm_ab.log)
-      const char* g = getenv("MIKMEANS_UPDATE_KS_GM");
-      const int gm = (g && *g) ? atoi(g) : 0;
+      const int gm = variant(V_UPDATE_KS_GM);
       if (gm == 2 || gm == 3 || gm == 6) kp.gm = gm;
     }
     return dtype == DT_BF16 ? launch_ks<uint16_t>(a, kp, s) : launch_ks<float>(a, kp, s);

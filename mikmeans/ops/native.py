@@ -84,6 +84,42 @@ def warn_once(msg: str) -> None:
         warnings.warn("mikmeans: " + msg, stacklevel=3)
 
 
+def _variant_index(name: str) -> int:
+    names = [n.lower() for n in require().variant_names()]
+    key = name.lower().removeprefix("mikmeans_")
+    if key not in names:
+        raise KeyError(f"unknown kernel variant {name!r} (known: {names})")
+    return names.index(key)
+
+
+def get_variant(name: str) -> int:
+    """Current value of a kernel A/B switch (-1 = the built-in rule)."""
+    return int(require().get_variant(_variant_index(name)))
+
+
+def set_variant(name: str, value: int) -> None:
+    """Set a kernel A/B switch (``assign_varg``, ``assign_pmaj``, ``assign_geom``,
+    ``update_ks``, ``update_ks_gm``, ``blobs_tpr``; -1 = built-in rule).  The launchers never
+    read the environment: ``MIKMEANS_<NAME>`` is read once when the extension loads."""
+    require().set_variant(_variant_index(name), int(value))
+
+
+class variant:
+    """``with native.variant("assign_varg", 1): ...`` -- a switch for the block's launches."""
+
+    def __init__(self, name: str, value):
+        self.name, self.value = name, -1 if value is None else int(value)
+
+    def __enter__(self):
+        self.old = get_variant(self.name)
+        set_variant(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_variant(self.name, self.old)
+        return False
+
+
 def loaded_path() -> str | None:
     m = _load()
     return getattr(m, "__file__", None) if m is not None else None

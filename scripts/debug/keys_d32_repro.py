@@ -8,6 +8,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 
+from mikmeans.ops import native
+
 from mikmeans import ops
 from mikmeans.ops import cpu as ref
 
@@ -55,9 +57,9 @@ def main():
               flush=True)
         Xd, Cd = Xb.to(DEV), C.to(DEV)
         for pm in ("0", "1"):
-            os.environ["MIKMEANS_ASSIGN_PMAJ"] = pm
+            native.set_variant("assign_pmaj", int(pm))
             for env in ("0", "1"):
-                os.environ["MIKMEANS_ASSIGN_VARG"] = env
+                native.set_variant("assign_varg", int(env))
                 nbad_launches, tot = 0, 0
                 for r in range(NL):
                     dirty(r)
@@ -75,8 +77,8 @@ def main():
                               f"blocks {sorted(set(((off % (wgp // 4)) // 16).tolist()))} labels {sorted(set(lab[bad].tolist()))[:8]}",
                               flush=True)
                 print(f"  PMAJ={pm} VARG={env}: {nbad_launches}/{NL} launches wrong, {tot} rows", flush=True)
-    os.environ.pop("MIKMEANS_ASSIGN_VARG", None)
-    os.environ.pop("MIKMEANS_ASSIGN_PMAJ", None)
+    native.set_variant("assign_varg", -1)
+    native.set_variant("assign_pmaj", -1)
 
 
 if __name__ == "__main__":

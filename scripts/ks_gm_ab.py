@@ -33,7 +33,7 @@ def main():
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for rd in range(5):
             for g in (arms if rd % 2 == 0 else arms[::-1]):
-                os.environ["MIKMEANS_UPDATE_KS_GM"] = g
+                native.set_variant("update_ks_gm", int(g))
                 C.update(eng.X, eng.labels, k, slab, cnt, nch, None, eng.col_exp, eng.cnt_exp, False)
                 ev[0].record()
                 for _ in range(5):
@@ -42,7 +42,7 @@ def main():
                 torch.cuda.synchronize()
                 t[g].append(ev[0].elapsed_time(ev[1]) / 5)
                 sums[g] = slab.view(nch, -1).sum(0)
-        os.environ.pop("MIKMEANS_UPDATE_KS_GM", None)
+        native.set_variant("update_ks_gm", -1)
         print(json.dumps({"n": n, "d": d, "k": k, **{g: round(statistics.median(v), 4) for g, v in t.items()},
                           "sums_equal": all(torch.equal(sums[g], sums["2"]) for g in arms)}), flush=True)
         del eng, X

@@ -11,6 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 from mikmeans import ops
+from mikmeans.ops import native
 from mikmeans.data import blobs as B
 
 
@@ -19,7 +20,7 @@ def main():
     ap.add_argument("--shapes", default="10000000,64,4096;2000000,64,2048;2000000,64,1024;4000000,32,1024;4000000,32,512;4000000,32,256")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--env", default="MIKMEANS_ASSIGN_VARG", help="variable switched between the arms")
+    ap.add_argument("--env", default="assign_varg", help="kernel variant switched between the arms (native.set_variant)")
     ap.add_argument("--values", default="0,1", help="its values, one arm each (first = baseline)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     args = ap.parse_args()
@@ -36,7 +37,7 @@ def main():
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for rd in range(args.rounds):
             for v in (vals if rd % 2 == 0 else vals[::-1]):
-                os.environ[args.env] = v
+                native.set_variant(args.env, int(v))
                 pack.assign(X, xn, labels[v])            # warm
                 ev[0].record()
                 for _ in range(args.reps):
@@ -53,7 +54,7 @@ def main():
                       "tflops": round(flop / ms / 1e9, 1), "speedup": round(base / ms, 4),
                       "label_mismatch": int((labels[vals[0]] != labels[v]).sum())}
         print(json.dumps(out), flush=True)
-    os.environ.pop(args.env, None)
+    native.set_variant(args.env, -1)
 
 
 if __name__ == "__main__":

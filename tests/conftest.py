@@ -28,3 +28,20 @@ def native():
     from mikmeans.ops import native as nat
 
     return nat.require()
+
+
+@pytest.fixture
+def kvariant(native):
+    """Set kernel A/B switches for one test (mikmeans.ops.native.set_variant), restored after."""
+    from mikmeans.ops import native as nat
+
+    saved = {}
+
+    def set_(name, value):
+        if name not in saved:
+            saved[name] = nat.get_variant(name)
+        nat.set_variant(name, int(value))
+
+    yield set_
+    for k, v in saved.items():
+        nat.set_variant(k, v)

@@ -699,7 +699,7 @@ def test_assign_bf16_key_resolution_distance_relative(native):
 
 @pytest.mark.parametrize("pmaj", ["0", "1"])
 @pytest.mark.parametrize("varg", ["0", "1"])
-def test_assign_per_point_offset_seeds_repeatable(native, monkeypatch, pmaj, varg):
+def test_assign_per_point_offset_seeds_repeatable(native, kvariant, pmaj, varg):
     """Per-point-offset workgroups (N(0,1) rows at D=32: most workgroups) under both MFMA
     issue orders and both epilogues, launched repeatedly with other kernels in between (they
     leave their own data in LDS and registers): every launch gives the same labels, and no
@@ -714,8 +714,8 @@ def test_assign_per_point_offset_seeds_repeatable(native, monkeypatch, pmaj, var
     exp = _first_argmin(dist)
     srt = dist.sort(1).values
     clear = (srt[:, 1] - srt[:, 0]) > 1e-3
-    monkeypatch.setenv("MIKMEANS_ASSIGN_PMAJ", pmaj)
-    monkeypatch.setenv("MIKMEANS_ASSIGN_VARG", varg)
+    kvariant("assign_pmaj", pmaj)
+    kvariant("assign_varg", varg)
     Xd, Cd = Xb.to(DEV), C.to(DEV)
     first = None
     for r in range(6):
@@ -733,7 +733,7 @@ def test_assign_per_point_offset_seeds_repeatable(native, monkeypatch, pmaj, var
 @pytest.mark.parametrize("n,outlier,d,k", [(20_000, False, 64, 4096), (300_000, False, 64, 4096),
                                            (300_000, True, 64, 4096), (40_000, True, 64, 4096),
                                            (300_000, False, 32, 1024), (30_000, True, 32, 1024)])
-def test_assign_value_argmin_d64(native, monkeypatch, n, outlier, d, k):
+def test_assign_value_argmin_d64(native, kvariant, n, outlier, d, k):
     """The value-only argmin (bf16 D=64 K >= 2048, D=32 K >= 1024: running minimum + tile in the main loop,
     the row inside the winning tile recovered on the matrix cores afterwards) gives the f64
     argmin on every row resolvable at fp32 resolution of the seeded score, on the split and
@@ -746,9 +746,9 @@ def test_assign_value_argmin_d64(native, monkeypatch, n, outlier, d, k):
     if outlier:
         X[7] *= 300.0
     Xb = X.to(torch.bfloat16)
-    monkeypatch.setenv("MIKMEANS_ASSIGN_VARG", "1")
+    kvariant("assign_varg", "1")
     lv, dv = ops.assign(Xb.to(DEV), C.to(DEV), with_dist=True)
-    monkeypatch.setenv("MIKMEANS_ASSIGN_VARG", "0")
+    kvariant("assign_varg", "0")
     lk, _ = ops.assign(Xb.to(DEV), C.to(DEV), with_dist=False)
     xx, Cq, dist = _bf16_dist(Xb, C)
     exp = _first_argmin(dist)

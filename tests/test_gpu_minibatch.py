@@ -146,7 +146,7 @@ def test_minibatch_fit_steps_do_not_sync(native):
                                                 (64, 4096, torch.bfloat16, None), (128, 256, torch.float32, None),
                                                 (40, 20000, torch.float32, None), (256, 512, torch.bfloat16, "1"),
                                                 (256, 600, torch.bfloat16, None)])
-def test_gathered_rows_step_equals_materialised_batch(native, monkeypatch, D, K, dtype, force_ks):
+def test_gathered_rows_step_equals_materialised_batch(native, kvariant, D, K, dtype, force_ks):
     """partial_fit_rows (assign + M-step reading X[rows] through the index list: slice,
     K-split and global-atomic M-step kernels; force_ks: the K-split kernel where the slice
     kernel is the default; K=600 at D=256: the slice kernel without its LDS index staging,
@@ -155,7 +155,7 @@ def test_gathered_rows_step_equals_materialised_batch(native, monkeypatch, D, K,
     from mikmeans.ops import col_stats, pad_columns
 
     if force_ks is not None:
-        monkeypatch.setenv("MIKMEANS_UPDATE_KS", force_ks)
+        kvariant("update_ks", force_ks)
 
     n, b = 600_000, 270_000     # b > SPLIT_MAX_ROWS: both paths take the one-pass assign grid
     X = pad_columns(B.make_blobs(n, D, 64, seed=D, dtype=dtype, device=DEV))

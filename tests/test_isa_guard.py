@@ -1,0 +1,60 @@
+"""ISA guard for the assign kernels' seed-add workaround (CPU: hipcc + LLVM tools, no GPU).
+
+A packed ``v_pk_add_f32`` that builds an MFMA's accumulator seed intermittently reached the
+matrix core wrong on gfx950 (5 of 12 launches gave one point block wrong labels,
+profiles/r3_15_ppo_seed_race.md): the toolchain emits no wait state between the packed
+VALU write and the MFMA's srcC read.  csrc/assign16.hip therefore adds seeds as scalar
+``v_add_f32`` and is compiled with ``-fno-slp-vectorize`` (mikmeans/_build.py).  These tests
+read the built gfx950 code object and fail if any assign16 MFMA's srcC was last written by
+a packed-f32 op -- and show that dropping the flag brings the pattern back, so the guard
+is live.  scripts/microbench/seed_hazard.hip is the standalone repro.
+"""
+import shutil
+from pathlib import Path
+
+import pytest
+
+from mikmeans import _build
+from mikmeans.utils import isa
+
+pytestmark = pytest.mark.skipif(shutil.which(_build._hipcc()) is None and not Path(_build._hipcc()).exists(),
+                                reason="hipcc not available")
+SRC = _build.CSRC / "assign16.hip"
+
+
+def _hazards(obj: Path, tmp: Path):
+    funcs = isa.functions(isa.disassemble(isa.device_elf(obj, tmp / "dev.o")))
+    assert any("assign16_kernel" in f for f in funcs), "no assign16 kernels in the code object"
+    return isa.packed_seed_hazards(funcs), funcs
+
+
+def test_built_assign16_has_no_packed_seed_writes(tmp_path):
+    """The production object (same flags and sources as the shipped _C .so; cached)."""
+    flags = _build.source_flags(SRC.name)
+    assert "-fno-slp-vectorize" in flags
+    obj = _build._compile(SRC, flags, verbose=False)
+    hz, funcs = _hazards(obj, tmp_path)
+    assert not hz, [(h.function[:80], h.writer, h.mfma) for h in hz[:5]]
+    # the bf16 kernels really use the per-point-offset seeds (the path the flag protects)
+    assert sum("assign16_kernelIt" in f for f in funcs) >= 8
+
+
+@pytest.mark.slow
+def test_guard_detects_packed_seeds_without_the_flag(tmp_path):
+    """Negative control: the same source without -fno-slp-vectorize vectorises seed_add into
+    v_pk_add_f32 feeding MFMA srcC, and the checker flags it (so removing the flag from
+    _build.py fails the test above's premise, not silently)."""
+    flags = [f for f in _build.source_flags(SRC.name) if f != "-fno-slp-vectorize"]
+    obj = _build._compile(SRC, flags, verbose=False, build_dir=tmp_path / "build")
+    hz, _ = _hazards(obj, tmp_path)
+    assert hz, "expected packed-f32 seed writes without -fno-slp-vectorize"
+    assert all(h.writer.startswith("v_pk_") for h in hz)
+
+
+def test_launchers_never_read_the_environment():
+    """Kernel geometry switches live in one registry (kernels.h ``Variant``), read from the
+    environment once when the extension loads; no .hip launcher calls getenv (verdict r3:
+    per-launch reads were silently frozen into captured graphs)."""
+    for src in sorted(_build.CSRC.glob("*.hip")) + sorted(_build.CSRC.glob("*.h")):
+        assert "getenv" not in src.read_text(), src.name
+    assert _build.CSRC.joinpath("binding.cpp").read_text().count("getenv(") == 1
