@@ -641,8 +641,10 @@ class MiniBatchKMeans(_Serving):
         self.memory_plan_ = None
         resident = True
         if gpu:
+            x_ready = (torch.is_tensor(X) and X.device == device and X.dtype == self.dtype
+                       and (not n or pad_columns(X[:0]).data_ptr() == X[:0].data_ptr()))
             plan = memplan.plan_minibatch(n, D, self.n_clusters, self.dtype, batch_rows=self.batch_size,
-                                          resident=True, init_rows=self.init_size)
+                                          resident=True, init_rows=self.init_size, copy_x=not x_ready)
             plan.budget = memplan.hbm_budget(device)
             if not plan.fits and not X.is_cuda:
                 plan = memplan.plan_minibatch(n, D, self.n_clusters, self.dtype, batch_rows=self.batch_size,
@@ -693,11 +695,16 @@ class MiniBatchKMeans(_Serving):
         n_global, _ = _shard_info(n, comm, comm.device)
         steps = self.max_steps or max(1, math.ceil(self.max_iter * n_global / (self.batch_size * comm.world)))
         buf = rows = None
+        self._fit_buffers = {}
+        if eng.gpu and Xt is not None and Xt.data_ptr() != getattr(X, "data_ptr", lambda: None)():
+            self._fit_buffers["X"] = Xt          # the fit's device copy of the shard
         if eng.gpu and b:
             if Xt is not None:    # device shard: the step reads X[rows] in place, nothing gathered
                 rows = torch.empty(b, dtype=torch.int64, device=device)
+                self._fit_buffers["rows"] = rows
             else:                 # host shard: the batch's rows are gathered on the host
                 buf = torch.zeros((b, eng.Dp), dtype=self.dtype, device=device)
+                self._fit_buffers["batch"] = buf
         C = native_mod() if eng.gpu else None
         while eng.steps < steps:
             s = eng.steps
@@ -827,6 +834,16 @@ class MiniBatchKMeans(_Serving):
         eng.partial_fit(Xt)
         self._finish(eng)
         return self
+
+    def device_buffers(self) -> dict:
+        """Allocator bytes of the last ``fit``'s persistent device buffers (engine + the fit's
+        shard copy / row list / batch buffer), named as ``memplan.plan_minibatch`` plans them."""
+        from .parallel.memplan import _r
+
+        out = dict(self._eng.device_buffers()) if self._eng is not None else {}
+        for k, v in getattr(self, "_fit_buffers", {}).items():
+            out[k] = _r(v.numel() * v.element_size())
+        return out
 
     def _finish(self, eng):
         self.cluster_centers_ = eng.centers.clone()

@@ -68,7 +68,6 @@ class MiniBatchEngine:
             self.bounded = value_bound is not None   # scales cover every value: no clamp, no sync
             self.clampc = torch.zeros(1, dtype=torch.int32, device=dev)
             self.labels = torch.empty(self.batch, dtype=torch.int32, device=dev)
-            self.xn = torch.empty(self.batch, dtype=torch.float32, device=dev)
 
     def set_centers(self, centers: torch.Tensor, counts=None):
         self.C.zero_()
@@ -82,6 +81,20 @@ class MiniBatchEngine:
     @property
     def centers(self):
         return self.C[:, : self.D]
+
+    def device_buffers(self) -> dict:
+        """Allocator bytes of every device buffer the engine holds, under the names
+        parallel/memplan.py ``plan_minibatch`` plans them by (tests/test_gpu_memplan.py)."""
+        from ..parallel.memplan import _r
+
+        if not self.gpu:
+            return {}
+        t = {"C": self.C, "Cnew": self.Cnew, "vcount": self.vcount, "shift": self.shift, "counts": self.counts,
+             "packed": self.packed, "pack": self.pk.pack, "cn": self.pk.cn, "slots": self.slots,
+             "slab": self.slab, "cnt_slab": self.cnt_slab, "batch_labels": self.labels, "clampc": self.clampc}
+        if self.pk._keys is not None:
+            t["split_keys"] = self.pk._keys
+        return {k: _r(v.numel() * v.element_size()) for k, v in t.items()}
 
     def partial_fit(self, Xb: torch.Tensor, norms: torch.Tensor | None = None):
         """One mini-batch step on this rank's batch ``Xb`` (may be empty).  ``norms`` is

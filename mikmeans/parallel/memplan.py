@@ -325,24 +325,29 @@ def stream_chunk_rows(chunk_rows: int, n: int) -> int:
 
 def plan_minibatch(n: int, D: int, K: int, dtype="bfloat16", *, batch_rows: int, resident: bool = True,
                    init="k-means++", init_rows: int | None = None, copy_x: bool = True) -> MemoryPlan:
-    """Mini-batch fit (api.MiniBatchKMeans.fit, models/minibatch.py): the engine's batch
-    buffers and slab, plus the shard itself when it is device-resident."""
+    """Mini-batch fit (api.MiniBatchKMeans.fit, models/minibatch.py): the engine's buffers
+    (``MiniBatchEngine.device_buffers``) plus the fit's own -- the shard itself when it is
+    device-resident (each step then reads ``X[rows]`` in place through an int64 index list
+    drawn on the device), or one gathered batch buffer for a host shard."""
     es = esize_of(dtype)
     Dp = padded_cols(D, es)
     b = int(batch_rows)
     p = {}
-    if resident and copy_x:
-        p["X"] = _r(n * Dp * es)
-    p["batch"] = _r(b * Dp * es)
+    if resident:
+        if copy_x:
+            p["X"] = _r(n * Dp * es)
+        p["rows"] = _r(b * 8)
+    else:
+        p["batch"] = _r(b * Dp * es)
     p["batch_labels"] = _r(b * 4)
-    p["batch_xn"] = _r(b * 4)
+    p["clampc"] = _r(4)
     nch = update_n_chunks(es, K, Dp, b, False)
     p["slab"] = _r(nch * K * Dp * 8)
     p["cnt_slab"] = _r(nch * K * 8)
     p["packed"] = _r((K * Dp + K + 3) * 8)
     p.update(_centroid_items(K, Dp, es, with_vcount=True))
-    if 0 < b <= SPLIT_MAX_ROWS:
-        p["split_keys"] = _r(b * 8)
+    if not resident and 0 < b <= SPLIT_MAX_ROWS:
+        p["split_keys"] = _r(b * 8)     # (gathered batches take the one-pass grid: no keys)
     m = min(n, init_rows or max(3 * b, 3 * K))
     tr = {"init": {"sample": _r(m * Dp * es), **_init_items(init, m, Dp, D, K, 0)},
           "predict": {"labels_out": _r(n * 4)}}

@@ -91,9 +91,11 @@ def test_plan_fit_choice():
 def test_minibatch_plan():
     p = M.plan_minibatch(125_000_000, 256, 512, "bfloat16", batch_rows=1 << 24)
     assert p.persistent["X"] == 64_000_000_000
-    assert p.persistent["batch"] == (1 << 24) * 256 * 2
+    # a resident shard is read in place through the step's int64 row list: no batch copy
+    assert p.persistent["rows"] == (1 << 24) * 8 and "batch" not in p.persistent
     h = M.plan_minibatch(10**9, 256, 512, "bfloat16", batch_rows=1 << 24, resident=False)
     assert "X" not in h.persistent and h.mode == "minibatch-host"
+    assert h.persistent["batch"] == (1 << 24) * 256 * 2 and "rows" not in h.persistent
 
 
 def test_budget_env_override(monkeypatch):
