@@ -136,8 +136,14 @@ __device__ __forceinline__ float sq16(const u32x4& w, float*) {
 // per score instead of the packed keys' 1.5); the row inside the winning tile is recovered
 // once per point after the loop by recomputing the winning tile's candidates on the
 // matrix cores (bitwise the main loop's scores), right after the chunk loop.
+// PERSIST: a grid of one workgroup per resident slot (occupancy x CUs) loops over the point
+// blocks (blk += gridDim.x).  Across a block boundary the centre ring keeps streaming (the
+// next pass's first chunk is issued at the last chunk's barrier of this one) and the next
+// block's fragments are loaded before this block's argmin epilogue, so their memory
+// latency hides under the epilogue instead of opening every workgroup's life; the inertia
+// and changed counts go to the slots once per workgroup.  Same scores, same labels.
 template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false,
-          bool VARG = false, int PMAJ = 0>
+          bool VARG = false, int PMAJ = 0, bool PERSIST = false>
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
@@ -162,9 +168,12 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   const uint32_t loff = (uint32_t)lane * 16u;
   const __amdgpu_buffer_rsrc_t rC = make_rsrc(a.Cpack, (uint32_t)a.Kpad * DPAD * sizeof(T));
   const __amdgpu_buffer_rsrc_t rN = make_rsrc(a.cn, (uint32_t)a.Kpad * 4u);
-  auto issue_chunk = [&](int c) {  // c: chunk index within this split (ring slot c % NBUF)
+  // Ring slots: chunk c of the workgroup's p-th pass sits in slot (p * ncl + c) % NBUF
+  // (ring = p * ncl); one pass per workgroup unless PERSIST.
+  int ring = 0;
+  auto issue_chunk = [&](int c, int slot) {  // c: chunk index within this split
     const uint32_t src = (uint32_t)(c0 + c) * C::CHUNK_BYTES;
-    char* dst = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
+    char* dst = bufs + slot * C::CHUNK_BYTES;
 #pragma unroll
     for (int i = 0; i < C::NPW; ++i) {
       const int pc = wid + i * C::NW;
@@ -172,7 +181,9 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     }
   };
 
-  const int64_t pbase = (int64_t)blockIdx.x * C::PTS + (int64_t)wid * (C::P * 16);
+  const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
+  int64_t blk = blockIdx.x;
+  int64_t pbase = blk * C::PTS + (int64_t)wid * (C::P * 16);
   u32x4 xr[C::P][C::NQ];
   float xnr[C::P];
   // The P blocks' fragment loads go out back to back: one memory round trip (two for a
@@ -192,389 +203,450 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       else xr[p][q] = u32x4{0u, 0u, 0u, 0u};
     }
   };
-  if (a.rows) {   // gathered batch: logical row -> X row
-    int64_t src[C::P];
+  auto load_block = [&]() {   // fragments (+ caller norms) of the block at pbase
+    if (a.rows) {   // gathered batch: logical row -> X row
+      int64_t src[C::P];
 #pragma unroll
-    for (int p = 0; p < C::P; ++p) src[p] = a.rows[row_of(p)];
-    __builtin_amdgcn_sched_barrier(0);   // all index loads in flight before the first use
+      for (int p = 0; p < C::P; ++p) src[p] = a.rows[row_of(p)];
+      __builtin_amdgcn_sched_barrier(0);   // all index loads in flight before the first use
 #pragma unroll
-    for (int p = 0; p < C::P; ++p) load_frags(p, src[p]);
-  } else {
-#pragma unroll
-    for (int p = 0; p < C::P; ++p) load_frags(p, row_of(p));
-  }
-  if (!EXACT && a.xn) {
-#pragma unroll
-    for (int p = 0; p < C::P; ++p) xnr[p] = a.xn[row_of(p)];
-  } else {
-#pragma unroll
-    for (int p = 0; p < C::P; ++p) xnr[p] = 0.f;
-  }
-  // |c|^2 and the first centre chunk by LDS-DMA, issued after the fragments so no wait for a
-  // fragment address (the gathered row indices) also waits for them
-  __builtin_amdgcn_sched_barrier(0);
-  for (int p = wid; p < cn_bytes / 1024; p += C::NW)
-    blds16(rN, (MK_LDS void*)(cn_lds + p * 1024), loff, (uint32_t)p * 1024u);
-  issue_chunk(0);
-  wait_vmcnt<0>();  // retire the fragments before the LDS-DMA loop (its vmcnt waits count chunks)
-  if (C::NBUF == 3 && ncl > 1) issue_chunk(1);
-
-  // bf16 seed offset (see the header): o = (1 + 2^-12) max |x|^2 over the workgroup's
-  // points, from the caller's row norms when given (loaded with the fragments) or from
-  // the fragments themselves, folded into this workgroup's LDS copy of |c|^2 once.
-  // A workgroup whose max |x|^2 exceeds 4x its min (an outlier row, or data around the
-  // origin) takes per-point offsets o_p = (1 + 2^-12) |x_p|^2 instead, parked in LDS and
-  // added to each tile's seed (second chunk-loop instantiation): a shared offset would coarsen every
-  // neighbour's keys to 2^-17 of the outlier's norm.  Either way a key resolves
-  // 2^-17 (|x - c|^2 + 3 |x|^2) or better.
-  float off = 0.f;
-  bool ppo = false;
-  float* opt = (float*)(bufs + C::NBUF * C::CHUNK_BYTES + 16 * C::NW);  // [NW][16][PP] offsets
-  float* xnl = opt + C::NW * 16 * C::PP;                                 // [NW][16][PP] |x|^2
-  if (!a.xn && (!EXACT || a.slots)) {
-#pragma unroll
-    for (int p = 0; p < C::P; ++p) {
-      float s = 0.f;
-#pragma unroll
-      for (int q = 0; q < C::NQ; ++q) s += sq16(xr[p][q], (T*)nullptr);
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      xnr[p] = s;
-    }
-    if (a.slots && g == 0) {   // no caller norms: the epilogue's inertia reads them back
-#pragma unroll
-      for (int p = 0; p < C::P; ++p) xnl[(wid * 16 + r) * C::PP + p] = xnr[p];
-    }
-  }
-  if constexpr (!EXACT) {
-    float m = 0.f, mn = 3.0e38f;
-#pragma unroll
-    for (int p = 0; p < C::P; ++p) { m = fmaxf(m, xnr[p]); mn = fminf(mn, xnr[p]); }
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      m = fmaxf(m, __shfl_xor(m, o, 64));
-      mn = fminf(mn, __shfl_xor(mn, o, 64));
-    }
-    float* red = (float*)(bufs + C::NBUF * C::CHUNK_BYTES);
-    if (lane == 0) { red[2 * wid] = m; red[2 * wid + 1] = mn; }
-    __syncthreads();  // (every wave's cn / chunk-0 DMA has landed: vmcnt(0) above)
-    float mnw = 3.0e38f;
-#pragma unroll
-    for (int w = 0; w < C::NW; ++w) { off = fmaxf(off, red[2 * w]); mnw = fminf(mnw, red[2 * w + 1]); }
-    ppo = __builtin_amdgcn_readfirstlane((int)(off > 4.f * mnw)) != 0;
-    if (!ppo) {
-      off = __builtin_fmaf(off, 2.44140625e-04f, off);  // * (1 + 2^-12)
-      off = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(off)));
-      for (int k = threadIdx.x; k < a.Kpad; k += C::NW * 64) ((float*)cn_lds)[k] += off;
+      for (int p = 0; p < C::P; ++p) load_frags(p, src[p]);
     } else {
-      off = 0.f;
-      if (g == 0) {
 #pragma unroll
-        for (int p = 0; p < C::P; ++p) opt[(wid * 16 + r) * C::PP + p] = __builtin_fmaf(xnr[p], 2.44140625e-04f, xnr[p]);
-      }
+      for (int p = 0; p < C::P; ++p) load_frags(p, row_of(p));
     }
-    // (published by the main loop's first wait_lgkm0 + barrier)
-  }
-
-  float best[C::P], seg_best[C::P];
-  int bg[C::P];
-  uint32_t vb[C::P], tb[C::P];   // VARG: running minimum (bits of a positive float), its tile
+    if (!EXACT && a.xn) {
 #pragma unroll
-  for (int p = 0; p < C::P; ++p) {
-    best[p] = 3.0e38f; seg_best[p] = 3.0e38f; bg[p] = 0;
-    vb[p] = 0x7f7fffffu; tb[p] = 0u;
-  }
-  const int ngrp = nch * C::CT;   // one past the last tile (global tile numbering)
-  const unsigned kmask = key6_mask();
-
-  // The chunk loop, instantiated twice: per-point offsets (PPO, outlier workgroups) seed a
-  // tile's accumulators with its points' offsets; the common instantiation has no such
-  // code at all -- a per-tile branch cost 1-3 % (one-process A/B against round 2).
-  auto chunk_loop = [&](auto ppo_tag) {
-    constexpr bool PPO = decltype(ppo_tag)::value;
-    for (int c = 0; c < ncl; ++c) {
-      // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
-      if (C::NBUF == 3 && c + 1 < ncl) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
-      wait_lgkm0();
-      raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
-      // (the next chunk's pieces all go out right after the barrier: spreading them one group
-      // per tile after that tile's epilogue measured -2.5 % at D=128, -5 % at D=256 and far
-      // slower at D=64, profiles/r3_28_ab_spread_dma.log)
-      if (c + C::NBUF - 1 < ncl) issue_chunk(c + C::NBUF - 1);
-      const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
-      // A fragments + |c|^2 of a tile from the LDS ring
-      auto load_a = [&](int tl_i, u32x4* aw_, f32x4& ci_) {
-        const int tile = (c0 + c) * C::CT + tl_i;
-        ci_ = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
-        const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
-  #pragma unroll
-        for (int q = 0; q < C::NQ; ++q) aw_[q] = *(const u32x4*)(tl + q * 1024);
-      };
-      // EARLY (bf16 D=64): the next tile's fragments are read right after this tile's
-      // MFMAs are issued, so their LDS latency hides under the argmin epilogue (+2 % at D=64
-      // in one-process A/B, profiles/r2_08_assign_clock_study.md; no gain at D=128)
-      constexpr bool EARLY = !EXACT && DPAD == 64;
-      u32x4 awe[C::NQ];
-      f32x4 cie;
-      if constexpr (EARLY) load_a(0, awe, cie);
-  #pragma unroll
-      for (int tl_i = 0; tl_i < C::CT; ++tl_i) {
-        const int tile = (c0 + c) * C::CT + tl_i;
-        u32x4 aw[C::NQ];
-        f32x4 ci;
-        if constexpr (EARLY) {
-  #pragma unroll
-          for (int q = 0; q < C::NQ; ++q) aw[q] = awe[q];
-          ci = cie;
-        } else {
-          load_a(tl_i, aw, ci);
-        }
-        f32x4 acc[C::P];
-  #pragma unroll
-        for (int p = 0; p < C::P; ++p) acc[p] = ci;
-        if constexpr (PPO) {  // per-point offsets seed the accumulators (one LDS read per tile)
-          // (added BEFORE the MFMAs: VALU writes the MFMA then reads as src C.  Adding them
-          // to the MFMA results instead raced the matrix pipe: a v_pk_add_f32 read the
-          // result registers early when the LDS read ahead of it returned fast, a rare,
-          // nondeterministic wrong label, tests/test_gpu_kernels.py split-batch test)
-          const float* o = opt + (wid * 16 + r) * C::PP;
-  #pragma unroll
-          for (int p4 = 0; p4 < C::P; p4 += 4) {
-            const f32x4 ov = *(const f32x4*)(o + p4);
-  #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (p4 + j < C::P) seed_add(acc[p4 + j], ov[j]);
-          }
-        }
-        // bf16: the wave issues its MFMAs at raised priority and drops back for the epilogue,
-        // so a SIMD's arbiter feeds the matrix core before another wave's argmin VALU work
-        // (profiles/r2_29_assign_setprio_ab.log, one process each: the harness copy -2.2 % at
-        // D=128 K=1024 and -1.4 % at D=64 K=4096; this kernel against that copy +0.8 % at D=128,
-        // +0.3 % at D=64, about +5 % at D=256 K=512)
-        if constexpr (!EXACT) {
-          __builtin_amdgcn_sched_barrier(0);
-          __builtin_amdgcn_s_setprio(1);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        // per-block argmin epilogue (bf16): packed 6-bit keys or the value-only running minimum
-        unsigned t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-        if constexpr (!EXACT && !VARG) {
-          // 6-bit keys over a segment of 16 tiles (tile-in-segment * 4 + reg): 4 key packs
-          // + 2 v_min3 per tile and point block; the running best is merged with its
-          // segment id once per segment.  The four indices as opaque SGPRs, so each key is
-          // one v_and_or_b32.
-          const unsigned tis = (unsigned)(tile & 15) << 2;
-          asm volatile("s_mov_b32 %0, %4\n\ts_or_b32 %1, %4, 1\n\ts_or_b32 %2, %4, 2\n\ts_or_b32 %3, %4, 3"
-                       : "=s"(t0), "=s"(t1), "=s"(t2), "=s"(t3) : "s"(tis) : "scc");  // s_or_b32 writes SCC
-        }
-        auto epi = [&](int p) {
-          if constexpr (VARG) {
-            // scores are positive (seed offset, see the header), so they order as their bits;
-            // a tie with the running minimum keeps the earlier tile (the lower index)
-            const uint32_t u0 = __float_as_uint(acc[p][0]), u1 = __float_as_uint(acc[p][1]);
-            const uint32_t u2 = __float_as_uint(acc[p][2]), u3 = __float_as_uint(acc[p][3]);
-            const uint32_t nb = min(min(u0, u1), min(u2, min(u3, vb[p])));
-            tb[p] = nb != vb[p] ? (uint32_t)tile : tb[p];
-            vb[p] = nb;
-          } else {
-            const f32x4& sv = acc[p];
-            const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
-            const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
-            seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
-          }
-        };
-        auto chain = [&](int p) {   // block p's NQ MFMAs back to back (srcC = the previous vDst)
-  #pragma unroll
-          for (int q = 0; q < C::NQ; ++q) {
-            acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        };
-        if constexpr (PMAJ) {
-          // point-block-major issue, pinned in this order
+      for (int p = 0; p < C::P; ++p) xnr[p] = a.xn[row_of(p)];
+    } else {
 #pragma unroll
-          for (int p = 0; p < C::P; ++p) chain(p);
-        } else {
-#pragma unroll
-          for (int q = 0; q < C::NQ; ++q) {
-#pragma unroll
-            for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
-          }
-        }
-        if constexpr (!EXACT) {
-          __builtin_amdgcn_sched_barrier(0);
-          __builtin_amdgcn_s_setprio(0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (EARLY) {
-          if (tl_i + 1 < C::CT) load_a(tl_i + 1, awe, cie);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (EXACT) {
-          // (tile*4 + reg) as wave-uniform values: the index select needs no VALU add
-          const int u = tile * 4;
-#pragma unroll
-          for (int p = 0; p < C::P; ++p) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const bool lt = acc[p][e] < best[p];
-              best[p] = lt ? acc[p][e] : best[p];
-              bg[p] = lt ? u + e : bg[p];
-            }
-          }
-        } else {
-#pragma unroll
-          for (int p = 0; p < C::P; ++p) epi(p);
-        }
-        if constexpr (!EXACT && !VARG) {
-          if ((tile & 15) == 15 || tile == ngrp - 1) {
-  #pragma unroll
-            for (int p = 0; p < C::P; ++p) {
-              // compare values only: on equal (truncated) values the earlier segment keeps
-              // the lower centroid index (all keys are >= 0, see the header)
-              const float sv = __uint_as_float(__float_as_uint(seg_best[p]) & ~63u);
-              const float bv = __uint_as_float(__float_as_uint(best[p]) & ~63u);
-              if (sv < bv) { best[p] = seg_best[p]; bg[p] = tile >> 4; }
-              seg_best[p] = 3.0e38f;
-            }
-          }
-        }
-      }
+      for (int p = 0; p < C::P; ++p) xnr[p] = 0.f;
     }
   };
-  if (ppo) chunk_loop(std::true_type{});
-  else chunk_loop(std::false_type{});
+  load_block();
+  // per-wave (inertia, changed) totals over the workgroup's passes, in LDS after the offsets
+  double* wacc = (double*)(bufs + C::NBUF * C::CHUNK_BYTES + 16 * C::NW + C::OPT_BYTES);
+  for (bool first = true;; first = false) {
+    // |c|^2 and the first centre chunk by LDS-DMA, issued after the fragments so no wait for a
+    // fragment address (the gathered row indices) also waits for them.  (PERSIST: after the
+    // first pass the chunk is already in flight, issued at the previous pass's last barrier.)
+    __builtin_amdgcn_sched_barrier(0);
+    for (int p = wid; p < cn_bytes / 1024; p += C::NW)
+      blds16(rN, (MK_LDS void*)(cn_lds + p * 1024), loff, (uint32_t)p * 1024u);
+    if (!PERSIST || first) issue_chunk(0, ring % C::NBUF);
+    wait_vmcnt<0>();  // retire the fragments before the LDS-DMA loop (its vmcnt waits count chunks)
+    if (C::NBUF == 3 && ncl > 1) issue_chunk(1, (ring + 1) % C::NBUF);
+    const int64_t nxt = blk + (int64_t)gridDim.x;
+    const bool has_next = PERSIST && nxt < nblk;   // (wave-uniform)
 
-  // VARG: merge the 4 lane groups of each point on (value, tile, group) -- the centre index
-  // 16 t + 4 g + e orders like that triple -- then recover e: for the points 4m..4m+3 the
-  // 16 A rows carry the 4 candidates of each (row 4g'+e = candidate e of point 4m+g'), so
-  // lane (r = 4m+g, g) receives its own point's 4 candidate scores, computed exactly as in
-  // the main loop (same packed -2c, same seed from the LDS |c|^2 copy, same k-step order),
-  // and takes the first that equals the minimum.  4 MFMA groups per point block: 64/K of
-  // the main loop's matrix work.
-  uint32_t kv[C::P];
-  if constexpr (VARG) {
+    // bf16 seed offset (see the header): o = (1 + 2^-12) max |x|^2 over the workgroup's
+    // points, from the caller's row norms when given (loaded with the fragments) or from
+    // the fragments themselves, folded into this workgroup's LDS copy of |c|^2 once.
+    // A workgroup whose max |x|^2 exceeds 4x its min (an outlier row, or data around the
+    // origin) takes per-point offsets o_p = (1 + 2^-12) |x_p|^2 instead, parked in LDS and
+    // added to each tile's seed (second chunk-loop instantiation): a shared offset would coarsen every
+    // neighbour's keys to 2^-17 of the outlier's norm.  Either way a key resolves
+    // 2^-17 (|x - c|^2 + 3 |x|^2) or better.
+    float off = 0.f;
+    bool ppo = false;
+    float* opt = (float*)(bufs + C::NBUF * C::CHUNK_BYTES + 16 * C::NW);  // [NW][16][PP] offsets
+    float* xnl = opt + C::NW * 16 * C::PP;                                 // [NW][16][PP] |x|^2
+    if (!a.xn && (!EXACT || a.slots)) {
 #pragma unroll
-    for (int p = 0; p < C::P; ++p) {
-      uint32_t v = vb[p], tg = tb[p] * 4u + (uint32_t)g;
+      for (int p = 0; p < C::P; ++p) {
+        float s = 0.f;
 #pragma unroll
-      for (int o = 16; o <= 32; o <<= 1) {
-        const uint32_t vo = (uint32_t)__shfl_xor((int)v, o, 64), to = (uint32_t)__shfl_xor((int)tg, o, 64);
-        if (vo < v || (vo == v && to < tg)) { v = vo; tg = to; }
+        for (int q = 0; q < C::NQ; ++q) s += sq16(xr[p][q], (T*)nullptr);
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        xnr[p] = s;
       }
-      vb[p] = v;
-      tb[p] = tg;
-    }
-    const T* pack = (const T*)a.Cpack;
-    int efound[C::P];
+      if (a.slots && g == 0) {   // no caller norms: the epilogue's inertia reads them back
 #pragma unroll
-    for (int p = 0; p < C::P; ++p) efound[p] = 0;
+        for (int p = 0; p < C::P; ++p) xnl[(wid * 16 + r) * C::PP + p] = xnr[p];
+      }
+    }
+    if constexpr (!EXACT) {
+      float m = 0.f, mn = 3.0e38f;
+#pragma unroll
+      for (int p = 0; p < C::P; ++p) { m = fmaxf(m, xnr[p]); mn = fminf(mn, xnr[p]); }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        m = fmaxf(m, __shfl_xor(m, o, 64));
+        mn = fminf(mn, __shfl_xor(mn, o, 64));
+      }
+      float* red = (float*)(bufs + C::NBUF * C::CHUNK_BYTES);
+      if (lane == 0) { red[2 * wid] = m; red[2 * wid + 1] = mn; }
+      __syncthreads();  // (every wave's cn / chunk-0 DMA has landed: vmcnt(0) above)
+      float mnw = 3.0e38f;
+#pragma unroll
+      for (int w = 0; w < C::NW; ++w) { off = fmaxf(off, red[2 * w]); mnw = fminf(mnw, red[2 * w + 1]); }
+      ppo = __builtin_amdgcn_readfirstlane((int)(off > 4.f * mnw)) != 0;
+      if (!ppo) {
+        off = __builtin_fmaf(off, 2.44140625e-04f, off);  // * (1 + 2^-12)
+        off = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(off)));
+        for (int k = threadIdx.x; k < a.Kpad; k += C::NW * 64) ((float*)cn_lds)[k] += off;
+      } else {
+        off = 0.f;
+        if (g == 0) {
+#pragma unroll
+          for (int p = 0; p < C::P; ++p) opt[(wid * 16 + r) * C::PP + p] = __builtin_fmaf(xnr[p], 2.44140625e-04f, xnr[p]);
+        }
+      }
+      // (published by the main loop's first wait_lgkm0 + barrier)
+    }
+
+    float best[C::P], seg_best[C::P];
+    int bg[C::P];
+    uint32_t vb[C::P], tb[C::P];   // VARG: running minimum (bits of a positive float), its tile
 #pragma unroll
     for (int p = 0; p < C::P; ++p) {
-      // MG candidate groups in flight at once (registers: MG * NQ fragments)
-      constexpr int MG = C::NQ <= 2 ? 4 : 1;
+      best[p] = 3.0e38f; seg_best[p] = 3.0e38f; bg[p] = 0;
+      vb[p] = 0x7f7fffffu; tb[p] = 0u;
+    }
+    const int ngrp = nch * C::CT;   // one past the last tile (global tile numbering)
+    const unsigned kmask = key6_mask();
+
+    // The chunk loop, instantiated twice: per-point offsets (PPO, outlier workgroups) seed a
+    // tile's accumulators with its points' offsets; the common instantiation has no such
+    // code at all -- a per-tile branch cost 1-3 % (one-process A/B against round 2).
+    auto chunk_loop = [&](auto ppo_tag) {
+      constexpr bool PPO = decltype(ppo_tag)::value;
+      for (int c = 0; c < ncl; ++c) {
+        // chunk c landed; with 3 slots chunk c+1 may stay in flight across the barrier
+        if (C::NBUF == 3 && c + 1 < ncl) wait_vmcnt<C::NPW>(); else wait_vmcnt<0>();
+        wait_lgkm0();
+        raw_barrier();  // RAW for chunk c, WAR for the slot refilled next (read at c-1)
+        // (the next chunk's pieces all go out right after the barrier: spreading them one group
+        // per tile after that tile's epilogue measured -2.5 % at D=128, -5 % at D=256 and far
+        // slower at D=64, profiles/r3_28_ab_spread_dma.log)
+        if (c + C::NBUF - 1 < ncl) issue_chunk(c + C::NBUF - 1, (ring + c + C::NBUF - 1) % C::NBUF);
+        else if (has_next && c + C::NBUF - 1 == ncl) issue_chunk(0, (ring + ncl) % C::NBUF);  // next pass
+        const char* buf = bufs + ((ring + c) % C::NBUF) * C::CHUNK_BYTES;
+        // A fragments + |c|^2 of a tile from the LDS ring
+        auto load_a = [&](int tl_i, u32x4* aw_, f32x4& ci_) {
+          const int tile = (c0 + c) * C::CT + tl_i;
+          ci_ = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
+          const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
+    #pragma unroll
+          for (int q = 0; q < C::NQ; ++q) aw_[q] = *(const u32x4*)(tl + q * 1024);
+        };
+        // EARLY (bf16 D=64): the next tile's fragments are read right after this tile's
+        // MFMAs are issued, so their LDS latency hides under the argmin epilogue (+2 % at D=64
+        // in one-process A/B, profiles/r2_08_assign_clock_study.md; no gain at D=128)
+        constexpr bool EARLY = !EXACT && DPAD == 64;
+        u32x4 awe[C::NQ];
+        f32x4 cie;
+        if constexpr (EARLY) load_a(0, awe, cie);
+    #pragma unroll
+        for (int tl_i = 0; tl_i < C::CT; ++tl_i) {
+          const int tile = (c0 + c) * C::CT + tl_i;
+          u32x4 aw[C::NQ];
+          f32x4 ci;
+          if constexpr (EARLY) {
+    #pragma unroll
+            for (int q = 0; q < C::NQ; ++q) aw[q] = awe[q];
+            ci = cie;
+          } else {
+            load_a(tl_i, aw, ci);
+          }
+          f32x4 acc[C::P];
+    #pragma unroll
+          for (int p = 0; p < C::P; ++p) acc[p] = ci;
+          if constexpr (PPO) {  // per-point offsets seed the accumulators (one LDS read per tile)
+            // (added BEFORE the MFMAs: VALU writes the MFMA then reads as src C.  Adding them
+            // to the MFMA results instead raced the matrix pipe: a v_pk_add_f32 read the
+            // result registers early when the LDS read ahead of it returned fast, a rare,
+            // nondeterministic wrong label, tests/test_gpu_kernels.py split-batch test)
+            const float* o = opt + (wid * 16 + r) * C::PP;
+    #pragma unroll
+            for (int p4 = 0; p4 < C::P; p4 += 4) {
+              const f32x4 ov = *(const f32x4*)(o + p4);
+    #pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (p4 + j < C::P) seed_add(acc[p4 + j], ov[j]);
+            }
+          }
+          // bf16: the wave issues its MFMAs at raised priority and drops back for the epilogue,
+          // so a SIMD's arbiter feeds the matrix core before another wave's argmin VALU work
+          // (profiles/r2_29_assign_setprio_ab.log, one process each: the harness copy -2.2 % at
+          // D=128 K=1024 and -1.4 % at D=64 K=4096; this kernel against that copy +0.8 % at D=128,
+          // +0.3 % at D=64, about +5 % at D=256 K=512)
+          if constexpr (!EXACT) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          // per-block argmin epilogue (bf16): packed 6-bit keys or the value-only running minimum
+          unsigned t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+          if constexpr (!EXACT && !VARG) {
+            // 6-bit keys over a segment of 16 tiles (tile-in-segment * 4 + reg): 4 key packs
+            // + 2 v_min3 per tile and point block; the running best is merged with its
+            // segment id once per segment.  The four indices as opaque SGPRs, so each key is
+            // one v_and_or_b32.
+            const unsigned tis = (unsigned)(tile & 15) << 2;
+            asm volatile("s_mov_b32 %0, %4\n\ts_or_b32 %1, %4, 1\n\ts_or_b32 %2, %4, 2\n\ts_or_b32 %3, %4, 3"
+                         : "=s"(t0), "=s"(t1), "=s"(t2), "=s"(t3) : "s"(tis) : "scc");  // s_or_b32 writes SCC
+          }
+          auto epi = [&](int p) {
+            if constexpr (VARG) {
+              // scores are positive (seed offset, see the header), so they order as their bits;
+              // a tie with the running minimum keeps the earlier tile (the lower index)
+              const uint32_t u0 = __float_as_uint(acc[p][0]), u1 = __float_as_uint(acc[p][1]);
+              const uint32_t u2 = __float_as_uint(acc[p][2]), u3 = __float_as_uint(acc[p][3]);
+              const uint32_t nb = min(min(u0, u1), min(u2, min(u3, vb[p])));
+              tb[p] = nb != vb[p] ? (uint32_t)tile : tb[p];
+              vb[p] = nb;
+            } else {
+              const f32x4& sv = acc[p];
+              const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
+              const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
+              seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
+            }
+          };
+          auto chain = [&](int p) {   // block p's NQ MFMAs back to back (srcC = the previous vDst)
+    #pragma unroll
+            for (int q = 0; q < C::NQ; ++q) {
+              acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          };
+          if constexpr (PMAJ) {
+            // point-block-major issue, pinned in this order
 #pragma unroll
-      for (int m0 = 0; m0 < 4; m0 += MG) {
-        u32x4 aw[MG][C::NQ];
-        f32x4 acc[MG];
+            for (int p = 0; p < C::P; ++p) chain(p);
+          } else {
 #pragma unroll
-        for (int mi = 0; mi < MG; ++mi) {
-          const int m = m0 + mi;
-          const uint32_t tga = (uint32_t)__shfl((int)tb[p], 4 * m + (r >> 2), 64);
-          const int ca = (int)(tga >> 2) * 16 + (int)(tga & 3u) * 4 + (r & 3);   // A row r's centre
-          const T* src = pack + ((int64_t)(ca >> 4) * C::NQ * 64 + (ca & 15) + 16 * g) * C::V;
+            for (int q = 0; q < C::NQ; ++q) {
 #pragma unroll
-          for (int q = 0; q < C::NQ; ++q) aw[mi][q] = *(const u32x4*)(src + (int64_t)q * 64 * C::V);
-          const uint32_t tgs = (uint32_t)__shfl((int)tb[p], 4 * m + g, 64);     // output rows' point
-          acc[mi] = *(const f32x4*)(cn_lds + ((int)(tgs >> 2) * 16 + (int)(tgs & 3u) * 4) * 4);
-          if (ppo) {
-            seed_add(acc[mi], opt[(wid * 16 + r) * C::PP + p]);
+              for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
+            }
+          }
+          if constexpr (!EXACT) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if constexpr (EARLY) {
+            if (tl_i + 1 < C::CT) load_a(tl_i + 1, awe, cie);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if constexpr (EXACT) {
+            // (tile*4 + reg) as wave-uniform values: the index select needs no VALU add
+            const int u = tile * 4;
+#pragma unroll
+            for (int p = 0; p < C::P; ++p) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const bool lt = acc[p][e] < best[p];
+                best[p] = lt ? acc[p][e] : best[p];
+                bg[p] = lt ? u + e : bg[p];
+              }
+            }
+          } else {
+#pragma unroll
+            for (int p = 0; p < C::P; ++p) epi(p);
+          }
+          if constexpr (!EXACT && !VARG) {
+            if ((tile & 15) == 15 || tile == ngrp - 1) {
+    #pragma unroll
+              for (int p = 0; p < C::P; ++p) {
+                // compare values only: on equal (truncated) values the earlier segment keeps
+                // the lower centroid index (all keys are >= 0, see the header)
+                const float sv = __uint_as_float(__float_as_uint(seg_best[p]) & ~63u);
+                const float bv = __uint_as_float(__float_as_uint(best[p]) & ~63u);
+                if (sv < bv) { best[p] = seg_best[p]; bg[p] = tile >> 4; }
+                seg_best[p] = 3.0e38f;
+              }
+            }
           }
         }
+      }
+    };
+    if (ppo) chunk_loop(std::true_type{});
+    else chunk_loop(std::false_type{});
+
+    // VARG: merge the 4 lane groups of each point on (value, tile, group) -- the centre index
+    // 16 t + 4 g + e orders like that triple -- then recover e: for the points 4m..4m+3 the
+    // 16 A rows carry the 4 candidates of each (row 4g'+e = candidate e of point 4m+g'), so
+    // lane (r = 4m+g, g) receives its own point's 4 candidate scores, computed exactly as in
+    // the main loop (same packed -2c, same seed from the LDS |c|^2 copy, same k-step order),
+    // and takes the first that equals the minimum.  4 MFMA groups per point block: 64/K of
+    // the main loop's matrix work.
+    uint32_t kv[C::P];
+    if constexpr (VARG) {
 #pragma unroll
-        for (int mi = 0; mi < MG; ++mi) {
+      for (int p = 0; p < C::P; ++p) {
+        uint32_t v = vb[p], tg = tb[p] * 4u + (uint32_t)g;
 #pragma unroll
-          for (int q = 0; q < C::NQ; ++q) acc[mi] = Mfma16<T>::run(aw[mi][q], xr[p][q], acc[mi]);
+        for (int o = 16; o <= 32; o <<= 1) {
+          const uint32_t vo = (uint32_t)__shfl_xor((int)v, o, 64), to = (uint32_t)__shfl_xor((int)tg, o, 64);
+          if (vo < v || (vo == v && to < tg)) { v = vo; tg = to; }
         }
+        vb[p] = v;
+        tb[p] = tg;
+      }
+      const T* pack = (const T*)a.Cpack;
+      int efound[C::P];
 #pragma unroll
-        for (int mi = 0; mi < MG; ++mi) {
-          if (r == 4 * (m0 + mi) + g) {
-            int e = 3;
+      for (int p = 0; p < C::P; ++p) efound[p] = 0;
 #pragma unroll
-            for (int j = 2; j >= 0; --j) e = __float_as_uint(acc[mi][j]) == vb[p] ? j : e;
-            efound[p] = e;
+      for (int p = 0; p < C::P; ++p) {
+        // MG candidate groups in flight at once (registers: MG * NQ fragments)
+        constexpr int MG = C::NQ <= 2 ? 4 : 1;
+#pragma unroll
+        for (int m0 = 0; m0 < 4; m0 += MG) {
+          u32x4 aw[MG][C::NQ];
+          f32x4 acc[MG];
+#pragma unroll
+          for (int mi = 0; mi < MG; ++mi) {
+            const int m = m0 + mi;
+            const uint32_t tga = (uint32_t)__shfl((int)tb[p], 4 * m + (r >> 2), 64);
+            const int ca = (int)(tga >> 2) * 16 + (int)(tga & 3u) * 4 + (r & 3);   // A row r's centre
+            const T* src = pack + ((int64_t)(ca >> 4) * C::NQ * 64 + (ca & 15) + 16 * g) * C::V;
+#pragma unroll
+            for (int q = 0; q < C::NQ; ++q) aw[mi][q] = *(const u32x4*)(src + (int64_t)q * 64 * C::V);
+            const uint32_t tgs = (uint32_t)__shfl((int)tb[p], 4 * m + g, 64);     // output rows' point
+            acc[mi] = *(const f32x4*)(cn_lds + ((int)(tgs >> 2) * 16 + (int)(tgs & 3u) * 4) * 4);
+            if (ppo) {
+              seed_add(acc[mi], opt[(wid * 16 + r) * C::PP + p]);
+            }
+          }
+#pragma unroll
+          for (int mi = 0; mi < MG; ++mi) {
+#pragma unroll
+            for (int q = 0; q < C::NQ; ++q) acc[mi] = Mfma16<T>::run(aw[mi][q], xr[p][q], acc[mi]);
+          }
+#pragma unroll
+          for (int mi = 0; mi < MG; ++mi) {
+            if (r == 4 * (m0 + mi) + g) {
+              int e = 3;
+#pragma unroll
+              for (int j = 2; j >= 0; --j) e = __float_as_uint(acc[mi][j]) == vb[p] ? j : e;
+              efound[p] = e;
+            }
           }
         }
       }
-    }
 #pragma unroll
-    for (int p = 0; p < C::P; ++p) {
-      const int e = __shfl(efound[p], r + 16 * (r & 3), 64);
-      kv[p] = (tb[p] >> 2) * 16u + (tb[p] & 3u) * 4u + (uint32_t)e;
+      for (int p = 0; p < C::P; ++p) {
+        const int e = __shfl(efound[p], r + 16 * (r & 3), 64);
+        kv[p] = (tb[p] >> 2) * 16u + (tb[p] & 3u) * 4u + (uint32_t)e;
+      }
     }
-  }
 
-  float inert = 0.f;
-  int changed = 0;
+    // The block's label epilogue.  Per point: the winning (score, centre) with the 4 lane
+    // groups merged, then the label / distance stores and the inertia.
+    auto merged = [&](int p, int& k, float& v) {
+      if constexpr (VARG) {  // merged and recovered above
+        k = (int)kv[p];
+        v = __uint_as_float(vb[p]);
+      } else {
+        if constexpr (EXACT) {  // bg = tile * 4 + reg of the first strict minimum
+          k = (bg[p] >> 2) * 16 + 4 * g + (bg[p] & 3);
+          v = best[p];
+        } else {               // bg = segment of 16 tiles, 6-bit key; undo the seed offset
+          const unsigned bits = __float_as_uint(best[p]);
+          const int idx = (int)(bits & 63u);
+          k = (bg[p] * 16 + (idx >> 2)) * 16 + 4 * g + (idx & 3);
+          v = __uint_as_float(bits & ~63u);
+        }
 #pragma unroll
-  for (int p = 0; p < C::P; ++p) {
-    int k;
-    float v;
-    if constexpr (VARG) {  // merged and recovered above
-      k = (int)kv[p];
-      v = __uint_as_float(vb[p]);
-    } else {
-      if constexpr (EXACT) {  // bg = tile * 4 + reg of the first strict minimum
-        k = (bg[p] >> 2) * 16 + 4 * g + (bg[p] & 3);
-        v = best[p];
-      } else {               // bg = segment of 16 tiles, 6-bit key; undo the seed offset
-        const unsigned bits = __float_as_uint(best[p]);
-        const int idx = (int)(bits & 63u);
-        k = (bg[p] * 16 + (idx >> 2)) * 16 + 4 * g + (idx & 3);
-        v = __uint_as_float(bits & ~63u);
+        for (int o = 16; o <= 32; o <<= 1) {
+          const float vo = __shfl_xor(v, o, 64);
+          const int ko = __shfl_xor(k, o, 64);
+          if (vo < v || (vo == v && ko < k)) { v = vo; k = ko; }
+        }
       }
-#pragma unroll
-      for (int o = 16; o <= 32; o <<= 1) {
-        const float vo = __shfl_xor(v, o, 64);
-        const int ko = __shfl_xor(k, o, 64);
-        if (vo < v || (vo == v && ko < k)) { v = vo; k = ko; }
-      }
-    }
-    // this point's seed offset (0 for f32)
-    const float offp = ppo ? opt[(wid * 16 + r) * C::PP + p] : off;
-    // inertia without caller norms: the prologue parked |x|^2 of the fragments in LDS
-    const float xv = (a.slots && !a.xn) ? xnl[(wid * 16 + r) * C::PP + p] : 0.f;
-    if ((p & 3) == g) {
-      const int64_t i = pbase + p * 16 + r;
+    };
+    float inert = 0.f;
+    int changed = 0;
+    const int64_t pcur = pbase;
+    // ``old``: the row's previous label, ``xnv``: its caller norm (read by the caller of
+    // this lambda, i < N, lanes with (p & 3) == g only)
+    auto store = [&](int p, int k, float v, int old, float xnv) {
+      const float offp = ppo ? opt[(wid * 16 + r) * C::PP + p] : off;   // the seed offset (0: f32)
+      // inertia without caller norms: the prologue parked |x|^2 of the fragments in LDS
+      const float xv = (a.slots && !a.xn) ? xnl[(wid * 16 + r) * C::PP + p] : xnv;
+      const int64_t i = pcur + p * 16 + r;
       if (a.split_keys) {
         // compare the (positive) keys across splits; split_finish undoes the offset
         // (parked in mind[], which the caller provides whenever xn is given)
-        if (i < a.N) {
-          atomicMin(a.split_keys + i, split_key(v, k));
-          if (a.mind) a.mind[i] = offp;
-        }
-      } else if (i < a.N) {
+        atomicMin(a.split_keys + i, split_key(v, k));
+        if (a.mind) a.mind[i] = offp;
+      } else {
         v -= offp;   // back to |c|^2 - 2 x.c
-        if (a.track_changed) changed += (a.labels[i] != k);
+        if (a.track_changed) changed += (old != k);
         a.labels[i] = k;
         if (a.xn || a.slots) {
-          const float d = fmaxf((a.xn ? a.xn[i] : xv) + v, 0.f);
+          const float d = fmaxf(xv + v, 0.f);
           inert += d;
           if (a.mind) a.mind[i] = d;
         }
       }
+    };
+    if constexpr (!PERSIST) {
+#pragma unroll
+      for (int p = 0; p < C::P; ++p) {
+        int k;
+        float v;
+        merged(p, k, v);
+        const int64_t i = pcur + p * 16 + r;
+        if ((p & 3) == g && i < a.N) {
+          const bool rd = !a.split_keys;
+          store(p, k, v, rd && a.track_changed ? a.labels[i] : -2, rd && a.xn ? a.xn[i] : 0.f);
+        }
+      }
+    } else {
+      // merge every block first (frees the running keys), then this block's global reads,
+      // then the next block's fragments -- after those reads, so neither waits on the
+      // other's round trip (vmcnt retires in order) -- whose latency hides under the stores
+      int kk[C::P], oldl[C::P];
+      float vv[C::P], xg[C::P];
+#pragma unroll
+      for (int p = 0; p < C::P; ++p) merged(p, kk[p], vv[p]);
+#pragma unroll
+      for (int p = 0; p < C::P; ++p) {
+        const int64_t i = pcur + p * 16 + r;
+        const bool mine = (p & 3) == g && i < a.N;
+        oldl[p] = mine && a.track_changed ? a.labels[i] : -2;
+        xg[p] = mine && a.xn ? a.xn[i] : 0.f;
+      }
+      if (has_next) {
+        __builtin_amdgcn_sched_barrier(0);
+        blk = nxt;
+        pbase = blk * C::PTS + (int64_t)wid * (C::P * 16);
+        load_block();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int p = 0; p < C::P; ++p)
+        if ((p & 3) == g && pcur + p * 16 + r < a.N) store(p, kk[p], vv[p], oldl[p], xg[p]);
     }
-  }
+    if (a.slots && !a.split_keys) {
+      // this pass's wave totals; over several passes (PERSIST) they accumulate in this
+      // wave's LDS slot, so no register stays live across the chunk loop
+      const double di = wave_sum((double)inert);
+      const int dc = wave_sum(changed);
+      if (lane == 0) {
+        wacc[2 * wid] = (PERSIST && !first) ? wacc[2 * wid] + di : di;
+        wacc[2 * wid + 1] = (PERSIST && !first) ? wacc[2 * wid + 1] + (double)dc : (double)dc;
+      }
+    }
+    if (!has_next) break;
+    // (PERSIST) every wave is past its last reads of this pass's |c|^2 copy, offsets and slot
+    // scratch before the next prologue rewrites them; a raw barrier, so the next block's
+    // fragments and first chunk stay in flight (__syncthreads would drain vmcnt)
+    wait_lgkm0();
+    raw_barrier();
+    ring += ncl;
+  }  // block loop
   if (a.slots && !a.split_keys) {
-    double di = wave_sum((double)inert);
-    int dc = wave_sum(changed);
-    double* red = (double*)(bufs + C::NBUF * C::CHUNK_BYTES);
-    if (lane == 0) { red[2 * wid] = di; red[2 * wid + 1] = (double)dc; }
     __syncthreads();
     if (threadIdx.x == 0) {
       double si = 0, sc = 0;
 #pragma unroll
-      for (int w = 0; w < C::NW; ++w) { si += red[2 * w]; sc += red[2 * w + 1]; }
+      for (int w = 0; w < C::NW; ++w) { si += wacc[2 * w]; sc += wacc[2 * w + 1]; }
       double* slot = a.slots + (blockIdx.x % NSLOT) * SLOT_STRIDE;
       atomicAdd(slot + 0, si);
       atomicAdd(slot + 1, sc);
@@ -633,13 +705,13 @@ static int assign16_splits(int64_t nblk, int nch) {
 // D=64 K=2048 +8.5 %, K=1024 -3.7 %; D=32 K=1024 +5.6 %, K=512 -8.8 %).
 // Variant V_ASSIGN_VARG = 0/1 forces it off / on (A/B, tests).
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST>
 static void set_lds_attr() {
   static bool done = false;
   if (done) return;
-  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ>,
+  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ>,
+  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   done = true;
 }
@@ -658,13 +730,42 @@ static void set_lds_attr() {
 // blocks' MFMA chains instead measured -1.1 % at D=128, -3.8 % at D=64 K=4096, +2.2 % at D=64
 // K=1024 (profiles/r3_23_ab_pmaj_interleaved.log) and is not built.
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ>
-static void launch16_kp(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ>();
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST>
+static void launch16_kpp(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
+  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST>();
   if (b.D == DPAD)
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ>), grid, dim3(NW_ * 64), lds, s, b);
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST>), grid,
+                       dim3(NW_ * 64), lds, s, b);
   else
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ>), grid, dim3(NW_ * 64), lds, s, b);
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST>), grid,
+                       dim3(NW_ * 64), lds, s, b);
+}
+
+// Resident workgroups the whole chip holds for a launch geometry: the smaller of the
+// wave-slot and the LDS limit per CU, times the CU count (the persistent grid).
+static int64_t resident_workgroups(int waves_per_wg, int occ_per_simd, size_t lds) {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    return n;
+  }();
+  const int by_waves = (4 * occ_per_simd) / waves_per_wg;
+  const int by_lds = lds ? (int)((160 * 1024) / lds) : by_waves;
+  const int per_cu = by_waves < by_lds ? by_waves : by_lds;
+  return (int64_t)(per_cu > 0 ? per_cu : 1) * cus;
+}
+
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ>
+static void launch16_kp(const AssignArgs& b, dim3 grid, size_t lds, hipStream_t s) {
+  // Persistent grid (variant V_ASSIGN_PERSIST = 1; default off): one-pass grids only (no
+  // centre split), and only where the point blocks outnumber the resident slots.
+  const int64_t slots = resident_workgroups(NW_, OCC, lds);
+  if (variant(V_ASSIGN_PERSIST) > 0 && grid.y == 1 && (int64_t)grid.x > slots) {
+    grid.x = (unsigned)slots;
+    return launch16_kpp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, true>(b, grid, lds, s);
+  }
+  launch16_kpp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, false>(b, grid, lds, s);
 }
 
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG>
@@ -680,8 +781,8 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   if (a.Kpad % (16 * C::CT) != 0) return hipErrorInvalidValue;
   const int cn_bytes = ((a.Kpad * 4 + 1023) / 1024) * 1024;
-  // + min/max / slot scratch + per-point offsets
-  const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW + C::OPT_BYTES;
+  // + min/max scratch + per-point offsets + per-wave slot totals
+  const size_t lds = cn_bytes + C::NBUF * C::CHUNK_BYTES + 16 * C::NW + C::OPT_BYTES + 16 * C::NW;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
   if (nblk <= 0) return hipSuccess;
@@ -742,6 +843,7 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
     if (gm == 1 && a.Kpad % (16 * 8) == 0) return launch16_t<T, DPAD, P, 8, 2, OCC, 8>(a, s);
     if (gm == 2) return launch16_t<T, DPAD, P, CT, 2, OCC, 8>(a, s);
     if (gm == 3) return launch16_t<T, DPAD, 6, CT, 2, 3>(a, s);   // 6 point blocks at 3 waves/SIMD
+    if (gm == 4) return launch16_t<T, DPAD, 8, CT, 2, 2>(a, s);   // 8 point blocks at 2 waves/SIMD (half the LDS reads)
   }
   return launch16_t<T, DPAD, P, CT, 2, OCC>(a, s);
 }

@@ -506,7 +506,8 @@ namespace mk {
 // The A/B switch registry (kernels.h): environment read once at load, then set_variant only.
 static const char* const kVariantEnv[V_COUNT] = {"MIKMEANS_ASSIGN_VARG", "MIKMEANS_ASSIGN_PMAJ",
                                                  "MIKMEANS_ASSIGN_GEOM", "MIKMEANS_UPDATE_KS",
-                                                 "MIKMEANS_UPDATE_KS_GM", "MIKMEANS_BLOBS_TPR"};
+                                                 "MIKMEANS_UPDATE_KS_GM", "MIKMEANS_BLOBS_TPR",
+                                                 "MIKMEANS_ASSIGN_PERSIST"};
 static int* variant_table() {
   static int t[V_COUNT] = {};
   static const bool init = [] {

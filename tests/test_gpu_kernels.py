@@ -785,3 +785,43 @@ def test_overlapped_segments_match_plain_step(native, n, segments):
         torch.cuda.synchronize()
         assert torch.equal(ea.centers, eb.centers) and torch.equal(ea.labels, eb.labels)
         assert ea.last_stats().n_changed == eb.last_stats().n_changed
+
+
+@pytest.mark.parametrize("dtype,d,k,geom", [(torch.bfloat16, 128, 1024, 0), (torch.bfloat16, 128, 1024, 4),
+                                            (torch.bfloat16, 64, 4096, 0), (torch.bfloat16, 32, 1024, 0),
+                                            (torch.bfloat16, 256, 512, 0), (torch.float32, 128, 256, 0),
+                                            (torch.float32, 40, 77, 0)])
+def test_assign_persistent_grid_bitwise(native, kvariant, dtype, d, k, geom):
+    """The persistent grid (workgroups loop over point blocks, the centre ring and the next
+    block's fragments stream across block boundaries) gives the one-pass grid's labels,
+    distances, inertia and changed count bit for bit -- on blob rows, with an outlier row
+    (per-point-offset workgroups), a ragged tail, caller norms or fragment norms, and on a
+    gathered batch."""
+    from mikmeans.ops import pad_columns
+
+    n = 1_500_001                       # > resident workgroup slots on every geometry; ragged
+    X = pad_columns(B.make_blobs(n, d, 64, seed=d + k, dtype=dtype, device=DEV))
+    X[12345] *= 40.0                   # outlier row: its workgroup takes per-point offsets
+    C = X[:k, :d].float() + 0.25
+    pk = ops.pack_centers(C, X.shape[1], dtype, DEV)
+    xn = ops.row_sqnorm(X)
+    rows = torch.randint(0, n, (700_003,), device=DEV)
+    kvariant("assign_geom", geom)
+    out = {}
+    for persist in (0, 1):
+        kvariant("assign_persist", persist)
+        lab = torch.full((n,), 7, dtype=torch.int32, device=DEV)
+        mind = torch.empty(n, device=DEV)
+        slots = torch.zeros(native.NSLOT * native.SLOT_STRIDE, dtype=torch.float64, device=DEV)
+        pk.assign(X, xn, lab, mind, slots, True)
+        glab = torch.empty(rows.numel(), dtype=torch.int32, device=DEV)
+        gslots = torch.zeros_like(slots)
+        pk.assign(X, None, glab, None, gslots, False, rows=rows)
+        torch.cuda.synchronize()
+        out[persist] = (lab, mind, slots.view(-1, native.SLOT_STRIDE)[:, :2].sum(0), glab,
+                        gslots.view(-1, native.SLOT_STRIDE)[:, 0].sum())
+    a, b = out[0], out[1]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[3], b[3])
+    assert float(a[2][1]) == float(b[2][1]) == n           # every row changed (labels were 7 / -)
+    assert float(b[2][0]) == pytest.approx(float(a[2][0]), rel=1e-9)
+    assert float(b[4]) == pytest.approx(float(a[4]), rel=1e-9)
