@@ -63,7 +63,7 @@ def _unit_rows(X: torch.Tensor, block: int = 1 << 22) -> torch.Tensor:
 
 
 def native_dpad(D: int, dtype) -> int:
-    """The MFMA kernels' padded width for D features (0: D > 256, PyTorch GEMM path)."""
+    """The MFMA kernels' padded width for D features (0: D > 1024, PyTorch GEMM path)."""
     from .ops import native
 
     return native.dpad_for(pad_columns(torch.empty((0, D), dtype=dtype)).shape[1], dtype)

@@ -147,6 +147,7 @@ template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, 
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
+  constexpr bool WIDE = DPAD > 256;        // rows of 384..1024 features (see the MFMA issue)
   static_assert(!(VARG && EXACT), "value-only argmin is the bf16 epilogue");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -328,8 +329,10 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
           const int tile = (c0 + c) * C::CT + tl_i;
           ci_ = *(const f32x4*)(cn_lds + (tile * 16 + 4 * g) * 4);
           const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
+          if constexpr (!WIDE) {   // (wide rows read their A fragments one at a time, below)
     #pragma unroll
-          for (int q = 0; q < C::NQ; ++q) aw_[q] = *(const u32x4*)(tl + q * 1024);
+            for (int q = 0; q < C::NQ; ++q) aw_[q] = *(const u32x4*)(tl + q * 1024);
+          }
         };
         // EARLY (bf16 D=64): the next tile's fragments are read right after this tile's
         // MFMAs are issued, so their LDS latency hides under the argmin epilogue (+2 % at D=64
@@ -411,7 +414,17 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
               __builtin_amdgcn_sched_barrier(0);
             }
           };
-          if constexpr (PMAJ) {
+          if constexpr (WIDE) {
+            // wide rows (DPAD > 256): one A fragment at a time, each against the P blocks --
+            // all NQ of a tile would not fit in registers beside the rows
+            const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
+#pragma unroll
+            for (int q = 0; q < C::NQ; ++q) {
+              const u32x4 aq = *(const u32x4*)(tl + q * 1024);
+#pragma unroll
+              for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aq, xr[p][q], acc[p]);
+            }
+          } else if constexpr (PMAJ) {
             // point-block-major issue, pinned in this order
 #pragma unroll
             for (int p = 0; p < C::P; ++p) chain(p);
@@ -852,6 +865,20 @@ int assign16_chunk_tiles(int dtype, int dpad) { return plan::assign16_chunk_tile
 int assign_kpad(int dtype, int dpad, int K) { return plan::assign_kpad(dtype == DT_BF16 ? 2 : 4, dpad, K); }
 int assign_cn_len(int kpad) { return plan::assign_cn_len(kpad); }
 
+// Wide rows (DPAD 384..1024, e.g. sentence-embedding widths): one centre tile per chunk
+// (12-32 KiB), one wave per SIMD, and as many point blocks as ~256 registers of rows hold --
+// bf16 4 blocks up to 512 features and 2 beyond, f32 2 and 1.  The fragment layout, the
+// seed offsets and the argmin epilogue are the narrow kernels'; only the MFMA issue reads
+// the A fragments one at a time (WIDE in assign16_kernel).
+template <typename T, int DPAD>
+static hipError_t launch16_w(const AssignArgs& a, hipStream_t s) {
+  constexpr int CT = chunk_tiles16(sizeof(T), DPAD);
+  static_assert(CT == 1, "wide rows: one tile per chunk");
+  constexpr int P = sizeof(T) == 2 ? (DPAD <= 512 ? 4 : 2) : (DPAD <= 512 ? 2 : 1);
+  static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
+  return launch16_t<T, DPAD, P, CT, 2, 1>(a, s);
+}
+
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s) {
   if (dtype == DT_BF16) {
     switch (dpad) {
@@ -859,6 +886,10 @@ hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t
       case 64: return launch16_d<uint16_t, 64>(a, s);
       case 128: return launch16_d<uint16_t, 128>(a, s);
       case 256: return launch16_d<uint16_t, 256>(a, s);
+      case 384: return launch16_w<uint16_t, 384>(a, s);
+      case 512: return launch16_w<uint16_t, 512>(a, s);
+      case 768: return launch16_w<uint16_t, 768>(a, s);
+      case 1024: return launch16_w<uint16_t, 1024>(a, s);
     }
   } else {
     switch (dpad) {
@@ -867,6 +898,10 @@ hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t
       case 64: return launch16_d<float, 64>(a, s);
       case 128: return launch16_d<float, 128>(a, s);
       case 256: return launch16_d<float, 256>(a, s);
+      case 384: return launch16_w<float, 384>(a, s);
+      case 512: return launch16_w<float, 512>(a, s);
+      case 768: return launch16_w<float, 768>(a, s);
+      case 1024: return launch16_w<float, 1024>(a, s);
     }
   }
   return hipErrorInvalidValue;

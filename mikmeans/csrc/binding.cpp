@@ -329,7 +329,6 @@ void col_absmax(const Tensor& X, const Tensor& out, const c10::optional<Tensor>&
   check_cuda(out, "out");
   TORCH_CHECK(out.scalar_type() == at::kInt && out.is_contiguous() && out.numel() == X.size(1),
               "mikmeans: col_absmax out must be int32 [D]");
-  TORCH_CHECK(X.size(1) / vec_of(dt) <= 64, "mikmeans: col_absmax supports D <= 64 16-B pieces");
   TORCH_CHECK(fstats.has_value() == nnz.has_value() && fstats.has_value() == lowbit.has_value(),
               "mikmeans: col_absmax statistics come together (fstats, nnz, lowbit)");
   if (fstats.has_value()) {

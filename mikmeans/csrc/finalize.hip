@@ -159,10 +159,12 @@ __device__ __forceinline__ int lowbit_exp(float f) {
   return e == 0u ? -149 + (int)__builtin_ctz(m) : (int)e - 150 + (int)__builtin_ctz(m | 0x800000u);
 }
 
+// One launch covers up to 64 16-B pieces of a row (a column block: X, out, fstats, nnz and
+// lowbit point at its first column; fstats rows are fstride columns apart).
 template <typename T, bool STATS>
 __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X, int64_t N, int NP,
                                                          int L, int64_t ldx, uint32_t* __restrict__ out,
-                                                         double* __restrict__ fstats,
+                                                         double* __restrict__ fstats, int64_t fstride,
                                                          unsigned long long* __restrict__ nnz,
                                                          int* __restrict__ lowbit) {
   constexpr int V = Elem<T>::V;
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
       __syncthreads();
       for (int j = threadIdx.x; j < NP * V; j += 256) {
         const double v = (rd[0][j] + rd[1][j]) + (rd[2][j] + rd[3][j]);
-        if (v != 0.0) atomicAdd(fstats + (int64_t)k * NP * V + j, v);
+        if (v != 0.0) atomicAdd(fstats + (int64_t)k * fstride + j, v);
       }
     }
     __syncthreads();
@@ -264,22 +266,32 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
 hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
                              hipStream_t s, double* fstats, unsigned long long* nnz, int* lowbit) {
   const int V = dtype == DT_BF16 ? 8 : 4;
-  const int NP = D / V;
-  if (N <= 0 || D % V || NP > 64 || NP < 1) return N <= 0 ? hipSuccess : hipErrorInvalidValue;
+  const int NPT = D / V;
+  if (N <= 0 || D % V || NPT < 1) return N <= 0 ? hipSuccess : hipErrorInvalidValue;
   if ((fstats != nullptr) != (nnz != nullptr) || (fstats != nullptr) != (lowbit != nullptr))
     return hipErrorInvalidValue;  // the statistics come together
-  int L = 1;
-  while (L < NP) L *= 2;
-  const int R = 256 / L;
-  int64_t nb = (N + R - 1) / R;
-  if (nb > 2048) nb = 2048;  // 8 per CU; each streams its rows with 4 loads in flight per lane
-  const dim3 g((unsigned)nb), b(256);
-  if (dtype == DT_BF16) {
-    if (fstats) hipLaunchKernelGGL((col_absmax_kernel<uint16_t, true>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, fstats, nnz, lowbit);
-    else hipLaunchKernelGGL((col_absmax_kernel<uint16_t, false>), g, b, 0, s, (const uint16_t*)X, N, NP, L, ldx, out, fstats, nnz, lowbit);
-  } else {
-    if (fstats) hipLaunchKernelGGL((col_absmax_kernel<float, true>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, fstats, nnz, lowbit);
-    else hipLaunchKernelGGL((col_absmax_kernel<float, false>), g, b, 0, s, (const float*)X, N, NP, L, ldx, out, fstats, nnz, lowbit);
+  // wide rows: one launch per block of 64 pieces (512 bf16 / 256 f32 columns)
+  for (int p0 = 0; p0 < NPT; p0 += 64) {
+    const int NP = NPT - p0 < 64 ? NPT - p0 : 64;
+    const int64_t c0 = (int64_t)p0 * V;
+    int L = 1;
+    while (L < NP) L *= 2;
+    const int R = 256 / L;
+    int64_t nb = (N + R - 1) / R;
+    if (nb > 2048) nb = 2048;  // 8 per CU; each streams its rows with 4 loads in flight per lane
+    const dim3 g((unsigned)nb), b(256);
+    double* fs = fstats ? fstats + c0 : nullptr;
+    unsigned long long* nz = nnz ? nnz + c0 : nullptr;
+    int* lb = lowbit ? lowbit + c0 : nullptr;
+    if (dtype == DT_BF16) {
+      const uint16_t* Xb = (const uint16_t*)X + c0;
+      if (fstats) hipLaunchKernelGGL((col_absmax_kernel<uint16_t, true>), g, b, 0, s, Xb, N, NP, L, ldx, out + c0, fs, (int64_t)D, nz, lb);
+      else hipLaunchKernelGGL((col_absmax_kernel<uint16_t, false>), g, b, 0, s, Xb, N, NP, L, ldx, out + c0, fs, (int64_t)D, nz, lb);
+    } else {
+      const float* Xf = (const float*)X + c0;
+      if (fstats) hipLaunchKernelGGL((col_absmax_kernel<float, true>), g, b, 0, s, Xf, N, NP, L, ldx, out + c0, fs, (int64_t)D, nz, lb);
+      else hipLaunchKernelGGL((col_absmax_kernel<float, false>), g, b, 0, s, Xf, N, NP, L, ldx, out + c0, fs, (int64_t)D, nz, lb);
+    }
   }
   return hipGetLastError();
 }

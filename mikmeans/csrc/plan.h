@@ -130,13 +130,22 @@ inline int update_n_chunks_ks(int ks, int nc_slice) {
   return nc > nc_slice ? nc : nc_slice;
 }
 
-// Assign kernel: centroid tiles (16 centroids) per 16 KiB LDS chunk, 0 = unsupported width.
+// Assign kernel: centroid tiles (16 centroids) per 16 KiB LDS chunk (one tile per chunk for
+// rows of 16 KiB tiles and wider), 0 = unsupported width.  Padded widths: powers of two up
+// to 256, then 384, 512, 768, 1024 (the wide-row kernels).
 constexpr int chunk_tiles16(int esize, int dpad) {
   return (16 * dpad * esize) >= 16384 ? 1 : 16384 / (16 * dpad * esize);
 }
+inline int assign_dpad(int esize, int D) {
+  int d = 4 * (16 / esize);
+  while (d < D && d < 256) d *= 2;
+  if (D <= d) return d;
+  for (int w : {384, 512, 768, 1024})
+    if (D <= w) return w;
+  return 0;
+}
 inline int assign16_chunk_tiles(int esize, int dpad) {
-  const bool ok = esize == 2 ? (dpad == 32 || dpad == 64 || dpad == 128 || dpad == 256)
-                             : (dpad == 16 || dpad == 32 || dpad == 64 || dpad == 128 || dpad == 256);
+  const bool ok = dpad >= 4 * (16 / esize) && assign_dpad(esize, dpad) == dpad;
   return ok ? chunk_tiles16(esize, dpad) : 0;
 }
 // K rounded up to a whole chunk (0 = unsupported width or K out of range).

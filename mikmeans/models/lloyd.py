@@ -95,9 +95,9 @@ class LloydEngine:
         self.X = pad_columns(X) if self.gpu else X
         self.Dp = int(self.X.shape[1])
         if self.gpu and native.dpad_for(self.Dp, self.X.dtype) == 0:
-            # D > 256: beyond the MFMA kernels' register-resident rows; run the PyTorch
-            # path on the device instead (hipBLASLt GEMM scores + index_add sums).
-            native.warn_once(f"D={self.D} > 256: Lloyd steps use the PyTorch GEMM path on {X.device}")
+            # D > 1024: wider than the MFMA kernels' register-resident rows (csrc/assign16.hip
+            # covers up to 1024 features); the PyTorch path runs on the device instead
+            native.warn_once(f"D={self.D} > 1024: Lloyd steps use the PyTorch GEMM path on {X.device}")
             self.gpu = False
         self.n = int(self.X.shape[0])
         self.dtype = self.X.dtype

@@ -44,7 +44,7 @@ class MiniBatchEngine:
         self.steps = 0
         self.batch_inertia = 0.0
         if self.gpu and native.dpad_for(self.Dp, dtype) == 0:
-            native.warn_once(f"D={self.D} > 256: mini-batch steps use the PyTorch GEMM path")
+            native.warn_once(f"D={self.D} > 1024: mini-batch steps use the PyTorch GEMM path")
             self.gpu = False
         if self.gpu:
             C = native.require()

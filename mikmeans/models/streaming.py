@@ -68,7 +68,7 @@ class StreamingLloydEngine(LloydEngine):
         self.dt = native.dtype_code(self.dtype)
         self.Dp = padded_cols(self.Dsrc, 2 if self.dtype == torch.bfloat16 else 4)
         if native.dpad_for(self.Dp, self.dtype) == 0:
-            raise NotImplementedError("streaming Lloyd supports D <= 256")
+            raise NotImplementedError("streaming Lloyd supports D <= 1024 (the MFMA kernels' widest rows)")
         # async H2D straight from the caller's rows: page-lock them in place (no pinned copy)
         self._registered = False
         if self.n and not self.Xh.is_pinned():

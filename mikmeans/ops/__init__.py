@@ -76,7 +76,7 @@ class CentroidPack:
         self.K, self.D, self.dtype = K, D, dtype
         self.dpad = dpad_for(D, dtype)
         if self.dpad == 0:
-            raise NotImplementedError(f"mikmeans: GPU assign supports D <= 256 (got {D})")
+            raise NotImplementedError(f"mikmeans: GPU assign supports D <= 1024 (got {D})")
         self.dt = dtype_code(dtype)
         self.Kpad = C.assign_kpad(self.dt, self.dpad, K)
         self._keys = None
@@ -133,7 +133,7 @@ def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True,
     same (padded) width, dtype and device (serving: pack once, assign many batches).
     """
     if not X.is_cuda or dpad_for(pad_columns(X[:1]).shape[1], X.dtype) == 0:
-        return cpu.assign(X, centers.to(X.device), with_dist=with_dist)  # CPU, or D > 256 on the GPU
+        return cpu.assign(X, centers.to(X.device), with_dist=with_dist)  # CPU, or D > 1024 on the GPU
     C = require()
     Xp = pad_columns(X)
     D = Xp.shape[1]
@@ -163,7 +163,7 @@ def max_abs(X: torch.Tensor) -> float:
 def _native_colstats_ok(X: torch.Tensor) -> bool:
     v = 16 // X.element_size()
     return (X.is_cuda and X.dtype in (torch.float32, torch.bfloat16) and X.dim() == 2 and X.stride(1) == 1
-            and X.shape[1] % v == 0 and X.shape[1] // v <= 64 and (X.shape[0] <= 1 or X.stride(0) % v == 0)
+            and X.shape[1] % v == 0 and (X.shape[0] <= 1 or X.stride(0) % v == 0)
             and X.data_ptr() % 16 == 0)
 
 

@@ -64,13 +64,19 @@ def vec_elems(dtype: torch.dtype) -> int:
     return 8 if dtype == torch.bfloat16 else 4
 
 
+WIDE_DPADS = (384, 512, 768, 1024)
+
+
 def dpad_for(D: int, dtype: torch.dtype) -> int:
-    """Power-of-two padded feature width the assign kernel is instantiated for (0 = unsupported):
-    at least four 16-byte pieces (one per lane group of the 16x16 MFMA tile), at most 256."""
+    """Padded feature width the assign kernel is instantiated for (0 = unsupported): a power
+    of two of at least four 16-byte pieces (one per lane group of the 16x16 MFMA tile) up to
+    256, then the wide-row widths 384 / 512 / 768 / 1024 (csrc/plan.h ``assign_dpad``)."""
     d = 4 * vec_elems(dtype)
-    while d < D:
+    while d < D and d < 256:
         d *= 2
-    return d if d <= 256 else 0
+    if D <= d:
+        return d
+    return next((w for w in WIDE_DPADS if D <= w), 0)
 
 
 _warned: set = set()

@@ -70,10 +70,13 @@ def padded_cols(D: int, esize: int) -> int:
 
 
 def dpad_for(D: int, esize: int) -> int:
+    """csrc/plan.h assign_dpad: powers of two up to 256, then 384 / 512 / 768 / 1024."""
     d = 4 * vec_elems(esize)
-    while d < D:
+    while d < D and d < 256:
         d *= 2
-    return d if d <= 256 else 0
+    if D <= d:
+        return d
+    return next((w for w in (384, 512, 768, 1024) if D <= w), 0)
 
 
 def upd_lds_bytes(K: int, ldc: int, weighted: bool) -> int:
@@ -147,7 +150,7 @@ def update_n_chunks(esize: int, K: int, D: int, N: int, weighted: bool) -> int:
 
 
 def assign_kpad(esize: int, dpad: int, K: int) -> int:
-    ok = dpad in ((32, 64, 128, 256) if esize == 2 else (16, 32, 64, 128, 256))
+    ok = dpad >= 4 * vec_elems(esize) and dpad_for(dpad, esize) == dpad
     if not ok or K < 1 or K > (1 << 24):
         return 0
     ct = 1 if 16 * dpad * esize >= 16384 else 16384 // (16 * dpad * esize)

@@ -42,7 +42,10 @@ def test_row_sqnorm(native, dtype, n, d):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n,d,k", [(1000, 2, 3), (513, 16, 37), (20000, 128, 256), (9000, 128, 1024),
-                                   (4096, 64, 4096), (3000, 256, 512), (255, 100, 70), (70000, 32, 9)])
+                                   (4096, 64, 4096), (3000, 256, 512), (255, 100, 70), (70000, 32, 9),
+                                   # wide rows (DPAD 384 / 512 / 768 / 1024 kernels)
+                                   (3000, 300, 77), (2500, 500, 130), (2000, 768, 1024), (1500, 1000, 300),
+                                   (1200, 1024, 33), (300_001, 768, 64)])
 def test_assign_matches_reference(native, dtype, n, d, k):
     X = _points(n, d, dtype, seed=k)
     C = _points(k, d, torch.float32, seed=k + 1)
@@ -458,26 +461,58 @@ def test_incremental_mstep_graph(native):
         assert torch.equal(ea.centers, eb.centers)
 
 
-def test_wide_features_use_gemm_path(native):
-    """D > 256: the MFMA kernels do not apply; fit/predict/mini-batch run the PyTorch
-    GEMM path on the device and agree with the CPU engine."""
-    import warnings
-
+@pytest.mark.parametrize("d", [300, 768, 1024])
+def test_wide_features_run_native_kernels(native, d):
+    """D = 300 / 768 / 1024: fit, predict and mini-batch run the wide-row MFMA kernels (no
+    PyTorch GEMM fallback) and agree with the CPU engine."""
     from mikmeans import KMeans, MiniBatchKMeans
 
-    X = B.make_blobs(6000, 300, 8, seed=4)
-    with warnings.catch_warnings():
-        warnings.simplefilter("ignore")
-        kg = KMeans(8, init="random", seed=1, max_iter=10, tol=-1.0, device=DEV).fit(X.to(DEV))
-        kc = KMeans(8, init="random", seed=1, max_iter=10, tol=-1.0, device="cpu").fit(X)
-        lab = kg.predict(X.to(DEV))
-        mb = MiniBatchKMeans(8, batch_size=1000, max_iter=5, device=DEV, seed=0).fit(X.to(DEV))
+    X = B.make_blobs(6000, d, 8, seed=4)
+    kg = KMeans(8, init="random", seed=1, max_iter=10, tol=-1.0, device=DEV, dtype="float32").fit(X.to(DEV))
+    assert kg._engine.gpu and kg._engine.pk.dpad == ops.dpad_for(d, torch.float32)
+    kc = KMeans(8, init="random", seed=1, max_iter=10, tol=-1.0, device="cpu").fit(X)
+    lab = kg.predict(X.to(DEV))
+    mb = MiniBatchKMeans(8, batch_size=1000, max_iter=5, device=DEV, seed=0).fit(X.to(DEV))
+    assert mb._eng.gpu
     assert lab.is_cuda and torch.equal(lab.cpu(), kg.labels_.cpu())
-    # GPU vs CPU GEMM rounding may flip near-tie points (a split blob): compare the fits
     agree = (kg.labels_.cpu() == kc.labels_).float().mean().item()
     assert agree > 0.99
     assert abs(kg.inertia_ - kc.inertia_) <= 1e-3 * kc.inertia_
-    assert mb.cluster_centers_.shape == (8, 300)
+    assert mb.cluster_centers_.shape == (8, d)
+    kb = KMeans(8, init="random", seed=1, max_iter=10, tol=-1.0, device=DEV, dtype="bfloat16").fit(X.to(DEV))
+    assert kb._engine.gpu and (kb.labels_.cpu() == kc.labels_).float().mean().item() > 0.99
+
+
+def test_features_past_1024_use_gemm_path(native):
+    """D > 1024 (wider than the widest MFMA kernel): the PyTorch GEMM path on the device."""
+    import warnings
+
+    from mikmeans import KMeans
+
+    X = B.make_blobs(3000, 1100, 6, seed=4)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        kg = KMeans(6, init="random", seed=1, max_iter=6, tol=-1.0, device=DEV).fit(X.to(DEV))
+    kc = KMeans(6, init="random", seed=1, max_iter=6, tol=-1.0, device="cpu").fit(X)
+    assert not kg._engine.gpu
+    assert (kg.labels_.cpu() == kc.labels_).float().mean().item() > 0.99
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_streamed_fit_d768_matches_resident(native, dtype):
+    """An out-of-core fit at D=768 (wide-row kernels, chunks of 7680 rows) is the resident
+    fit bit for bit."""
+    import mikmeans
+
+    n, d, k = 40_000, 768, 32
+    X = B.make_blobs(n, d, k, seed=12, dtype=torch.float32, device="cpu")
+    Xh = X.to(torch.bfloat16) if dtype == "bfloat16" else X
+    kw = dict(init=X[:k].clone(), dtype=dtype, max_iter=5, tol=0, device=DEV)
+    ref = mikmeans.KMeans(k, **kw).fit(Xh.to(DEV))
+    st = mikmeans.KMeans(k, chunk_rows=7_680, **kw).fit(Xh)
+    assert st.memory_plan_["mode"] == "streaming" and ref._engine.gpu
+    assert torch.equal(st.cluster_centers_, ref.cluster_centers_)
+    assert torch.equal(st.labels_, ref.labels_)
 
 
 def test_predict_reuses_pack_until_centres_change(native):
@@ -619,13 +654,13 @@ def test_cosine_metric_gpu(native):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("n,d", [(1, 64), (1000, 8), (12345, 128), (70001, 256), (3000, 512)])
+@pytest.mark.parametrize("n,d", [(1, 64), (1000, 8), (12345, 128), (70001, 256), (3000, 512), (4000, 768),
+                                 (2001, 1024), (999, 1504)])
 def test_col_absmax_matches_torch(native, dtype, n, d):
     """Native per-column max |x| (fixed-point M-step scales) vs torch.aminmax; strided rows too."""
     from mikmeans.ops import col_max_abs
 
-    if d * torch.tensor([], dtype=dtype).element_size() > 1024:
-        d = 1024 // torch.tensor([], dtype=dtype).element_size()   # kernel bound: 64 16-B pieces
+    # (rows wider than 64 16-B pieces go through the kernel in column blocks)
     g = torch.Generator(device=DEV).manual_seed(n + d)
     X = (torch.randn(n, d, device=DEV, generator=g) * torch.linspace(0.1, 50, d, device=DEV)).to(dtype)
     ref = X.float().abs().amax(0).double()
