@@ -24,7 +24,7 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 BUILD = PKG.parent / "build" / "native"
 ARCH = os.environ.get("MIKMEANS_ARCH", "gfx950")
-HIP_SOURCES = ["assign16.hip", "update.hip", "finalize.hip", "kpp.hip", "rows.hip"]
+HIP_SOURCES = ["assign16.hip", "update.hip", "finalize.hip", "kpp.hip", "rows.hip", "transform.hip"]
 BINDING = "binding.cpp"
 
 DEVICE_FLAGS = [

@@ -26,7 +26,6 @@ from .config import KMeansConfig, resolve_dtype
 from .models.init import resolve_init
 from .models.lloyd import LloydEngine, tol_to_abs
 from .models.minibatch import MiniBatchEngine
-from .ops import cpu as cpu_ops
 from .ops import pad_columns
 from .parallel.comm import Comm, get_comm
 from .utils import faults
@@ -173,11 +172,13 @@ class _Serving:
 
     def transform(self, X):
         """Euclidean distances to every centre, ``[n, K]`` (float32; for the cosine
-        metric, between unit rows and unit centres: sqrt(2 - 2 cos))."""
+        metric, between unit rows and unit centres: sqrt(2 - 2 cos)).  On the GPU: the MFMA
+        transform kernel on the serving pack (csrc/transform.hip)."""
+        from . import ops
+
         self._check_fitted()
         Xt, was_numpy = self._inputs(X)
-        c = cpu_ops.quantize_centers(self.cluster_centers_, self.dtype)
-        d = torch.cdist(Xt.to(torch.float32), c)
+        d = ops.transform(Xt, self.cluster_centers_, pack=self._serving_pack(Xt))
         return d.cpu().numpy() if was_numpy else d
 
     def fit_transform(self, X, *args, **kw):

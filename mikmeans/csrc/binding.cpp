@@ -120,6 +120,31 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
   hip_check(mk::launch_assign16(dt, (int)dpad, a, stream()), "assign");
 }
 
+void transform(const Tensor& X, const Tensor& pack, const Tensor& cn, int64_t K, int64_t Kpad, int64_t dpad,
+               const Tensor& xn, const Tensor& out, bool squared) {
+  const int dt = dtype_of(X);
+  const int64_t ldx = check_points(X, dt);
+  const int64_t N = X.size(0);
+  TORCH_CHECK(X.size(1) <= dpad, "mikmeans: D exceeds dpad");
+  TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, (int)K) == Kpad, "mikmeans: bad Kpad ", Kpad);
+  check_cuda(pack, "pack");
+  TORCH_CHECK(pack.is_contiguous() && pack.scalar_type() == X.scalar_type() && pack.numel() >= Kpad * dpad,
+              "mikmeans: pack must be the points' dtype, [Kpad * dpad]");
+  check_f32(cn, "cn", Kpad);
+  check_f32(xn, "xn", N);
+  check_cuda(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.dim() == 2 && out.size(0) == N && out.size(1) == K &&
+                  out.stride(1) == 1 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "mikmeans: out must be float32 [N, K] with unit column stride, 16-B aligned");
+  mk::TransformArgs a;
+  a.X = X.data_ptr(); a.N = N; a.D = (int)X.size(1); a.ldx = ldx;
+  a.pack = pack.data_ptr(); a.cn = cn.data_ptr<float>(); a.K = (int)K; a.Kpad = (int)Kpad;
+  a.xn = xn.data_ptr<float>();
+  a.out = out.data_ptr<float>(); a.ldo = N > 1 ? out.stride(0) : K;
+  a.squared = squared ? 1 : 0;
+  hip_check(mk::launch_transform(dt, (int)dpad, a, stream()), "transform");
+}
+
 void check_i64(const Tensor& t, const char* name, int64_t numel_min) {
   check_cuda(t, name);
   TORCH_CHECK(t.scalar_type() == at::kLong && t.is_contiguous(), "mikmeans: ", name,
@@ -581,6 +606,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("K"), py::arg("slab"), py::arg("cnt_slab"), py::arg("n_chunks"), py::arg("weights"),
         py::arg("col_exp"), py::arg("cnt_exp"), py::arg("clamp"), py::arg("clamp_count") = py::none(),
         py::arg("col_exp2") = py::none(), py::arg("rows") = py::none());
+  m.def("transform", &transform, "distances of every row to every centre on the MFMA tiles", py::arg("X"),
+        py::arg("pack"), py::arg("cn"), py::arg("K"), py::arg("Kpad"), py::arg("dpad"), py::arg("xn"), py::arg("out"),
+        py::arg("squared") = false);
   m.def("reduce_cols", &reduce_cols, "lo sums of the wide-range columns (residual pass)");
   m.def("reduce", &reduce, "slab reduction into the packed f64 all-reduce message");
   m.def("label_delta", &label_delta, "changed-row list for the incremental M-step");

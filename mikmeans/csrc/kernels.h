@@ -58,6 +58,16 @@ struct AssignArgs {
 };
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 
+// ---- transform: every row's distance to every centre (csrc/transform.hip) --------------
+struct TransformArgs {
+  const void* X; int64_t N; int D; int64_t ldx;
+  const void* pack; const float* cn; int K; int Kpad;   // the assign kernel's packed centres
+  const float* xn;      // |x|^2 per row
+  float* out; int64_t ldo;
+  int squared;          // 1: squared distances, 0: distances
+};
+hipError_t launch_transform(int dtype, int dpad, const TransformArgs& a, hipStream_t s);
+
 // ---- update (LDS-privatised scatter-add) -------------------------------------
 // Sums are accumulated in FIXED POINT: every contribution x*w is rounded to a
 // 32-bit integer at scale 2^sum_exp (|x*w| * 2^sum_exp <= 2^30) and added with

@@ -152,6 +152,31 @@ def assign(X: torch.Tensor, centers: torch.Tensor, *, with_dist: bool = True,
     return labels, mind
 
 
+def transform(X: torch.Tensor, centers: torch.Tensor, *, squared: bool = False,
+              pack: "CentroidPack | None" = None) -> torch.Tensor:
+    """Distance of every row to every centre, ``[n, K]`` float32 (squared with ``squared``):
+    on the GPU the MFMA transform kernel (csrc/transform.hip) on the assign kernel's packed
+    centres -- the distances its argmin ranks; elsewhere the PyTorch reference."""
+    if not X.is_cuda or dpad_for(pad_columns(X[:1]).shape[1], X.dtype) == 0:
+        c = cpu.quantize_centers(centers.to(X.device), X.dtype)
+        d = torch.cdist(X.to(torch.float32), c)
+        return d * d if squared else d
+    C = require()
+    Xp = pad_columns(X)
+    D = Xp.shape[1]
+    if pack is not None and (pack.D, pack.dtype, pack.pack.device) == (D, Xp.dtype, Xp.device):
+        pk = pack
+    else:
+        pk = pack_centers(centers, D, Xp.dtype, X.device)
+    n = Xp.shape[0]
+    xn = torch.empty(n, dtype=torch.float32, device=X.device)
+    out = torch.empty((n, pk.K), dtype=torch.float32, device=X.device)
+    if n:
+        C.row_sqnorm(Xp, xn)
+        C.transform(Xp, pk.pack, pk.cn, pk.K, pk.Kpad, pk.dpad, xn, out, squared)
+    return out
+
+
 def max_abs(X: torch.Tensor) -> float:
     """max |x| without materialising |X| (one host read)."""
     if X.numel() == 0:

@@ -860,3 +860,39 @@ def test_assign_persistent_grid_bitwise(native, kvariant, dtype, d, k, geom):
     assert float(a[2][1]) == float(b[2][1]) == n           # every row changed (labels were 7 / -)
     assert float(b[2][0]) == pytest.approx(float(a[2][0]), rel=1e-9)
     assert float(b[4]) == pytest.approx(float(a[4]), rel=1e-9)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,d,k", [(1000, 2, 3), (20001, 128, 1024), (5000, 64, 4097), (3000, 256, 77),
+                                   (2000, 768, 100), (1500, 1024, 16), (777, 30, 513)])
+def test_transform_kernel_matches_reference(native, dtype, n, d, k):
+    """KMeans.transform's MFMA kernel: every row's distance to every centre against the f64
+    distances to the quantised centres; argmin of the row equals the assign's label on rows
+    the scores resolve."""
+    X = _points(n, d, dtype, seed=n + k)
+    C = _points(k, d, torch.float32, seed=k + 3)
+    got = ops.transform(X.to(DEV), C.to(DEV))
+    assert got.shape == (n, k) and got.dtype == torch.float32
+    Cq = ref.quantize_centers(C, dtype).double()
+    exp = torch.cdist(X.double(), Cq)
+    scale = (X.double() ** 2).sum(1, keepdim=True).sqrt() + Cq.norm(dim=1).max()
+    err = (got.cpu().double() - exp).abs()
+    tol = (3e-5 if dtype == torch.float32 else 1e-4) * scale + 1e-3
+    assert bool((err <= tol).all()), float((err - tol).max())
+    sq = ops.transform(X.to(DEV), C.to(DEV), squared=True)
+    torch.testing.assert_close(sq.sqrt(), got, rtol=1e-5, atol=1e-5)
+
+
+def test_kmeans_transform_uses_kernel(native):
+    import mikmeans
+
+    X = B.make_blobs(30_000, 96, 12, seed=2, dtype=torch.bfloat16, device=DEV)
+    km = mikmeans.KMeans(12, dtype="bfloat16", seed=0, max_iter=10).fit(X)
+    D = km.transform(X)
+    lab = km.predict(X)
+    # the argmin of the distances is the label wherever the best two are apart
+    top2 = D.topk(2, largest=False)
+    clear = (top2.values[:, 1] - top2.values[:, 0]) > 1e-3
+    assert torch.equal(top2.indices[:, 0][clear].int(), lab[clear])
+    Dn = km.transform(X[:100].cpu().float().numpy())
+    assert Dn.shape == (100, 12)
