@@ -143,11 +143,13 @@ __device__ __forceinline__ float sq16(const u32x4& w, float*) {
 // latency hides under the epilogue instead of opening every workgroup's life; the inertia
 // and changed counts go to the slots once per workgroup.  Same scores, same labels.
 template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false,
-          bool VARG = false, int PMAJ = 0, bool PERSIST = false>
+          bool VARG = false, int PMAJ = 0, bool PERSIST = false, bool AST = false>
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
-  constexpr bool WIDE = DPAD > 256;        // rows of 384..1024 features (see the MFMA issue)
+  // A fragments streamed one at a time (see the MFMA issue): rows of 384..1024 features, or
+  // AST (a lower-register variant of the narrow kernels)
+  constexpr bool WIDE = AST || DPAD > 256;
   static_assert(!(VARG && EXACT), "value-only argmin is the bf16 epilogue");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -718,13 +720,13 @@ static int assign16_splits(int64_t nblk, int nch) {
 // D=64 K=2048 +8.5 %, K=1024 -3.7 %; D=32 K=1024 +5.6 %, K=512 -8.8 %).
 // Variant V_ASSIGN_VARG = 0/1 forces it off / on (A/B, tests).
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST>
 static void set_lds_attr() {
   static bool done = false;
   if (done) return;
-  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST>,
+  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST>,
+  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   done = true;
 }
@@ -743,14 +745,14 @@ static void set_lds_attr() {
 // blocks' MFMA chains instead measured -1.1 % at D=128, -3.8 % at D=64 K=4096, +2.2 % at D=64
 // K=1024 (profiles/r3_23_ab_pmaj_interleaved.log) and is not built.
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST>
 static void launch16_kpp(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST>();
+  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST>();
   if (b.D == DPAD)
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST>), grid,
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST>), grid,
                        dim3(NW_ * 64), lds, s, b);
   else
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST>), grid,
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST>), grid,
                        dim3(NW_ * 64), lds, s, b);
 }
 
@@ -769,27 +771,31 @@ static int64_t resident_workgroups(int waves_per_wg, int occ_per_simd, size_t ld
   return (int64_t)(per_cu > 0 ? per_cu : 1) * cus;
 }
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool AST>
 static void launch16_kp(const AssignArgs& b, dim3 grid, size_t lds, hipStream_t s) {
   // Persistent grid (variant V_ASSIGN_PERSIST = 1; default off): one-pass grids only (no
   // centre split), and only where the point blocks outnumber the resident slots.
   const int64_t slots = resident_workgroups(NW_, OCC, lds);
   if (variant(V_ASSIGN_PERSIST) > 0 && grid.y == 1 && (int64_t)grid.x > slots) {
     grid.x = (unsigned)slots;
-    return launch16_kpp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, true>(b, grid, lds, s);
+    return launch16_kpp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, true, AST>(b, grid, lds, s);
   }
-  launch16_kpp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, false>(b, grid, lds, s);
+  launch16_kpp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, false, AST>(b, grid, lds, s);
 }
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, bool AST>
 static void launch16_k(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  const int e = variant(V_ASSIGN_PMAJ);
-  const int pm = e >= 0 ? e : (sizeof(T) == 2 ? 1 : 0);
-  if (pm != 0) return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 1>(b, grid, lds, s);
-  launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 0>(b, grid, lds, s);
+  if constexpr (AST || DPAD > 256) {   // streamed A fragments: one issue order
+    return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 0, AST>(b, grid, lds, s);
+  } else {
+    const int e = variant(V_ASSIGN_PMAJ);
+    const int pm = e >= 0 ? e : (sizeof(T) == 2 ? 1 : 0);
+    if (pm != 0) return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 1, AST>(b, grid, lds, s);
+    launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 0, AST>(b, grid, lds, s);
+  }
 }
 
-template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4>
+template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool AST = false>
 static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   if (a.Kpad % (16 * C::CT) != 0) return hipErrorInvalidValue;
@@ -810,10 +816,10 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
     varg = e >= 0 ? e != 0 : a.Kpad >= (DPAD == 64 ? 2048 : 1024);
   }
   if constexpr (VARG_OK) {
-    if (varg) launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, true>(b, grid, lds, s);
-    else launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, false>(b, grid, lds, s);
+    if (varg) launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, AST>(b, grid, lds, s);
+    else launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, AST>(b, grid, lds, s);
   } else {
-    launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, false>(b, grid, lds, s);
+    launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, AST>(b, grid, lds, s);
   }
   if (splits > 1)
     hipLaunchKernelGGL(split_finish_kernel, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, s, b);
@@ -844,6 +850,9 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
     const int gm = variant(V_ASSIGN_GEOM);
     if (gm == 1) return launch16_t<T, DPAD, 3, CT, 2, 2, 8>(a, s);
     if (gm == 2) return launch16_t<T, DPAD, 2, CT, 2, 4, 8>(a, s);
+    // 3: streamed A fragments (the wide-row issue), 3 blocks at 3 waves/SIMD in 151-157
+    // VGPRs without the 4 spilled registers of the default (4 blocks spill hundreds)
+    if (gm == 3) return launch16_t<T, DPAD, 3, CT, 2, 3, 4, true>(a, s);
   }
   if constexpr (sizeof(T) == 2 && DPAD == 128) {
     // A/B switch V_ASSIGN_GEOM: 1 = 8 waves share a ring of 32 KiB chunks (a barrier
