@@ -272,6 +272,14 @@ class KMeans(_Serving):
             plan = memplan.plan_streaming(n_local, D, self.n_clusters, self.dtype, chunk_rows=self.chunk_rows,
                                           init_rows=self.init_size, src_itemsize=es_src, **kw)
             plan.budget = budget
+            # every rank learns whether any forced chunk does not fit (one collective, as below)
+            flags = torch.tensor([0.0 if plan.fits else 1.0], dtype=torch.float64, device=comm.device)
+            comm.allreduce_max_(flags)
+            if flags[0].item() > 0:
+                raise memplan.HBMCapacityError(
+                    f"KMeans.fit: chunk_rows={self.chunk_rows} does not fit "
+                    + (plan.summary() if not plan.fits else "another rank's HBM budget")
+                    + "; use a smaller chunk_rows or more ranks")
         else:
             try:
                 plan = memplan.plan_fit(n_local, D, self.n_clusters, self.dtype, budget=budget, x_on_device=x_dev,
@@ -286,11 +294,23 @@ class KMeans(_Serving):
             if flags[0].item() > 0:
                 raise plan if isinstance(plan, memplan.HBMCapacityError) else memplan.HBMCapacityError(
                     "KMeans.fit: another rank's shard does not fit its HBM budget")
-            if flags[1].item() > 0 and plan.mode != "streaming":
-                if x_dev:
-                    raise memplan.HBMCapacityError("KMeans.fit: other ranks stream their shards; pass this "
-                                                   "rank's rows as a host tensor too")
-                plan = self._stream_plan(n_local, D, es_src, budget, kw)
+            if flags[1].item() > 0:
+                # some rank streams: all must (the init sample and its collectives must match);
+                # a second agreement, so a rank that cannot follow fails every rank together
+                msg = None
+                if plan.mode != "streaming":
+                    if x_dev:
+                        msg = ("KMeans.fit: other ranks stream their shards; pass this rank's rows as a host "
+                               "tensor too")
+                    else:
+                        try:
+                            plan = self._stream_plan(n_local, D, es_src, budget, kw)
+                        except memplan.HBMCapacityError as e:
+                            msg = str(e)
+                f2 = torch.tensor([1.0 if msg else 0.0], dtype=torch.float64, device=comm.device)
+                comm.allreduce_max_(f2)
+                if f2[0].item() > 0:
+                    raise memplan.HBMCapacityError(msg or "KMeans.fit: another rank cannot stream its shard")
         if self.verbose and comm.rank == 0:
             print(f"[mikmeans] memory plan: {plan.summary()}", flush=True)
         return plan
@@ -305,8 +325,12 @@ class KMeans(_Serving):
             pl = memplan.plan_streaming(n_local, D, self.n_clusters, self.dtype, chunk_rows=R,
                                         init_rows=self.init_size, src_itemsize=es_src, **kw)
             pl.budget = budget
-            if pl.fits or R <= memplan.ROW_ALIGN:
+            if pl.fits:
                 return pl
+            if R <= memplan.ROW_ALIGN:
+                # (another rank chose streaming and this one cannot stream within its budget)
+                raise memplan.HBMCapacityError(f"KMeans.fit: {pl.summary()} does not fit even in "
+                                               f"{memplan.ROW_ALIGN}-row chunks")
             R //= 2
 
     def _x_ready(self, X, device) -> bool:

@@ -13,7 +13,9 @@ engine.  Per-row state stays on the device for all rows: labels and squared row 
 policy.
 
 Same options as the resident engine, with the same numerics (bitwise the resident fit
-from the same start): sample weights, the cosine metric (each chunk is normalised on the
+from the same start -- up to a column whose statistics sit within f64 rounding of the
+wide-column threshold or the tol scale: those are f64 sums, merged chunk by chunk here and
+accumulated by atomics in one pass there, so their last bits differ): sample weights, the cosine metric (each chunk is normalised on the
 device by the same kernel as the resident rows), empty_policy 'farthest' (the farthest
 rows are fetched from host memory), wide-range columns (residual lo pass per chunk, from
 column statistics merged over chunks).  Host rows of another dtype or an unpadded width
