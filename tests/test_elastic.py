@@ -1,0 +1,88 @@
+"""Live membership of the replicated room (parallel/elastic.py): members join and leave a
+running session -- the reference's peerconnect / peerclose with full-state sync on join
+(app.mjs:82-105, :96) -- and every member reports the same room after every round.
+
+CPU processes on 127.0.0.1 around one TCPStore the test hosts (the tracker's role)."""
+import datetime
+import json
+import time
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mikmeans.parallel.launch import free_port
+
+ROUNDS = 30
+
+
+def _store(port, master=False):
+    return dist.TCPStore("127.0.0.1", port, is_master=master, wait_for_workers=False,
+                         timeout=datetime.timedelta(seconds=60))
+
+
+def _record(store, rep):
+    store.set(f"dig/{rep.member}/{rep.round}", json.dumps({"d": rep.digest(), "epoch": rep.epoch,
+                                                          "peers": rep.peers}))
+
+
+def _member(port, member, delay, leave_at):
+    from mikmeans.parallel.elastic import ElasticRoomReplica
+
+    store = _store(port)
+    time.sleep(delay)
+    if member == "A":
+        rep = ElasticRoomReplica.found(store, member, "ROOM", user=member, seed=3)
+    else:
+        rep = ElasticRoomReplica.join(store, member, user=member, seed=3)
+    store.set(f"joined/{member}", str(rep.round))
+    asked = False
+    while rep.round < ROUNDS and not rep.left:
+        if rep.round % 3 == 0:
+            rep.add_card(f"{member}-{rep.round}", ["Mint", "Choc"])
+        if member == "A" and rep.round == 5:
+            rep.add_centroid("Fresh")
+        if leave_at is not None and rep.round >= leave_at and not asked:
+            rep.leave()
+            asked = True
+        rep.sync()
+        if not rep.left:
+            _record(store, rep)
+        time.sleep(0.05)
+    store.set(f"done/{member}", json.dumps({"round": rep.round, "left": rep.left,
+                                            "cards": [c["title"] for c in rep.room.cards]}))
+    if not rep.left:
+        assert rep.check()          # one more collective: every remaining replica identical
+
+
+@pytest.mark.timeout(240)
+def test_members_join_and_leave_a_running_session():
+    port = free_port()
+    store = _store(port, master=True)
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_member, args=(port, "A", 0.0, None)),
+             ctx.Process(target=_member, args=(port, "B", 0.3, 12)),     # joins early, leaves
+             ctx.Process(target=_member, args=(port, "C", 0.9, None))]   # joins later
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(200)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    done = {m: json.loads(store.get(f"done/{m}").decode()) for m in "ABC"}
+    assert done["A"]["round"] == done["C"]["round"] == ROUNDS
+    assert done["B"]["left"] and done["B"]["round"] < ROUNDS
+    joined = {m: int(store.get(f"joined/{m}").decode()) for m in "BC"}
+    assert 0 < joined["B"] < joined["C"] < ROUNDS
+    # every member present after a round reports the same room (digest) that round
+    for r in range(1, ROUNDS + 1):
+        ds = []
+        for m in "ABC":
+            if store.check([f"dig/{m}/{r}"]):
+                ds.append(json.loads(store.get(f"dig/{m}/{r}").decode()))
+        assert ds and len({d["d"] for d in ds}) == 1, (r, ds)
+        # (a member admitted in round r records from round r + 1 on)
+        assert len({(d["epoch"], d["peers"]) for d in ds}) == 1, (r, ds)
+    # the final room holds every member's cards, B's from before it left
+    cards = done["A"]["cards"]
+    assert cards == done["C"]["cards"]
+    assert any(t.startswith("B-") for t in cards) and any(t.startswith("C-") for t in cards)
