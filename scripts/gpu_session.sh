@@ -25,6 +25,17 @@ for s in ${STEPS:-smoke tests bench prof}; do
     kbench2) step kbench2 300 python scripts/kbench.py --n 1000000 --d 128 --k 256 --dtype f32 --reps 20 ;;
     mstep) step pytest_mstep 300 python -u -m pytest tests/test_gpu_mstep.py -x -v --timeout 120 --timeout-method thread ;;
     rccl) step pytest_rccl 300 python -u -m pytest tests/test_gpu_rccl.py -x -v --timeout 120 --timeout-method thread ;;
+    multirank) step pytest_multirank 400 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 400 --timeout-method thread ;;
+    memplan) step pytest_memplan 600 python -u -m pytest tests/test_gpu_memplan.py tests/test_gpu_minibatch.py -v --timeout 200 --timeout-method thread ;;
+    newkern) step pytest_newkern 600 python -u -m pytest tests/test_gpu_kernels.py -v --timeout 200 --timeout-method thread \
+               -k "persistent or wide or transform or d768 or col_absmax or matches_reference or past_1024" ;;
+    ab_head) step ab_head 300 python -u scripts/assign_ab.py --arms "default;assign_persist=1;assign_geom=4;assign_geom=4,assign_persist=1" ;;
+    ab_d256) step ab_d256 300 python -u scripts/assign_ab.py --d 256 --k 512 --n 16777216 \
+               --arms "default;assign_geom=3;assign_persist=1;assign_geom=3,assign_persist=1" ;;
+    ab_d64) step ab_d64 300 python -u scripts/assign_ab.py --d 64 --k 4096 --n 10000000 --arms "default;assign_persist=1" ;;
+    ab_f32) step ab_f32 300 python -u scripts/assign_ab.py --d 128 --k 256 --n 1000000 --dtype f32 --reps 20 \
+               --arms "default;assign_persist=1" ;;
+    ab_wide) step ab_wide 300 python -u scripts/assign_ab.py --d 768 --k 1024 --n 4000000 --arms "default" ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
     benchauto) step bench_nopg 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 --pg auto --no-also-incremental ;;
     bench2) step bench_cfg2 300 python bench.py --config cfg2 --steps 50 --warmup 5 ;;
