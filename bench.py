@@ -324,7 +324,7 @@ def _bench_minibatch(args, cfg, comm, dtype):
         extra["data_bytes_per_rank"] = S * D * X.element_size()
     else:
         stream = BlobStream(N, D, K, b, seed=args.seed, dtype=dtype, device=dev, rank=comm.rank,
-                            world=comm.world, with_norms=True,  # row norms fused into the generator
+                            world=comm.world, with_norms=False,  # (the assign takes |x|^2 from its fragments)
                             prefetch=args.prefetch)  # batch j+1 generated on a side stream during step j
         # the generator's value bound fixes the fixed-point scales up front (no per-step clamp check)
         eng = MiniBatchEngine(K, D, b, dtype=dtype, device=dev, comm=comm, value_bound=stream.value_bound)

@@ -439,7 +439,11 @@ __device__ __forceinline__ void box_muller(const U4& r, float* z) {
   }
 }
 
-template <typename T, int TPR>
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// NORMS: the squared row norms of the stored values are fused in (xn != nullptr).
+template <typename T, int TPR, bool NORMS>
 __global__ __launch_bounds__(256) void blobs_kernel(T* X, int64_t i0, int64_t n, int D, int64_t ldx,
                                                     const float* __restrict__ centers,
                                                     int n_centers, float stddev, uint32_t k0,
@@ -476,21 +480,24 @@ __global__ __launch_bounds__(256) void blobs_kernel(T* X, int64_t i0, int64_t n,
 #pragma unroll
         for (int j = 0; j < EL; ++j) f[j] = __builtin_fmaf(stddev, z[j], m[j / 4][j % 4]);
         if constexpr (sizeof(T) == 2) {
-          uint32_t h[EL];
-#pragma unroll
-          for (int j = 0; j < EL; ++j) {  // RNE to bf16; values are finite by construction
-            const uint32_t u = __float_as_uint(f[j]);
-            h[j] = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
-            const float q = __uint_as_float(h[j] << 16);
-            sq = __builtin_fmaf(q, q, sq);
-          }
+          // RNE to bf16 two values per v_cvt_pk_bf16_f32 (gfx950; values are finite by
+          // construction, so the bits equal the integer rounding of the NumPy mirror)
           u32x4 w;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) w[j] = h[2 * j] | (h[2 * j + 1] << 16);
+          for (int j = 0; j < 4; ++j) {
+            w[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{f[2 * j], f[2 * j + 1]}, bf16x2));
+            if constexpr (NORMS) {
+              const float q0 = __uint_as_float(w[j] << 16), q1 = __uint_as_float(w[j] & 0xffff0000u);
+              sq = __builtin_fmaf(q0, q0, sq);
+              sq = __builtin_fmaf(q1, q1, sq);
+            }
+          }
           *(u32x4*)(out + EL * g) = w;
         } else {
+          if constexpr (NORMS) {
 #pragma unroll
-          for (int j = 0; j < EL; ++j) sq = __builtin_fmaf(f[j], f[j], sq);
+            for (int j = 0; j < EL; ++j) sq = __builtin_fmaf(f[j], f[j], sq);
+          }
           *(f32x4*)(out + EL * g) = f32x4{f[0], f[1], f[2], f[3]};
         }
       }
@@ -512,7 +519,7 @@ __global__ __launch_bounds__(256) void blobs_kernel(T* X, int64_t i0, int64_t n,
       }
     }
   }
-  if (xn) {
+  if constexpr (NORMS) {
 #pragma unroll
     for (int o = 1; o < TPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
     if (row_ok && t == 0) xn[il] = sq;
@@ -540,9 +547,15 @@ hipError_t launch_blobs(int dtype, void* X, int64_t i0, int64_t n, int D, int64_
   const int64_t tot = n * tpr;
   const unsigned nb = (unsigned)((tot + 255) / 256);
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#define MK_BLOBS(TT, TP)                                                                         \
-  hipLaunchKernelGGL((blobs_kernel<TT, TP>), dim3(nb), dim3(256), 0, s, (TT*)X, i0, n, D, ldx,   \
-                     centers, n_centers, stddev, k0, k1, y, xn, vec)
+#define MK_BLOBS(TT, TP)                                                                           \
+  do {                                                                                             \
+    if (xn)                                                                                        \
+      hipLaunchKernelGGL((blobs_kernel<TT, TP, true>), dim3(nb), dim3(256), 0, s, (TT*)X, i0, n, D, \
+                         ldx, centers, n_centers, stddev, k0, k1, y, xn, vec);                     \
+    else                                                                                           \
+      hipLaunchKernelGGL((blobs_kernel<TT, TP, false>), dim3(nb), dim3(256), 0, s, (TT*)X, i0, n,  \
+                         D, ldx, centers, n_centers, stddev, k0, k1, y, xn, vec);                  \
+  } while (0)
 #define MK_BLOBS_T(TT)                                                                           \
   switch (tpr) {                                                                                 \
     case 1: MK_BLOBS(TT, 1); break;                                                              \

@@ -35,6 +35,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     ab_d64) step ab_d64 300 python -u scripts/assign_ab.py --d 64 --k 4096 --n 10000000 --arms "default;assign_persist=1" ;;
     ab_f32) step ab_f32 300 python -u scripts/assign_ab.py --d 128 --k 256 --n 1000000 --dtype f32 --reps 20 \
                --arms "default;assign_persist=1" ;;
+    blobs) step blobs 200 python -u scripts/blobs_bench.py ;;
     ab_wide) step ab_wide 300 python -u scripts/assign_ab.py --d 768 --k 1024 --n 4000000 --arms "default" ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
     benchauto) step bench_nopg 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 --pg auto --no-also-incremental ;;
