@@ -7,6 +7,9 @@ Commands (the reference's top-bar controls, app.mjs:240-288, as a CLI):
 * ``predict``  -- labels of a dataset under a saved model
 * ``blobs``    -- write a synthetic Gaussian-blob dataset
 * ``room``     -- the trait-card game headless: seed/populate/auto-assign/dashboard/export/import
+* ``session``  -- one participant of a live, replicated room session: found it (hosting the
+                  rendezvous store) or join it, submit edits, leave -- the reference's tab
+                  joining a room link (app.mjs:70-118)
 * ``export``   -- checkpoint -> flat-float centroid JSON or room-export JSON (app.mjs:263-267)
 * ``import``   -- room-export JSON -> numeric checkpoint of trait vectors (app.mjs:268-282)
 * ``bench``    -- the headline benchmark (same as ``python bench.py``)
@@ -150,6 +153,54 @@ def cmd_room(a) -> int:
     d = r.dashboard()
     print("\n".join(d["chips"] + [" ".join(x for x in (row["name"], f"{row['bar_pct']}%", row["cohesion"],
                                                              row["top"], row["suggested"])) for row in d["rows"]]))
+    return 0
+
+
+def cmd_session(a) -> int:
+    """A scripted participant of a live room session (parallel/elastic.py): ``--found ROOM``
+    hosts the rendezvous store and starts the session, otherwise ``--join`` enters it; the
+    edits given on the command line are submitted in the first round, every round prints one
+    JSON status line, and all participants stop together at ``--until-round`` (the round
+    counter is replicated)."""
+    import datetime
+    import os
+    import socket
+    import time
+
+    import torch.distributed as dist
+
+    from .parallel.elastic import ElasticRoomReplica
+
+    store = dist.TCPStore(a.host, a.port, is_master=a.found is not None, wait_for_workers=False,
+                          timeout=datetime.timedelta(seconds=a.timeout))
+    member = a.member or f"{socket.gethostname()}-{os.getpid()}"
+    kw = dict(user=a.user, seed=a.seed, timeout_s=a.timeout)
+    if a.found is not None:
+        state = Path(a.load).read_text() if a.load else None
+        rep = ElasticRoomReplica.found(store, member, a.found or None, state_json=state, **kw)
+    else:
+        rep = ElasticRoomReplica.join(store, member, **kw)
+    first = True
+    while rep.round < a.until_round and not rep.left:
+        if first:
+            if a.populate:
+                rep.populate_test_data()
+            for name in a.centroid or []:
+                rep.add_centroid(name)
+            for spec in a.card or []:
+                title, _, traits = spec.partition(":")
+                rep.add_card(title, [t for t in traits.split(",") if t] or ["", ""])
+            if a.auto:
+                rep.auto_assign(seed=a.seed)
+            first = False
+        if a.leave_at is not None and rep.round >= a.leave_at:
+            rep.leave()
+        rep.sync()
+        print(json.dumps({"member": member, "round": rep.round, "epoch": rep.epoch, "peers": rep.peers,
+                          "roster": rep.roster, "left": rep.left, "digest": rep.digest()[:16]}), flush=True)
+        time.sleep(a.interval)
+    if a.export:
+        Path(a.export).write_text(rep.room.export_json())
     return 0
 
 
@@ -320,6 +371,25 @@ def build_parser():
     r.add_argument("--coin", action="store_true", help="flip a coin (Heads/Tails)")
     r.add_argument("--d12", action="store_true", help="roll a twelve-sided die")
     r.add_argument("--shuffle-names", action="store_true", help="print a shuffled order of the card titles")
+    se = sub.add_parser("session", help="one participant of a live replicated room session")
+    se.add_argument("--host", default="127.0.0.1", help="rendezvous (TCPStore) host")
+    se.add_argument("--port", type=int, required=True)
+    g = se.add_mutually_exclusive_group(required=True)
+    g.add_argument("--found", nargs="?", const="", metavar="ROOM", help="start the session (hosts the store)")
+    g.add_argument("--join", action="store_true", help="join a running session")
+    se.add_argument("--member", help="unique member id (default host-pid)")
+    se.add_argument("--user", help="display name (the reference's presence name)")
+    se.add_argument("--load", help="--found: start from a room JSON export")
+    se.add_argument("--populate", action="store_true")
+    se.add_argument("--centroid", action="append")
+    se.add_argument("--card", action="append", metavar="TITLE:TRAIT1,TRAIT2")
+    se.add_argument("--auto", action="store_true")
+    se.add_argument("--until-round", type=int, default=10)
+    se.add_argument("--leave-at", type=int, help="leave once the session reaches this round")
+    se.add_argument("--interval", type=float, default=0.1, help="seconds between rounds")
+    se.add_argument("--seed", type=int, default=0)
+    se.add_argument("--timeout", type=float, default=120.0)
+    se.add_argument("--export", help="write the room JSON here at the end")
     e = sub.add_parser("export", help="checkpoint -> flat centroid JSON or room-export JSON")
     e.add_argument("--model", required=True)
     e.add_argument("--format", choices=["flat", "room"], default="flat")
@@ -359,7 +429,7 @@ def main(argv=None) -> int:
         a, rest = la.parse_known_args(argv[1:])
         return cmd_launch(a, rest)
     a = build_parser().parse_args(argv)
-    return {"fit": cmd_fit, "predict": cmd_predict, "blobs": cmd_blobs, "room": cmd_room,
+    return {"fit": cmd_fit, "predict": cmd_predict, "blobs": cmd_blobs, "room": cmd_room, "session": cmd_session,
             "export": cmd_export, "import": cmd_import, "info": cmd_info, "plan": cmd_plan}[a.cmd](a)
 
 

@@ -86,3 +86,31 @@ def test_members_join_and_leave_a_running_session():
     cards = done["A"]["cards"]
     assert cards == done["C"]["cards"]
     assert any(t.startswith("B-") for t in cards) and any(t.startswith("C-") for t in cards)
+
+
+def test_cli_session_found_and_join(tmp_path):
+    """`python -m mikmeans session`: a founder hosting the rendezvous and a joiner editing the
+    same room end with byte-identical exports holding both members' edits."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = str(free_port())
+    base = [sys.executable, "-m", "mikmeans", "session", "--port", port, "--until-round", "40",
+            "--interval", "0.1"]
+    a = subprocess.Popen(base + ["--found", "CLIR", "--user", "Ann", "--centroid", "Sweet",
+                                 "--card", "Mango:Fruity,Sweet", "--export", str(tmp_path / "a.json")],
+                         cwd=root, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    b = subprocess.Popen(base + ["--join", "--user", "Bob", "--card", "Lime:Sour", "--export",
+                                 str(tmp_path / "b.json")],
+                         cwd=root, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    out_a, err_a = a.communicate(timeout=120)
+    out_b, err_b = b.communicate(timeout=120)
+    assert a.returncode == 0 and b.returncode == 0, (err_a[-2000:], err_b[-2000:])
+    ja, jb = (tmp_path / "a.json").read_text(), (tmp_path / "b.json").read_text()
+    assert ja == jb
+    titles = [c["title"] for c in json.loads(ja)["cards"]]
+    assert "Mango" in titles and "Lime" in titles
+    last_b = json.loads(out_b.strip().splitlines()[-1])
+    assert last_b["round"] == 40 and last_b["peers"] == 1 and sorted(last_b["roster"]) == ["Ann", "Bob"]
