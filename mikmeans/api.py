@@ -200,7 +200,7 @@ class KMeans(_Serving):
                  verbose: int = 0, mode: str = "learn", run_id: str | None = None,
                  checkpoint_every: int = 0, checkpoint_dir: str | None = None, metrics_path: str | None = None,
                  graph: bool = False, incremental: bool = True, chunk_rows: int | None = None,
-                 init_size: int | None = None, metric: str = "euclidean"):
+                 init_size: int | None = None, metric: str = "euclidean", algorithm: str = "lloyd"):
         self.n_clusters = int(n_clusters)
         self.init = init
         self.n_init = int(n_init)
@@ -229,6 +229,13 @@ class KMeans(_Serving):
             raise ValueError(f"metric must be 'euclidean' or 'cosine', got {metric!r}")
         # cosine = spherical k-means: unit rows, centres re-normalised after every M-step
         self.metric = metric
+        # 'hamerly' (sklearn's 'elkan' maps here too): the GPU E-step keeps per-row distance
+        # bounds and re-assigns only the rows they cannot vouch for (models/lloyd.py); the
+        # same Lloyd iterates up to bf16 near-ties, far fewer MFMA passes once few rows move
+        algo = {"elkan": "hamerly", "auto": "lloyd", "full": "lloyd"}.get(algorithm, algorithm)
+        if algo not in ("lloyd", "hamerly"):
+            raise ValueError(f"algorithm must be 'lloyd' or 'hamerly' ('elkan'), got {algorithm!r}")
+        self.algorithm = algo
         self.init_size = init_size
         self.history_: list[dict] = []
 
@@ -241,7 +248,8 @@ class KMeans(_Serving):
                    n_local_trials=cfg.n_local_trials, verbose=cfg.verbose, mode=cfg.mode,
                    run_id=cfg.run_id, checkpoint_every=cfg.checkpoint_every,
                    checkpoint_dir=cfg.checkpoint_dir, metrics_path=cfg.metrics_path, graph=cfg.graph,
-                   incremental=cfg.incremental, chunk_rows=cfg.chunk_rows, metric=cfg.metric, **kw)
+                   incremental=cfg.incremental, chunk_rows=cfg.chunk_rows, metric=cfg.metric,
+                   algorithm=cfg.algorithm, **kw)
 
     def get_config(self) -> KMeansConfig:
         return KMeansConfig(n_clusters=self.n_clusters, init=self.init if isinstance(self.init, str) else "array",
@@ -253,7 +261,7 @@ class KMeans(_Serving):
                             verbose=self.verbose, checkpoint_every=self.checkpoint_every,
                             checkpoint_dir=self.checkpoint_dir, metrics_path=self.metrics_path,
                             graph=self.graph, incremental=self.incremental, chunk_rows=self.chunk_rows,
-                            metric=self.metric)
+                            metric=self.metric, algorithm=self.algorithm)
 
     # ------------------------------------------------------------------- fit
     def _memory_plan(self, X, comm, device, D, weighted):
@@ -403,7 +411,7 @@ class KMeans(_Serving):
             else:
                 eng = LloydEngine(Xt, self.n_clusters, comm=comm, sample_weight=w, frozen=self.frozen,
                                   empty_policy=self.empty_cluster, n_features=D, incremental=self.incremental,
-                                  spherical=spherical)
+                                  spherical=spherical, bounded=self.algorithm == "hamerly")
                 if trial == 0:
                     stats = eng.stats if eng.gpu else None
                     tol_abs = tol_to_abs(self.tol, Xt, comm, n_global, D, stats=stats)
@@ -426,6 +434,8 @@ class KMeans(_Serving):
                 rec = st.as_dict()
                 counts = _eng.counts.tolist() if (self.verbose > 1 or _mlog is not None) else None
                 rec["counts"] = counts if self.verbose > 1 else None
+                if getattr(_eng, "bounded", False):
+                    rec["reassigned"] = _eng.reassigned     # rows the bounded E-step re-assigned
                 _hist.append(rec)
                 if _mlog is not None:
                     _mlog.log(st, counts)

@@ -143,7 +143,7 @@ __device__ __forceinline__ float sq16(const u32x4& w, float*) {
 // latency hides under the epilogue instead of opening every workgroup's life; the inertia
 // and changed counts go to the slots once per workgroup.  Same scores, same labels.
 template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false,
-          bool VARG = false, int PMAJ = 0, bool PERSIST = false, bool AST = false>
+          bool VARG = false, int PMAJ = 0, bool PERSIST = false, bool AST = false, bool TOP2 = false>
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
@@ -151,6 +151,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   // AST (a lower-register variant of the narrow kernels)
   constexpr bool WIDE = AST || DPAD > 256;
   static_assert(!(VARG && EXACT), "value-only argmin is the bf16 epilogue");
+  static_assert(!(TOP2 && (VARG || PERSIST)), "bounded E-step: keys / exact epilogues, one pass per block");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -302,11 +303,20 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     float best[C::P], seg_best[C::P];
     int bg[C::P];
     uint32_t vb[C::P], tb[C::P];   // VARG: running minimum (bits of a positive float), its tile
+    // TOP2 (bounded E-step): this lane's smallest and second-smallest score (keys: index bits
+    // included, <= 2^-17 relative -- the bounds' slack covers it), merged over lanes later
+    float m1[C::P], m2[C::P];
 #pragma unroll
     for (int p = 0; p < C::P; ++p) {
       best[p] = 3.0e38f; seg_best[p] = 3.0e38f; bg[p] = 0;
       vb[p] = 0x7f7fffffu; tb[p] = 0u;
+      m1[p] = 3.0e38f; m2[p] = 3.0e38f;
     }
+    // (m1 <= m2 stays true: the median of (m1, m2, k) is the new second smallest)
+    auto push2 = [&](int p, float k) {
+      m2[p] = __builtin_amdgcn_fmed3f(m1[p], m2[p], k);
+      m1[p] = fminf(m1[p], k);
+    };
     const int ngrp = nch * C::CT;   // one past the last tile (global tile numbering)
     const unsigned kmask = key6_mask();
 
@@ -406,6 +416,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
               const f32x4& sv = acc[p];
               const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
               const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
+              if constexpr (TOP2) { push2(p, k0); push2(p, k1); push2(p, k2); push2(p, k3); }
               seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
             }
           };
@@ -453,6 +464,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
             for (int p = 0; p < C::P; ++p) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
+                if constexpr (TOP2) m2[p] = __builtin_amdgcn_fmed3f(best[p], m2[p], acc[p][e]);
                 const bool lt = acc[p][e] < best[p];
                 best[p] = lt ? acc[p][e] : best[p];
                 bg[p] = lt ? u + e : bg[p];
@@ -577,26 +589,43 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     float inert = 0.f;
     int changed = 0;
     const int64_t pcur = pbase;
-    // ``old``: the row's previous label, ``xnv``: its caller norm (read by the caller of
-    // this lambda, i < N, lanes with (p & 3) == g only)
-    auto store = [&](int p, int k, float v, int old, float xnv) {
+    // TOP2: the second-smallest score of the point, merged over its 4 lane groups like the
+    // winner (two sorted pairs -> their two smallest); every lane takes part (shuffles)
+    auto second = [&](int p) -> float {
+      float a1 = EXACT ? best[p] : m1[p], a2 = m2[p];
+#pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) {
+        const float b1 = __shfl_xor(a1, o, 64), b2 = __shfl_xor(a2, o, 64);
+        const float n2 = fminf(fmaxf(a1, b1), fminf(a2, b2));
+        a1 = fminf(a1, b1);
+        a2 = n2;
+      }
+      return EXACT ? a2 : __uint_as_float(__float_as_uint(a2) & ~63u);
+    };
+    // ``oi``: where the row's outputs go (its row when a gathered batch scatters, else i);
+    // ``old``: the row's previous label, ``xnv``: its caller norm (read by the caller of this
+    // lambda, i < N, lanes with (p & 3) == g only); ``sec``: the second-smallest score (TOP2)
+    auto store = [&](int p, int64_t oi, int k, float v, int old, float xnv, float sec) {
       const float offp = ppo ? opt[(wid * 16 + r) * C::PP + p] : off;   // the seed offset (0: f32)
       // inertia without caller norms: the prologue parked |x|^2 of the fragments in LDS
       const float xv = (a.slots && !a.xn) ? xnl[(wid * 16 + r) * C::PP + p] : xnv;
-      const int64_t i = pcur + p * 16 + r;
       if (a.split_keys) {
         // compare the (positive) keys across splits; split_finish undoes the offset
         // (parked in mind[], which the caller provides whenever xn is given)
-        atomicMin(a.split_keys + i, split_key(v, k));
-        if (a.mind) a.mind[i] = offp;
+        atomicMin(a.split_keys + oi, split_key(v, k));
+        if (a.mind) a.mind[oi] = offp;
       } else {
         v -= offp;   // back to |c|^2 - 2 x.c
         if (a.track_changed) changed += (old != k);
-        a.labels[i] = k;
+        a.labels[oi] = k;
         if (a.xn || a.slots) {
           const float d = fmaxf(xv + v, 0.f);
           inert += d;
-          if (a.mind) a.mind[i] = d;
+          if (a.mind) a.mind[oi] = d;
+          if constexpr (TOP2) {   // Hamerly bounds: distances to the nearest and second nearest
+            a.ub[oi] = __builtin_sqrtf(d);
+            a.lb[oi] = __builtin_sqrtf(fmaxf(xv + (sec - offp), 0.f));
+          }
         }
       }
     };
@@ -606,10 +635,13 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         int k;
         float v;
         merged(p, k, v);
+        float sec = 0.f;
+        if constexpr (TOP2) sec = second(p);
         const int64_t i = pcur + p * 16 + r;
         if ((p & 3) == g && i < a.N) {
           const bool rd = !a.split_keys;
-          store(p, k, v, rd && a.track_changed ? a.labels[i] : -2, rd && a.xn ? a.xn[i] : 0.f);
+          const int64_t oi = a.scatter ? a.rows[i] : i;
+          store(p, oi, k, v, rd && a.track_changed ? a.labels[oi] : -2, rd && a.xn ? a.xn[oi] : 0.f, sec);
         }
       }
     } else {
@@ -636,7 +668,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       }
 #pragma unroll
       for (int p = 0; p < C::P; ++p)
-        if ((p & 3) == g && pcur + p * 16 + r < a.N) store(p, kk[p], vv[p], oldl[p], xg[p]);
+        if ((p & 3) == g && pcur + p * 16 + r < a.N) store(p, pcur + p * 16 + r, kk[p], vv[p], oldl[p], xg[p], 0.f);
     }
     if (a.slots && !a.split_keys) {
       // this pass's wave totals; over several passes (PERSIST) they accumulate in this
@@ -720,40 +752,39 @@ static int assign16_splits(int64_t nblk, int nch) {
 // D=64 K=2048 +8.5 %, K=1024 -3.7 %; D=32 K=1024 +5.6 %, K=512 -8.8 %).
 // Variant V_ASSIGN_VARG = 0/1 forces it off / on (A/B, tests).
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST,
+          bool TOP2>
 static void set_lds_attr() {
   static bool done = false;
   if (done) return;
-  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute(
+      (const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST, TOP2>,
+      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute(
+      (const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST, TOP2>,
+      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   done = true;
 }
 
-// Point-block-major MFMA issue (PMAJ), the bf16 default: each accumulator's NQ MFMAs back to
-// back instead of one A fragment against the P blocks in turn.  One-process A/B, bitwise the
-// same labels (profiles/r3_15_ab_pmaj*.log): D=128 K=1024 +2.8 %, K=2048 +3.8 %; D=256 K=512
-// +3.3 %; D=64 K=4096 (value-only argmin) +4.0 %, K=1024 +3.9 %; D=32 +1 %; f32 -0.5..-1 %
-// (its 16x16x4 MFMAs already chain 4 deep).  Same MFMAs, same registers; the gain is MFMA
-// pipe utilisation, not clock: block 0's scores are final 12 MFMAs before the last issue
-// instead of 3, so the epilogue's first reads no longer wait on the matrix pipe
-// (scripts/microbench/mfma_shape.hip mode 1, profiles/r3_17_mfma_issue_order.log: with the
-// key epilogue 84.4 -> 91.6 % at 1780 -> 1762 MHz, +7.5 % TF/s; 32x32x16 gains 3.6 % the
-// same way and stays 12 % behind).
-// Variant V_ASSIGN_PMAJ = 0/1 forces it off / on.  Issuing each block's epilogue between the next
-// blocks' MFMA chains instead measured -1.1 % at D=128, -3.8 % at D=64 K=4096, +2.2 % at D=64
-// K=1024 (profiles/r3_23_ab_pmaj_interleaved.log) and is not built.
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST,
+          bool TOP2>
+static void launch16_kt(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
+  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, TOP2>();
+  if (b.D == DPAD)
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST, TOP2>), grid,
+                       dim3(NW_ * 64), lds, s, b);
+  else
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST, TOP2>), grid,
+                       dim3(NW_ * 64), lds, s, b);
+}
 
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST>
 static void launch16_kpp(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST>();
-  if (b.D == DPAD)
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST>), grid,
-                       dim3(NW_ * 64), lds, s, b);
-  else
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST>), grid,
-                       dim3(NW_ * 64), lds, s, b);
+  if constexpr (!VARG && !PERSIST) {
+    // bounded E-step: the second-smallest score too (launch16_t keeps such calls on this path)
+    if (b.ub) return launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, true>(b, grid, lds, s);
+  }
+  launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, false>(b, grid, lds, s);
 }
 
 // Resident workgroups the whole chip holds for a launch geometry: the smaller of the
@@ -776,7 +807,7 @@ static void launch16_kp(const AssignArgs& b, dim3 grid, size_t lds, hipStream_t 
   // Persistent grid (variant V_ASSIGN_PERSIST = 1; default off): one-pass grids only (no
   // centre split), and only where the point blocks outnumber the resident slots.
   const int64_t slots = resident_workgroups(NW_, OCC, lds);
-  if (variant(V_ASSIGN_PERSIST) > 0 && grid.y == 1 && (int64_t)grid.x > slots) {
+  if (variant(V_ASSIGN_PERSIST) > 0 && grid.y == 1 && (int64_t)grid.x > slots && !b.ub && !b.scatter) {
     grid.x = (unsigned)slots;
     return launch16_kpp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, true, AST>(b, grid, lds, s);
   }
@@ -805,15 +836,17 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
   if (nblk <= 0) return hipSuccess;
-  const int splits = a.split_keys ? assign16_splits(nblk, a.Kpad / (16 * C::CT)) : 1;
+  // (bounded E-step: one-pass grid, keys or exact epilogue)
+  const int splits = (a.split_keys && !a.ub) ? assign16_splits(nblk, a.Kpad / (16 * C::CT)) : 1;
   AssignArgs b = a;
+  if ((a.ub != nullptr) != (a.lb != nullptr) || (a.scatter && !a.rows)) return hipErrorInvalidValue;
   if (splits == 1) b.split_keys = nullptr;
   const dim3 grid((unsigned)nblk, (unsigned)splits);
   bool varg = false;
   constexpr bool VARG_OK = sizeof(T) == 2 && DPAD <= 64;   // D=128: -12 % at K=1024, -4 % at 2048 (r3_11)
   if constexpr (VARG_OK) {
     const int e = variant(V_ASSIGN_VARG);
-    varg = e >= 0 ? e != 0 : a.Kpad >= (DPAD == 64 ? 2048 : 1024);
+    varg = (e >= 0 ? e != 0 : a.Kpad >= (DPAD == 64 ? 2048 : 1024)) && !a.ub;
   }
   if constexpr (VARG_OK) {
     if (varg) launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, AST>(b, grid, lds, s);

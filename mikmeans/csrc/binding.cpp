@@ -75,7 +75,8 @@ void check_i64(const Tensor& t, const char* name, int64_t numel_min);
 void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::optional<Tensor>& xn,
             const Tensor& labels, const c10::optional<Tensor>& mind,
             const c10::optional<Tensor>& slots, int64_t Kpad, int64_t dpad, bool track_changed,
-            const c10::optional<Tensor>& keys, const c10::optional<Tensor>& rows) {
+            const c10::optional<Tensor>& keys, const c10::optional<Tensor>& rows,
+            const c10::optional<Tensor>& ub, const c10::optional<Tensor>& lb, bool scatter) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   // gathered batch: N logical rows, row i = X[rows[i]] (indices from sample_index: in range
@@ -87,20 +88,30 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
     TORCH_CHECK(!(keys.has_value() && keys->defined()), "mikmeans: gathered rows take the one-pass grid");
   }
   const int64_t N = gathered ? rows->numel() : X.size(0);
+  TORCH_CHECK(!scatter || gathered, "mikmeans: scatter needs rows");
+  const int64_t NO = scatter ? X.size(0) : N;   // per-row outputs / inputs: at rows[i] when scattering
   const int D = (int)X.size(1);
   TORCH_CHECK(D <= dpad, "mikmeans: D exceeds dpad");
   TORCH_CHECK(mk::assign_kpad(dt, (int)dpad, (int)Kpad) == Kpad, "mikmeans: bad Kpad ", Kpad, " for dpad ",
               dpad);
+  const bool bounds = ub.has_value() && ub->defined();
+  TORCH_CHECK(bounds == (lb.has_value() && lb->defined()), "mikmeans: ub and lb come together");
+  if (bounds) {
+    check_f32(*ub, "ub", NO);
+    check_f32(*lb, "lb", NO);
+    TORCH_CHECK(xn.has_value() && !(keys.has_value() && keys->defined()),
+                "mikmeans: bounds need xn and the one-pass grid");
+  }
   check_cuda(pack, "pack");
   TORCH_CHECK(pack.is_contiguous() && pack.scalar_type() == X.scalar_type(),
               "mikmeans: pack dtype must match X");
   TORCH_CHECK(pack.numel() >= Kpad * dpad, "mikmeans: pack too small");
   check_f32(cn, "cn", mk::assign_cn_len((int)Kpad));
   TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kInt && labels.is_contiguous() &&
-                  labels.numel() >= N,
+                  labels.numel() >= NO,
               "mikmeans: labels must be contiguous int32 [N]");
-  if (xn.has_value()) check_f32(*xn, "xn", N);
-  if (mind.has_value()) check_f32(*mind, "mind", N);
+  if (xn.has_value()) check_f32(*xn, "xn", NO);
+  if (mind.has_value()) check_f32(*mind, "mind", NO);
   if (slots.has_value()) check_f64(*slots, "slots", mk::NSLOT * mk::SLOT_STRIDE);
   TORCH_CHECK(!mind.has_value() || xn.has_value(), "mikmeans: mind needs xn");
   mk::AssignArgs a;
@@ -117,6 +128,11 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
     a.split_keys = (unsigned long long*)keys->data_ptr<int64_t>();
   }
   if (gathered) a.rows = rows->data_ptr<int64_t>();
+  if (bounds) {
+    a.ub = ub->data_ptr<float>();
+    a.lb = lb->data_ptr<float>();
+  }
+  a.scatter = scatter ? 1 : 0;
   hip_check(mk::launch_assign16(dt, (int)dpad, a, stream()), "assign");
 }
 
@@ -550,6 +566,28 @@ void set_variant(Variant v, int value) { variant_table()[v] = value; }
 
 namespace {
 
+// Hamerly bounds step (csrc/rows.hip): work = 4 floats of device scratch (top-2 shifts, the
+// largest's centre, max |c|^2).
+void bounds_update(const Tensor& labels, const Tensor& ub, const Tensor& lb, const Tensor& shift2, const Tensor& cn,
+                   const Tensor& xn, const Tensor& cand, const Tensor& work, double qeps) {
+  const int64_t n = labels.numel();
+  const int K = (int)shift2.numel();
+  check_i32(labels, "labels", n);
+  check_f32(ub, "ub", n);
+  check_f32(lb, "lb", n);
+  check_f32(xn, "xn", n);
+  check_f32(shift2, "shift2", 1);
+  check_f32(cn, "cn", K);
+  check_f32(work, "work", 4);
+  check_cuda(cand, "cand");
+  TORCH_CHECK(cand.scalar_type() == at::kByte && cand.is_contiguous() && cand.numel() >= n,
+              "mikmeans: cand must be contiguous uint8 [n]");
+  hip_check(mk::launch_bounds_update(labels.data_ptr<int32_t>(), ub.data_ptr<float>(), lb.data_ptr<float>(),
+                                     shift2.data_ptr<float>(), cn.data_ptr<float>(), K, xn.data_ptr<float>(), n,
+                                     cand.data_ptr<uint8_t>(), work.data_ptr<float>(), (float)qeps, stream()),
+            "bounds_update");
+}
+
 // Tear down a stream capture that an error left open.  When a capture is invalidated,
 // hipStreamEndCapture inside torch's capture_end can fail and leave the stream in the
 // capturing state; every later launch on the legacy stream then fails with "operation
@@ -601,7 +639,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mikmeans native ops (gfx950 HIP kernels + host helpers)";
   m.def("assign", &assign, "fused MFMA distance + argmin (K2)", py::arg("X"), py::arg("pack"), py::arg("cn"),
         py::arg("xn"), py::arg("labels"), py::arg("mind"), py::arg("slots"), py::arg("Kpad"), py::arg("dpad"),
-        py::arg("track_changed"), py::arg("keys") = py::none(), py::arg("rows") = py::none());
+        py::arg("track_changed"), py::arg("keys") = py::none(), py::arg("rows") = py::none(),
+        py::arg("ub") = py::none(), py::arg("lb") = py::none(), py::arg("scatter") = false);
   m.def("update", &update, "LDS-privatised per-cluster sums/counts (K3)", py::arg("X"), py::arg("labels"),
         py::arg("K"), py::arg("slab"), py::arg("cnt_slab"), py::arg("n_chunks"), py::arg("weights"),
         py::arg("col_exp"), py::arg("cnt_exp"), py::arg("clamp"), py::arg("clamp_count") = py::none(),
@@ -657,6 +696,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_variant", [](int64_t i, int64_t v) { mk::set_variant((mk::Variant)i, (int)v); },
         "set an A/B switch (-1 = built-in rule); launchers never read the environment");
   (void)mk::variant(mk::V_ASSIGN_VARG);   // snapshot the environment now, at load
+  m.def("bounds_update", &bounds_update, "Hamerly bounds moved by the centre shifts; flags the rows to re-assign");
   m.def("capture_teardown", &capture_teardown, "end a stream capture an error left open (status found)");
   m.def("js_format", &js_format, "ECMAScript Number::toString of a double");
   m.def("js_array", &js_array, "JSON array of a CPU float tensor with JS number formatting");

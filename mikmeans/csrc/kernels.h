@@ -55,6 +55,13 @@ struct AssignArgs {
   // optional gathered batch: logical row i is X row rows[i] (labels / mind / xn stay
   // logical; without xn the inertia uses |x|^2 of the gathered fragments)
   const int64_t* rows = nullptr;
+  // bounded E-step (models/lloyd.py, Hamerly bounds): with ub/lb the kernel also tracks each
+  // point's second-smallest score and writes ub = distance to the chosen centre, lb = distance
+  // to the second nearest (one-pass grid, no value-only argmin); scatter: a gathered batch's
+  // outputs (labels, mind, ub, lb) and inputs (old labels, xn) live at row rows[i], not at i
+  float* ub = nullptr;
+  float* lb = nullptr;
+  int scatter = 0;
 };
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 
@@ -67,6 +74,16 @@ struct TransformArgs {
   int squared;          // 1: squared distances, 0: distances
 };
 hipError_t launch_transform(int dtype, int dpad, const TransformArgs& a, hipStream_t s);
+
+// ---- Hamerly bounds (csrc/rows.hip) ----------------------------------------------------
+// Moves every point's bounds by the last M-step's centre shifts (ub += |dc_label|,
+// lb -= the largest |dc_k| over k != label) and flags the points whose bounds no longer prove
+// their label (cand[i] = 1): shift2 = squared shifts [K], cn = |c|^2 of the packed centres
+// and xn = |x|^2 size the rounding slack of the kernel's distances, qeps the relative
+// rounding of the stored centres (bf16 2^-8, f32 2^-23); work: 4 floats scratch.
+hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, const float* shift2, const float* cn,
+                                int K, const float* xn, int64_t n, uint8_t* cand, float* work, float qeps,
+                                hipStream_t s);
 
 // ---- update (LDS-privatised scatter-add) -------------------------------------
 // Sums are accumulated in FIXED POINT: every contribution x*w is rounded to a

@@ -208,4 +208,81 @@ hipError_t launch_wdot(const float* a, const float* b, int64_t n, double* out, d
   return hipGetLastError();
 }
 
+// ---- Hamerly bounds ----------------------------------------------------------------------
+// Slack of a kernel distance: the assign's scores carry at most ~2^-17 of (|x|^2 + |c|^2 +
+// seed offset) of rounding (bf16 keys; f32 is finer), so |d_computed - d| <= sqrt(that); the
+// test below leaves 2^-14 of the score scale on each bound.
+constexpr float BOUND_EPS = 6.103515625e-05f;   // 2^-14
+
+// One workgroup: the largest and second-largest centre shift, the largest's centre, and the
+// largest |c|^2 (the slack's centre term) -> work[0..3].
+__global__ __launch_bounds__(1024) void shift_top2_kernel(const float* __restrict__ shift2,
+                                                         const float* __restrict__ cn, int K,
+                                                         float* __restrict__ work) {
+  float a1 = -1.f, a2 = -1.f, cm = 0.f;
+  int i1 = -1;
+  for (int k = threadIdx.x; k < K; k += 1024) {
+    const float d = sqrtf(fmaxf(shift2[k], 0.f));
+    if (d > a1) { a2 = a1; a1 = d; i1 = k; } else if (d > a2) { a2 = d; }
+    cm = fmaxf(cm, cn[k]);
+  }
+  __shared__ float s1[1024], s2[1024], sc[1024];
+  __shared__ int si[1024];
+  s1[threadIdx.x] = a1; s2[threadIdx.x] = a2; si[threadIdx.x] = i1; sc[threadIdx.x] = cm;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const int j = threadIdx.x + o;
+      const float b1 = s1[j], b2 = s2[j], x1 = s1[threadIdx.x], x2 = s2[threadIdx.x];
+      const bool take = b1 > x1 || (b1 == x1 && si[j] >= 0 && (si[threadIdx.x] < 0 || si[j] < si[threadIdx.x]));
+      s1[threadIdx.x] = take ? b1 : x1;
+      s2[threadIdx.x] = fmaxf(fminf(x1, b1), fmaxf(x2, b2));
+      si[threadIdx.x] = take ? si[j] : si[threadIdx.x];
+      sc[threadIdx.x] = fmaxf(sc[threadIdx.x], sc[j]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    work[0] = fmaxf(s1[0], 0.f);
+    work[1] = fmaxf(s2[0], 0.f);
+    work[2] = __int_as_float(si[0]);
+    work[3] = sc[0];
+  }
+}
+
+__global__ __launch_bounds__(256) void bounds_update_kernel(const int32_t* __restrict__ labels,
+                                                           float* __restrict__ ub, float* __restrict__ lb,
+                                                           const float* __restrict__ shift2,
+                                                           const float* __restrict__ xn, int64_t n,
+                                                           uint8_t* __restrict__ cand,
+                                                           const float* __restrict__ work, float qeps) {
+  const float d1 = work[0], d2 = work[1], cmax2 = work[3];
+  const int a1 = __float_as_int(work[2]);
+  // a centre's stored (quantised) copy moves by at most its shift plus its two roundings
+  const float qe = qeps * sqrtf(cmax2);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int a = labels[i];
+    if (a < 0) { cand[i] = 1; continue; }       // unassigned: a full assign decides
+    const float u = ub[i] + sqrtf(fmaxf(shift2[a], 0.f)) + qe;
+    const float l = lb[i] - (a == a1 ? d2 : d1) - qe;
+    ub[i] = u;
+    lb[i] = l;
+    const float e = sqrtf(BOUND_EPS * (2.f * xn[i] + cmax2));
+    cand[i] = (u + 2.f * e >= l) ? 1 : 0;
+  }
+}
+
+hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, const float* shift2, const float* cn,
+                                int K, const float* xn, int64_t n, uint8_t* cand, float* work, float qeps,
+                                hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (K < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(shift_top2_kernel, dim3(1), dim3(1024), 0, s, shift2, cn, K, work);
+  int64_t nb = (n + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  hipLaunchKernelGGL(bounds_update_kernel, dim3((unsigned)nb), dim3(256), 0, s, labels, ub, lb, shift2, xn, n,
+                     cand, work, qeps);
+  return hipGetLastError();
+}
+
 }  // namespace mk

@@ -73,9 +73,16 @@ class LloydEngine:
                  sample_weight: torch.Tensor | None = None, frozen=None,
                  empty_policy: str = "keep", n_features: int | None = None, segments: int = 1,
                  overlap_sw: int = 8, incremental: bool = False, delta_cap: float = 0.125,
-                 spherical: bool = False):
+                 spherical: bool = False, bounded: bool = False):
         from ..ops import pad_columns
 
+        # Bounded E-step (Hamerly 2010): per-point bounds on the distance to the assigned
+        # centre (ub) and to the second nearest (lb), moved by each M-step's centre shifts;
+        # only points whose bounds no longer prove their label are re-assigned (a gathered
+        # assign over them).  The same Lloyd iterates up to bf16 near-ties (a re-assigned
+        # point's workgroup seed offset differs from the full assign's); per-step inertia is
+        # not tracked (the fit's final inertia is exact).  GPU, keys / exact epilogues.
+        self.bounded = bool(bounded)
         # Incremental M-step: keep per-rank integer running totals of the cluster sums and
         # re-scatter only the rows whose label changed (+ to the new label, - from the old).
         # Bitwise identical to the full M-step (integer fixed point); the full pass runs
@@ -123,6 +130,7 @@ class LloydEngine:
             self._init_gpu()
         else:
             self.xn = cpu_ops.row_sqnorm(self.X)
+            self.bounded = False          # (the CPU path assigns every row each step)
 
     # ------------------------------------------------------------------ setup
     def _init_gpu(self):
@@ -185,6 +193,16 @@ class LloydEngine:
             self.mind = torch.empty(self.n, dtype=torch.float32, device=dev)
         if self.weights is not None:
             self._wscratch = torch.empty(C.WDOT_SCRATCH, dtype=torch.float64, device=dev)
+        if self.bounded and (self.segments > 1 or self.empty_policy == "farthest" or self.weights is not None):
+            native.warn_once("bounded E-step: not with segment overlap, 'farthest' or sample weights; full E-steps")
+            self.bounded = False
+        if self.bounded:
+            self.ub = torch.zeros(self.n, dtype=torch.float32, device=dev)
+            self.lb = torch.zeros(self.n, dtype=torch.float32, device=dev)
+            self.cand = torch.empty(self.n, dtype=torch.uint8, device=dev)
+            self._bwork = torch.empty(4, dtype=torch.float32, device=dev)
+            self._bvalid = False          # bounds not yet set: the next E-step is a full one
+            self.reassigned = self.n      # rows the last E-step re-assigned
         self.delta = None
         if self.incremental:
             if self.scales.nw:
@@ -222,6 +240,8 @@ class LloydEngine:
         if self.delta is not None:
             t.update(delta_prev=self.delta["prev"], delta_list=self.delta["list"],
                      delta_count=self.delta["count"], delta_tot=self.delta["tot"])
+        if getattr(self, "bounded", False):
+            t.update(bound_ub=self.ub, bound_lb=self.lb, bound_cand=self.cand, bound_work=self._bwork)
         out = {k: _r(v.numel() * v.element_size()) for k, v in t.items()}
         for name in ("bufs", "stage"):          # streaming: two chunk / staging buffers
             bl = getattr(self, name, None)
@@ -236,6 +256,7 @@ class LloydEngine:
         """Unassign every point (the reference's Restart, app.mjs:167-178); the next
         step re-assigns from the current centres and counts every point as changed."""
         self.labels.fill_(-1)
+        self._bvalid = False
         return self
 
     def set_centers(self, centers: torch.Tensor):
@@ -248,6 +269,7 @@ class LloydEngine:
         self.C[:, : self.D] = c
         if self.gpu:
             self.pk.finalize(0, None, self.C)
+        self._bvalid = False              # centres replaced: bounds no longer hold
         return self
 
     @property
@@ -291,6 +313,9 @@ class LloydEngine:
         (tests/test_gpu_rccl.py)."""
         self.capture_error = None
         if not self.gpu or not self.n or getattr(self, "_graphs", None) is not None:
+            return self
+        if self.bounded:
+            self.capture_error = "bounded E-step: the rows to re-assign are counted on the host"
             return self
         dev = self.device
         main = torch.cuda.current_stream(dev)
@@ -393,7 +418,10 @@ class LloydEngine:
                 self._weighted_inertia()
         elif self.n:
             with _phase("mikmeans.assign"):
-                self.pk.assign(self.X, self.xn, self.labels, self.mind, self.slots, True)
+                if self.bounded:
+                    self._bounded_assign()
+                else:
+                    self.pk.assign(self.X, self.xn, self.labels, self.mind, self.slots, True)
             with _phase("mikmeans.update"):
                 d = self.delta
                 if d is not None:
@@ -418,6 +446,23 @@ class LloydEngine:
                      self.col_exp, self.cnt_exp, False, col_exp2=sc.col_exp2)
             C.reduce_cols(self.slab, self.n_chunks, self.K, self.Dp, sc.wide_cols, sc.wide_exps,
                           self.packed[KD + self.K + 2:])
+
+    def _bounded_assign(self):
+        """E-step over the points the Hamerly bounds cannot vouch for (all of them the first
+        time).  One host read per step: the number of rows to re-assign."""
+        if not self._bvalid:
+            self.pk.assign(self.X, self.xn, self.labels, None, self.slots, True, ub=self.ub, lb=self.lb)
+            self._bvalid = True
+            self.reassigned = self.n
+            return
+        qeps = 2.0 ** -8 if self.dtype == torch.bfloat16 else 2.0 ** -22
+        self._C.bounds_update(self.labels, self.ub, self.lb, self.shift, self.pk.cn, self.xn, self.cand,
+                              self._bwork, qeps)
+        rows = torch.nonzero(self.cand[: self.n]).flatten()
+        self.reassigned = int(rows.numel())
+        if self.reassigned:
+            self.pk.assign(self.X, self.xn, self.labels, None, self.slots, True, rows=rows, ub=self.ub, lb=self.lb,
+                           scatter=True)
 
     def _weighted_inertia(self):
         """packed[inertia] = sum_i w_i mind_i (f64, one pass, no n x 8-byte temporaries)."""
@@ -535,7 +580,9 @@ class LloydEngine:
         K, KD = self.K, self.K * self.Dp
         s = torch.stack([self.packed[KD + K], self.packed[KD + K + 1], self.shift.double().sum(),
                          self.shift.double().max()]).cpu().tolist()
-        return IterStats(self.iteration, s[0], int(round(s[1])), s[2], s[3])
+        # (bounded E-step: the slots hold only the re-assigned rows' distances)
+        inertia = math.nan if getattr(self, "bounded", False) else s[0]
+        return IterStats(self.iteration, inertia, int(round(s[1])), s[2], s[3])
 
     def run(self, max_iter: int, tol: float = 0.0, *, check_every: int = 1, callback=None):
         """Iterate until ``shift <= tol`` (absolute), no label changes, or ``max_iter``.

@@ -96,15 +96,18 @@ class CentroidPack:
         self._C.finalize(mode, packed, Cold, Cnew, frozen, mb_counts, self.pack, self.cn, shift, counts,
                          self.dpad, self.Kpad)
 
-    def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False, rows=None):
+    def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False, rows=None,
+               ub=None, lb=None, scatter: bool = False):
         """K2 on these centres (``X`` column-padded, 16-B rows).  ``rows`` (int64, device):
-        assign the gathered batch X[rows] without materialising it (labels etc. logical)."""
+        assign the gathered batch X[rows] without materialising it (labels etc. logical, or
+        at the rows themselves with ``scatter``).  ``ub`` / ``lb``: also write every point's
+        distance to its nearest and second-nearest centre (the bounded E-step's bounds)."""
         if rows is not None:
             self._C.assign(X, self.pack, self.cn, xn, labels, mind, slots, self.Kpad, self.dpad,
-                           track_changed, None, rows)
+                           track_changed, None, rows, ub, lb, scatter)
             return
         keys = None
-        if 0 < X.shape[0] <= SPLIT_MAX_ROWS:
+        if 0 < X.shape[0] <= SPLIT_MAX_ROWS and ub is None:
             # small batches split the centre range across workgroups (assign16 grid.y);
             # the kernels leave the scratch all-ones again, so it is filled only once
             if self._keys is None or self._keys.numel() < X.shape[0]:
@@ -113,7 +116,7 @@ class CentroidPack:
             if xn is not None and mind is None:   # the splits park each point's seed offset there
                 mind = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)
         self._C.assign(X, self.pack, self.cn, xn, labels, mind, slots, self.Kpad, self.dpad,
-                       track_changed, keys)
+                       track_changed, keys, None, ub, lb, False)
 
 
 def pack_centers(centers: torch.Tensor, D: int, dtype: torch.dtype, device):

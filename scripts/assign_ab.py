@@ -27,6 +27,8 @@ from mikmeans.parallel import Comm  # noqa: E402
 def parse_arm(spec: str) -> dict:
     out = {}
     for kv in filter(None, spec.split(",")):
+        if kv.strip() in ("default", "-"):
+            continue
         k, v = kv.split("=")
         out[k.strip()] = int(v)
     return out

@@ -28,7 +28,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     multirank) step pytest_multirank 400 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 400 --timeout-method thread ;;
     memplan) step pytest_memplan 600 python -u -m pytest tests/test_gpu_memplan.py tests/test_gpu_minibatch.py -v --timeout 200 --timeout-method thread ;;
     newkern) step pytest_newkern 600 python -u -m pytest tests/test_gpu_kernels.py -v --timeout 200 --timeout-method thread \
-               -k "persistent or wide or transform or d768 or col_absmax or matches_reference or past_1024" ;;
+               -k "${NK_SEL:-persistent or wide or transform or d768 or col_absmax or matches_reference or past_1024}" ;;
+    bounded) step pytest_bounded 400 python -u -m pytest tests/test_gpu_bounded.py -v --timeout 200 --timeout-method thread ;;
     ab_head) step ab_head 300 python -u scripts/assign_ab.py --arms "default;assign_persist=1;assign_geom=4;assign_geom=4,assign_persist=1" ;;
     ab_d256) step ab_d256 300 python -u scripts/assign_ab.py --d 256 --k 512 --n 16777216 \
                --arms "default;assign_geom=3;assign_persist=1;assign_geom=3,assign_persist=1" ;;

@@ -203,6 +203,19 @@ def test_chunk_rows_on_cpu_is_the_resident_fit():
     assert b.get_config().chunk_rows == 512
 
 
+def test_algorithm_option_cpu():
+    """algorithm='hamerly' (alias 'elkan') is the GPU bounded E-step; on the CPU path every
+    row is assigned each step, so the fit is Lloyd's, bit for bit."""
+    X, _ = blobs(3000, 8, 6, seed=5)
+    a = mikmeans.KMeans(6, device="cpu", seed=1).fit(X)
+    b = mikmeans.KMeans(6, device="cpu", seed=1, algorithm="elkan").fit(X)
+    assert b.algorithm == "hamerly" and b.get_config().algorithm == "hamerly"
+    assert torch.equal(a.cluster_centers_, b.cluster_centers_) and a.inertia_ == b.inertia_
+    assert mikmeans.KMeans.from_config(b.get_config()).algorithm == "hamerly"
+    with pytest.raises(ValueError):
+        mikmeans.KMeans(3, algorithm="exact")
+
+
 def _spherical_reference(X, C0, iters):
     """Plain NumPy spherical k-means (Dhillon & Modha): unit rows, cosine argmax, mean, renormalise."""
     Xn = X / np.linalg.norm(X, axis=1, keepdims=True)

@@ -1,0 +1,101 @@
+"""Bounded (Hamerly) E-step on the GPU (models/lloyd.py ``bounded``; csrc/assign16.hip TOP2,
+csrc/rows.hip bounds_update): the bounds the kernels keep are valid bounds on the true
+distances, the rows they cannot vouch for are the only ones re-assigned, and the fit follows
+the full-E-step Lloyd iterates."""
+import pytest
+import torch
+
+from mikmeans import KMeans, ops
+from mikmeans.data import blobs as B
+from mikmeans.models.lloyd import LloydEngine
+from mikmeans.ops import cpu as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _true_dists(X, C, dtype):
+    """Distances of every row to every (quantised) centre, f64 on the host."""
+    Cq = ref.quantize_centers(C.cpu(), dtype).double()
+    return torch.cdist(X.cpu().double(), Cq)
+
+
+@pytest.mark.parametrize("dtype,d,k", [(torch.float32, 64, 100), (torch.bfloat16, 128, 256),
+                                       (torch.bfloat16, 32, 40)])
+def test_full_assign_writes_nearest_and_second_distances(native, dtype, d, k):
+    """The first (full) bounded E-step: ub = distance to the label's centre, lb = distance to
+    the second nearest centre, both against the quantised centres the kernel ranks."""
+    X = B.make_blobs(60_000, d, 16, seed=k, dtype=dtype, device=DEV)
+    C0 = X[:k].float() + 0.1
+    e = LloydEngine(X, k, bounded=True).set_centers(C0)
+    e._bounded_assign()
+    torch.cuda.synchronize()
+    dist = _true_dists(X, C0, dtype)
+    two = dist.topk(2, dim=1, largest=False).values
+    lab = e.labels.cpu().long()
+    scale = (X.cpu().double() ** 2).sum(1).sqrt() + dist.max()
+    assert (dist.gather(1, lab[:, None])[:, 0] - two[:, 0]).abs().max() <= 1e-3 * scale.max()
+    torch.testing.assert_close(e.ub.cpu().double(), two[:, 0], rtol=2e-3, atol=2e-3 * float(scale.mean()))
+    torch.testing.assert_close(e.lb.cpu().double(), two[:, 1], rtol=2e-3, atol=2e-3 * float(scale.mean()))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bounds_stay_valid_and_skip_rows(native, dtype):
+    """After every step: every row the bounds vouch for (not a candidate) really is nearest to
+    its label's centre, ub >= its distance, lb <= the second distance; and once the centres
+    settle, most rows are skipped."""
+    X = B.make_blobs(200_000, 64, 32, seed=3, dtype=dtype, device=DEV)
+    K = 48
+    C0 = X[:K].float()
+    e = LloydEngine(X, K, bounded=True).set_centers(C0)
+    skipped = []
+    for it in range(12):
+        e.step()
+        torch.cuda.synchronize()
+        C = e.centers.clone()
+        if it >= 1:
+            skipped.append(1.0 - e.reassigned / e.n)
+        # bounds of the step's labels against the centres that step assigned with (its C0)
+        dist = _true_dists(X, C0, dtype)
+        lab = e.labels.cpu().long()
+        dl = dist.gather(1, lab[:, None])[:, 0]
+        masked = dist.clone()
+        masked.scatter_(1, lab[:, None], float("inf"))
+        d2 = masked.min(1).values
+        slack = 1e-3 * ((X.cpu().double() ** 2).sum(1).sqrt() + dist.max())
+        assert bool((e.ub.cpu().double() >= dl - slack).all()), it
+        assert bool((e.lb.cpu().double() <= d2 + slack).all()), it
+        assert bool((dl <= d2 + slack).all()), it            # the label is (near-)nearest
+        C0 = C
+    assert skipped[-1] > 0.5, skipped
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bounded_engine_follows_lloyd(native, dtype):
+    X = B.make_blobs(300_000, 128, 64, seed=9, dtype=dtype, device=DEV)
+    C0 = X[:64].float()
+    ea = LloydEngine(X, 64).set_centers(C0)
+    eb = LloydEngine(X, 64, bounded=True).set_centers(C0)
+    for it in range(15):
+        ea.step()
+        eb.step()
+        torch.cuda.synchronize()
+        agree = (ea.labels == eb.labels).float().mean().item()
+        assert agree >= 0.9999, (it, agree)
+        assert ea.last_stats().n_changed == pytest.approx(eb.last_stats().n_changed, abs=0.0002 * ea.n)
+    torch.testing.assert_close(eb.centers, ea.centers, rtol=1e-3, atol=1e-3)
+    assert eb.reassigned < ea.n // 4
+
+
+def test_kmeans_hamerly_fit(native):
+    X = B.make_blobs(400_000, 64, 50, seed=2, dtype=torch.float32, device=DEV)
+    ka = KMeans(50, init="random", seed=4, max_iter=40, tol=1e-6, device=DEV).fit(X)
+    kb = KMeans(50, init="random", seed=4, max_iter=40, tol=1e-6, device=DEV, algorithm="hamerly").fit(X)
+    assert kb._engine.bounded and not ka._engine.bounded
+    assert kb.inertia_ == pytest.approx(ka.inertia_, rel=1e-5)
+    assert (kb.labels_ == ka.labels_).float().mean().item() >= 0.9999
+    re = [h["reassigned"] for h in kb.history_]
+    assert re[0] == X.shape[0] and min(re) < X.shape[0] // 10
+    assert KMeans(4, algorithm="elkan").algorithm == "hamerly"
+    with pytest.raises(ValueError):
+        KMeans(4, algorithm="bogus")
