@@ -73,6 +73,8 @@ def main(argv=None):
                          "all-reduce, one launch; eager fallback if capture fails).  auto: on for one rank "
                          "(cfg2's 0.7 ms steps gain ~1 %%); off for N > 1, where the host already runs "
                          "far ahead of ~3 ms steps")
+    ap.add_argument("--kpp-sampling", default="exact", choices=["exact", "two-stage"],
+                    help="cfg4 multi-rank k-means++: exact (2 collectives per centre) or two-stage (1)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="host: host-staged gloo collectives, rank r on GPU r %% device_count -- a "
                          "rehearsal of the N-rank job on fewer GPUs (N ranks may share one GPU; the "
@@ -128,7 +130,8 @@ def main(argv=None):
         extra["datagen_s"] = round(time.perf_counter() - t0, 3)
         t0 = time.perf_counter()
         if args.config == "cfg4":
-            C0 = init_kmeanspp(X, D, K, N, s, comm, args.seed)
+            C0 = init_kmeanspp(X, D, K, N, s, comm, args.seed, sampling=args.kpp_sampling)
+            extra["init_sampling"] = args.kpp_sampling
         else:
             C0 = init_random(X, D, K, N, s, comm, args.seed)
         sync()
@@ -142,6 +145,12 @@ def main(argv=None):
             sync()
             extra["init_owner_path_s"] = round(time.perf_counter() - t0, 3)
             extra["init_owner_path_same_centres"] = bool(torch.equal(C0, C1))
+            # the one-all-gather-per-centre draw through the same group (same centres at W=1)
+            t0 = time.perf_counter()
+            C2 = init_kmeanspp(X, D, K, N, s, comm, args.seed, owner_path=True, sampling="two-stage")
+            sync()
+            extra["init_two_stage_s"] = round(time.perf_counter() - t0, 3)
+            extra["init_two_stage_same_centres"] = bool(torch.equal(C0, C2))
         from mikmeans.parallel import memplan
 
         mp = memplan.plan_resident(e - s, D, K, dtype, incremental=args.incremental,

@@ -200,7 +200,8 @@ class KMeans(_Serving):
                  verbose: int = 0, mode: str = "learn", run_id: str | None = None,
                  checkpoint_every: int = 0, checkpoint_dir: str | None = None, metrics_path: str | None = None,
                  graph: bool = False, incremental: bool = True, chunk_rows: int | None = None,
-                 init_size: int | None = None, metric: str = "euclidean", algorithm: str = "lloyd"):
+                 init_size: int | None = None, metric: str = "euclidean", algorithm: str = "lloyd",
+                 init_sampling: str = "exact"):
         self.n_clusters = int(n_clusters)
         self.init = init
         self.n_init = int(n_init)
@@ -236,6 +237,11 @@ class KMeans(_Serving):
         if algo not in ("lloyd", "hamerly"):
             raise ValueError(f"algorithm must be 'lloyd' or 'hamerly' ('elkan'), got {algorithm!r}")
         self.algorithm = algo
+        # multi-rank k-means++: 'exact' (world-size invariant, two collectives per centre) or
+        # 'two-stage' (one all-gather per centre; models/init.py)
+        if init_sampling not in ("exact", "two-stage"):
+            raise ValueError(f"init_sampling must be 'exact' or 'two-stage', got {init_sampling!r}")
+        self.init_sampling = init_sampling
         self.init_size = init_size
         self.history_: list[dict] = []
 
@@ -249,7 +255,7 @@ class KMeans(_Serving):
                    run_id=cfg.run_id, checkpoint_every=cfg.checkpoint_every,
                    checkpoint_dir=cfg.checkpoint_dir, metrics_path=cfg.metrics_path, graph=cfg.graph,
                    incremental=cfg.incremental, chunk_rows=cfg.chunk_rows, metric=cfg.metric,
-                   algorithm=cfg.algorithm, **kw)
+                   algorithm=cfg.algorithm, init_sampling=cfg.init_sampling, **kw)
 
     def get_config(self) -> KMeansConfig:
         return KMeansConfig(n_clusters=self.n_clusters, init=self.init if isinstance(self.init, str) else "array",
@@ -261,7 +267,7 @@ class KMeans(_Serving):
                             verbose=self.verbose, checkpoint_every=self.checkpoint_every,
                             checkpoint_dir=self.checkpoint_dir, metrics_path=self.metrics_path,
                             graph=self.graph, incremental=self.incremental, chunk_rows=self.chunk_rows,
-                            metric=self.metric, algorithm=self.algorithm)
+                            metric=self.metric, algorithm=self.algorithm, init_sampling=self.init_sampling)
 
     # ------------------------------------------------------------------- fit
     def _memory_plan(self, X, comm, device, D, weighted):
@@ -500,7 +506,7 @@ class KMeans(_Serving):
         seed = self.seed + trial
         if not streaming:
             return resolve_init(self.init, src, D, self.n_clusters, n_global, start, comm, seed,
-                                self.n_local_trials)
+                                self.n_local_trials, sampling=self.init_sampling)
         name = self.init.lower().replace("_", "-") if isinstance(self.init, str) else None
         if name == "random":
             from .models.init import init_random
@@ -514,7 +520,7 @@ class KMeans(_Serving):
         Xs = src.sample_rows(m, self.seed)
         s_global, s_start = _shard_info(Xs.shape[0], comm, comm.device)
         return resolve_init(self.init, Xs, D, self.n_clusters, s_global, s_start, comm, seed,
-                            self.n_local_trials)
+                            self.n_local_trials, sampling=self.init_sampling)
 
     def fit_predict(self, X, y=None, sample_weight=None):
         return self.fit(X, sample_weight=sample_weight)._out(self.labels_)
@@ -609,9 +615,12 @@ class MiniBatchKMeans(_Serving):
     def __init__(self, n_clusters: int = 8, *, batch_size: int = 1024, max_iter: int = 100,
                  max_steps: int | None = None, init="k-means++", init_size: int | None = None,
                  dtype="float32", device=None, seed: int = 0, comm: Comm | None = None, frozen=None,
-                 tol: float = 0.0, verbose: int = 0):
+                 tol: float = 0.0, verbose: int = 0, init_sampling: str = "exact"):
         self.n_clusters = int(n_clusters)
         self.batch_size = int(batch_size)
+        if init_sampling not in ("exact", "two-stage"):
+            raise ValueError(f"init_sampling must be 'exact' or 'two-stage', got {init_sampling!r}")
+        self.init_sampling = init_sampling
         self.max_iter = int(max_iter)
         self.max_steps = max_steps
         self.init = init
@@ -638,7 +647,7 @@ class MiniBatchKMeans(_Serving):
         n_global, start = _shard_info(sample.shape[0], comm, sample.device)
         Xs = pad_columns(sample) if sample.is_cuda else sample
         return resolve_init(self.init, Xs, D, self.n_clusters, n_global, start, comm, self.seed,
-                            None)[:, :D]
+                            None, sampling=self.init_sampling)[:, :D]
 
     def fit(self, X, *, resume_from=None, checkpoint_every: int = 0, checkpoint_dir=None):
         """Fit on a tensor/array (random batches each step; ``max_iter`` epochs).
@@ -923,7 +932,7 @@ def fit_predict(X, k: int, **kw):
 
 
 def kmeans_plusplus(X, n_clusters: int, *, seed: int = 0, n_local_trials=None, comm: Comm | None = None,
-                    dtype="float32", device=None):
+                    dtype="float32", device=None, sampling: str = "exact"):
     """k-means++ seeding only; returns the ``[K, D]`` initial centres."""
     comm = comm or get_comm()
     dev = _default_device(device, X)
@@ -932,5 +941,5 @@ def kmeans_plusplus(X, n_clusters: int, *, seed: int = 0, n_local_trials=None, c
     Xp = pad_columns(Xt) if Xt.is_cuda else Xt
     n_global, start = _shard_info(Xt.shape[0], comm, dev)
     name = "greedy-k-means++" if (n_local_trials or 1) > 1 else "k-means++"
-    c = resolve_init(name, Xp, D, n_clusters, n_global, start, comm, seed, n_local_trials)
+    c = resolve_init(name, Xp, D, n_clusters, n_global, start, comm, seed, n_local_trials, sampling=sampling)
     return c.cpu().numpy() if was_numpy else c

@@ -209,9 +209,13 @@ hipError_t launch_wdot(const float* a, const float* b, int64_t n, double* out, d
 }
 
 // ---- Hamerly bounds ----------------------------------------------------------------------
-// Slack of a kernel distance: the assign's scores carry at most ~2^-17 of (|x|^2 + |c|^2 +
-// seed offset) of rounding (bf16 keys; f32 is finer), so |d_computed - d| <= sqrt(that); the
-// test below leaves 2^-14 of the score scale on each bound.
+// ub / lb bound the TRUE distances of a row to its label's f32 centre and to every other f32
+// centre.  The assign writes raw kernel distances (sqrt of scores against the quantised
+// pack); the step after, while cand[i] still marks the row as freshly assigned, they are
+// widened once: the scores carry at most ~2^-17 of (|x|^2 + |c|^2 + seed offset) of rounding
+// (bf16 keys; f32 is finer), so d^2 moves by at most delta = 2^-14 (2|x|^2 + |c|max^2) --
+// sqrt(d^2 +- delta), which costs delta / 2d, not sqrt(delta) -- and the quantised centre
+// sits within q = qeps |c|max of the f32 one.  Every later step only adds the f32 shifts.
 constexpr float BOUND_EPS = 6.103515625e-05f;   // 2^-14
 
 // One workgroup: the largest and second-largest centre shift, the largest's centre, and the
@@ -256,19 +260,25 @@ __global__ __launch_bounds__(256) void bounds_update_kernel(const int32_t* __res
                                                            const float* __restrict__ xn, int64_t n,
                                                            uint8_t* __restrict__ cand,
                                                            const float* __restrict__ work, float qeps) {
-  const float d1 = work[0], d2 = work[1], cmax2 = work[3];
+  const float d1 = work[0], d2 = work[1];
   const int a1 = __float_as_int(work[2]);
-  // a centre's stored (quantised) copy moves by at most its shift plus its two roundings
-  const float qe = qeps * sqrtf(cmax2);
+  // |c|max of the centres the last E-step ranked (the pack now holds the moved ones)
+  const float cmax = sqrtf(work[3]) + d1;
+  const float q = qeps * cmax, cmax2 = cmax * cmax;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int a = labels[i];
     if (a < 0) { cand[i] = 1; continue; }       // unassigned: a full assign decides
-    const float u = ub[i] + sqrtf(fmaxf(shift2[a], 0.f)) + qe;
-    const float l = lb[i] - (a == a1 ? d2 : d1) - qe;
+    float u = ub[i], l = lb[i];
+    if (cand[i]) {                               // raw kernel distances: widen them once
+      const float delta = BOUND_EPS * (2.f * xn[i] + cmax2);
+      u = sqrtf(u * u + delta) + q;
+      l = sqrtf(fmaxf(l * l - delta, 0.f)) - q;
+    }
+    u += sqrtf(fmaxf(shift2[a], 0.f));
+    l -= (a == a1 ? d2 : d1);
     ub[i] = u;
     lb[i] = l;
-    const float e = sqrtf(BOUND_EPS * (2.f * xn[i] + cmax2));
-    cand[i] = (u + 2.f * e >= l) ? 1 : 0;
+    cand[i] = (u >= l) ? 1 : 0;
   }
 }
 

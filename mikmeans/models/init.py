@@ -74,7 +74,8 @@ def init_random(X, D, K, n_global, start, comm: Comm, seed: int, *, fetch=None,
 
 def init_kmeanspp(X: torch.Tensor, D: int, K: int, n_global: int, start: int, comm: Comm, seed: int,
                   n_local_trials: int = 1, xn: torch.Tensor | None = None,
-                  prune: bool | None = None, owner_path: bool | None = None) -> torch.Tensor:
+                  prune: bool | None = None, owner_path: bool | None = None,
+                  sampling: str = "exact") -> torch.Tensor:
     """k-means++ seeding; returns replicated f32 centres [K, D].
 
     ``X`` may be column-padded (only the first ``D`` columns are real).  ``prune``
@@ -83,7 +84,18 @@ def init_kmeanspp(X: torch.Tensor, D: int, K: int, n_global: int, start: int, co
     ``owner_path`` (GPU): draw through the multi-rank owner selection (all-gather of the
     potentials, owner kernel, all-reduce of the row) -- default only when world > 1; a
     one-rank RCCL group can force it to rehearse the collectives.
+
+    ``sampling``: ``"exact"`` draws each centre at ``u * (global potential)`` through the
+    rank that owns that point -- two dependent collectives per seeding step (the potentials'
+    all-gather, then the drawn row's all-reduce), world-size invariant.  ``"two-stage"``
+    draws a row inside every rank first (at ``u * local potential``) and ships it with the
+    potential in ONE all-gather; a second number ``v`` then picks the rank with probability
+    potential_r / total.  Same D^2 distribution (P(rank) P(row | rank) = d2_i / total), one
+    round trip per step -- what a W = 8 seeding of K = 4096 centres is bound by -- but the
+    centres drawn depend on how the rows are sharded.  W = 1 gives the exact centres.
     """
+    if sampling not in ("exact", "two-stage"):
+        raise ValueError(f"k-means++ sampling must be 'exact' or 'two-stage', got {sampling!r}")
     if prune is None:
         prune = os.environ.get("MIKMEANS_KPP_PRUNE", "1") not in ("0", "")
     rng = np.random.default_rng(seed)
@@ -95,12 +107,27 @@ def init_kmeanspp(X: torch.Tensor, D: int, K: int, n_global: int, start: int, co
     L = max(1, int(n_local_trials))
     # every random number up front: the GPU loop then never waits for the host
     u = torch.as_tensor(rng.random((K - 1) * L), dtype=torch.float64)
+    # (the rank-choice numbers come after u: the exact path's stream is unchanged)
+    v = torch.as_tensor(rng.random((K - 1) * L), dtype=torch.float64) if sampling == "two-stage" else None
     if X.is_cuda:
         multi = comm.world > 1 if owner_path is None else bool(owner_path)
-        _kpp_gpu(X, centers, K, comm, u.to(X.device), L, prune, multi)
+        if v is not None and multi:
+            _kpp_gpu_two_stage(X, centers, K, comm, u.to(X.device), v.to(X.device), L, prune)
+        else:
+            _kpp_gpu(X, centers, K, comm, u.to(X.device), L, prune, multi)
     else:
-        _kpp_cpu(X, centers, K, comm, u, L)
+        _kpp_cpu(X, centers, K, comm, u, L, v)
     return centers[:, :D].contiguous()
+
+
+def pick_rank(totals: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+    """Index r with probability totals[r] / sum (inverse CDF at ``v * sum``), on the tensors'
+    device without a host read; past-the-end (rounding) goes to the last non-empty rank."""
+    cum = torch.cumsum(totals, 0)
+    r = torch.searchsorted(cum, (v * cum[-1]).reshape(1), right=True)[0]
+    nz = (totals > 0).to(torch.int64)
+    last = (nz * torch.arange(totals.numel(), device=totals.device)).max()
+    return torch.minimum(r, last)
 
 
 def _local_target(totals_all: torch.Tensor, u: torch.Tensor, rank: int) -> tuple[torch.Tensor, torch.Tensor]:
@@ -185,7 +212,62 @@ def _kpp_gpu(X, centers, K, comm: Comm, u, L, prune: bool = True, multi: bool = 
             d2_pass(centers[k], k, d2, bs, True)
 
 
-def _kpp_cpu(X, centers, K, comm: Comm, u, L):
+def _kpp_gpu_two_stage(X, centers, K, comm: Comm, u, v, L, prune: bool = True):
+    """Multi-rank k-means++ with one all-gather per seeding step (``sampling='two-stage'``):
+    every rank draws its L candidates from its own D^2 (csrc/kpp.hip sample, target
+    ``u * local potential``), the message [potential, L rows] is all-gathered, and every
+    rank picks the same source rank per trial with ``v`` (:func:`pick_rank`).  Greedy
+    trials add the one all-reduce of their L potentials, as in the exact path."""
+    C = native.require()
+    n, dev, D = X.shape[0], X.device, X.shape[1]
+    rpb = max(256, -(-n // 2048)) if n else 256
+    nb = max(1, -(-n // rpb))
+    d2 = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+    bs = torch.zeros(nb, dtype=torch.float64, device=dev)
+    d2c = torch.empty_like(d2) if L > 1 else None
+    bsc = torch.zeros_like(bs) if L > 1 else None
+    rows = torch.zeros((L, D), dtype=torch.float32, device=dev)
+    msg = torch.zeros(1 + L * D, dtype=torch.float64, device=dev)
+    owner = torch.zeros(max(n, 1), dtype=torch.int32, device=dev) if prune else None
+    cc = torch.empty(K, dtype=torch.float32, device=dev) if prune else None
+
+    def d2_pass(c, k, d2_, bs_, record):
+        if owner is None:
+            C.kpp_d2(X, c, False, d2_, bs_, rpb)
+        else:
+            C.kpp_cc(centers, k, c, cc)
+            C.kpp_d2(X, c, False, d2_, bs_, rpb, owner, cc, k, k if record else -1)
+
+    if n:
+        C.kpp_d2(X, centers[0], True, d2, bs, rpb)
+    for k in range(1, K):
+        if n:
+            msg[0] = bs.sum()
+            for t in range(L):
+                C.kpp_sample(bs, d2, rpb, u[(k - 1) * L + t: (k - 1) * L + t + 1], X, rows[t], None, 1, None, 0)
+            msg[1:] = rows.reshape(-1)
+        else:
+            msg.zero_()
+        allm = comm.all_gather(msg).reshape(comm.world, 1 + L * D)
+        tots = allm[:, 0]
+        cand = torch.stack([allm.index_select(0, pick_rank(tots, v[(k - 1) * L + t]).reshape(1))[0,
+                                                1 + t * D: 1 + (t + 1) * D] for t in range(L)]).float()
+        if L == 1:
+            centers[k] = cand[0]
+        else:
+            pots = torch.zeros(L, dtype=torch.float64, device=dev)
+            for t in range(L):
+                if n:
+                    d2c.copy_(d2)
+                    d2_pass(cand[t], k, d2c, bsc, False)
+                    pots[t] = bsc.sum()
+            comm.allreduce_(pots)
+            centers[k] = cand[torch.argmin(pots)]
+        if n:
+            d2_pass(centers[k], k, d2, bs, True)
+
+
+def _kpp_cpu(X, centers, K, comm: Comm, u, L, v=None):
     n = X.shape[0]
     Xf = X.to(torch.float32)
     D = X.shape[1]
@@ -197,44 +279,70 @@ def _kpp_cpu(X, centers, K, comm: Comm, u, L):
     for k in range(1, K):
         # one all-gather of the rank potentials and one all-reduce of the L drawn rows per
         # step (the trials draw from the same D^2), as on the GPU
+        cs = torch.cumsum(d2.double(), 0) if n else None
+        if v is not None and comm.world > 1:
+            # two-stage: a row per trial drawn inside this rank, one all-gather, rank by v
+            msg = torch.zeros(1 + L * D, dtype=torch.float64)
+            if n:
+                msg[0] = cs[-1]
+                for t in range(L):
+                    msg[1 + t * D: 1 + (t + 1) * D] = Xf[_draw(cs, d2, float(u[(k - 1) * L + t]) * float(cs[-1]))]
+            allm = comm.all_gather(msg).reshape(comm.world, 1 + L * D)
+            cand = torch.stack([allm[int(pick_rank(allm[:, 0], v[(k - 1) * L + t])), 1 + t * D: 1 + (t + 1) * D]
+                                for t in range(L)]).float()
+            _finish_step(comm, centers, k, cand, d2, dist_to, L)
+            if n:
+                d2 = torch.minimum(d2, dist_to(centers[k]))
+            continue
         allt = comm.all_gather(d2.double().sum().reshape(1)).reshape(-1)
         cand = torch.zeros((L, D), dtype=torch.float32)
-        cs = torch.cumsum(d2.double(), 0) if n else None
         for t in range(L):
             target, _ = _local_target(allt, u[(k - 1) * L + t], comm.rank)
             tv = float(target.item())
             if tv >= 0 and n:
-                i = int(torch.searchsorted(cs, torch.tensor([tv], dtype=torch.float64), right=True).item())
-                if i >= n or d2[min(i, n - 1)] <= 0:
-                    pos = torch.nonzero(d2 > 0).flatten()
-                    i = int(pos[-1].item()) if pos.numel() else 0
-                cand[t] = Xf[i]
+                cand[t] = Xf[_draw(cs, d2, tv)]
         comm.allreduce_(cand)
-        if L == 1:
-            centers[k] = cand[0]
-        else:
-            pots = torch.tensor([float(torch.minimum(d2, dist_to(cand[t])).double().sum()) for t in range(L)],
-                                dtype=torch.float64)
-            comm.allreduce_(pots)
-            centers[k] = cand[int(torch.argmin(pots))]
+        _finish_step(comm, centers, k, cand, d2, dist_to, L)
         if n:
             d2 = torch.minimum(d2, dist_to(centers[k]))
+
+
+def _draw(cs: torch.Tensor, d2: torch.Tensor, tv: float) -> int:
+    """Row at cumulative potential ``tv`` (host path); rounding past the end -> last row with d2 > 0."""
+    n = d2.numel()
+    i = int(torch.searchsorted(cs, torch.tensor([tv], dtype=torch.float64), right=True).item())
+    if i >= n or d2[min(i, n - 1)] <= 0:
+        pos = torch.nonzero(d2 > 0).flatten()
+        i = int(pos[-1].item()) if pos.numel() else 0
+    return i
+
+
+def _finish_step(comm, centers, k, cand, d2, dist_to, L):
+    if L == 1:
+        centers[k] = cand[0]
+        return
+    n = d2.numel()
+    pots = torch.tensor([float(torch.minimum(d2, dist_to(cand[t])).double().sum()) if n else 0.0
+                         for t in range(L)], dtype=torch.float64)
+    comm.allreduce_(pots)
+    centers[k] = cand[int(torch.argmin(pots))]
 
 
 def default_local_trials(K: int) -> int:
     return 2 + int(math.log(K)) if K > 1 else 1
 
 
-def resolve_init(init, X, D, K, n_global, start, comm: Comm, seed: int, n_local_trials=None):
+def resolve_init(init, X, D, K, n_global, start, comm: Comm, seed: int, n_local_trials=None,
+                 sampling: str = "exact"):
     if isinstance(init, str):
         name = init.lower().replace("_", "-")
         if name == "random":
             return init_random(X, D, K, n_global, start, comm, seed)
         if name in ("k-means++", "kmeans++", "kpp"):
-            return init_kmeanspp(X, D, K, n_global, start, comm, seed, n_local_trials or 1)
+            return init_kmeanspp(X, D, K, n_global, start, comm, seed, n_local_trials or 1, sampling=sampling)
         if name in ("greedy-k-means++", "greedy-kmeans++"):
             return init_kmeanspp(X, D, K, n_global, start, comm, seed,
-                                 n_local_trials or default_local_trials(K))
+                                 n_local_trials or default_local_trials(K), sampling=sampling)
         raise ValueError(f"unknown init {init!r}")
     c = torch.as_tensor(np.asarray(init) if not torch.is_tensor(init) else init, dtype=torch.float32)
     if c.shape != (K, D):

@@ -452,9 +452,11 @@ class LloydEngine:
         time).  One host read per step: the number of rows to re-assign."""
         if not self._bvalid:
             self.pk.assign(self.X, self.xn, self.labels, None, self.slots, True, ub=self.ub, lb=self.lb)
+            self.cand.fill_(1)            # every row's bounds are raw kernel distances
             self._bvalid = True
             self.reassigned = self.n
             return
+        # (distance of a quantised centre from its f32 copy, relative to |c|: bf16 RNE)
         qeps = 2.0 ** -8 if self.dtype == torch.bfloat16 else 2.0 ** -22
         self._C.bounds_update(self.labels, self.ub, self.lb, self.shift, self.pk.cn, self.xn, self.cand,
                               self._bwork, qeps)

@@ -30,6 +30,9 @@ for s in ${STEPS:-smoke tests bench prof}; do
     newkern) step pytest_newkern 600 python -u -m pytest tests/test_gpu_kernels.py -v --timeout 200 --timeout-method thread \
                -k "${NK_SEL:-persistent or wide or transform or d768 or col_absmax or matches_reference or past_1024}" ;;
     bounded) step pytest_bounded 400 python -u -m pytest tests/test_gpu_bounded.py -v --timeout 200 --timeout-method thread ;;
+    hamerly) step hamerly 400 python -u scripts/hamerly_ab.py ${HAM_ARGS:-} ;;
+    dp2host) step bench_dp2host 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+               --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --comm host --steps 10 --warmup 2 ;;
     ab_head) step ab_head 300 python -u scripts/assign_ab.py --arms "default;assign_persist=1;assign_geom=4;assign_geom=4,assign_persist=1" ;;
     ab_d256) step ab_d256 300 python -u scripts/assign_ab.py --d 256 --k 512 --n 16777216 \
                --arms "default;assign_geom=3;assign_persist=1;assign_geom=3,assign_persist=1" ;;

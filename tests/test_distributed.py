@@ -176,3 +176,69 @@ def test_kmeanspp_world_size_invariant(trials):
         outs = spawn_local(_kpp, world, trials)
         for o in outs:
             assert torch.equal(o, ref), (world, trials)
+
+
+def _kpp2(comm, trials):
+    from mikmeans.models.init import init_kmeanspp
+
+    X = _data()
+    s, e = shard_range(N, comm.rank, comm.world)
+    return init_kmeanspp(X[s:e], D, K, N, s, comm, seed=9, n_local_trials=trials, sampling="two-stage")
+
+
+@pytest.mark.parametrize("trials", [1, 3])
+def test_kmeanspp_two_stage(trials):
+    """sampling='two-stage' (one all-gather per centre): every rank holds the same centres,
+    each a data row, no row drawn twice; W = 1 gives the exact path's centres; empty
+    shards (W = 8 over 6000 rows) never win a draw."""
+    from mikmeans.parallel import Comm
+
+    X = _data()
+    ref = _kpp(Comm.local(), trials)
+    assert torch.equal(_kpp2(Comm.local(), trials), ref)
+    for world in (2, 8):
+        outs = spawn_local(_kpp2, world, trials)
+        for o in outs:
+            assert torch.equal(o, outs[0]), (world, trials)
+        C = outs[0]
+        hit = (C[:, None, :] == X.float()[None, :, :C.shape[1]]).all(-1).any(1)
+        assert bool(hit.all()) and torch.unique(C, dim=0).shape[0] == K
+
+
+def test_pick_rank_is_proportional():
+    """pick_rank(totals, v) selects rank r with probability totals[r] / sum (inverse CDF),
+    never an empty rank, and the rounding edge (v -> 1) lands on the last non-empty rank."""
+    from mikmeans.models.init import pick_rank
+
+    tots = torch.tensor([3.0, 0.0, 1.0, 4.0, 0.0], dtype=torch.float64)
+    v = (torch.arange(80_000, dtype=torch.float64) + 0.5) / 80_000
+    got = torch.bincount(torch.stack([pick_rank(tots, x) for x in v[::8]]), minlength=5).double()
+    freq = got / got.sum()
+    assert torch.allclose(freq, tots / tots.sum(), atol=2e-3) and got[1] == 0 and got[4] == 0
+    assert int(pick_rank(tots, torch.tensor(1.0, dtype=torch.float64))) == 3
+    assert int(pick_rank(tots, torch.tensor(0.0, dtype=torch.float64))) == 0
+
+
+def test_two_stage_draw_distribution():
+    """The two-stage draw is the D^2 distribution: with 2 shards and a fixed first centre,
+    the second centre's frequency over many seeds matches d2_i / sum d2 (chi-square-ish)."""
+    from mikmeans.models.init import _draw, pick_rank
+
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(12, 2, generator=g)
+    d2 = ((X - X[0]) ** 2).sum(1).double()
+    shards = [(0, 5), (5, 12)]
+    cs = [torch.cumsum(d2[a:b], 0) for a, b in shards]
+    tots = torch.stack([c[-1] for c in cs])
+    rng = torch.Generator().manual_seed(1)
+    trials = 60_000
+    u = torch.rand(trials, generator=rng, dtype=torch.float64)
+    v = torch.rand(trials, generator=rng, dtype=torch.float64)
+    hits = torch.zeros(12, dtype=torch.float64)
+    for j in range(trials):
+        r = int(pick_rank(tots, v[j]))
+        a, b = shards[r]
+        hits[a + _draw(cs[r], d2[a:b], float(u[j]) * float(cs[r][-1]))] += 1
+    p = d2 / d2.sum()
+    assert hits[0] == 0
+    assert torch.allclose(hits / trials, p, atol=0.006)

@@ -81,7 +81,8 @@ def test_bounded_engine_follows_lloyd(native, dtype):
         eb.step()
         torch.cuda.synchronize()
         agree = (ea.labels == eb.labels).float().mean().item()
-        assert agree >= 0.9999, (it, agree)
+        # (bf16: a re-assigned row's workgroup seed differs from the full pass's -> near-ties)
+        assert agree >= (0.9999 if dtype == torch.float32 else 0.999), (it, agree)
         assert ea.last_stats().n_changed == pytest.approx(eb.last_stats().n_changed, abs=0.0002 * ea.n)
     torch.testing.assert_close(eb.centers, ea.centers, rtol=1e-3, atol=1e-3)
     assert eb.reassigned < ea.n // 4

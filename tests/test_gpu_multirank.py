@@ -80,6 +80,18 @@ def case_kpp_greedy(comm):
     return {"C": init_kmeanspp(Xl, D, K, N, s, comm, seed=9, n_local_trials=3)}
 
 
+def case_kpp_two_stage(comm):
+    """sampling='two-stage': one all-gather per centre (the drawn rows ride with the
+    potentials); rank-count dependent, so checked for replica agreement, not W=1 equality."""
+    from mikmeans.models.init import init_kmeanspp
+    from mikmeans.ops import pad_columns
+
+    X = pad_columns(_data())
+    Xl, s = _shard(comm, X)
+    return {f"C{t}": init_kmeanspp(Xl, D, K, N, s, comm, seed=9, n_local_trials=t, sampling="two-stage")
+            for t in (1, 3)}
+
+
 def _fit(comm, **kw):
     import mikmeans
 
@@ -192,7 +204,7 @@ def case_ckpt_resume(comm, path):
 CASES = {f.__name__[5:]: f for f in (case_lloyd_random_bf16, case_lloyd_random_f32, case_lloyd_kpp,
                                      case_kpp_greedy, case_fit_farthest, case_fit_weighted, case_fit_cosine,
                                      case_fit_graph, case_stream_agreement, case_minibatch_fit,
-                                     case_fit_empty_shard)}
+                                     case_fit_empty_shard, case_kpp_two_stage)}
 CASES["fit_kpp_greedy_f32"] = _fit_kpp
 
 
@@ -279,9 +291,11 @@ def _check(name, ref, outs):
 
 
 W2_CASES = ["lloyd_random_bf16", "lloyd_random_f32", "lloyd_kpp", "kpp_greedy", "fit_farthest", "fit_weighted",
-            "fit_cosine", "fit_graph", "fit_kpp_greedy_f32", "stream_agreement", "minibatch_fit"]
+            "fit_cosine", "fit_graph", "fit_kpp_greedy_f32", "stream_agreement", "minibatch_fit",
+            "kpp_two_stage"]
 W4_CASES = ["lloyd_random_bf16", "lloyd_kpp", "kpp_greedy", "fit_farthest", "fit_weighted", "minibatch_fit",
-            "fit_empty_shard"]
+            "fit_empty_shard", "kpp_two_stage"]
+_NOT_W1 = ("minibatch_fit", "stream_agreement", "fit_empty_shard", "kpp_two_stage")
 
 
 @pytest.fixture(scope="module")
@@ -297,15 +311,31 @@ def w4(w2):
     return spawn_local(_suite, 4, W4_CASES, ("ckpt_resume", path), device="cuda", timeout=600)
 
 
-@pytest.mark.parametrize("name", [n for n in W2_CASES if n not in ("minibatch_fit", "stream_agreement")])
+@pytest.mark.parametrize("name", [n for n in W2_CASES if n not in _NOT_W1])
 def test_w2_equals_w1(refs, w2, name):
     outs, _ = w2
     _check(name, refs[name], [o[name] for o in outs])
 
 
-@pytest.mark.parametrize("name", [n for n in W4_CASES if n not in ("minibatch_fit", "fit_empty_shard")])
+@pytest.mark.parametrize("name", [n for n in W4_CASES if n not in _NOT_W1])
 def test_w4_equals_w1(refs, w4, name):
     _check(name, refs[name], [o[name] for o in w4])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_kpp_two_stage_replicas(refs, w2, w4, world):
+    """Two-stage k-means++ on real ranks: every rank holds the same centres, each one a data
+    row, none drawn twice; at W = 1 it is the exact path (refs)."""
+    from mikmeans.ops import pad_columns
+
+    res = [o["kpp_two_stage"] for o in (w2[0] if world == 2 else w4)]
+    X = pad_columns(_data()).float().cpu()[:, :D]
+    for t in (1, 3):
+        for r in res:
+            assert torch.equal(r[f"C{t}"], res[0][f"C{t}"])
+        C = res[0][f"C{t}"].cpu()
+        assert bool((C[:, None, :] == X[None]).all(-1).any(1).all()) and torch.unique(C, dim=0).shape[0] == K
+    assert torch.equal(refs["kpp_two_stage"]["C3"].cpu(), refs["kpp_greedy"]["C"].cpu())
 
 
 def test_w2_stream_agreement(w2):

@@ -213,6 +213,9 @@ def test_rccl_kmeanspp_multi_rank_path(rccl, trials):
     b = init_kmeanspp(X, d, k, n, 0, rccl, seed=5, n_local_trials=trials, owner_path=True)
     # the owner path draws with target - 0 on the only rank: same row every step
     assert torch.equal(a, b)
+    # two-stage (one all-gather per centre): on one rank the in-rank draw is the exact one
+    c = init_kmeanspp(X, d, k, n, 0, rccl, seed=5, n_local_trials=trials, owner_path=True, sampling="two-stage")
+    assert torch.equal(a, c)
 
 
 def test_rccl_minibatch_and_api(rccl):
