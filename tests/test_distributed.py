@@ -156,6 +156,29 @@ def test_minibatch_fit_uneven_shards_same_step_count():
         assert torch.equal(o["C"], outs[0]["C"])
 
 
+def _minibatch_tol(comm, tol):
+    import mikmeans
+
+    n = 1025
+    X = _data()[:n]
+    s, e = shard_range(n, comm.rank, comm.world, align=1)
+    km = mikmeans.MiniBatchKMeans(4, batch_size=64, max_iter=3, seed=2, comm=comm, tol=tol).fit(X[s:e])
+    return {"C": km.cluster_centers_.clone(), "steps": km.n_steps_}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_minibatch_tol_stops_every_rank_together(world):
+    """The mini-batch tolerance check reads the replicated centre shift, so every rank stops
+    at the same step (the first check, with a huge tol) and keeps the same centres; tol=0
+    runs all max_iter epochs."""
+    stop = spawn_local(_minibatch_tol, world, 1e30)
+    full = spawn_local(_minibatch_tol, world, 0.0)
+    assert {o["steps"] for o in stop} == {10}
+    assert len({o["steps"] for o in full}) == 1 and full[0]["steps"] > 10
+    for o in stop:
+        assert torch.equal(o["C"], stop[0]["C"])
+
+
 def _kpp(comm, trials):
     from mikmeans.models.init import init_kmeanspp
 
