@@ -185,7 +185,11 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     }
   };
 
-  const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
+  // rows this launch assigns: N, or the device count of a compacted batch (wave-uniform;
+  // a workgroup past it leaves before any barrier)
+  const int64_t N = a.n_dev ? min(a.N, *a.n_dev) : a.N;
+  if (a.n_dev && (int64_t)blockIdx.x * C::PTS >= N) return;
+  const int64_t nblk = (N + C::PTS - 1) / C::PTS;
   int64_t blk = blockIdx.x;
   int64_t pbase = blk * C::PTS + (int64_t)wid * (C::P * 16);
   u32x4 xr[C::P][C::NQ];
@@ -196,7 +200,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   // or a row norm under a data-dependent branch) serialised the P round trips.
   auto row_of = [&](int p) -> int64_t {
     const int64_t row = pbase + p * 16 + r;
-    return row < a.N ? row : (a.N - 1);
+    return row < N ? row : (N - 1);
   };
   auto load_frags = [&](int p, int64_t src) {
     const T* rp = (const T*)a.X + src * a.ldx + g * C::V;
@@ -638,7 +642,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         float sec = 0.f;
         if constexpr (TOP2) sec = second(p);
         const int64_t i = pcur + p * 16 + r;
-        if ((p & 3) == g && i < a.N) {
+        if ((p & 3) == g && i < N) {
           const bool rd = !a.split_keys;
           const int64_t oi = a.scatter ? a.rows[i] : i;
           store(p, oi, k, v, rd && a.track_changed ? a.labels[oi] : -2, rd && a.xn ? a.xn[oi] : 0.f, sec);
@@ -655,7 +659,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
 #pragma unroll
       for (int p = 0; p < C::P; ++p) {
         const int64_t i = pcur + p * 16 + r;
-        const bool mine = (p & 3) == g && i < a.N;
+        const bool mine = (p & 3) == g && i < N;
         oldl[p] = mine && a.track_changed ? a.labels[i] : -2;
         xg[p] = mine && a.xn ? a.xn[i] : 0.f;
       }
@@ -668,7 +672,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       }
 #pragma unroll
       for (int p = 0; p < C::P; ++p)
-        if ((p & 3) == g && pcur + p * 16 + r < a.N) store(p, pcur + p * 16 + r, kk[p], vv[p], oldl[p], xg[p], 0.f);
+        if ((p & 3) == g && pcur + p * 16 + r < N) store(p, pcur + p * 16 + r, kk[p], vv[p], oldl[p], xg[p], 0.f);
     }
     if (a.slots && !a.split_keys) {
       // this pass's wave totals; over several passes (PERSIST) they accumulate in this
@@ -807,7 +811,8 @@ static void launch16_kp(const AssignArgs& b, dim3 grid, size_t lds, hipStream_t 
   // Persistent grid (variant V_ASSIGN_PERSIST = 1; default off): one-pass grids only (no
   // centre split), and only where the point blocks outnumber the resident slots.
   const int64_t slots = resident_workgroups(NW_, OCC, lds);
-  if (variant(V_ASSIGN_PERSIST) > 0 && grid.y == 1 && (int64_t)grid.x > slots && !b.ub && !b.scatter) {
+  if (variant(V_ASSIGN_PERSIST) > 0 && grid.y == 1 && (int64_t)grid.x > slots && !b.ub && !b.scatter &&
+      !b.n_dev) {
     grid.x = (unsigned)slots;
     return launch16_kpp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, true, AST>(b, grid, lds, s);
   }
@@ -837,7 +842,7 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   const int64_t nblk = (a.N + C::PTS - 1) / C::PTS;
   if (nblk <= 0) return hipSuccess;
   // (bounded E-step: one-pass grid, keys or exact epilogue)
-  const int splits = (a.split_keys && !a.ub) ? assign16_splits(nblk, a.Kpad / (16 * C::CT)) : 1;
+  const int splits = (a.split_keys && !a.ub && !a.n_dev) ? assign16_splits(nblk, a.Kpad / (16 * C::CT)) : 1;
   AssignArgs b = a;
   if ((a.ub != nullptr) != (a.lb != nullptr) || (a.scatter && !a.rows)) return hipErrorInvalidValue;
   if (splits == 1) b.split_keys = nullptr;

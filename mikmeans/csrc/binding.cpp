@@ -76,7 +76,8 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
             const Tensor& labels, const c10::optional<Tensor>& mind,
             const c10::optional<Tensor>& slots, int64_t Kpad, int64_t dpad, bool track_changed,
             const c10::optional<Tensor>& keys, const c10::optional<Tensor>& rows,
-            const c10::optional<Tensor>& ub, const c10::optional<Tensor>& lb, bool scatter) {
+            const c10::optional<Tensor>& ub, const c10::optional<Tensor>& lb, bool scatter,
+            const c10::optional<Tensor>& count) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   // gathered batch: N logical rows, row i = X[rows[i]] (indices from sample_index: in range
@@ -133,6 +134,12 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
     a.lb = lb->data_ptr<float>();
   }
   a.scatter = scatter ? 1 : 0;
+  if (count.has_value() && count->defined()) {   // device row count: assign rows[:min(N, count)]
+    check_i64(*count, "count", 1);
+    TORCH_CHECK(gathered && !(keys.has_value() && keys->defined()),
+                "mikmeans: a device row count takes a gathered batch on the one-pass grid");
+    a.n_dev = count->data_ptr<int64_t>();
+  }
   hip_check(mk::launch_assign16(dt, (int)dpad, a, stream()), "assign");
 }
 
@@ -568,6 +575,18 @@ namespace {
 
 // Hamerly bounds step (csrc/rows.hip): work = 4 floats of device scratch (top-2 shifts, the
 // largest's centre, max |c|^2).
+void compact(const Tensor& cand, const Tensor& rows, const Tensor& count, const Tensor& scratch) {
+  check_cuda(cand, "cand");
+  TORCH_CHECK(cand.scalar_type() == at::kByte && cand.is_contiguous(), "mikmeans: cand must be contiguous uint8");
+  const int64_t n = cand.numel();
+  check_i64(rows, "rows", n);
+  check_i64(count, "count", 1);
+  check_i64(scratch, "scratch", mk::compact_blocks(n));
+  hip_check(mk::launch_compact(cand.data_ptr<uint8_t>(), n, rows.data_ptr<int64_t>(), count.data_ptr<int64_t>(),
+                               scratch.data_ptr<int64_t>(), stream()),
+            "compact");
+}
+
 void bounds_update(const Tensor& labels, const Tensor& ub, const Tensor& lb, const Tensor& shift2, const Tensor& cn,
                    const Tensor& xn, const Tensor& cand, const Tensor& work, double qeps) {
   const int64_t n = labels.numel();
@@ -637,10 +656,13 @@ std::string js_array(const Tensor& t) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mikmeans native ops (gfx950 HIP kernels + host helpers)";
+  m.def("compact", &compact, "rows of the nonzero flags, ascending; count on the device");
+  m.def("compact_blocks", &mk::compact_blocks);
   m.def("assign", &assign, "fused MFMA distance + argmin (K2)", py::arg("X"), py::arg("pack"), py::arg("cn"),
         py::arg("xn"), py::arg("labels"), py::arg("mind"), py::arg("slots"), py::arg("Kpad"), py::arg("dpad"),
         py::arg("track_changed"), py::arg("keys") = py::none(), py::arg("rows") = py::none(),
-        py::arg("ub") = py::none(), py::arg("lb") = py::none(), py::arg("scatter") = false);
+        py::arg("ub") = py::none(), py::arg("lb") = py::none(), py::arg("scatter") = false,
+        py::arg("count") = py::none());
   m.def("update", &update, "LDS-privatised per-cluster sums/counts (K3)", py::arg("X"), py::arg("labels"),
         py::arg("K"), py::arg("slab"), py::arg("cnt_slab"), py::arg("n_chunks"), py::arg("weights"),
         py::arg("col_exp"), py::arg("cnt_exp"), py::arg("clamp"), py::arg("clamp_count") = py::none(),

@@ -62,6 +62,10 @@ struct AssignArgs {
   float* ub = nullptr;
   float* lb = nullptr;
   int scatter = 0;
+  // optional device row count (int64): the launch covers N rows, the kernel assigns the first
+  // min(N, *n_dev) -- a compacted batch whose size only the device knows (no host sync, so
+  // the bounded E-step captures into a graph); workgroups past it exit at once
+  const int64_t* n_dev = nullptr;
 };
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 
@@ -84,6 +88,11 @@ hipError_t launch_transform(int dtype, int dpad, const TransformArgs& a, hipStre
 hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, const float* shift2, const float* cn,
                                 int K, const float* xn, int64_t n, uint8_t* cand, float* work, float qeps,
                                 hipStream_t s);
+// rows[0..*count) = indices of the nonzero flags, ascending (deterministic, no host sync);
+// bscratch: int64 [compact_blocks(n)]
+int64_t compact_blocks(int64_t n);
+hipError_t launch_compact(const uint8_t* cand, int64_t n, int64_t* rows, int64_t* count, int64_t* bscratch,
+                          hipStream_t s);
 
 // ---- update (LDS-privatised scatter-add) -------------------------------------
 // Sums are accumulated in FIXED POINT: every contribution x*w is rounded to a

@@ -295,4 +295,110 @@ hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, con
   return hipGetLastError();
 }
 
+// ---- candidate compaction ----------------------------------------------------------------
+// rows[0..count) = the indices i with cand[i] != 0, ascending; count stays on the device.
+// Three launches, no atomics (so the order -- and with it each row's workgroup in the
+// gathered assign that follows -- is the same every run): per-block counts of 4096 flags,
+// one workgroup's exclusive scan of those counts, and a write pass whose threads place
+// their 16 flags' rows after the block offset plus an in-block scan.
+constexpr int CMP_T = 256, CMP_R = 16, CMP_ROWS = CMP_T * CMP_R;
+
+__device__ __forceinline__ int flags16(const uint8_t* __restrict__ cand, int64_t base, int64_t n, unsigned& bits) {
+  bits = 0u;
+  if (base + CMP_R <= n) {
+    const uint4 w = *(const uint4*)(cand + base);
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) bits |= ((ws[q] >> (8 * b)) & 0xffu) ? (1u << (4 * q + b)) : 0u;
+  } else {
+    for (int j = 0; j < CMP_R; ++j)
+      if (base + j < n && cand[base + j]) bits |= 1u << j;
+  }
+  return __builtin_popcount(bits);
+}
+
+__global__ __launch_bounds__(CMP_T) void compact_count_kernel(const uint8_t* __restrict__ cand, int64_t n,
+                                                           int64_t* __restrict__ bcnt) {
+  unsigned bits;
+  int c = flags16(cand, (int64_t)blockIdx.x * CMP_ROWS + threadIdx.x * CMP_R, n, bits);
+  c = wave_sum(c);
+  __shared__ int ws[CMP_T / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+#pragma unroll
+    for (int w = 0; w < CMP_T / 64; ++w) t += ws[w];
+    bcnt[blockIdx.x] = t;
+  }
+}
+
+// inclusive scan of one value per thread over a workgroup of T threads (T / 64 waves)
+template <int T>
+__device__ __forceinline__ int64_t block_incl_scan(int64_t v, int64_t* lds_waves) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  if (lane == 63) lds_waves[w] = v;
+  __syncthreads();
+  int64_t before = 0;
+  for (int j = 0; j < w; ++j) before += lds_waves[j];
+  __syncthreads();   // (lds_waves is reused by the caller's next scan)
+  return v + before;
+}
+
+__global__ __launch_bounds__(1024) void compact_scan_kernel(int64_t* __restrict__ bcnt, int64_t nb,
+                                                         int64_t* __restrict__ count) {
+  __shared__ int64_t wsum[16];
+  __shared__ int64_t tot;
+  int64_t carry = 0;
+  for (int64_t s0 = 0; s0 < nb; s0 += 1024) {
+    const int64_t i = s0 + threadIdx.x;
+    const int64_t v = i < nb ? bcnt[i] : 0;
+    const int64_t incl = block_incl_scan<1024>(v, wsum);
+    if (i < nb) bcnt[i] = carry + incl - v;   // exclusive offset
+    if (threadIdx.x == 1023) tot = incl;      // this slice's total
+    __syncthreads();
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) count[0] = carry;
+}
+
+__global__ __launch_bounds__(CMP_T) void compact_write_kernel(const uint8_t* __restrict__ cand, int64_t n,
+                                                           const int64_t* __restrict__ boff,
+                                                           int64_t* __restrict__ rows) {
+  __shared__ int64_t wsum[CMP_T / 64];
+  const int64_t base = (int64_t)blockIdx.x * CMP_ROWS + threadIdx.x * CMP_R;
+  unsigned bits;
+  const int c = flags16(cand, base, n, bits);
+  const int64_t incl = block_incl_scan<CMP_T>((int64_t)c, wsum);
+  int64_t pos = boff[blockIdx.x] + incl - c;
+  while (bits) {
+    const int j = __builtin_ctz(bits);
+    bits &= bits - 1u;
+    rows[pos++] = base + j;
+  }
+}
+
+int64_t compact_blocks(int64_t n) { return (n + CMP_ROWS - 1) / CMP_ROWS; }
+
+hipError_t launch_compact(const uint8_t* cand, int64_t n, int64_t* rows, int64_t* count, int64_t* bscratch,
+                          hipStream_t s) {
+  const int64_t nb = compact_blocks(n);
+  if (nb <= 0) {
+    hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, s, bscratch, (int64_t)0, count);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nb), dim3(CMP_T), 0, s, cand, n, bscratch);
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, s, bscratch, nb, count);
+  hipLaunchKernelGGL(compact_write_kernel, dim3((unsigned)nb), dim3(CMP_T), 0, s, cand, n, bscratch, rows);
+  return hipGetLastError();
+}
+
 }  // namespace mk

@@ -197,12 +197,16 @@ class LloydEngine:
             native.warn_once("bounded E-step: not with segment overlap, 'farthest' or sample weights; full E-steps")
             self.bounded = False
         if self.bounded:
-            self.ub = torch.zeros(self.n, dtype=torch.float32, device=dev)
-            self.lb = torch.zeros(self.n, dtype=torch.float32, device=dev)
+            # per-row bounds (f32), the rows to re-assign (flags, then their compacted indices
+            # and count -- on the device, so the step stays sync-free and capturable)
+            self.ub = torch.empty(self.n, dtype=torch.float32, device=dev)
+            self.lb = torch.empty(self.n, dtype=torch.float32, device=dev)
             self.cand = torch.empty(self.n, dtype=torch.uint8, device=dev)
+            self._brows = torch.empty(self.n, dtype=torch.int64, device=dev)
+            self._bcount = torch.zeros(1, dtype=torch.int64, device=dev)
+            self._bscratch = torch.empty(max(1, C.compact_blocks(self.n)), dtype=torch.int64, device=dev)
             self._bwork = torch.empty(4, dtype=torch.float32, device=dev)
-            self._bvalid = False          # bounds not yet set: the next E-step is a full one
-            self.reassigned = self.n      # rows the last E-step re-assigned
+            self._invalidate_bounds()
         self.delta = None
         if self.incremental:
             if self.scales.nw:
@@ -241,7 +245,8 @@ class LloydEngine:
             t.update(delta_prev=self.delta["prev"], delta_list=self.delta["list"],
                      delta_count=self.delta["count"], delta_tot=self.delta["tot"])
         if getattr(self, "bounded", False):
-            t.update(bound_ub=self.ub, bound_lb=self.lb, bound_cand=self.cand, bound_work=self._bwork)
+            t.update(bound_ub=self.ub, bound_lb=self.lb, bound_cand=self.cand, bound_rows=self._brows,
+                     bound_count=self._bcount, bound_scratch=self._bscratch, bound_work=self._bwork)
         out = {k: _r(v.numel() * v.element_size()) for k, v in t.items()}
         for name in ("bufs", "stage"):          # streaming: two chunk / staging buffers
             bl = getattr(self, name, None)
@@ -256,7 +261,7 @@ class LloydEngine:
         """Unassign every point (the reference's Restart, app.mjs:167-178); the next
         step re-assigns from the current centres and counts every point as changed."""
         self.labels.fill_(-1)
-        self._bvalid = False
+        self._invalidate_bounds()
         return self
 
     def set_centers(self, centers: torch.Tensor):
@@ -269,8 +274,16 @@ class LloydEngine:
         self.C[:, : self.D] = c
         if self.gpu:
             self.pk.finalize(0, None, self.C)
-        self._bvalid = False              # centres replaced: bounds no longer hold
+        self._invalidate_bounds()         # centres replaced: bounds no longer hold
         return self
+
+    def _invalidate_bounds(self):
+        """(bounded E-step) ub = inf: the next E-step re-assigns every row (device writes
+        only, so a captured step replays it correctly after new centres or a label reset)."""
+        if getattr(self, "bounded", False):
+            self.ub.fill_(float("inf"))
+            self.lb.zero_()
+            self.cand.zero_()
 
     @property
     def centers(self) -> torch.Tensor:
@@ -313,9 +326,6 @@ class LloydEngine:
         (tests/test_gpu_rccl.py)."""
         self.capture_error = None
         if not self.gpu or not self.n or getattr(self, "_graphs", None) is not None:
-            return self
-        if self.bounded:
-            self.capture_error = "bounded E-step: the rows to re-assign are counted on the host"
             return self
         dev = self.device
         main = torch.cuda.current_stream(dev)
@@ -375,6 +385,8 @@ class LloydEngine:
         st = {"slots": self.slots.clone()}
         if self.delta is not None:
             st.update({k: v.clone() for k, v in self.delta.items()})
+        if self.bounded:
+            st.update(ub=self.ub.clone(), lb=self.lb.clone(), cand=self.cand.clone(), shift=self.shift.clone())
         return st
 
     def _restore_capture_state(self, st: dict):
@@ -382,6 +394,9 @@ class LloydEngine:
         if self.delta is not None:
             for k, v in self.delta.items():
                 v.copy_(st[k])
+        if self.bounded:
+            for k in ("ub", "lb", "cand", "shift"):
+                getattr(self, k).copy_(st[k])
 
     def _step_gpu(self):
         self._pre_collective()
@@ -448,23 +463,22 @@ class LloydEngine:
                           self.packed[KD + self.K + 2:])
 
     def _bounded_assign(self):
-        """E-step over the points the Hamerly bounds cannot vouch for (all of them the first
-        time).  One host read per step: the number of rows to re-assign."""
-        if not self._bvalid:
-            self.pk.assign(self.X, self.xn, self.labels, None, self.slots, True, ub=self.ub, lb=self.lb)
-            self.cand.fill_(1)            # every row's bounds are raw kernel distances
-            self._bvalid = True
-            self.reassigned = self.n
-            return
+        """E-step over the rows the Hamerly bounds cannot vouch for (every row after new
+        centres or a label reset): bounds moved by the last shifts -> the flagged rows
+        compacted in ascending order (count on the device) -> a gathered assign that
+        scatters labels and fresh bounds back to those rows.  No host read."""
         # (distance of a quantised centre from its f32 copy, relative to |c|: bf16 RNE)
         qeps = 2.0 ** -8 if self.dtype == torch.bfloat16 else 2.0 ** -22
         self._C.bounds_update(self.labels, self.ub, self.lb, self.shift, self.pk.cn, self.xn, self.cand,
                               self._bwork, qeps)
-        rows = torch.nonzero(self.cand[: self.n]).flatten()
-        self.reassigned = int(rows.numel())
-        if self.reassigned:
-            self.pk.assign(self.X, self.xn, self.labels, None, self.slots, True, rows=rows, ub=self.ub, lb=self.lb,
-                           scatter=True)
+        self._C.compact(self.cand, self._brows, self._bcount, self._bscratch)
+        self.pk.assign(self.X, self.xn, self.labels, None, self.slots, True, rows=self._brows, ub=self.ub,
+                       lb=self.lb, scatter=True, count=self._bcount)
+
+    @property
+    def reassigned(self) -> int:
+        """(bounded E-step) rows the last E-step re-assigned (a host read)."""
+        return int(self._bcount.item()) if getattr(self, "bounded", False) else self.n
 
     def _weighted_inertia(self):
         """packed[inertia] = sum_i w_i mind_i (f64, one pass, no n x 8-byte temporaries)."""

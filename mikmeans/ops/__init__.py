@@ -97,14 +97,15 @@ class CentroidPack:
                          self.dpad, self.Kpad)
 
     def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False, rows=None,
-               ub=None, lb=None, scatter: bool = False):
+               ub=None, lb=None, scatter: bool = False, count=None):
         """K2 on these centres (``X`` column-padded, 16-B rows).  ``rows`` (int64, device):
         assign the gathered batch X[rows] without materialising it (labels etc. logical, or
         at the rows themselves with ``scatter``).  ``ub`` / ``lb``: also write every point's
-        distance to its nearest and second-nearest centre (the bounded E-step's bounds)."""
+        distance to its nearest and second-nearest centre (the bounded E-step's bounds).
+        ``count`` (int64 [1], device): assign only ``rows[:count]`` (a compacted batch)."""
         if rows is not None:
             self._C.assign(X, self.pack, self.cn, xn, labels, mind, slots, self.Kpad, self.dpad,
-                           track_changed, None, rows, ub, lb, scatter)
+                           track_changed, None, rows, ub, lb, scatter, count)
             return
         keys = None
         if 0 < X.shape[0] <= SPLIT_MAX_ROWS and ub is None:

@@ -100,3 +100,66 @@ def test_kmeans_hamerly_fit(native):
     assert KMeans(4, algorithm="elkan").algorithm == "hamerly"
     with pytest.raises(ValueError):
         KMeans(4, algorithm="bogus")
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 4095, 4097, 1_000_003])
+@pytest.mark.parametrize("density", [0.0, 0.003, 0.5, 1.0])
+def test_compact_matches_nonzero(native, n, density):
+    """csrc/rows.hip compaction: the flagged rows in ascending order and their count, both on
+    the device, for ragged sizes (16-flag thread groups, 4096-flag blocks, a multi-slice scan)."""
+    g = torch.Generator(device="cpu").manual_seed(n)
+    cand = (torch.rand(n, generator=g) < density).to(torch.uint8).to(DEV)
+    rows = torch.full((n,), -7, dtype=torch.int64, device=DEV)
+    count = torch.full((1,), -1, dtype=torch.int64, device=DEV)
+    scratch = torch.empty(max(1, native.compact_blocks(n)), dtype=torch.int64, device=DEV)
+    native.compact(cand, rows, count, scratch)
+    ref = torch.nonzero(cand).flatten()
+    assert int(count) == ref.numel()
+    assert torch.equal(rows[: ref.numel()], ref)
+
+
+def test_device_count_assign_matches_host_count(native):
+    """A gathered assign bounded by a device count equals the one over rows[:count]."""
+    X = B.make_blobs(50_000, 64, 20, seed=1, dtype=torch.bfloat16, device=DEV)
+    from mikmeans.ops import pad_columns
+
+    X = pad_columns(X)
+    pk = ops.pack_centers(X[:300, :64].float(), X.shape[1], torch.bfloat16, DEV)
+    xn = ops.row_sqnorm(X)
+    rows = torch.randperm(50_000, device=DEV)[:20_000].sort().values
+    for m in (0, 1, 777, 20_000):
+        out = []
+        for use_count in (False, True):
+            lab = torch.full((50_000,), 5, dtype=torch.int32, device=DEV)
+            ub = torch.zeros(50_000, device=DEV)
+            lb = torch.zeros(50_000, device=DEV)
+            slots = torch.zeros(native.NSLOT * native.SLOT_STRIDE, dtype=torch.float64, device=DEV)
+            if use_count:
+                pk.assign(X, xn, lab, None, slots, True, rows=rows, ub=ub, lb=lb, scatter=True,
+                          count=torch.tensor([m], dtype=torch.int64, device=DEV))
+            elif m:
+                pk.assign(X, xn, lab, None, slots, True, rows=rows[:m].contiguous(), ub=ub, lb=lb, scatter=True)
+            out.append((lab, ub, lb, slots.view(-1, native.SLOT_STRIDE)[:, 1].sum()))
+        a, b = out
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2]), m
+        assert float(a[3]) == float(b[3])
+
+
+def test_bounded_graph_replay_matches_eager(native):
+    """The bounded E-step is sync-free, so it captures into the Lloyd hipGraph; replays give
+    the eager bounded engine's centres and labels bit for bit, also across set_centers."""
+    X = B.make_blobs(120_000, 64, 24, seed=5, dtype=torch.bfloat16, device=DEV)
+    C0 = X[:24].float()
+    ea = LloydEngine(X, 24, bounded=True).set_centers(C0)
+    eb = LloydEngine(X, 24, bounded=True).set_centers(C0).capture()
+    assert eb._graphs is not None, eb.capture_error
+    for it in range(10):
+        if it == 6:          # new centres: bounds invalidated by device writes the graph sees
+            ea.set_centers(X[100:124].float())
+            eb.set_centers(X[100:124].float())
+        ea.step()
+        eb.step()
+        torch.cuda.synchronize()
+        assert torch.equal(ea.centers, eb.centers), it
+        assert torch.equal(ea.labels, eb.labels), it
+        assert ea.reassigned == eb.reassigned, it
