@@ -298,7 +298,8 @@ class KMeans(_Serving):
             try:
                 plan = memplan.plan_fit(n_local, D, self.n_clusters, self.dtype, budget=budget, x_on_device=x_dev,
                                         incremental=self.incremental, init_rows=self.init_size,
-                                        src_itemsize=es_src, copy_x=not self._x_ready(X, device), **kw)
+                                        src_itemsize=es_src, copy_x=not self._x_ready(X, device),
+                                        bounded=self.algorithm == "hamerly", **kw)
                 err = 0.0
             except memplan.HBMCapacityError as e:
                 plan, err = e, 1.0

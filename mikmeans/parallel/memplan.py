@@ -34,6 +34,7 @@ ROW_ALIGN = 1536                 # parallel/shard.py: shard / chunk row grid
 SPLIT_MAX_ROWS = 1 << 18         # ops.SPLIT_MAX_ROWS: small batches keep u64 split keys
 NSLOT, SLOT_STRIDE = 256, 8      # csrc/kernels.h
 WDOT_SCRATCH = 1024              # csrc/rows.hip WDOT_BLOCKS (weighted-inertia partials)
+COMPACT_ROWS = 4096              # csrc/rows.hip CMP_ROWS (candidate compaction block)
 UPD_LDS_MAX = 160 * 1024         # csrc/plan.h
 KS_NT = 1024
 KS_LIST_BYTES = 2 * (KS_NT // 64) * 64 * 4
@@ -249,9 +250,10 @@ class MemoryPlan:
 
 def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = False,
                   incremental: bool = True, init="k-means++", n_local_trials: int | None = None,
-                  copy_x: bool = True, empty_policy: str = "keep") -> MemoryPlan:
+                  copy_x: bool = True, empty_policy: str = "keep", bounded: bool = False) -> MemoryPlan:
     """Device-resident Lloyd fit of an ``n``-row shard (``KMeans.fit``): the engine's buffers
-    (models/lloyd.py ``LloydEngine._init_gpu``), the seeding workspace and the final E-step."""
+    (models/lloyd.py ``LloydEngine._init_gpu``), the seeding workspace and the final E-step.
+    ``bounded``: the Hamerly E-step's per-row bounds, flags and compacted rows (17 B/row)."""
     es = esize_of(dtype)
     Dp = padded_cols(D, es)
     wted = weighted
@@ -277,6 +279,9 @@ def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = 
         cap = max(1, min(n, int(n * 0.125)))
         p.update(delta_prev=_r(n * 4), delta_list=_r(cap * 8), delta_count=_r(4),
                  delta_tot=_r((K * Dp + K) * 8))
+    if bounded and not weighted and empty_policy != "farthest":
+        p.update(bound_ub=_r(n * 4), bound_lb=_r(n * 4), bound_cand=_r(n), bound_rows=_r(n * 8),
+                 bound_count=_r(8), bound_scratch=_r(max(1, -(-n // COMPACT_ROWS)) * 8), bound_work=_r(16))
     tr = {"init": _init_items(init, n, Dp, D, K, n_local_trials or 0),
           "final_assign": {"labels_out": _r(n * 4), "mind_out": _r(n * 4)}}
     return MemoryPlan("resident", n, D, Dp, K, "bfloat16" if es == 2 else "float32", p, tr)
@@ -379,13 +384,14 @@ def plan_fit(n: int, D: int, K: int, dtype="bfloat16", *, budget: int, x_on_devi
              weighted: bool = False, incremental: bool = True, init="k-means++",
              n_local_trials: int | None = None, init_rows: int | None = None,
              src_itemsize: int | None = None, empty_policy: str = "keep", copy_x: bool = True,
-             max_chunk_rows: int = 1 << 24) -> MemoryPlan:
+             max_chunk_rows: int = 1 << 24, bounded: bool = False) -> MemoryPlan:
     """Choose how a Lloyd fit of an ``n``-row shard runs within ``budget`` bytes of HBM:
     resident when it fits (or when X already lives on the device), else streamed in the
     largest power-of-two multiple of 1536 rows that fits; :class:`HBMCapacityError` when
     neither does."""
     res = plan_resident(n, D, K, dtype, weighted=weighted, incremental=incremental, init=init,
-                        n_local_trials=n_local_trials, copy_x=copy_x, empty_policy=empty_policy)
+                        n_local_trials=n_local_trials, copy_x=copy_x, empty_policy=empty_policy,
+                        bounded=bounded)
     res.budget = budget
     if res.fits:
         return res

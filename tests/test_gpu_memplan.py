@@ -30,6 +30,22 @@ def test_memory_plan_matches_engine_buffers(native, n, D, K, dtype, weighted, in
     assert plan.persistent == inv
 
 
+def test_memory_plan_bounded_engine(native):
+    """algorithm='hamerly': the plan lists the bounds, flags and compacted-row buffers the
+    bounded engine allocates, byte for byte."""
+    from mikmeans.models.lloyd import LloydEngine
+    from mikmeans.ops import pad_columns
+
+    n, D, K = 250_001, 64, 300
+    X = pad_columns(B.make_blobs(n, D, 40, seed=1, dtype=torch.bfloat16, device=DEV))
+    eng = LloydEngine(X, K, incremental=True, bounded=True, n_features=D).set_centers(X[:K, :D].float())
+    eng.step()
+    inv = eng.device_buffers()
+    plan = M.plan_resident(n, D, K, torch.bfloat16, incremental=True, copy_x=False, bounded=True)
+    assert {k for k in inv if k.startswith("bound_")} == {k for k in plan.persistent if k.startswith("bound_")}
+    assert plan.persistent == inv
+
+
 @pytest.mark.parametrize("n,D,K", [(4_000_000, 64, 256), (2_000_000, 128, 1024)])
 def test_fit_peak_memory_within_plan(native, n, D, K):
     """A mid-size fit from host rows: torch's measured peak allocation within +-10 % of the
