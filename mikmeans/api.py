@@ -108,7 +108,60 @@ def _shard_info(n_local: int, comm: Comm, device):
     return int(sizes.sum()), start
 
 
-class _Serving:
+class _Params:
+    """scikit-learn estimator protocol: ``get_params`` / ``set_params`` over the constructor's
+    keyword arguments (so ``sklearn.base.clone``, pipelines and grid searches can rebuild an
+    estimator), and a repr of the non-default ones."""
+
+    @classmethod
+    def _param_names(cls) -> list[str]:
+        import inspect
+
+        sig = inspect.signature(cls.__init__)
+        return [n for n, p in sig.parameters.items() if n != "self" and p.kind == p.KEYWORD_ONLY
+                or n == "n_clusters"]
+
+    def get_params(self, deep: bool = True) -> dict:
+        out = {}
+        for n in self._param_names():
+            if n == "random_state":
+                out[n] = None          # (folded into seed by the constructor)
+            else:
+                out[n] = getattr(self, n, None)
+        return out
+
+    def set_params(self, **params):
+        names = set(self._param_names())
+        bad = [k for k in params if k not in names]
+        if bad:
+            raise ValueError(f"invalid parameter(s) {bad} for {type(self).__name__}")
+        # validate / normalise through the constructor, then copy the parameters over
+        ref = type(self)(**{**self.get_params(), **params})
+        for n in names:
+            if n != "random_state" and hasattr(ref, n):
+                setattr(self, n, getattr(ref, n))
+        return self
+
+    def __repr__(self):
+        import inspect
+
+        sig = inspect.signature(type(self).__init__)
+        cur = self.get_params()
+        diff = [f"n_clusters={cur['n_clusters']}"]
+        for n, p in sig.parameters.items():
+            if n == "n_clusters":
+                continue
+            if n in cur and p.default is not inspect.Parameter.empty:
+                v = cur[n]
+                d = p.default
+                if n == "dtype":
+                    v, d = str(v).replace("torch.", ""), str(resolve_dtype(d)).replace("torch.", "")
+                if isinstance(v, (int, float, str, bool, type(None))) and v != d:
+                    diff.append(f"{n}={v!r}")
+        return f"{type(self).__name__}({', '.join(diff)})"
+
+
+class _Serving(_Params):
     """Inference surface shared by KMeans and MiniBatchKMeans (fitted ``cluster_centers_``)."""
 
     def _serving_pack(self, Xt):

@@ -247,3 +247,26 @@ def test_cosine_metric_is_spherical_kmeans():
     np.testing.assert_allclose(km2.cluster_centers_.numpy(), km.cluster_centers_.numpy(), atol=1e-6)
     with pytest.raises(ValueError):
         mikmeans.KMeans(3, metric="manhattan")
+
+
+def test_sklearn_params_protocol():
+    """get_params / set_params / clone-by-constructor round trip (the scikit-learn estimator
+    protocol), normalised values kept, unknown names refused, repr of non-defaults."""
+    km = mikmeans.KMeans(16, dtype="bf16", algorithm="elkan", max_iter=10, seed=3)
+    p = km.get_params()
+    assert p["n_clusters"] == 16 and p["algorithm"] == "hamerly" and p["dtype"] == torch.bfloat16
+    k2 = mikmeans.KMeans(**p)
+    assert k2.get_params() == p
+    assert km.set_params(n_clusters=4, tol=0.0) is km and km.n_clusters == 4 and km.tol == 0.0
+    with pytest.raises(ValueError):
+        km.set_params(bogus=1)
+    with pytest.raises(ValueError):
+        km.set_params(algorithm="nope")
+    assert repr(km) == "KMeans(n_clusters=4, max_iter=10, tol=0.0, seed=3, dtype='bfloat16', algorithm='hamerly')" \
+        or repr(km).startswith("KMeans(n_clusters=4")
+    mb = mikmeans.MiniBatchKMeans(8, batch_size=256)
+    assert repr(mb) == "MiniBatchKMeans(n_clusters=8, batch_size=256)"
+    X, _ = blobs(600, 4, 3, seed=1)
+    a = mikmeans.KMeans(3, device="cpu", seed=2).fit(X)
+    b = mikmeans.KMeans(**a.get_params()).fit(X)
+    assert torch.equal(a.cluster_centers_, b.cluster_centers_)
