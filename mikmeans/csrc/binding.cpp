@@ -587,6 +587,19 @@ void compact(const Tensor& cand, const Tensor& rows, const Tensor& count, const 
             "compact");
 }
 
+void kpar_select(const Tensor& d2, int64_t start, const Tensor& psi, double ell, int64_t seed, int64_t round,
+                 const Tensor& cand) {
+  const int64_t n = d2.numel();
+  check_f32(d2, "d2", n);
+  check_f64(psi, "psi", 1);
+  check_cuda(cand, "cand");
+  TORCH_CHECK(cand.scalar_type() == at::kByte && cand.is_contiguous() && cand.numel() >= n,
+              "mikmeans: cand must be contiguous uint8 [n]");
+  hip_check(mk::launch_kpar_select(d2.data_ptr<float>(), n, start, psi.data_ptr<double>(), ell, (uint64_t)seed,
+                                   (uint32_t)round, cand.data_ptr<uint8_t>(), stream()),
+            "kpar_select");
+}
+
 void bounds_update(const Tensor& labels, const Tensor& ub, const Tensor& lb, const Tensor& shift2, const Tensor& cn,
                    const Tensor& xn, const Tensor& cand, const Tensor& work, double qeps) {
   const int64_t n = labels.numel();
@@ -656,6 +669,7 @@ std::string js_array(const Tensor& t) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mikmeans native ops (gfx950 HIP kernels + host helpers)";
+  m.def("kpar_select", &kpar_select, "k-means|| oversampling flags (philox keyed by the global row)");
   m.def("compact", &compact, "rows of the nonzero flags, ascending; count on the device");
   m.def("compact_blocks", &mk::compact_blocks);
   m.def("assign", &assign, "fused MFMA distance + argmin (K2)", py::arg("X"), py::arg("pack"), py::arg("cn"),

@@ -91,6 +91,9 @@ hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, con
 // rows[0..*count) = indices of the nonzero flags, ascending (deterministic, no host sync);
 // bscratch: int64 [compact_blocks(n)]
 int64_t compact_blocks(int64_t n);
+// k-means|| round: cand[i] = u(start + i) < ell * d2[i] / psi[0] (philox uniform keyed by the global row)
+hipError_t launch_kpar_select(const float* d2, int64_t n, int64_t start, const double* psi, double ell,
+                              uint64_t seed, uint32_t round, uint8_t* cand, hipStream_t s);
 hipError_t launch_compact(const uint8_t* cand, int64_t n, int64_t* rows, int64_t* count, int64_t* bscratch,
                           hipStream_t s);
 

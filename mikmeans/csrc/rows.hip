@@ -401,4 +401,34 @@ hipError_t launch_compact(const uint8_t* cand, int64_t n, int64_t* rows, int64_t
   return hipGetLastError();
 }
 
+// ---- k-means|| oversampling (models/init.py init_kmeans_parallel) ---------------------------
+// Global row g is a candidate of round r when u_g < ell * d2_g / psi, u_g the 53-bit uniform
+// of philox(g_lo, g_hi, r, TAG_KPAR; seed): a pure function of the global row, so the
+// candidates do not depend on how rows are sharded.  psi (f64) stays on the device.  The
+// NumPy mirror (data/sampler.py kpar_uniform) draws the same u.
+constexpr uint32_t TAG_KPAR = 0x4B504152u;  // "KPAR"
+
+__global__ __launch_bounds__(256) void kpar_select_kernel(const float* __restrict__ d2, int64_t n, int64_t start,
+                                                        const double* __restrict__ psi, double ell, uint32_t k0,
+                                                        uint32_t k1, uint32_t round, uint8_t* __restrict__ cand) {
+  const double ps = psi[0];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint64_t g = (uint64_t)(start + i);
+    const U4 r = philox(U4{(uint32_t)g, (uint32_t)(g >> 32), round, TAG_KPAR}, k0, k1);
+    const uint64_t w = ((uint64_t)r.y << 32) | r.x;
+    const double u = (double)(w >> 11) * 0x1p-53;
+    cand[i] = (ps > 0.0 && u < ell * (double)d2[i] / ps) ? 1 : 0;
+  }
+}
+
+hipError_t launch_kpar_select(const float* d2, int64_t n, int64_t start, const double* psi, double ell,
+                              uint64_t seed, uint32_t round, uint8_t* cand, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  int64_t nb = (n + 255) / 256;
+  if (nb > 16384) nb = 16384;
+  hipLaunchKernelGGL(kpar_select_kernel, dim3((unsigned)nb), dim3(256), 0, s, d2, n, start, psi, ell,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), round, cand);
+  return hipGetLastError();
+}
+
 }  // namespace mk

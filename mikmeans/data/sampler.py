@@ -18,6 +18,7 @@ import numpy as np
 from .blobs import philox4x32
 
 TAG_SMP = 0x53414D50
+TAG_KPAR = 0x4B504152
 
 
 def sample_indices(n: int, b: int, seed: int, rank: int, step: int) -> np.ndarray:
@@ -32,3 +33,13 @@ def sample_indices(n: int, b: int, seed: int, rank: int, step: int) -> np.ndarra
     u = (w >> np.uint64(11)).astype(np.float64) * 2.0**-53
     idx = (u * float(n)).astype(np.int64)
     return np.minimum(idx, n - 1)
+
+
+def kpar_uniform(start: int, n: int, seed: int, rnd: int) -> np.ndarray:
+    """k-means|| round ``rnd``: the f64 uniform of global rows start..start+n-1 (mirror of
+    csrc/rows.hip kpar_select: philox(g_lo, g_hi, rnd, TAG_KPAR; seed), 53 bits)."""
+    g = np.arange(start, start + n, dtype=np.uint64)
+    r0, r1, _, _ = philox4x32(g & np.uint64(0xFFFFFFFF), g >> np.uint64(32), np.uint64(rnd & 0xFFFFFFFF),
+                              TAG_KPAR, int(seed))
+    w = (r1 << np.uint64(32)) | r0
+    return (w >> np.uint64(11)).astype(np.float64) * 2.0**-53

@@ -13,6 +13,11 @@ world size given the same seed:
   contributes it to an all-reduce (C4).
 * ``greedy k-means++`` (``n_local_trials > 1``, sklearn's default 2+log K): each
   step draws several candidates and keeps the one with the lowest potential.
+* ``k-means||`` (Bahmani et al. 2012, "scalable k-means++"): a few oversampling rounds
+  each keep every row with probability ``min(1, l D^2(x) / psi)`` (``l = 2K``), so the
+  whole seeding is ~2 collectives per round instead of per centre; the candidates,
+  weighted by the rows they attract, are then reclustered by weighted k-means++ on every
+  rank alike.  Rows are drawn with a philox uniform keyed by the global row.
 
 Reference parity: the reference seeds one fixed card (``JESSICA``,
 app.mjs:188-196) and leaves centroid placement to humans (addCentroid,
@@ -343,8 +348,156 @@ def resolve_init(init, X, D, K, n_global, start, comm: Comm, seed: int, n_local_
         if name in ("greedy-k-means++", "greedy-kmeans++"):
             return init_kmeanspp(X, D, K, n_global, start, comm, seed,
                                  n_local_trials or default_local_trials(K), sampling=sampling)
+        if name in ("k-means||", "kmeans||", "scalable-k-means++"):
+            return init_kmeans_parallel(X, D, K, n_global, start, comm, seed)
         raise ValueError(f"unknown init {init!r}")
     c = torch.as_tensor(np.asarray(init) if not torch.is_tensor(init) else init, dtype=torch.float32)
     if c.shape != (K, D):
         raise ValueError(f"init array must be [{K}, {D}], got {tuple(c.shape)}")
     return c.to(X.device)
+
+
+# ----------------------------------------------------------------------------- k-means||
+KPAR_BLOCK = 8192          # centres per assign launch (the kernel keeps |c|^2 of all in LDS)
+
+
+def _nearest(X, xn, Cb: torch.Tensor, want_labels: bool):
+    """(squared distance to, index of) the nearest row of ``Cb`` [m, D] for every local row:
+    the MFMA assign on the GPU (centre blocks of KPAR_BLOCK), f32 matmul distances on the
+    CPU.  Ties across blocks keep the earlier block."""
+    from .. import ops
+
+    n = X.shape[0]
+    best = torch.full((n,), float("inf"), dtype=torch.float32, device=X.device)
+    lab = torch.zeros(n, dtype=torch.int64, device=X.device) if want_labels else None
+    for b0 in range(0, Cb.shape[0], KPAR_BLOCK):
+        cb = Cb[b0:b0 + KPAR_BLOCK]
+        if X.is_cuda:
+            pk = ops.pack_centers(cb, X.shape[1], X.dtype, X.device)
+            lb = torch.empty(n, dtype=torch.int32, device=X.device)
+            md = torch.empty(n, dtype=torch.float32, device=X.device)
+            pk.assign(X, xn, lb, md)
+        else:
+            Xf = X[:, : cb.shape[1]].to(torch.float32)
+            md = torch.empty(n, dtype=torch.float32)
+            lb = torch.empty(n, dtype=torch.int64)
+            for r0 in range(0, n, 65536):
+                xs = Xf[r0:r0 + 65536]
+                d = (xs * xs).sum(1, keepdim=True) - 2.0 * xs @ cb.T + (cb * cb).sum(1)[None, :]
+                v, i = d.clamp_min(0).min(1)
+                md[r0:r0 + 65536], lb[r0:r0 + 65536] = v, i
+        if want_labels:
+            upd = md < best
+            lab = torch.where(upd, lb.to(torch.int64) + b0, lab)
+        best = torch.minimum(best, md)
+    return best, lab
+
+
+def _gather_varlen(rows: torch.Tensor, comm: Comm) -> torch.Tensor:
+    """Every rank's ``[m_r, D]`` rows, concatenated in rank order (one all-gather of the
+    counts, one of the rows padded to the largest m_r)."""
+    m = torch.tensor([rows.shape[0]], dtype=torch.int64, device=comm.device)
+    counts = comm.all_gather(m).reshape(-1).tolist()
+    mx = max(counts)
+    if mx == 0:
+        return rows[:0]
+    pad = torch.zeros((mx, rows.shape[1]), dtype=torch.float32, device=comm.device)
+    pad[: rows.shape[0]] = rows.to(device=comm.device, dtype=torch.float32)
+    allr = comm.all_gather(pad)
+    return torch.cat([allr[r, : counts[r]] for r in range(comm.world)]).to(rows.device)
+
+
+def weighted_kmeanspp(C: torch.Tensor, w: torch.Tensor, K: int, u: torch.Tensor) -> torch.Tensor:
+    """k-means++ over the rows of ``C`` [M, D] weighted by ``w`` (D^2 x weight sampling),
+    ``u`` [K] uniforms (``u[0]`` draws the first centre by weight).  Device ops only, no
+    host read; identical inputs give identical centres on every rank."""
+    M = C.shape[0]
+    Cd = C.double()
+    wd = w.double()
+    out = torch.empty((K, C.shape[1]), dtype=torch.float32, device=C.device)
+
+    def draw(p, uk):
+        cum = torch.cumsum(p, 0)
+        i = torch.searchsorted(cum, (uk * cum[-1]).reshape(1), right=True)
+        return torch.clamp(i, max=M - 1)
+
+    i = draw(wd, u[0])
+    c = Cd.index_select(0, i)
+    out[0:1] = c.float()
+    d2 = ((Cd - c) ** 2).sum(1)
+    for k in range(1, K):
+        i = draw(wd * d2, u[k])
+        c = Cd.index_select(0, i)
+        out[k:k + 1] = c.float()
+        d2 = torch.minimum(d2, ((Cd - c) ** 2).sum(1))
+    return out
+
+
+def init_kmeans_parallel(X: torch.Tensor, D: int, K: int, n_global: int, start: int, comm: Comm, seed: int,
+                         *, rounds: int = 5, oversampling: float = 2.0, xn: torch.Tensor | None = None) -> torch.Tensor:
+    """k-means|| seeding (Bahmani et al. 2012); returns replicated f32 centres [K, D].
+
+    Per round: psi = the global potential (one all-reduce), every row g kept with probability
+    ``min(1, l d2_g / psi)`` by the uniform keyed by g (csrc/rows.hip ``kpar_select``, NumPy
+    mirror on the CPU), the kept rows compacted on the device and all-gathered in global row
+    order, and d2 lowered against them on the MFMA assign.  Then every candidate's weight
+    (rows nearest to it, one all-reduce) and a weighted k-means++ recluster run alike on
+    every rank.  About 2 collectives per round plus 3 -- against 2 per centre for exact
+    k-means++ -- and the candidates do not depend on the sharding (up to the f64 association
+    of psi)."""
+    rng = np.random.default_rng(seed)
+    first = int(rng.integers(0, n_global))
+    C = gather_rows(X, D, np.array([first]), start, comm)
+    n = X.shape[0]
+    dev = X.device
+    if X.is_cuda and xn is None:
+        from .. import ops
+
+        xn = ops.row_sqnorm(X)
+    ell = float(oversampling) * K
+    d2 = _nearest(X, xn, C, False)[0] if n else torch.zeros(0, device=dev)
+    if X.is_cuda:
+        Cn = native.require()
+        cand = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        rows = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        scratch = torch.empty(max(1, Cn.compact_blocks(n)), dtype=torch.int64, device=dev)
+    for rnd in range(int(rounds)):
+        psi = (d2.sum(dtype=torch.float64) if n else torch.zeros((), dtype=torch.float64, device=dev)).reshape(1)
+        psi = psi.to(comm.device)
+        comm.allreduce_(psi)
+        if float(psi.item()) <= 0.0:
+            break                       # every row sits on a candidate
+        if n and X.is_cuda:
+            Cn.kpar_select(d2, start, psi.to(dev), ell, seed, rnd, cand)
+            Cn.compact(cand[:n], rows, cnt, scratch)
+            sel = rows[: int(cnt.item())]
+        elif n:
+            from ..data.sampler import kpar_uniform
+
+            u = torch.from_numpy(kpar_uniform(start, n, seed, rnd))
+            sel = torch.nonzero(u < ell * d2.double() / float(psi.item())).flatten()
+        else:
+            sel = torch.zeros(0, dtype=torch.int64, device=dev)
+        new = _gather_varlen(X[sel][:, :D].to(torch.float32) if n else torch.zeros((0, D), device=dev), comm)
+        if new.shape[0] == 0:
+            continue
+        C = torch.cat([C, new.to(C.device)])
+        if n:
+            d2 = torch.minimum(d2, _nearest(X, xn, new.to(dev), False)[0])
+    M = C.shape[0]
+    if M <= K:
+        # (tiny data: every candidate is a centre; the rest by exact k-means++)
+        if M < K:
+            return init_kmeanspp(X, D, K, n_global, start, comm, seed)
+        return C
+    # candidate weights: rows nearest to each candidate (integer counts, exact in f64)
+    if n:
+        _, lab = _nearest(X, xn, C.to(dev), True)
+        w = torch.bincount(lab, minlength=M).to(torch.float64)
+    else:
+        w = torch.zeros(M, dtype=torch.float64, device=dev)
+    w = w.to(comm.device)
+    comm.allreduce_(w)
+    u = torch.as_tensor(rng.random(K), dtype=torch.float64, device=C.device)
+    return weighted_kmeanspp(C, w.to(C.device), K, u)

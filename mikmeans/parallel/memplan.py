@@ -198,6 +198,13 @@ def _init_items(init, n: int, Dp: int, D: int, K: int, trials: int) -> dict:
     if name in ("k-means++", "kmeans++", "kpp", "greedy-k-means++", "greedy-kmeans++"):
         t = trials if trials else (2 + int(math.log(K)) if name.startswith("greedy") and K > 1 else 1)
         return kpp_workspace(n, Dp, K, max(1, t))
+    if name in ("k-means||", "kmeans||", "scalable-k-means++"):
+        # models/init.py init_kmeans_parallel: d2, flags, compacted rows, row norms, and the
+        # nearest-candidate pass (best distance, int64 labels, one launch's labels / distances)
+        m = 5 * 2 * K + 1
+        return {"kpar_d2": _r(n * 4), "kpar_cand": _r(n), "kpar_rows": _r(n * 8), "kpar_xn": _r(n * 4),
+                "kpar_best": _r(n * 4), "kpar_labels": _r(n * 8), "kpar_launch": 2 * _r(n * 4),
+                "kpar_candidates": _r(m * D * 8), "kpar_scratch": _r(max(1, -(-n // COMPACT_ROWS)) * 8)}
     return {"init_rows": _r(K * D * 8)}
 
 

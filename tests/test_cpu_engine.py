@@ -270,3 +270,32 @@ def test_sklearn_params_protocol():
     a = mikmeans.KMeans(3, device="cpu", seed=2).fit(X)
     b = mikmeans.KMeans(**a.get_params()).fit(X)
     assert torch.equal(a.cluster_centers_, b.cluster_centers_)
+
+
+def test_kmeans_parallel_init_quality_and_weights():
+    """k-means|| (init='k-means||'): K distinct data rows whose potential is as good as
+    k-means++'s on blob data (within 1.5x); the weighted recluster never picks a zero-weight
+    candidate; the NumPy uniform mirror is a pure function of the global row."""
+    from mikmeans.data.sampler import kpar_uniform
+    from mikmeans.models.init import init_kmeanspp, weighted_kmeanspp
+    from mikmeans.parallel import Comm
+
+    X, _ = blobs(6000, 8, 25, seed=7)
+    X = torch.as_tensor(X)
+    km = mikmeans.KMeans(25, init="k-means||", device="cpu", max_iter=1, seed=2).fit(X)
+    C = mikmeans.models.init.init_kmeans_parallel(X, 8, 25, 6000, 0, Comm.local(), seed=2)
+    hit = (C[:, None, :] == X.float()[None]).all(-1).any(1)
+    assert bool(hit.all()) and torch.unique(C, dim=0).shape[0] == 25
+    Cp = init_kmeanspp(X, 8, 25, 6000, 0, Comm.local(), seed=2)
+    pot = lambda c: float(torch.cdist(X.double(), c.double()).min(1).values.pow(2).sum())  # noqa: E731
+    assert pot(C) <= 1.5 * pot(Cp)
+    assert km.cluster_centers_.shape == (25, 8)
+    Cc = torch.randn(40, 3)
+    w = torch.zeros(40, dtype=torch.float64)
+    w[[2, 5, 8, 13, 21]] = 1.0
+    out = weighted_kmeanspp(Cc, w, 5, torch.rand(5, dtype=torch.float64))
+    got = sorted(int(((Cc - o).abs().sum(1) == 0).nonzero()[0]) for o in out)
+    assert got == [2, 5, 8, 13, 21]
+    a = kpar_uniform(100, 50, 9, 2)
+    b = kpar_uniform(0, 200, 9, 2)[100:150]
+    assert np.array_equal(a, b) and ((a >= 0) & (a < 1)).all()

@@ -228,6 +228,27 @@ def test_kmeanspp_two_stage(trials):
         assert bool(hit.all()) and torch.unique(C, dim=0).shape[0] == K
 
 
+def _kpar(comm):
+    from mikmeans.models.init import init_kmeans_parallel
+
+    X = _data()
+    s, e = shard_range(N, comm.rank, comm.world)
+    return init_kmeans_parallel(X[s:e], D, K, N, s, comm, seed=4)
+
+
+def test_kmeans_parallel_world_size_invariant():
+    """k-means||: candidates keyed by the global row, gathered in row order, integer weights
+    -> the same centres on W = 1 / 2 / 3 gloo ranks (empty-ish shards included)."""
+    from mikmeans.parallel import Comm
+
+    ref = _kpar(Comm.local())
+    assert ref.shape == (K, D)
+    for world in (2, 3):
+        outs = spawn_local(_kpar, world)
+        for o in outs:
+            assert torch.equal(o, ref), world
+
+
 def test_pick_rank_is_proportional():
     """pick_rank(totals, v) selects rank r with probability totals[r] / sum (inverse CDF),
     never an empty rank, and the rounding edge (v -> 1) lands on the last non-empty rank."""

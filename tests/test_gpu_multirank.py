@@ -92,6 +92,16 @@ def case_kpp_two_stage(comm):
             for t in (1, 3)}
 
 
+def case_kpar(comm):
+    """k-means||: candidates keyed by the global row -> the W=1 centres on real ranks."""
+    from mikmeans.models.init import init_kmeans_parallel
+    from mikmeans.ops import pad_columns
+
+    X = pad_columns(_data())
+    Xl, s = _shard(comm, X)
+    return {"C": init_kmeans_parallel(Xl, D, K, N, s, comm, seed=6)}
+
+
 def _fit(comm, **kw):
     import mikmeans
 
@@ -204,7 +214,7 @@ def case_ckpt_resume(comm, path):
 CASES = {f.__name__[5:]: f for f in (case_lloyd_random_bf16, case_lloyd_random_f32, case_lloyd_kpp,
                                      case_kpp_greedy, case_fit_farthest, case_fit_weighted, case_fit_cosine,
                                      case_fit_graph, case_stream_agreement, case_minibatch_fit,
-                                     case_fit_empty_shard, case_kpp_two_stage)}
+                                     case_fit_empty_shard, case_kpp_two_stage, case_kpar)}
 CASES["fit_kpp_greedy_f32"] = _fit_kpp
 
 
@@ -280,7 +290,7 @@ def _check_fit(ref, outs):
 def _check(name, ref, outs):
     if name.startswith("lloyd"):
         _check_lloyd(ref, outs)
-    elif name == "kpp_greedy":
+    elif name in ("kpp_greedy", "kpar"):
         for o in outs:
             assert torch.equal(o["C"], ref["C"].cpu())
     elif name == "fit_kpp_greedy_f32":
@@ -292,9 +302,9 @@ def _check(name, ref, outs):
 
 W2_CASES = ["lloyd_random_bf16", "lloyd_random_f32", "lloyd_kpp", "kpp_greedy", "fit_farthest", "fit_weighted",
             "fit_cosine", "fit_graph", "fit_kpp_greedy_f32", "stream_agreement", "minibatch_fit",
-            "kpp_two_stage"]
+            "kpp_two_stage", "kpar"]
 W4_CASES = ["lloyd_random_bf16", "lloyd_kpp", "kpp_greedy", "fit_farthest", "fit_weighted", "minibatch_fit",
-            "fit_empty_shard", "kpp_two_stage"]
+            "fit_empty_shard", "kpp_two_stage", "kpar"]
 _NOT_W1 = ("minibatch_fit", "stream_agreement", "fit_empty_shard", "kpp_two_stage")
 
 
