@@ -136,6 +136,21 @@ def main(argv=None):
             C0 = init_random(X, D, K, N, s, comm, args.seed)
         sync()
         extra["init_s"] = round(time.perf_counter() - t0, 3)
+        if args.config == "cfg4" and dev.type == "cuda":
+            # k-means|| (init='k-means||'): ~2 collectives per round instead of per centre;
+            # its seeding time and the potential of both seedings, reported beside the bench
+            from mikmeans.models.init import init_kmeans_parallel
+
+            t0 = time.perf_counter()
+            Ck = init_kmeans_parallel(X, D, K, N, s, comm, args.seed)
+            sync()
+            extra["init_kmeans_parallel_s"] = round(time.perf_counter() - t0, 3)
+            pots = torch.zeros(2, dtype=torch.float64, device=dev)
+            for j, Cj in enumerate((C0, Ck)):
+                pots[j] = mikmeans.ops.assign(X, Cj, with_dist=True)[1].sum(dtype=torch.float64)
+            comm.allreduce_(pots)
+            extra["init_potential_kpp_vs_kpar"] = [float(pots[0]), float(pots[1])]
+            del Ck
         if args.config == "cfg4" and world == 1 and comm.grouped and dev.type == "cuda":
             # the multi-rank owner path (all-gather of the potentials + owner sampling +
             # all-reduce of the drawn row per step) on the 1-rank RCCL group: its collective
