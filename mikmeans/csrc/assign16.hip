@@ -219,13 +219,19 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       __builtin_amdgcn_sched_barrier(0);   // all index loads in flight before the first use
 #pragma unroll
       for (int p = 0; p < C::P; ++p) load_frags(p, src[p]);
+      if (!EXACT && a.xn && a.scatter) {   // (scattering: the caller's norms sit at the X rows)
+#pragma unroll
+        for (int p = 0; p < C::P; ++p) xnr[p] = a.xn[src[p]];
+      }
     } else {
 #pragma unroll
       for (int p = 0; p < C::P; ++p) load_frags(p, row_of(p));
     }
     if (!EXACT && a.xn) {
+      if (!(a.rows && a.scatter)) {
 #pragma unroll
-      for (int p = 0; p < C::P; ++p) xnr[p] = a.xn[row_of(p)];
+        for (int p = 0; p < C::P; ++p) xnr[p] = a.xn[row_of(p)];
+      }
     } else {
 #pragma unroll
       for (int p = 0; p < C::P; ++p) xnr[p] = 0.f;

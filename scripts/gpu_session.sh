@@ -29,6 +29,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     memplan) step pytest_memplan 600 python -u -m pytest tests/test_gpu_memplan.py tests/test_gpu_minibatch.py -v --timeout 200 --timeout-method thread ;;
     newkern) step pytest_newkern 600 python -u -m pytest tests/test_gpu_kernels.py -v --timeout 200 --timeout-method thread \
                -k "${NK_SEL:-persistent or wide or transform or d768 or col_absmax or matches_reference or past_1024}" ;;
+    init) step pytest_init 300 python -u -m pytest tests/test_gpu_init.py -v --timeout 200 --timeout-method thread ;;
     bounded) step pytest_bounded 400 python -u -m pytest tests/test_gpu_bounded.py -v --timeout 200 --timeout-method thread ;;
     hamerly) step hamerly 400 python -u scripts/hamerly_ab.py ${HAM_ARGS:-} ;;
     dp2host) step bench_dp2host 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
