@@ -307,7 +307,8 @@ def cmd_plan(a) -> int:
                 pl.budget = budget
         else:
             pl = memplan.plan_fit(n_local, a.d, a.k, a.dtype, budget=budget, x_on_device=False,
-                                  incremental=not a.full_mstep, init=a.init)
+                                  incremental=not a.full_mstep, init=a.init,
+                                  bounded=a.algorithm in ("hamerly", "elkan"))
     except memplan.HBMCapacityError as e:
         print(json.dumps({"error": str(e)}))
         return 1
@@ -413,6 +414,8 @@ def build_parser():
     pl.add_argument("--init", default="k-means++")
     pl.add_argument("--batch-size", type=int, default=0, help="> 0: plan a mini-batch fit")
     pl.add_argument("--full-mstep", action="store_true", help="no incremental M-step buffers")
+    pl.add_argument("--algorithm", default="lloyd", choices=["lloyd", "hamerly", "elkan"],
+                    help="hamerly: the bounded E-step's per-row bounds too")
     pl.add_argument("--budget-gb", type=float, default=None)
     pl.add_argument("--compact", action="store_true")
     return ap
