@@ -746,7 +746,8 @@ class MiniBatchKMeans(_Serving):
             plan.budget = memplan.hbm_budget(device)
             if not plan.fits and not X.is_cuda:
                 plan = memplan.plan_minibatch(n, D, self.n_clusters, self.dtype, batch_rows=self.batch_size,
-                                              resident=False, init_rows=self.init_size)
+                                              resident=False, init_rows=self.init_size,
+                                              src_itemsize=X.element_size() if torch.is_tensor(X) else 4)
                 plan.budget = memplan.hbm_budget(device)
                 resident = False
             if not plan.fits:

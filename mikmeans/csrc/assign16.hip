@@ -788,12 +788,27 @@ static void launch16_kt(const AssignArgs& b, const dim3& grid, size_t lds, hipSt
                        dim3(NW_ * 64), lds, s, b);
 }
 
+// The geometries that run the bounded E-step's TOP2 epilogue (launch16_d routes every call
+// with bounds to them).  The bf16 defaults at D = 64 / 128 / 256 have no registers for the
+// per-lane second minimum: their TOP2 builds spilled 500-940 VGPRs and ran 5.7x slower
+// (profiles/r4_05_hamerly.md), so the bounded pass takes fewer point blocks per wave there.
+template <typename T, int DPAD, int P, int OCC, int NW_, bool AST>
+constexpr bool top2_geom() {
+  if (sizeof(T) == 4 || DPAD == 32 || DPAD > 256) return true;   // (the defaults hold it, 0 spills)
+  if (AST) return false;
+  if (DPAD == 64) return P == 2 && OCC == 4 && NW_ == 4;
+  if (DPAD == 128) return P == 2 && OCC == 4 && NW_ == 4;
+  if (DPAD == 256) return P == 3 && OCC == 2 && NW_ == 8;
+  return false;
+}
+
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST>
 static void launch16_kpp(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  if constexpr (!VARG && !PERSIST) {
-    // bounded E-step: the second-smallest score too (launch16_t keeps such calls on this path)
+  if constexpr (!VARG && !PERSIST && top2_geom<T, DPAD, P, OCC, NW_, AST>()) {
+    // bounded E-step: the second-smallest score too
     if (b.ub) return launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, true>(b, grid, lds, s);
   }
+  if (b.ub) return;   // (unreachable: launch16_d sends bounds to a top2_geom geometry)
   launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, false>(b, grid, lds, s);
 }
 
@@ -888,6 +903,11 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   constexpr int P = sizeof(T) == 2 ? (DPAD == 64 ? 8 : DPAD == 256 ? 3 : 4) : (NQ >= 8 ? 2 : 4);
   constexpr int OCC = sizeof(T) == 2 ? ((DPAD == 64 || DPAD == 256) ? 3 : 4) : 1;
   static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
+  if (a.ub) {   // bounded E-step (TOP2): the geometries of top2_geom
+    if constexpr (sizeof(T) == 2 && DPAD == 64) return launch16_t<T, DPAD, 2, CT, 2, 4>(a, s);
+    if constexpr (sizeof(T) == 2 && DPAD == 128) return launch16_t<T, DPAD, 2, CT, 2, 4>(a, s);
+    if constexpr (sizeof(T) == 2 && DPAD == 256) return launch16_t<T, DPAD, 3, CT, 2, 2, 8>(a, s);
+  }
   if constexpr (sizeof(T) == 2 && DPAD == 256) {
     // A/B switch V_ASSIGN_GEOM: 8 waves per ring (half the per-point centre stream and
     // per-workgroup start-up): 1 = 3 point blocks at 2 waves/SIMD, 2 = 2 blocks at 4

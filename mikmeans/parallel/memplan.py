@@ -280,8 +280,12 @@ def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = 
     p["cnt_slab"] = _r(nch * K * 8)
     p["packed"] = _r((K * Dp + K + 2) * 8)
     p.update(_centroid_items(K, Dp, es))
+    final = {"labels_out": _r(n * 4), "mind_out": _r(n * 4)}
     if 0 < n <= SPLIT_MAX_ROWS:
-        p["split_keys"] = _r(n * 8)
+        if bounded:
+            final["split_keys"] = _r(n * 8)   # (the bounded E-step's gathered passes take no keys)
+        else:
+            p["split_keys"] = _r(n * 8)
     if incremental and n and n < 2**31 and choose_sw(es, K, Dp, True)[0] > 0:
         cap = max(1, min(n, int(n * 0.125)))
         p.update(delta_prev=_r(n * 4), delta_list=_r(cap * 8), delta_count=_r(4),
@@ -289,8 +293,7 @@ def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = 
     if bounded and not weighted and empty_policy != "farthest":
         p.update(bound_ub=_r(n * 4), bound_lb=_r(n * 4), bound_cand=_r(n), bound_rows=_r(n * 8),
                  bound_count=_r(8), bound_scratch=_r(max(1, -(-n // COMPACT_ROWS)) * 8), bound_work=_r(16))
-    tr = {"init": _init_items(init, n, Dp, D, K, n_local_trials or 0),
-          "final_assign": {"labels_out": _r(n * 4), "mind_out": _r(n * 4)}}
+    tr = {"init": _init_items(init, n, Dp, D, K, n_local_trials or 0), "final_assign": final}
     return MemoryPlan("resident", n, D, Dp, K, "bfloat16" if es == 2 else "float32", p, tr)
 
 
@@ -339,7 +342,8 @@ def stream_chunk_rows(chunk_rows: int, n: int) -> int:
 
 
 def plan_minibatch(n: int, D: int, K: int, dtype="bfloat16", *, batch_rows: int, resident: bool = True,
-                   init="k-means++", init_rows: int | None = None, copy_x: bool = True) -> MemoryPlan:
+                   init="k-means++", init_rows: int | None = None, copy_x: bool = True,
+                   src_itemsize: int = 4) -> MemoryPlan:
     """Mini-batch fit (api.MiniBatchKMeans.fit, models/minibatch.py): the engine's buffers
     (``MiniBatchEngine.device_buffers``) plus the fit's own -- the shard itself when it is
     device-resident (each step then reads ``X[rows]`` in place through an int64 index list
@@ -364,8 +368,19 @@ def plan_minibatch(n: int, D: int, K: int, dtype="bfloat16", *, batch_rows: int,
     if not resident and 0 < b <= SPLIT_MAX_ROWS:
         p["split_keys"] = _r(b * 8)     # (gathered batches take the one-pass grid: no keys)
     m = min(n, init_rows or max(3 * b, 3 * K))
+    pred = {"labels_out": _r(n * 4)}
+    if not resident and n:
+        # api._Serving._assign_rows: host rows go through in ~256 MB blocks -- the block as
+        # copied (source dtype), its cast to the compute dtype and padding, its labels
+        B = min(n, max(1, (1 << 28) // max(1, D * 4)))
+        pred["block_src"] = _r(B * D * src_itemsize)
+        if src_itemsize != es:
+            pred["block_cast"] = _r(B * D * es)
+        if Dp != D:
+            pred["block_padded"] = _r(B * Dp * es)
+        pred["block_labels"] = _r(B * 4)
     tr = {"init": {"sample": _r(m * Dp * es), **_init_items(init, m, Dp, D, K, 0)},
-          "predict": {"labels_out": _r(n * 4)}}
+          "predict": pred}
     pl = MemoryPlan("minibatch-resident" if resident else "minibatch-host", n, D, Dp, K,
                     "bfloat16" if es == 2 else "float32", p, tr)
     pl.batch_rows = b
