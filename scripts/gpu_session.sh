@@ -32,6 +32,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     init) step pytest_init 300 python -u -m pytest tests/test_gpu_init.py -v --timeout 200 --timeout-method thread ;;
     bounded) step pytest_bounded 400 python -u -m pytest tests/test_gpu_bounded.py -v --timeout 200 --timeout-method thread ;;
     hamerly) step hamerly 400 python -u scripts/hamerly_ab.py ${HAM_ARGS:-} ;;
+    hamerly2) step hamerly_kpar 400 python -u scripts/hamerly_ab.py --init "k-means||" --iters 40 ;;
     dp2host) step bench_dp2host 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --comm host --steps 10 --warmup 2 ;;
     ab_head) step ab_head 300 python -u scripts/assign_ab.py --arms "default;assign_persist=1;assign_geom=4;assign_geom=4,assign_persist=1" ;;

@@ -25,11 +25,19 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--blobs", type=int, default=0, help="blob count (default: K)")
+    ap.add_argument("--init", default="random", choices=["random", "k-means||"],
+                    help="random rows (the bench's start) or k-means|| seeding")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     X = make_blobs(a.n, a.d, a.blobs or a.k, seed=7, dtype=dt, device="cuda")
     g = torch.Generator(device="cpu").manual_seed(1)
-    C0 = X[torch.randint(0, a.n, (a.k,), generator=g).cuda()].float()
+    if a.init == "random":
+        C0 = X[torch.randint(0, a.n, (a.k,), generator=g).cuda()].float()
+    else:
+        from mikmeans.models.init import init_kmeans_parallel
+        from mikmeans.parallel import Comm
+
+        C0 = init_kmeans_parallel(X, a.d, a.k, a.n, 0, Comm.local(X.device), seed=1)
     ea = LloydEngine(X, a.k, incremental=True).set_centers(C0)
     eb = LloydEngine(X, a.k, incremental=True, bounded=True).set_centers(C0)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -51,7 +59,7 @@ def main():
                      "changed": ea.last_stats().n_changed, "agree": round(agree, 6)})
         print(json.dumps(rows[-1]), flush=True)
     dc = float((ea.centers - eb.centers).abs().max())
-    print(json.dumps({"n": a.n, "d": a.d, "k": a.k, "dtype": a.dtype, "iters": a.iters,
+    print(json.dumps({"n": a.n, "d": a.d, "k": a.k, "dtype": a.dtype, "iters": a.iters, "init": a.init,
                       "full_total_ms": round(tot[0], 2), "bounded_total_ms": round(tot[1], 2),
                       "speedup": round(tot[0] / max(tot[1], 1e-9), 3), "max_centre_diff": dc}), flush=True)
 
