@@ -198,10 +198,11 @@ class _Serving(_Params):
                 Xt = _unit_rows(Xt)
         return Xt, was_numpy
 
-    def _assign_rows(self, X, with_dist: bool):
+    def _assign_rows(self, X, with_dist: bool, block_rows: int | None = None):
         """(labels, squared distances or None) of every row of X under the fitted centres.
-        Host rows bound for a GPU model go through in blocks of ~256 MB, so a shard larger
-        than HBM (a streamed fit's) is never copied to the device whole."""
+        Host rows bound for a GPU model go through in blocks of ~256 MB (or ``block_rows``:
+        a host-shard fit labels its rows in batch-sized blocks, the memory plan's), so a
+        shard larger than HBM (a streamed fit's) is never copied to the device whole."""
         from . import ops
 
         dev = self.cluster_centers_.device
@@ -212,7 +213,7 @@ class _Serving(_Params):
             lab, mind = ops.assign(Xt, self.cluster_centers_, with_dist=with_dist, pack=self._serving_pack(Xt))
             return lab, mind, was_numpy
         was_numpy = not torch.is_tensor(X)
-        block = max(1, (1 << 28) // max(1, X.shape[1] * 4))
+        block = int(block_rows) if block_rows else max(1, (1 << 28) // max(1, X.shape[1] * 4))
         labels = torch.empty(n, dtype=torch.int32, device=dev)
         mind = torch.empty(n, dtype=torch.float32, device=dev) if with_dist else None
         for i in range(0, n, block):
@@ -827,7 +828,10 @@ class MiniBatchKMeans(_Serving):
                 if float(eng.shift.sum()) <= self.tol:
                     break
         self._finish(eng)
-        self.labels_ = self.predict(Xt if Xt is not None else X)
+        if Xt is not None:
+            self.labels_ = self.predict(Xt)
+        else:   # host shard: label it in batch-sized blocks (memplan.plan_minibatch "predict")
+            self.labels_ = self._assign_rows(Xh, False, block_rows=max(1, b))[0]
         if self._numpy_io and torch.is_tensor(self.labels_):
             self.labels_ = self.labels_.cpu().numpy()
         return self

@@ -370,9 +370,10 @@ def plan_minibatch(n: int, D: int, K: int, dtype="bfloat16", *, batch_rows: int,
     m = min(n, init_rows or max(3 * b, 3 * K))
     pred = {"labels_out": _r(n * 4)}
     if not resident and n:
-        # api._Serving._assign_rows: host rows go through in ~256 MB blocks -- the block as
-        # copied (source dtype), its cast to the compute dtype and padding, its labels
-        B = min(n, max(1, (1 << 28) // max(1, D * 4)))
+        # api.MiniBatchKMeans.fit labels a host shard in batch-sized blocks
+        # (_Serving._assign_rows): the block as copied (source dtype), its cast to the compute
+        # dtype and padding, its labels
+        B = min(n, max(1, b))
         pred["block_src"] = _r(B * D * src_itemsize)
         if src_itemsize != es:
             pred["block_cast"] = _r(B * D * es)

@@ -30,6 +30,9 @@ for s in ${STEPS:-smoke tests bench prof}; do
     newkern) step pytest_newkern 600 python -u -m pytest tests/test_gpu_kernels.py -v --timeout 200 --timeout-method thread \
                -k "${NK_SEL:-persistent or wide or transform or d768 or col_absmax or matches_reference or past_1024}" ;;
     init) step pytest_init 300 python -u -m pytest tests/test_gpu_init.py -v --timeout 200 --timeout-method thread ;;
+    abr3) for sh in "--d 128 --k 1024 --n 20000000" "--d 64 --k 4096 --n 10000000" "--d 256 --k 512 --n 16777216"; do
+            step "ab_r3_$(echo $sh | cut -d' ' -f2)" 300 python -u scripts/ab_ext.py run ${AB_MOD:-scripts/abbin/_C_ab_2c7aa1c1dd03.so} $sh
+          done ;;
     bounded) step pytest_bounded 400 python -u -m pytest tests/test_gpu_bounded.py -v --timeout 200 --timeout-method thread ;;
     hamerly) step hamerly 400 python -u scripts/hamerly_ab.py ${HAM_ARGS:-} ;;
     hamerly2) step hamerly_kpar 400 python -u scripts/hamerly_ab.py --init "k-means||" --iters 40 ;;
