@@ -407,29 +407,50 @@ def _gather_varlen(rows: torch.Tensor, comm: Comm) -> torch.Tensor:
     return torch.cat([allr[r, : counts[r]] for r in range(comm.world)]).to(rows.device)
 
 
-def weighted_kmeanspp(C: torch.Tensor, w: torch.Tensor, K: int, u: torch.Tensor) -> torch.Tensor:
+def weighted_kmeanspp(C: torch.Tensor, w: torch.Tensor, K: int, u: torch.Tensor, *, graph_steps: int = 64) -> torch.Tensor:
     """k-means++ over the rows of ``C`` [M, D] weighted by ``w`` (D^2 x weight sampling),
     ``u`` [K] uniforms (``u[0]`` draws the first centre by weight).  Device ops only, no
-    host read; identical inputs give identical centres on every rank."""
+    host read; identical inputs give identical centres on every rank.  On a GPU the steps
+    replay as a hipGraph of ``graph_steps`` steps each (the step index lives on the device),
+    so K = 4096 seeding steps cost a few hundred graph launches instead of ~40k op launches."""
     M = C.shape[0]
     Cd = C.double()
     wd = w.double()
     out = torch.empty((K, C.shape[1]), dtype=torch.float32, device=C.device)
-
-    def draw(p, uk):
-        cum = torch.cumsum(p, 0)
-        i = torch.searchsorted(cum, (uk * cum[-1]).reshape(1), right=True)
-        return torch.clamp(i, max=M - 1)
-
-    i = draw(wd, u[0])
+    cum = torch.cumsum(wd, 0)
+    i = torch.clamp(torch.searchsorted(cum, (u[0] * cum[-1]).reshape(1), right=True), max=M - 1)
     c = Cd.index_select(0, i)
     out[0:1] = c.float()
     d2 = ((Cd - c) ** 2).sum(1)
-    for k in range(1, K):
-        i = draw(wd * d2, u[k])
-        c = Cd.index_select(0, i)
-        out[k:k + 1] = c.float()
-        d2 = torch.minimum(d2, ((Cd - c) ** 2).sum(1))
+    kdev = torch.ones(1, dtype=torch.int64, device=C.device)
+
+    def step():
+        cum_ = torch.cumsum(wd * d2, 0)
+        j = torch.searchsorted(cum_, u.index_select(0, kdev) * cum_[-1:], right=True).clamp_(max=M - 1)
+        cj = Cd.index_select(0, j)
+        out.index_copy_(0, kdev, cj.float())
+        torch.minimum(d2, ((Cd - cj) ** 2).sum(1), out=d2)
+        kdev.add_(1)
+
+    done = 1
+    G = int(graph_steps)
+    if C.is_cuda and G > 0 and K - 1 >= 3 + 2 * G:
+        side = torch.cuda.Stream(device=C.device)
+        side.wait_stream(torch.cuda.current_stream(C.device))
+        with torch.cuda.stream(side):       # warm-up: real steps 1..3
+            for _ in range(3):
+                step()
+        torch.cuda.current_stream(C.device).wait_stream(side)
+        done += 3
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):           # recorded, not run
+            for _ in range(G):
+                step()
+        for _ in range((K - done) // G):
+            g.replay()
+            done += G
+    for _ in range(K - done):
+        step()
     return out
 
 

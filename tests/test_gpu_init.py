@@ -55,3 +55,19 @@ def test_kmeans_parallel_gpu(native, dtype):
     assert pot(C) <= 1.3 * pot(Cp)
     km = mikmeans.KMeans(k, init="k-means||", dtype=dtype, max_iter=3, device=DEV).fit(X[:, :d].contiguous())
     assert km.cluster_centers_.shape == (k, d)
+
+
+def test_weighted_kmeanspp_graph_equals_eager(native):
+    """The k-means|| recluster replayed as hipGraphs of 64 steps gives the eager steps'
+    centres bit for bit (the step index and the draws live on the device)."""
+    from mikmeans.models.init import weighted_kmeanspp
+
+    g = torch.Generator().manual_seed(2)
+    C = torch.randn(5000, 24, generator=g).to(DEV)
+    w = torch.randint(0, 50, (5000,), generator=g).double().to(DEV)
+    u = torch.rand(300, generator=g, dtype=torch.float64).to(DEV)
+    a = weighted_kmeanspp(C, w, 300, u, graph_steps=0)
+    b = weighted_kmeanspp(C, w, 300, u, graph_steps=64)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert torch.unique(b, dim=0).shape[0] == 300
