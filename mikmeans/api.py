@@ -74,10 +74,11 @@ def native_mod():
     return native.require()
 
 
-def _device_rows(X: torch.Tensor, device, dtype, gpu: bool, block_bytes: int = 1 << 28) -> torch.Tensor:
+def _device_rows(X: torch.Tensor, device, dtype, gpu: bool, block_bytes: int = 1 << 26) -> torch.Tensor:
     """``X`` on ``device`` in ``dtype`` -- column-padded to 16-byte rows for the GPU kernels --
-    built block by block, so no full-size temporary in another dtype ever exists on the
-    device (host blocks are converted on the host).  ``X`` itself when it already qualifies."""
+    built block by block: a host block lands on the device in its own dtype (≤ 64 MB,
+    memplan.staging_items) and is converted there, so no full-size temporary in another
+    dtype ever exists.  ``X`` itself when it already qualifies."""
     if not gpu:
         t = X.to(device=device)
         return t if t.dtype == dtype else t.to(dtype)
@@ -742,13 +743,14 @@ class MiniBatchKMeans(_Serving):
         if gpu:
             x_ready = (torch.is_tensor(X) and X.device == device and X.dtype == self.dtype
                        and (not n or pad_columns(X[:0]).data_ptr() == X[:0].data_ptr()))
+            src_es = X.element_size() if torch.is_tensor(X) else 4
             plan = memplan.plan_minibatch(n, D, self.n_clusters, self.dtype, batch_rows=self.batch_size,
-                                          resident=True, init_rows=self.init_size, copy_x=not x_ready)
+                                          resident=True, init_rows=self.init_size, copy_x=not x_ready,
+                                          src_itemsize=src_es if not X.is_cuda else memplan.esize_of(self.dtype))
             plan.budget = memplan.hbm_budget(device)
             if not plan.fits and not X.is_cuda:
                 plan = memplan.plan_minibatch(n, D, self.n_clusters, self.dtype, batch_rows=self.batch_size,
-                                              resident=False, init_rows=self.init_size,
-                                              src_itemsize=X.element_size() if torch.is_tensor(X) else 4)
+                                              resident=False, init_rows=self.init_size, src_itemsize=src_es)
                 plan.budget = memplan.hbm_budget(device)
                 resident = False
             if not plan.fits:

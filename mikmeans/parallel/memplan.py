@@ -35,6 +35,7 @@ SPLIT_MAX_ROWS = 1 << 18         # ops.SPLIT_MAX_ROWS: small batches keep u64 sp
 NSLOT, SLOT_STRIDE = 256, 8      # csrc/kernels.h
 WDOT_SCRATCH = 1024              # csrc/rows.hip WDOT_BLOCKS (weighted-inertia partials)
 COMPACT_ROWS = 4096              # csrc/rows.hip CMP_ROWS (candidate compaction block)
+STAGING_BYTES = 1 << 26          # api._device_rows: host rows cross in blocks of this size
 UPD_LDS_MAX = 160 * 1024         # csrc/plan.h
 KS_NT = 1024
 KS_LIST_BYTES = 2 * (KS_NT // 64) * 64 * 4
@@ -163,6 +164,19 @@ def assign_cn_len(kpad: int) -> int:
     return _cdiv(kpad, 256) * 256
 
 
+def staging_items(n: int, D: int, src_es: int, es: int, prefix: str) -> dict:
+    """api._device_rows moving host rows to the device: one block at a time lands in its
+    source dtype (and, when the destination rows are padded, converted to a contiguous
+    block before the strided copy)."""
+    if n <= 0:
+        return {}
+    rows = min(n, max(1, STAGING_BYTES // max(1, D * max(src_es, es))))
+    it = {f"{prefix}_staging": _r(rows * D * src_es)}
+    if padded_cols(D, es) != D and src_es != es:
+        it[f"{prefix}_staging_cast"] = _r(rows * D * es)
+    return it
+
+
 # ------------------------------------------------------------------ inventories
 def _centroid_items(K: int, Dp: int, esize: int, with_vcount: bool = False) -> dict:
     dpad = dpad_for(Dp, esize)
@@ -257,7 +271,8 @@ class MemoryPlan:
 
 def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = False,
                   incremental: bool = True, init="k-means++", n_local_trials: int | None = None,
-                  copy_x: bool = True, empty_policy: str = "keep", bounded: bool = False) -> MemoryPlan:
+                  copy_x: bool = True, empty_policy: str = "keep", bounded: bool = False,
+                  src_itemsize: int | None = None) -> MemoryPlan:
     """Device-resident Lloyd fit of an ``n``-row shard (``KMeans.fit``): the engine's buffers
     (models/lloyd.py ``LloydEngine._init_gpu``), the seeding workspace and the final E-step.
     ``bounded``: the Hamerly E-step's per-row bounds, flags and compacted rows (17 B/row)."""
@@ -294,6 +309,8 @@ def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = 
         p.update(bound_ub=_r(n * 4), bound_lb=_r(n * 4), bound_cand=_r(n), bound_rows=_r(n * 8),
                  bound_count=_r(8), bound_scratch=_r(max(1, -(-n // COMPACT_ROWS)) * 8), bound_work=_r(16))
     tr = {"init": _init_items(init, n, Dp, D, K, n_local_trials or 0), "final_assign": final}
+    if copy_x and (src_itemsize or es) != es:
+        tr["load"] = staging_items(n, D, src_itemsize or es, es, "x")
     return MemoryPlan("resident", n, D, Dp, K, "bfloat16" if es == 2 else "float32", p, tr)
 
 
@@ -380,8 +397,16 @@ def plan_minibatch(n: int, D: int, K: int, dtype="bfloat16", *, batch_rows: int,
         if Dp != D:
             pred["block_padded"] = _r(B * Dp * es)
         pred["block_labels"] = _r(B * 4)
-    tr = {"init": {"sample": _r(m * Dp * es), **_init_items(init, m, Dp, D, K, 0)},
-          "predict": pred}
+    init_tr = {"sample": _r(m * Dp * es), **_init_items(init, m, Dp, D, K, 0)}
+    tr = {"init": init_tr, "predict": pred}
+    if resident and copy_x and src_itemsize != es:
+        tr["load"] = staging_items(n, D, src_itemsize, es, "x")
+    if not resident:
+        # the init sample crosses from the host through api._device_rows' staging block, and
+        # every step's gathered host batch lands in its source dtype before the cast into
+        # the batch buffer
+        init_tr.update(staging_items(m, D, src_itemsize, es, "sample"))
+        tr["step"] = {"batch_src": _r(b * D * src_itemsize)}
     pl = MemoryPlan("minibatch-resident" if resident else "minibatch-host", n, D, Dp, K,
                     "bfloat16" if es == 2 else "float32", p, tr)
     pl.batch_rows = b
@@ -414,7 +439,7 @@ def plan_fit(n: int, D: int, K: int, dtype="bfloat16", *, budget: int, x_on_devi
     neither does."""
     res = plan_resident(n, D, K, dtype, weighted=weighted, incremental=incremental, init=init,
                         n_local_trials=n_local_trials, copy_x=copy_x, empty_policy=empty_policy,
-                        bounded=bounded)
+                        bounded=bounded, src_itemsize=src_itemsize)
     res.budget = budget
     if res.fits:
         return res

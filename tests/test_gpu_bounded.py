@@ -196,10 +196,9 @@ def test_scatter_assign_uses_row_norms(native):
     torch.testing.assert_close(ub[rows], gmind.sqrt(), rtol=1e-6, atol=1e-6)
     r = rows.cpu()
     Xc = Xb[:, :d].float().cpu()[r]
-    sc = ref.scores(Xc, C)
+    sc = ref.scores(Xb[:, :d].cpu()[r], C)          # (bf16 rows: against the bf16-quantised centres)
     got = sc.gather(1, glab.cpu().long()[:, None])[:, 0]
     best = sc.min(1).values
-    # (a key resolves 2^-17 (|x - c|^2 + 3|x|^2) <= 2^-17 * 5 scale, truncated twice in the
-    # merges: high-norm rows are near-ties of many centres at that resolution)
+    # (a key resolves 2^-17 (|x - c|^2 + 3|x|^2) or better)
     scale = (Xc ** 2).sum(1) + (ref.quantize_centers(C, torch.bfloat16) ** 2).sum(1).max()
-    assert int(((got - best) > 8e-5 * scale + 1e-6).sum()) == 0
+    assert int(((got - best) > 4e-5 * scale + 1e-6).sum()) == 0
