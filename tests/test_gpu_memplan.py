@@ -156,14 +156,22 @@ def test_minibatch_buffers_match_plan(native, monkeypatch, resident):
     X = B.make_blobs(n, D, K, seed=6, dtype=torch.float32, device="cpu")
     kw = dict(batch_size=b, max_steps=6, init="random", seed=3, dtype="bfloat16", device=DEV)
     if not resident:
-        full = M.plan_minibatch(n, D, K, "bfloat16", batch_rows=b, resident=True)
-        monkeypatch.setenv("MIKMEANS_HBM_BYTES", str(int(full.peak * 0.5)))
+        monkeypatch.setenv("MIKMEANS_HBM_BYTES", str(host_budget(n, D, K, b)))
     km = mikmeans.MiniBatchKMeans(K, **kw).fit(X)
     plan = km.memory_plan_
     assert plan["mode"] == ("minibatch-resident" if resident else "minibatch-host")
     inv = km.device_buffers()
     assert set(plan["persistent"]) == set(inv), set(plan["persistent"]) ^ set(inv)
     assert plan["persistent"] == inv
+
+
+def host_budget(n, D, K, b):
+    """A budget between the host-shard and the device-resident mini-batch plans (host f32
+    rows), so MiniBatchKMeans.fit must pick the host plan."""
+    res = M.plan_minibatch(n, D, K, "bfloat16", batch_rows=b, resident=True, src_itemsize=4)
+    host = M.plan_minibatch(n, D, K, "bfloat16", batch_rows=b, resident=False, src_itemsize=4)
+    assert host.peak < res.peak
+    return (host.peak + res.peak) // 2
 
 
 def _peak_of(fn):
@@ -189,8 +197,7 @@ def test_fit_peak_memory_within_plan_other_engines(native, monkeypatch, mode):
     else:
         b = 262_144
         if mode == "minibatch-host":
-            full = M.plan_minibatch(n, D, K, "bfloat16", batch_rows=b, resident=True)
-            monkeypatch.setenv("MIKMEANS_HBM_BYTES", str(int(full.peak * 0.5)))
+            monkeypatch.setenv("MIKMEANS_HBM_BYTES", str(host_budget(n, D, K, b)))
         km, peak = _peak_of(lambda: mikmeans.MiniBatchKMeans(K, batch_size=b, max_steps=5, init="random", seed=1,
                                                              dtype="bfloat16", device=DEV).fit(X))
     plan = km.memory_plan_

@@ -66,7 +66,9 @@ def test_minibatch_fit_device_vs_host_shard(native, monkeypatch):
     kw = dict(batch_size=4096, max_steps=25, init="random", seed=3, dtype="bfloat16", device=DEV)
     a = mikmeans.MiniBatchKMeans(K, **kw).fit(X)
     assert a.memory_plan_["mode"] == "minibatch-resident"
-    monkeypatch.setenv("MIKMEANS_HBM_BYTES", str(int(a.memory_plan_["peak"] * 0.5)))
+    from tests.test_gpu_memplan import host_budget
+
+    monkeypatch.setenv("MIKMEANS_HBM_BYTES", str(host_budget(n, D, K, 4096)))
     b = mikmeans.MiniBatchKMeans(K, **kw).fit(X)
     assert b.memory_plan_["mode"] == "minibatch-host"
     assert torch.equal(a.cluster_centers_, b.cluster_centers_)
