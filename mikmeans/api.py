@@ -791,6 +791,7 @@ class MiniBatchKMeans(_Serving):
             sample = (Xt[sample_idx.to(Xt.device)] if Xt is not None
                       else _device_rows(Xh[sample_idx], device, self.dtype, True))
             eng.set_centers(self._init_centers(sample))
+            del sample                         # (the plan's "init" phase: freed before the steps)
             eng.steps = 0
         # the step count must be the same on every rank (each step is a collective): derive
         # it from the global row count, never from this rank's shard size
