@@ -600,6 +600,31 @@ void kpar_select(const Tensor& d2, int64_t start, const Tensor& psi, double ell,
             "kpar_select");
 }
 
+void tighten(const Tensor& X, int64_t D, const Tensor& labels, const Tensor& C, const Tensor& rows,
+             const Tensor& count, const Tensor& ub, const Tensor& lb, const Tensor& cand) {
+  const int dt = dtype_of(X);
+  const int64_t ldx = check_points(X, dt);
+  const int64_t n = X.size(0);
+  TORCH_CHECK(D >= 1 && D <= X.size(1), "mikmeans: bad D");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= n,
+              "mikmeans: labels must be contiguous int32 [n]");
+  check_cuda(C, "C");
+  TORCH_CHECK(C.scalar_type() == at::kFloat && C.dim() == 2 && C.stride(1) == 1 && C.size(1) >= D,
+              "mikmeans: C must be f32 [K, >=D] with unit column stride");
+  check_i64(rows, "rows", 0);
+  TORCH_CHECK(rows.numel() <= n, "mikmeans: more candidate rows than X rows");
+  check_i64(count, "count", 1);
+  check_f32(ub, "ub", n);
+  check_f32(lb, "lb", n);
+  check_cuda(cand, "cand");
+  TORCH_CHECK(cand.scalar_type() == at::kByte && cand.is_contiguous() && cand.numel() >= n,
+              "mikmeans: cand must be contiguous uint8 [n]");
+  hip_check(mk::launch_tighten(dt, X.data_ptr(), ldx, (int)D, labels.data_ptr<int32_t>(), C.data_ptr<float>(),
+                               C.stride(0), rows.data_ptr<int64_t>(), count.data_ptr<int64_t>(), rows.numel(),
+                               ub.data_ptr<float>(), lb.data_ptr<float>(), cand.data_ptr<uint8_t>(), stream()),
+            "tighten");
+}
+
 void bounds_update(const Tensor& labels, const Tensor& ub, const Tensor& lb, const Tensor& shift2, const Tensor& cn,
                    const Tensor& xn, const Tensor& cand, const Tensor& work, double qeps) {
   const int64_t n = labels.numel();
@@ -670,6 +695,7 @@ std::string js_array(const Tensor& t) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mikmeans native ops (gfx950 HIP kernels + host helpers)";
   m.def("kpar_select", &kpar_select, "k-means|| oversampling flags (philox keyed by the global row)");
+  m.def("tighten", &tighten, "Hamerly tightening: exact distance to the label's centre for the candidates");
   m.def("compact", &compact, "rows of the nonzero flags, ascending; count on the device");
   m.def("compact_blocks", &mk::compact_blocks);
   m.def("assign", &assign, "fused MFMA distance + argmin (K2)", py::arg("X"), py::arg("pack"), py::arg("cn"),

@@ -91,6 +91,11 @@ hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, con
 // rows[0..*count) = indices of the nonzero flags, ascending (deterministic, no host sync);
 // bscratch: int64 [compact_blocks(n)]
 int64_t compact_blocks(int64_t n);
+// Hamerly's tightening over the compacted candidates rows[0..*count): ub = |x - c_label| (f32
+// centres C [K][ldc]); cand = 0 where that is below lb.  n_max bounds *count (grid sizing)
+hipError_t launch_tighten(int dtype, const void* X, int64_t ldx, int D, const int32_t* labels, const float* C,
+                          int64_t ldc, const int64_t* rows, const int64_t* count, int64_t n_max, float* ub,
+                          const float* lb, uint8_t* cand, hipStream_t s);
 // k-means|| round: cand[i] = u(start + i) < ell * d2[i] / psi[0] (philox uniform keyed by the global row)
 hipError_t launch_kpar_select(const float* d2, int64_t n, int64_t start, const double* psi, double ell,
                               uint64_t seed, uint32_t round, uint8_t* cand, hipStream_t s);

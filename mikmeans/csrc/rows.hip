@@ -295,6 +295,75 @@ hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, con
   return hipGetLastError();
 }
 
+// ---- Hamerly tightening ----------------------------------------------------------------
+// A row whose moved bounds no longer prove its label first gets the exact distance to its
+// label's f32 centre (Hamerly 2010's second test): ub drops to it, and a row whose tight ub
+// is below lb keeps its label without the full assign.  A wave takes 4 rows per pass, 16
+// lanes per row in 16-B pieces (one coalesced load per piece), |x - c|^2 summed directly
+// (no |x|^2 + |c|^2 cancellation).  rows[0..*count): the compacted candidates.
+template <typename T>
+__global__ __launch_bounds__(256) void tighten_kernel(const T* __restrict__ X, int64_t ldx, int D,
+                                                     const int32_t* __restrict__ labels,
+                                                     const float* __restrict__ C, int64_t ldc,
+                                                     const int64_t* __restrict__ rows,
+                                                     const int64_t* __restrict__ count, float* __restrict__ ub,
+                                                     const float* __restrict__ lb, uint8_t* __restrict__ cand) {
+  constexpr int V = Elem<T>::V;
+  const int64_t m = count[0];
+  const int lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t nwave = ((int64_t)gridDim.x * 256) >> 6;
+  const int pieces = (D + V - 1) / V;
+  for (int64_t base = wave * 4; base < m; base += nwave * 4) {   // (wave-uniform loop)
+    const int64_t j = base + grp;
+    int64_t row = 0;
+    int a = -1;
+    if (j < m) {
+      row = rows[j];
+      a = labels[row];
+    }
+    float s = 0.f;
+    if (a >= 0) {
+      const T* xp = X + row * ldx;
+      const float* cp = C + (int64_t)a * ldc;
+      for (int p = gl; p < pieces; p += 16) {
+        float f[V];
+        unpack16(*(const u32x4*)(xp + p * V), f, (T*)nullptr);
+#pragma unroll
+        for (int q = 0; q < V; ++q) {
+          const int col = p * V + q;
+          if (col < D) {
+            const float d = f[q] - cp[col];
+            s = __builtin_fmaf(d, d, s);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);   // (within the 16-lane group)
+    if (gl == 0 && a >= 0) {
+      const float u = __builtin_sqrtf(s) * (1.f + 1e-6f);   // (+ the f32 rounding of D terms)
+      ub[row] = u;
+      if (u < lb[row]) cand[row] = 0;
+    }
+  }
+}
+
+hipError_t launch_tighten(int dtype, const void* X, int64_t ldx, int D, const int32_t* labels, const float* C,
+                          int64_t ldc, const int64_t* rows, const int64_t* count, int64_t n_max, float* ub,
+                          const float* lb, uint8_t* cand, hipStream_t s) {
+  if (n_max <= 0) return hipSuccess;
+  int64_t nb = (n_max + 15) / 16;   // 16 rows per block and pass
+  if (nb > 8192) nb = 8192;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(tighten_kernel<uint16_t>, dim3((unsigned)nb), dim3(256), 0, s, (const uint16_t*)X, ldx, D,
+                       labels, C, ldc, rows, count, ub, lb, cand);
+  else
+    hipLaunchKernelGGL(tighten_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, (const float*)X, ldx, D, labels,
+                       C, ldc, rows, count, ub, lb, cand);
+  return hipGetLastError();
+}
+
 // ---- candidate compaction ----------------------------------------------------------------
 // rows[0..count) = the indices i with cand[i] != 0, ascending; count stays on the device.
 // Three launches, no atomics (so the order -- and with it each row's workgroup in the

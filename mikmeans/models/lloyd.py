@@ -296,11 +296,11 @@ class LloydEngine:
         if graphs is not None:
             # two graph launches around the (eager) collective: everything up to the packed
             # message, then everything after it for this centre-buffer parity
-            graphs[0].replay()
+            graphs[2 * self._gphase].replay()
             self._collective()
             if self.empty_policy == "farthest":
                 self._relocate_empty()
-            graphs[1 + self._gphase].replay()
+            graphs[2 * self._gphase + 1].replay()
             self._gphase ^= 1
         elif self.gpu:
             self._step_gpu()
@@ -315,7 +315,7 @@ class LloydEngine:
         """Record a Lloyd iteration as hipGraphs so each later :meth:`step` is two graph
         launches instead of ~6-12 kernel launches.  The graphs hold the device work on
         either side of the iteration's collective -- the packed message (assign, M-step,
-        reduce) and the finalize (one graph per centre-buffer parity); the all-reduce and the
+        reduce) and the finalize, one pair per centre-buffer parity; the all-reduce and the
         'farthest' empty-cluster relocation (host reads) run eagerly between them.  So no
         RCCL call is ever recorded, and a host-staged communicator works too.
 
@@ -341,7 +341,9 @@ class LloydEngine:
                 self._post_collective(relocate=False)
             torch.cuda.synchronize(dev)
             graphs = []
-            for part in ("pre", "post", "post"):
+            # one (pre, post) pair per centre-buffer parity: C and Cnew swap every step, and
+            # both halves may read them (the bounded E-step's tightening reads C)
+            for part in ("pre", "post", "pre", "post"):
                 g = torch.cuda.CUDAGraph()
                 # thread_local: other threads (the RCCL watchdog polling earlier collectives)
                 # may keep making calls that are illegal while a stream captures
@@ -353,7 +355,7 @@ class LloydEngine:
                     else:
                         self._post_collective(relocate=False)
                 graphs.append(g)
-                if part == "post":   # the second finalize graph: the other centre-buffer parity
+                if part == "post":   # the next pair: the other centre-buffer parity
                     self.C, self.Cnew = self.Cnew, self.C
         except Exception as e:  # noqa: BLE001 -- any capture failure: eager from here on
             self.capture_error = f"{type(e).__name__}: {e}".splitlines()[0]
@@ -465,12 +467,18 @@ class LloydEngine:
     def _bounded_assign(self):
         """E-step over the rows the Hamerly bounds cannot vouch for (every row after new
         centres or a label reset): bounds moved by the last shifts -> the flagged rows
-        compacted in ascending order (count on the device) -> a gathered assign that
-        scatters labels and fresh bounds back to those rows.  No host read."""
+        compacted in ascending order (count on the device) -> their exact distance to the
+        label's centre (tightening) -> the rows still flagged compacted again -> a gathered
+        assign that scatters labels and fresh bounds back to those rows.  No host read."""
         # (distance of a quantised centre from its f32 copy, relative to |c|: bf16 RNE)
         qeps = 2.0 ** -8 if self.dtype == torch.bfloat16 else 2.0 ** -22
         self._C.bounds_update(self.labels, self.ub, self.lb, self.shift, self.pk.cn, self.xn, self.cand,
                               self._bwork, qeps)
+        self._C.compact(self.cand, self._brows, self._bcount, self._bscratch)
+        # Hamerly's second test: the exact distance to the label's centre; rows it clears
+        # keep their label, the rest are compacted again for the full assign
+        self._C.tighten(self.X, self.D, self.labels, self.C, self._brows, self._bcount, self.ub, self.lb,
+                        self.cand)
         self._C.compact(self.cand, self._brows, self._bcount, self._bscratch)
         self.pk.assign(self.X, self.xn, self.labels, None, self.slots, True, rows=self._brows, ub=self.ub,
                        lb=self.lb, scatter=True, count=self._bcount)

@@ -202,3 +202,38 @@ def test_scatter_assign_uses_row_norms(native):
     # (a key resolves 2^-17 (|x - c|^2 + 3|x|^2) or better)
     scale = (Xc ** 2).sum(1) + (ref.quantize_centers(C, torch.bfloat16) ** 2).sum(1).max()
     assert int(((got - best) > 4e-5 * scale + 1e-6).sum()) == 0
+
+
+@pytest.mark.parametrize("dtype,d", [(torch.bfloat16, 128), (torch.bfloat16, 40), (torch.float32, 77)])
+def test_tighten_exact_distance(native, dtype, d):
+    """Hamerly's tightening (csrc/rows.hip tighten_kernel): for the listed candidates ub
+    becomes |x - C[label]| (f32 centres, direct sum of squares), the flag clears where that
+    is below lb, unlisted and unassigned rows are untouched."""
+    from mikmeans.ops import pad_columns
+
+    n, k = 50_000, 37
+    g = torch.Generator().manual_seed(d)
+    X = pad_columns((torch.randn(n, d, generator=g) * 3).to(dtype).to(DEV))
+    C = torch.zeros(k, X.shape[1], device=DEV)
+    C[:, :d] = torch.randn(k, d, generator=g).to(DEV)
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32).to(DEV)
+    lab[5] = -1
+    rows = torch.randperm(n, generator=g)[:20_000].sort().values.to(DEV)
+    rows[0] = 5
+    rows = rows.sort().values
+    count = torch.tensor([rows.numel() - 100], dtype=torch.int64, device=DEV)   # the tail is not listed
+    ub = torch.full((n,), -1.0, device=DEV)
+    lb = torch.where(torch.arange(n, device=DEV) % 2 == 0, torch.full((n,), 1e9, device=DEV),
+                     torch.zeros(n, device=DEV))
+    cand = torch.ones(n, dtype=torch.uint8, device=DEV)
+    native.tighten(X, d, lab, C, rows, count, ub, lb, cand)
+    torch.cuda.synchronize()
+    listed = rows[: int(count)]
+    listed = listed[lab[listed] >= 0]
+    ref = (X[listed, :d].double() - C[lab[listed].long(), :d].double()).norm(dim=1)
+    torch.testing.assert_close(ub[listed].double(), ref, rtol=2e-6, atol=1e-6)
+    even = (listed % 2 == 0)
+    assert bool((cand[listed[even]] == 0).all()) and bool((cand[listed[~even]] == 1).all())
+    mask = torch.ones(n, dtype=torch.bool, device=DEV)
+    mask[listed] = False
+    assert bool((ub[mask] == -1.0).all()) and bool((cand[mask] == 1).all())
