@@ -94,7 +94,11 @@ def _device_rows(X: torch.Tensor, device, dtype, gpu: bool, block_bytes: int = 1
         out[:, D:].zero_()
     rows = max(1, block_bytes // max(1, D * max(X.element_size(), out.element_size())))
     for i in range(0, n, rows):
-        out[i : i + rows, :D].copy_(X[i : i + rows])
+        blk = X[i : i + rows]
+        if blk.device != out.device:
+            blk = blk.to(out.device)          # the staging block, in the source dtype
+        out[i : i + rows, :D].copy_(blk)      # cast (and pad) on the device
+        del blk
     return out
 
 
