@@ -39,15 +39,16 @@ def test_full_assign_writes_nearest_and_second_distances(native, dtype, d, k):
     torch.testing.assert_close(e.lb.cpu().double(), two[:, 1], rtol=2e-3, atol=2e-3 * float(scale.mean()))
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_bounds_stay_valid_and_skip_rows(native, dtype):
+@pytest.mark.parametrize("dtype,tighten", [(torch.float32, False), (torch.bfloat16, False),
+                                           (torch.bfloat16, True)])
+def test_bounds_stay_valid_and_skip_rows(native, dtype, tighten):
     """After every step: every row the bounds vouch for (not a candidate) really is nearest to
     its label's centre, ub >= its distance, lb <= the second distance; and once the centres
     settle, most rows are skipped."""
     X = B.make_blobs(200_000, 64, 32, seed=3, dtype=dtype, device=DEV)
     K = 48
     C0 = X[:K].float()
-    e = LloydEngine(X, K, bounded=True).set_centers(C0)
+    e = LloydEngine(X, K, bounded=True, tighten=tighten).set_centers(C0)
     skipped = []
     for it in range(12):
         e.step()
