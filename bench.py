@@ -73,6 +73,9 @@ def main(argv=None):
                          "all-reduce, one launch; eager fallback if capture fails).  auto: on for one rank "
                          "(cfg2's 0.7 ms steps gain ~1 %%); off for N > 1, where the host already runs "
                          "far ahead of ~3 ms steps")
+    ap.add_argument("--also-bounded", action=argparse.BooleanOptionalAction, default=True,
+                    help="cfg3: also time KMeans(algorithm='hamerly')'s bounded E-step from the same start "
+                         "(an extra field)")
     ap.add_argument("--kpp-sampling", default="exact", choices=["exact", "two-stage"],
                     help="cfg4 multi-rank k-means++: exact (2 collectives per centre) or two-stage (1)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
@@ -204,6 +207,22 @@ def main(argv=None):
                 "assignments_per_s": args.steps / el_inc * N,
                 "centres_bitwise_equal_to_full": bool(torch.equal(inc.centers, C_full)),
             }
+            if args.also_bounded:
+                # KMeans(algorithm="hamerly"): the bounded E-step re-assigns only the rows its
+                # bounds cannot vouch for (the same Lloyd iterates up to bf16 near-ties).  From
+                # the same start, same warm-up and step count; an extra field, not the headline.
+                C_inc = inc.centers.clone()
+                del inc
+                bnd = LloydEngine(X, K, comm=comm, incremental=True, bounded=True).set_centers(C0)
+                _capture(bnd, use_graph)
+                el_b = _timed_steps(bnd, comm, args.warmup, args.steps, sync)
+                extra["bounded_estep"] = {
+                    "value": args.steps / el_b,
+                    "ms_per_step": el_b * 1e3 / args.steps,
+                    "rows_reassigned_last_step": bnd.reassigned,
+                    "max_centre_diff_vs_full": float((bnd.centers - C_inc).abs().max()),
+                }
+                del bnd
     if comm.rank == 0:
         out = {
             "metric": METRIC if args.config == "cfg3" else f"{cfg['model']} ({unit})",
