@@ -777,6 +777,19 @@ class MiniBatchKMeans(_Serving):
                     xb = Xh[i : i + (1 << 20)].to(self.dtype).float().abs()
                     bound = torch.maximum(bound, xb.amax(0).double())
             eng.set_bound(bound)
+        # the fit's own device buffers, allocated before the seeding so the plan's phases
+        # (persistent + the largest transient) bound the real peak
+        buf = rows = None
+        self._fit_buffers = {}
+        if eng.gpu and Xt is not None and Xt.data_ptr() != getattr(X, "data_ptr", lambda: None)():
+            self._fit_buffers["X"] = Xt          # the fit's device copy of the shard
+        if eng.gpu and b:
+            if Xt is not None:    # device shard: the step reads X[rows] in place, nothing gathered
+                rows = torch.empty(b, dtype=torch.int64, device=device)
+                self._fit_buffers["rows"] = rows
+            else:                 # host shard: the batch's rows are gathered on the host
+                buf = torch.zeros((b, eng.Dp), dtype=self.dtype, device=device)
+                self._fit_buffers["batch"] = buf
         if resume_from is not None:
             ck = load_checkpoint(resume_from, comm=comm)
             if ck.get("kind") != "minibatch" or int(ck["n_features"]) != D:
@@ -801,17 +814,6 @@ class MiniBatchKMeans(_Serving):
         # it from the global row count, never from this rank's shard size
         n_global, _ = _shard_info(n, comm, comm.device)
         steps = self.max_steps or max(1, math.ceil(self.max_iter * n_global / (self.batch_size * comm.world)))
-        buf = rows = None
-        self._fit_buffers = {}
-        if eng.gpu and Xt is not None and Xt.data_ptr() != getattr(X, "data_ptr", lambda: None)():
-            self._fit_buffers["X"] = Xt          # the fit's device copy of the shard
-        if eng.gpu and b:
-            if Xt is not None:    # device shard: the step reads X[rows] in place, nothing gathered
-                rows = torch.empty(b, dtype=torch.int64, device=device)
-                self._fit_buffers["rows"] = rows
-            else:                 # host shard: the batch's rows are gathered on the host
-                buf = torch.zeros((b, eng.Dp), dtype=self.dtype, device=device)
-                self._fit_buffers["batch"] = buf
         C = native_mod() if eng.gpu else None
         while eng.steps < steps:
             s = eng.steps
