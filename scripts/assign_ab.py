@@ -43,14 +43,27 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--arms", default="assign_persist=0;assign_persist=1")
+    ap.add_argument("--gather", type=int, default=0,
+                    help="> 0: time the gathered assign of this many random rows (the mini-batch "
+                         "resident path: X[rows] read in place, norms from the fragments)")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     dev = torch.device("cuda")
     comm = Comm.local(dev)
     X = make_blobs(a.n, a.d, a.k, seed=0, dtype=dt, device=dev, centers=blob_centers(a.k, a.d, 10.0, 0, device=dev))
     eng = LloydEngine(X, a.k, comm=comm).set_centers(init_random(X, a.d, a.k, a.n, 0, comm, 0))
-    for _ in range(3):
+    for _ in range(3 if not a.gather else 1):
         eng.step()
+    if a.gather:
+        g = torch.Generator(device=dev).manual_seed(5)
+        rows = torch.randint(0, a.n, (a.gather,), device=dev, generator=g)
+        glab = torch.empty(a.gather, dtype=torch.int32, device=dev)
+
+        def call():
+            eng.pk.assign(eng.X, None, glab, None, eng.slots, False, rows=rows)
+    else:
+        def call():
+            eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True)
     arms = [parse_arm(s) for s in a.arms.split(";")]
     names = [s or "default" for s in a.arms.split(";")]
     labels = {}
@@ -62,13 +75,13 @@ def main():
         for k, v in arm.items():
             native.set_variant(k, v)
         try:
-            eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True)   # warm / attributes
+            call()   # warm / attributes
             ev[0].record()
             for _ in range(a.reps):
-                eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True)
+                call()
             ev[1].record()
             torch.cuda.synchronize()
-            return ev[0].elapsed_time(ev[1]) / a.reps, eng.labels.clone()
+            return ev[0].elapsed_time(ev[1]) / a.reps, (glab if a.gather else eng.labels).clone()
         finally:
             for k, v in old.items():
                 native.set_variant(k, v)
@@ -80,11 +93,13 @@ def main():
             times[n].append(t)
             labels.setdefault(n, lab)
     ref = labels[names[0]]
-    res = {"n": a.n, "d": a.d, "k": a.k, "dtype": a.dtype, "rounds": a.rounds, "reps": a.reps}
+    res = {"n": a.n, "d": a.d, "k": a.k, "dtype": a.dtype, "rounds": a.rounds, "reps": a.reps,
+           "gathered_rows": a.gather}
+    m = a.gather or a.n
     for n in names:
         med = statistics.median(times[n])
         res[n] = {"median_ms": round(med, 4), "min_ms": round(min(times[n]), 4),
-                  "tflops": round(2.0 * a.n * a.k * a.d / (med * 1e-3) / 1e12, 1),
+                  "tflops": round(2.0 * m * a.k * a.d / (med * 1e-3) / 1e12, 1),
                   "labels_equal": bool(torch.equal(labels[n], ref))}
     print(json.dumps(res), flush=True)
 

@@ -45,6 +45,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     ab_f32) step ab_f32 300 python -u scripts/assign_ab.py --d 128 --k 256 --n 1000000 --dtype f32 --reps 20 \
                --arms "default;assign_persist=1" ;;
     blobs) step blobs 200 python -u scripts/blobs_bench.py ;;
+    ab_g256) step ab_g256 400 python -u scripts/assign_ab.py --d 256 --k 512 --n 125000000 --gather 16777216 \
+               --arms "default;assign_geom=1;assign_geom=2;assign_geom=3" ;;
     ab_wide) step ab_wide 300 python -u scripts/assign_ab.py --d 768 --k 1024 --n 4000000 --arms "default" ;;
     bench) step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 ;;
     benchauto) step bench_nopg 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 3 --pg auto --no-also-incremental ;;
