@@ -66,7 +66,8 @@ def cmd_fit(a) -> int:
         X = make_blobs(end - start, d, c, seed=cfg.seed, i0=start, device=comm.device, dtype=dtype)
     if cfg.batch_size > 0:
         km = MiniBatchKMeans(cfg.n_clusters, batch_size=cfg.batch_size, max_iter=cfg.max_iter, init=cfg.init,
-                             dtype=dtype, device=comm.device, seed=cfg.seed, comm=comm)
+                             dtype=dtype, device=comm.device, seed=cfg.seed, comm=comm,
+                             init_sampling=cfg.init_sampling)
         if resume and comm.rank == 0:
             print(f"[mikmeans] resuming from {resume}", file=sys.stderr, flush=True)
         # batch rows are drawn by (seed, rank, step): a restart on the same world size

@@ -59,6 +59,19 @@ def test_cli_fit_predict_room(tmp_path):
     assert again.splitlines()[:4] == txt.splitlines()[:4]
 
 
+def test_cli_fit_algorithm_and_init_options(tmp_path):
+    """`fit --algorithm hamerly --init k-means|| --init-sampling two-stage`: the options reach
+    the estimator and its saved config (the CPU path assigns every row, so the fit is exact)."""
+    _run(["blobs", "--n", "2000", "--d", "3", "--centers", "4", "--output", "p.npy"], tmp_path)
+    rec = json.loads(_run(["fit", "--input", "p.npy", "--n-clusters", "4", "--output", "m", "--device", "cpu",
+                           "--algorithm", "hamerly", "--init", "k-means||", "--init-sampling", "two-stage"],
+                          tmp_path).strip().splitlines()[-1])
+    assert sum(rec["metrics"]["counts"]) == 2000
+    state = json.loads((tmp_path / "m" / "state.json").read_text())
+    cfg = state.get("config", state)
+    assert cfg["algorithm"] == "hamerly" and cfg["init"] == "k-means||" and cfg["init_sampling"] == "two-stage"
+
+
 def test_resume_matches_uninterrupted(tmp_path):
     from mikmeans import KMeans
     from mikmeans.data.blobs import make_blobs

@@ -238,3 +238,38 @@ def test_tighten_exact_distance(native, dtype, d):
     mask = torch.ones(n, dtype=torch.bool, device=DEV)
     mask[listed] = False
     assert bool((ub[mask] == -1.0).all()) and bool((cand[mask] == 1).all())
+
+
+@pytest.mark.parametrize("dtype,d,k,spherical,frozen", [
+    (torch.float32, 40, 77, False, False),
+    (torch.bfloat16, 96, 50, True, False),
+    (torch.bfloat16, 64, 40, False, True),
+])
+def test_bounded_option_combinations(native, dtype, d, k, spherical, frozen):
+    """The bounded E-step with ragged K / D, the cosine metric's sphere projection and frozen
+    centres: it follows the full-E-step engine, and frozen centres never move."""
+    n = 150_000
+    X = B.make_blobs(n, d, 30, seed=k, dtype=dtype, device=DEV)
+    if spherical:
+        from mikmeans.ops import pad_columns
+
+        X = pad_columns(X).clone()
+        native.row_normalize(X)
+        X = X[:, :d] if X.shape[1] != d else X
+    C0 = X[:k, :d].float()
+    fz = None
+    if frozen:
+        fz = torch.zeros(k, dtype=torch.int32, device=DEV)
+        fz[::5] = 1
+    ea = LloydEngine(X, k, spherical=spherical, frozen=fz, n_features=d).set_centers(C0)
+    eb = LloydEngine(X, k, spherical=spherical, frozen=fz, n_features=d, bounded=True).set_centers(C0)
+    assert eb.bounded
+    for _ in range(8):
+        ea.step()
+        eb.step()
+    torch.cuda.synchronize()
+    agree = (ea.labels == eb.labels).float().mean().item()
+    assert agree >= (0.999 if dtype == torch.float32 else 0.99), agree
+    assert eb.inertia() == pytest.approx(ea.inertia(), rel=1e-3)
+    if frozen:
+        assert torch.equal(eb.centers[::5], C0[::5])
