@@ -507,8 +507,10 @@ class KMeans(_Serving):
                     _mlog.log(st, counts)
                 faults.maybe_fail(comm.rank, st.iteration)
                 if self.verbose and comm.rank == 0:
-                    print(f"[mikmeans] iter {st.iteration} inertia {st.inertia:.6g} "
-                          f"shift {st.shift:.3g} changed {st.n_changed}", flush=True)
+                    what = (f"reassigned {rec['reassigned']}" if "reassigned" in rec
+                            else f"inertia {st.inertia:.6g}")
+                    print(f"[mikmeans] iter {st.iteration} {what} shift {st.shift:.3g} changed {st.n_changed}",
+                          flush=True)
                 if self.checkpoint_every and self.checkpoint_dir and st.iteration % self.checkpoint_every == 0:
                     from .utils.checkpoint import save_checkpoint
 
