@@ -128,3 +128,41 @@ def packed_seed_hazards(funcs: dict[str, list[str]], name_filter: str = "assign1
 
 def packed_ops(funcs: dict[str, list[str]], name_filter: str = "assign16_kernel") -> int:
     return sum(1 for fn, ls in funcs.items() if name_filter in fn for x in ls if x.split(None, 1)[0] in _PACKED_F32)
+
+
+@dataclass
+class KernelResources:
+    name: str            # demangled
+    vgprs: int
+    vgpr_spills: int
+    scratch_bytes: int   # .private_segment_fixed_size
+
+
+def kernel_resources(elf: Path) -> list[KernelResources]:
+    """Per-kernel register use from the code object's AMDGPU metadata note."""
+    r = subprocess.run([_tool("llvm-readelf"), "--notes", str(elf)], check=True, capture_output=True,
+                       text=True).stdout
+    raw = []
+    for blk in r.split("- .agpr_count")[1:]:
+        name = re.search(r"\.name:\s+(\S+)", blk)
+        vg = re.search(r"\.vgpr_count:\s+(\d+)", blk)
+        sp = re.search(r"\.vgpr_spill_count:\s+(\d+)", blk)
+        pr = re.search(r"\.private_segment_fixed_size:\s+(\d+)", blk)
+        if name and vg:
+            raw.append((name.group(1), int(vg.group(1)), int(sp.group(1)) if sp else 0,
+                        int(pr.group(1)) if pr else 0))
+    dem = subprocess.run(["c++filt"], input="\n".join(x[0] for x in raw), capture_output=True,
+                         text=True).stdout.splitlines() if raw else []
+    if len(dem) != len(raw):
+        dem = [x[0] for x in raw]
+    return [KernelResources(d, v, s_, p_) for (_, v, s_, p_), d in zip(raw, dem)]
+
+
+def assign16_template_args(demangled: str) -> list[str] | None:
+    """The template arguments of an assign16_kernel instantiation (T, DPAD, P, CT, NBUF, OCC,
+    NW, FULLD, VARG, PMAJ, PERSIST, AST, TOP2), or None."""
+    if "assign16_kernel<" not in demangled:
+        return None
+    inner = demangled[demangled.index("assign16_kernel<") + len("assign16_kernel<"):]
+    inner = inner[: inner.rindex(">(")]
+    return [a.strip() for a in inner.split(",")]

@@ -58,3 +58,22 @@ def test_launchers_never_read_the_environment():
     for src in sorted(_build.CSRC.glob("*.hip")) + sorted(_build.CSRC.glob("*.h")):
         assert "getenv" not in src.read_text(), src.name
     assert _build.CSRC.joinpath("binding.cpp").read_text().count("getenv(") == 1
+
+
+def test_assign_kernels_register_budget(tmp_path):
+    """Spill guard (round 4): every bounded-E-step (TOP2) instantiation and the headline
+    geometry (bf16 D=128, 4 blocks at 4 waves/SIMD) fit their register budget.  TOP2 builds
+    of the bf16 D=64/128/256 default geometries spilled 500-940 VGPRs and ran 5.7x slower
+    (profiles/r4_05_hamerly_ab_top2_spills.log), which no functional test notices."""
+    obj = _build._compile(SRC, _build.source_flags(SRC.name), verbose=False)
+    res = isa.kernel_resources(isa.device_elf(obj, tmp_path / "dev.o"))
+    a16 = [(r, isa.assign16_template_args(r.name)) for r in res]
+    a16 = [(r, t) for r, t in a16 if t]
+    assert len(a16) > 50
+    top2 = [(r, t) for r, t in a16 if t[-1] == "true"]
+    assert top2, "no TOP2 instantiations"
+    bad = [(t[:7], r.vgpr_spills) for r, t in top2 if r.vgpr_spills > 0]
+    assert not bad, bad
+    head = [r for r, t in a16 if t[:7] == ["unsigned short", "128", "4", "4", "2", "4", "4"]
+            and t[8:] == ["false", "1", "false", "false", "false"]]
+    assert head and max(r.vgpr_spills for r in head) <= 2, [(r.name[-60:], r.vgpr_spills) for r in head]
