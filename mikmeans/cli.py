@@ -157,6 +157,14 @@ def cmd_room(a) -> int:
     return 0
 
 
+def cmd_serve(a) -> int:
+    """`mikmeans serve`: the room board and model serving over HTTP (mikmeans/serve.py)."""
+    from .serve import serve
+
+    serve(a.room, a.model, host=a.host, port=a.port, device=a.device)
+    return 0
+
+
 def cmd_session(a) -> int:
     """A scripted participant of a live room session (parallel/elastic.py): ``--found ROOM``
     hosts the rendezvous store and starts the session, otherwise ``--join`` enters it; the
@@ -373,6 +381,12 @@ def build_parser():
     r.add_argument("--coin", action="store_true", help="flip a coin (Heads/Tails)")
     r.add_argument("--d12", action="store_true", help="roll a twelve-sided die")
     r.add_argument("--shuffle-names", action="store_true", help="print a shuffled order of the card titles")
+    sv = sub.add_parser("serve", help="HTTP service: the room board page + JSON API, and model serving")
+    sv.add_argument("--room", default=None, help="room export JSON to start from")
+    sv.add_argument("--model", default=None, help="fitted model directory (KMeans.save) to serve /api/predict")
+    sv.add_argument("--host", default="127.0.0.1")
+    sv.add_argument("--port", type=int, default=8000)
+    sv.add_argument("--device", default=None)
     se = sub.add_parser("session", help="one participant of a live replicated room session")
     se.add_argument("--host", default="127.0.0.1", help="rendezvous (TCPStore) host")
     se.add_argument("--port", type=int, required=True)
@@ -434,7 +448,8 @@ def main(argv=None) -> int:
         return cmd_launch(a, rest)
     a = build_parser().parse_args(argv)
     return {"fit": cmd_fit, "predict": cmd_predict, "blobs": cmd_blobs, "room": cmd_room, "session": cmd_session,
-            "export": cmd_export, "import": cmd_import, "info": cmd_info, "plan": cmd_plan}[a.cmd](a)
+            "export": cmd_export, "import": cmd_import, "info": cmd_info, "plan": cmd_plan,
+            "serve": cmd_serve}[a.cmd](a)
 
 
 if __name__ == "__main__":
