@@ -20,7 +20,8 @@ Endpoints (JSON in and out):
   paths, locks respected); ``POST /api/centroids/{id}/lock``, ``DELETE /api/centroids/{id}``;
 * ``POST /api/auto`` numeric k-means over the cards' trait vectors; ``GET /api/dashboard``;
 * ``GET /api/model`` the served model's centroids as flat floats; ``POST /api/predict``
-  {points[, distances]} -> labels (and squared distances), ``POST /api/transform``.
+  {points[, distances]} -> labels (and squared distances), ``POST /api/predict.npy`` (a
+  ``.npy`` body in, ``.npy`` labels out), ``POST /api/transform``.
 
 ``mikmeans serve [--room FILE] [--model DIR] [--host 127.0.0.1] [--port 8000]``.
 """
@@ -30,6 +31,8 @@ import threading
 
 import numpy as np
 import torch
+from fastapi import Body, FastAPI, HTTPException, Request
+from fastapi.responses import HTMLResponse, Response
 
 from .models.room import Room
 
@@ -130,9 +133,6 @@ def _jsonable(obj):
 def create_app(room: Room | None = None, model=None, *, device=None):
     """The FastAPI app serving ``room`` (a new one when None) and, when given, a fitted
     ``model`` (:class:`~mikmeans.KMeans` / :class:`~mikmeans.MiniBatchKMeans`)."""
-    from fastapi import Body, FastAPI, HTTPException
-    from fastapi.responses import HTMLResponse, Response
-
     app = FastAPI(title="mikmeans", docs_url=None, redoc_url=None, openapi_url=None)
     state = {"room": room if room is not None else Room(seed=0)}
     lock = threading.Lock()
@@ -258,6 +258,28 @@ def create_app(room: Room | None = None, model=None, *, device=None):
         if mind is not None:
             out["distances"] = mind.cpu().tolist()
         return out
+
+    @app.post("/api/predict.npy")
+    async def predict_npy(request: Request):
+        """Binary serving: the body is a ``.npy`` array [n, D] (``numpy.save``; loaded with
+        ``allow_pickle=False``), the answer the int32 labels as ``.npy`` -- no JSON
+        parsing of large batches."""
+        import io
+
+        m = _model()
+        raw = await request.body()
+        try:
+            arr = np.load(io.BytesIO(raw), allow_pickle=False)
+        except Exception as e:  # noqa: BLE001 -- any malformed payload is the client's error
+            raise HTTPException(400, f"body must be a .npy array: {e}") from None
+        if arr.ndim != 2 or arr.shape[1] != m.cluster_centers_.shape[1]:
+            raise HTTPException(400, f"array must be [n, {m.cluster_centers_.shape[1]}]")
+        X = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float32)).to(m.cluster_centers_.device)
+        with lock:
+            labels, _, _ = m._assign_rows(X, False)
+        buf = io.BytesIO()
+        np.save(buf, labels.cpu().numpy().astype(np.int32), allow_pickle=False)
+        return Response(buf.getvalue(), media_type="application/octet-stream")
 
     @app.post("/api/transform")
     def transform(body: dict = Body(...)):

@@ -80,6 +80,15 @@ def test_model_serving_matches_predict():
     t = c.post("/api/transform", json={"points": X[:3].tolist()}).json()["distances"]
     assert np.allclose(np.asarray(t), km.transform(X[:3]).numpy(), rtol=1e-5, atol=1e-5)
     assert c.post("/api/predict", json={"points": [[1.0, 2.0]]}).status_code == 400
+    import io
+
+    buf = io.BytesIO()
+    np.save(buf, X[:200].numpy())
+    rb = c.post("/api/predict.npy", content=buf.getvalue(), headers={"Content-Type": "application/octet-stream"})
+    assert rb.status_code == 200
+    lab = np.load(io.BytesIO(rb.content), allow_pickle=False)
+    assert lab.dtype == np.int32 and lab.tolist() == km.predict(X[:200]).tolist()
+    assert c.post("/api/predict.npy", content=b"not npy").status_code == 400
     assert _client(Room(seed=0)).post("/api/predict", json={"points": [[0.0] * 5]}).status_code == 404
 
 
