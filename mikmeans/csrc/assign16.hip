@@ -313,20 +313,17 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     float best[C::P], seg_best[C::P];
     int bg[C::P];
     uint32_t vb[C::P], tb[C::P];   // VARG: running minimum (bits of a positive float), its tile
-    // TOP2 (bounded E-step): this lane's smallest and second-smallest score (keys: index bits
-    // included, <= 2^-17 relative -- the bounds' slack covers it), merged over lanes later
-    float m1[C::P], m2[C::P];
+    // TOP2 (bounded E-step): this lane's second-smallest score (keys: index bits included,
+    // <= 2^-17 relative -- the bounds' slack covers it), merged over lanes later; the smallest
+    // is the epilogue's own running minimum (min(best, seg_best)), so TOP2 adds one register
+    // per point block
+    float m2[C::P];
 #pragma unroll
     for (int p = 0; p < C::P; ++p) {
       best[p] = 3.0e38f; seg_best[p] = 3.0e38f; bg[p] = 0;
       vb[p] = 0x7f7fffffu; tb[p] = 0u;
-      m1[p] = 3.0e38f; m2[p] = 3.0e38f;
+      m2[p] = 3.0e38f;
     }
-    // (m1 <= m2 stays true: the median of (m1, m2, k) is the new second smallest)
-    auto push2 = [&](int p, float k) {
-      m2[p] = __builtin_amdgcn_fmed3f(m1[p], m2[p], k);
-      m1[p] = fminf(m1[p], k);
-    };
     const int ngrp = nch * C::CT;   // one past the last tile (global tile numbering)
     const unsigned kmask = key6_mask();
 
@@ -426,8 +423,19 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
               const f32x4& sv = acc[p];
               const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
               const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
-              if constexpr (TOP2) { push2(p, k0); push2(p, k1); push2(p, k2); push2(p, k3); }
-              seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
+              if constexpr (TOP2) {
+                // the two smallest of the tile's four keys, merged with the running pair
+                // (min(best, seg_best), m2): second = min(max(old min, new min), m2, new second)
+                const float lo01 = fminf(k0, k1), hi01 = fmaxf(k0, k1);
+                const float lo23 = fminf(k2, k3), hi23 = fmaxf(k2, k3);
+                const float kmin = fminf(lo01, lo23);
+                const float ksec = fminf(fmaxf(lo01, lo23), fminf(hi01, hi23));
+                const float omin = fminf(best[p], seg_best[p]);
+                m2[p] = min3f(fmaxf(omin, kmin), m2[p], ksec);
+                seg_best[p] = fminf(seg_best[p], kmin);
+              } else {
+                seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
+              }
             }
           };
           auto chain = [&](int p) {   // block p's NQ MFMAs back to back (srcC = the previous vDst)
@@ -602,7 +610,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     // TOP2: the second-smallest score of the point, merged over its 4 lane groups like the
     // winner (two sorted pairs -> their two smallest); every lane takes part (shuffles)
     auto second = [&](int p) -> float {
-      float a1 = EXACT ? best[p] : m1[p], a2 = m2[p];
+      float a1 = EXACT ? best[p] : fminf(best[p], seg_best[p]), a2 = m2[p];
 #pragma unroll
       for (int o = 16; o <= 32; o <<= 1) {
         const float b1 = __shfl_xor(a1, o, 64), b2 = __shfl_xor(a2, o, 64);
@@ -796,8 +804,8 @@ template <typename T, int DPAD, int P, int OCC, int NW_, bool AST>
 constexpr bool top2_geom() {
   if (sizeof(T) == 4 || DPAD == 32 || DPAD > 256) return true;   // (the defaults hold it, 0 spills)
   if (AST) return false;
-  if (DPAD == 64) return P == 2 && OCC == 4 && NW_ == 4;
-  if (DPAD == 128) return P == 2 && OCC == 4 && NW_ == 4;
+  if (DPAD == 64) return (P == 2 || P == 4) && OCC == 4 && NW_ == 4;
+  if (DPAD == 128) return (P == 2 || P == 4) && OCC == 4 && NW_ == 4;
   if (DPAD == 256) return P == 3 && OCC == 2 && NW_ == 8;
   return false;
 }
@@ -904,8 +912,16 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   constexpr int OCC = sizeof(T) == 2 ? ((DPAD == 64 || DPAD == 256) ? 3 : 4) : 1;
   static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
   if (a.ub) {   // bounded E-step (TOP2): the geometries of top2_geom
-    if constexpr (sizeof(T) == 2 && DPAD == 64) return launch16_t<T, DPAD, 2, CT, 2, 4>(a, s);
-    if constexpr (sizeof(T) == 2 && DPAD == 128) return launch16_t<T, DPAD, 2, CT, 2, 4>(a, s);
+    // (A/B switch V_ASSIGN_TOP2_GEOM: 1 = 4 point blocks per wave at D = 64 / 128)
+    const bool p4 = variant(V_ASSIGN_TOP2_GEOM) == 1;
+    if constexpr (sizeof(T) == 2 && DPAD == 64) {
+      if (p4) return launch16_t<T, DPAD, 4, CT, 2, 4>(a, s);
+      return launch16_t<T, DPAD, 2, CT, 2, 4>(a, s);
+    }
+    if constexpr (sizeof(T) == 2 && DPAD == 128) {
+      if (p4) return launch16_t<T, DPAD, 4, CT, 2, 4>(a, s);
+      return launch16_t<T, DPAD, 2, CT, 2, 4>(a, s);
+    }
     if constexpr (sizeof(T) == 2 && DPAD == 256) return launch16_t<T, DPAD, 3, CT, 2, 2, 8>(a, s);
   }
   if constexpr (sizeof(T) == 2 && DPAD == 256) {

@@ -554,7 +554,7 @@ namespace mk {
 static const char* const kVariantEnv[V_COUNT] = {"MIKMEANS_ASSIGN_VARG", "MIKMEANS_ASSIGN_PMAJ",
                                                  "MIKMEANS_ASSIGN_GEOM", "MIKMEANS_UPDATE_KS",
                                                  "MIKMEANS_UPDATE_KS_GM", "MIKMEANS_BLOBS_TPR",
-                                                 "MIKMEANS_ASSIGN_PERSIST"};
+                                                 "MIKMEANS_ASSIGN_PERSIST", "MIKMEANS_ASSIGN_TOP2_GEOM"};
 static int* variant_table() {
   static int t[V_COUNT] = {};
   static const bool init = [] {

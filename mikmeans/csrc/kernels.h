@@ -33,7 +33,7 @@ constexpr int SLOT_STRIDE = 8;
 // changed only through set_variant (mikmeans.ops.native.variant); -1 = the built-in rule.
 // A captured hipGraph keeps the geometry that was in force when it was recorded.
 enum Variant { V_ASSIGN_VARG = 0, V_ASSIGN_PMAJ, V_ASSIGN_GEOM, V_UPDATE_KS, V_UPDATE_KS_GM, V_BLOBS_TPR,
-               V_ASSIGN_PERSIST, V_COUNT };
+               V_ASSIGN_PERSIST, V_ASSIGN_TOP2_GEOM, V_COUNT };
 int variant(Variant v);
 void set_variant(Variant v, int value);
 
