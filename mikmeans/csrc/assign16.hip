@@ -797,9 +797,10 @@ static void launch16_kt(const AssignArgs& b, const dim3& grid, size_t lds, hipSt
 }
 
 // The geometries that run the bounded E-step's TOP2 epilogue (launch16_d routes every call
-// with bounds to them).  The bf16 defaults at D = 64 / 128 / 256 have no registers for the
-// per-lane second minimum: their TOP2 builds spilled 500-940 VGPRs and ran 5.7x slower
-// (profiles/r4_05_hamerly.md), so the bounded pass takes fewer point blocks per wave there.
+// with bounds to them).  With a running (min, second) pair per point block the bf16
+// defaults at D = 64 / 128 / 256 spilled 400-940 VGPRs and ran 5.7x slower
+// (profiles/r4_05_hamerly_ab_top2_spills.log); the state is now the second minimum alone
+// (profiles/r4_16_top2_register_study.md), and D = 256 keeps 3 blocks at 8 waves per ring.
 template <typename T, int DPAD, int P, int OCC, int NW_, bool AST>
 constexpr bool top2_geom() {
   if (sizeof(T) == 4 || DPAD == 32 || DPAD > 256) return true;   // (the defaults hold it, 0 spills)
@@ -912,8 +913,11 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   constexpr int OCC = sizeof(T) == 2 ? ((DPAD == 64 || DPAD == 256) ? 3 : 4) : 1;
   static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
   if (a.ub) {   // bounded E-step (TOP2): the geometries of top2_geom
-    // (A/B switch V_ASSIGN_TOP2_GEOM: 1 = 4 point blocks per wave at D = 64 / 128)
-    const bool p4 = variant(V_ASSIGN_TOP2_GEOM) == 1;
+    // 4 point blocks per wave at D = 64 / 128 (the single-register TOP2 state: 0 / 14 spilled
+    // VGPRs, the latter outside the MFMA loop); a 40-iteration bounded fit at N=2e7 D=128
+    // K=1024 ran 6 % faster than with 2 blocks (profiles/r4_17_top2_geom_ab.md).  A/B switch
+    // V_ASSIGN_TOP2_GEOM: 0 = 2 blocks
+    const bool p4 = variant(V_ASSIGN_TOP2_GEOM) != 0;
     if constexpr (sizeof(T) == 2 && DPAD == 64) {
       if (p4) return launch16_t<T, DPAD, 4, CT, 2, 4>(a, s);
       return launch16_t<T, DPAD, 2, CT, 2, 4>(a, s);
