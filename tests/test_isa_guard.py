@@ -72,8 +72,8 @@ def test_assign_kernels_register_budget(tmp_path):
     assert len(a16) > 50
     top2 = [(r, t) for r, t in a16 if t[-1] == "true"]
     assert top2, "no TOP2 instantiations"
-    # the production TOP2 geometries (2 point blocks at D = 64 / 128, see top2_geom) spill
-    # nothing; the A/B 4-block geometry (V_ASSIGN_TOP2_GEOM) at most a few, outside the loop
+    # TOP2 geometries (top2_geom) spill nothing, except the 4-block D = 128 one (the default
+    # since round 4: 14 VGPRs, outside the MFMA loop; profiles/r4_16_top2_register_study.md)
     bad = [(t[:7], r.vgpr_spills) for r, t in top2
            if r.vgpr_spills > (16 if (t[1] in ("64", "128") and t[2] == "4") else 0)]
     assert not bad, bad
