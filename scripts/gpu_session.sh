@@ -38,6 +38,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     top2ab) step pytest_bounded_p4 400 env MIKMEANS_ASSIGN_TOP2_GEOM=1 python -u -m pytest tests/test_gpu_bounded.py -q --timeout 200 --timeout-method thread
             step hamerly_kpar_p2 400 python -u scripts/hamerly_ab.py --init "k-means||" --iters 40
             step hamerly_kpar_p4 400 env MIKMEANS_ASSIGN_TOP2_GEOM=1 python -u scripts/hamerly_ab.py --init "k-means||" --iters 40 ;;
+    hamerly_big) step hamerly_kpar_n1e8 600 python -u scripts/hamerly_ab.py --n 100000000 --init "k-means||" --iters 30 ;;
     hamerly2) step hamerly_kpar 400 python -u scripts/hamerly_ab.py --init "k-means||" --iters 40 ;;
     dp2host) step bench_dp2host 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --comm host --steps 10 --warmup 2 ;;
