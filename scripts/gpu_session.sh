@@ -61,6 +61,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     bench4ts) step bench_cfg4_2s 300 python bench.py --config cfg4 --steps 20 --warmup 3 --kpp-sampling two-stage ;;
     prof5r) cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$OLDPWD}"
           step rocprof5r 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5r -- python3 bench.py --config cfg5 --resident --steps 5 --warmup 1 ;;
+    profb) cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$OLDPWD}"
+          step rocprof_bounded 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profb -- python3 scripts/hamerly_ab.py --n 20000000 --init "k-means||" --iters 20 ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$OLDPWD}"
           step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -- python3 bench.py --steps 5 --warmup 1 ;;
   esac
