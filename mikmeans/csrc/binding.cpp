@@ -223,6 +223,26 @@ void update(const Tensor& X, const Tensor& labels, int64_t K, const Tensor& slab
 }
 
 // Incremental M-step (LloydEngine(incremental=True)): the changed-row list ...
+void label_delta_rows(const Tensor& labels, const Tensor& prev, const Tensor& rows, const Tensor& rcount,
+                      const Tensor& list, const Tensor& count) {
+  const int64_t N = labels.numel();
+  check_i32(labels, "labels", N);
+  check_i32(prev, "prev", N);
+  check_i32(count, "count", 1);
+  check_i64(rows, "rows", 0);
+  check_i64(rcount, "rcount", 1);
+  TORCH_CHECK(rows.numel() <= N, "mikmeans: more candidate rows than labels");
+  check_cuda(list, "list");
+  TORCH_CHECK(list.scalar_type() == at::kInt && list.dim() == 2 && list.size(1) == 2 && list.is_contiguous(),
+              "mikmeans: list must be contiguous int32 [cap, 2]");
+  TORCH_CHECK(N < ((int64_t)1 << 31) && list.size(0) < ((int64_t)1 << 31), "mikmeans: shard too large");
+  hip_check(mk::launch_label_delta_rows(labels.data_ptr<int32_t>(), prev.data_ptr<int32_t>(),
+                                        rows.data_ptr<int64_t>(), rcount.data_ptr<int64_t>(), rows.numel(),
+                                        (int2*)list.data_ptr<int32_t>(), (int)list.size(0),
+                                        count.data_ptr<int32_t>(), stream()),
+            "label_delta_rows");
+}
+
 void label_delta(const Tensor& labels, const Tensor& prev, const Tensor& list, const Tensor& count) {
   const int64_t N = labels.numel();
   check_i32(labels, "labels", N);
@@ -713,6 +733,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("reduce_cols", &reduce_cols, "lo sums of the wide-range columns (residual pass)");
   m.def("reduce", &reduce, "slab reduction into the packed f64 all-reduce message");
   m.def("label_delta", &label_delta, "changed-row list for the incremental M-step");
+  m.def("label_delta_rows", &label_delta_rows, "changed-row list over a candidate list (bounded E-step)");
   m.def("update_delta", &update_delta, "incremental M-step scatter-add (+new / -old label)");
   m.def("reduce_delta", &reduce_delta, "slab reduction into running totals + packed message");
   m.def("finalize", &finalize, "new centroids, shift, fragment re-pack (K4)");

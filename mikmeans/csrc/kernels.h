@@ -144,6 +144,9 @@ hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s);
 // Zeroes *count first (stream-ordered).
 hipError_t launch_label_delta(const int32_t* labels, int32_t* prev, int64_t N, int2* list, int cap,
                               int* count, hipStream_t s);
+// The same over the candidate rows rows[0..*rcount) only (bounded E-step; n_max >= *rcount)
+hipError_t launch_label_delta_rows(const int32_t* labels, int32_t* prev, const int64_t* rows, const int64_t* rcount,
+                                   int64_t n_max, int2* list, int cap, int* count, hipStream_t s);
 
 // Reduce slabs (+ assign slots) into the packed f64 message
 // [K*D sums | K counts | inertia | n_changed] (length K*D + K + 2).

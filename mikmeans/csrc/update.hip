@@ -1149,6 +1149,52 @@ __global__ __launch_bounds__(256) void label_delta_kernel(const int32_t* __restr
   }
 }
 
+// The same over a candidate list rows[0..*rcount) (the bounded E-step re-assigned only those
+// rows, so no other label can have changed): a pass over the candidates instead of all N.
+__global__ __launch_bounds__(256) void label_delta_rows_kernel(const int32_t* __restrict__ labels,
+                                                               int32_t* __restrict__ prev,
+                                                               const int64_t* __restrict__ rows,
+                                                               const int64_t* __restrict__ rcount,
+                                                               int2* __restrict__ list, int cap, int* count) {
+  __shared__ int wg_n, wg_base;
+  const int64_t m = rcount[0];
+  for (int64_t base = (int64_t)blockIdx.x * 256; base < m; base += (int64_t)gridDim.x * 256) {  // block-uniform
+    if (threadIdx.x == 0) wg_n = 0;
+    __syncthreads();
+    const int64_t j = base + threadIdx.x;
+    int64_t i = 0;
+    int lab = 0, old = 0;
+    bool ch = false;
+    if (j < m) {
+      i = rows[j];
+      lab = labels[i];
+      old = prev[i];
+      ch = lab != old;
+    }
+    const int off = ch ? atomicAdd(&wg_n, 1) : 0;
+    __syncthreads();
+    if (threadIdx.x == 0) wg_base = wg_n ? atomicAdd(count, wg_n) : 0;
+    __syncthreads();
+    if (ch) {
+      prev[i] = lab;
+      const int pos = wg_base + off;
+      if (pos < cap) list[pos] = make_int2((int)i, old);
+    }
+    __syncthreads();   // (wg_n / wg_base are rewritten by the next pass)
+  }
+}
+
+hipError_t launch_label_delta_rows(const int32_t* labels, int32_t* prev, const int64_t* rows, const int64_t* rcount,
+                                   int64_t n_max, int2* list, int cap, int* count, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(count, 0, sizeof(int), s);
+  if (e != hipSuccess || n_max <= 0) return e;
+  int64_t nb = (n_max + 255) / 256;
+  if (nb > 4096) nb = 4096;
+  hipLaunchKernelGGL(label_delta_rows_kernel, dim3((unsigned)nb), dim3(256), 0, s, labels, prev, rows, rcount,
+                     list, cap, count);
+  return hipGetLastError();
+}
+
 hipError_t launch_label_delta(const int32_t* labels, int32_t* prev, int64_t N, int2* list, int cap,
                               int* count, hipStream_t s) {
   if (N >= (int64_t)1 << 31) return hipErrorInvalidValue;

@@ -447,7 +447,10 @@ class LloydEngine:
             with _phase("mikmeans.update"):
                 d = self.delta
                 if d is not None:
-                    C.label_delta(self.labels, d["prev"], d["list"], d["count"])
+                    if self.bounded:   # only the re-assigned candidates can have changed
+                        C.label_delta_rows(self.labels, d["prev"], self._brows, self._bcount, d["list"], d["count"])
+                    else:
+                        C.label_delta(self.labels, d["prev"], d["list"], d["count"])
                     C.update_delta(self.X, self.labels, self.K, self.slab, self.cnt_slab, self.n_chunks,
                                    self.weights, self.col_exp, self.cnt_exp, d["list"], d["count"])
                     C.reduce_delta(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots,

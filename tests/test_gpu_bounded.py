@@ -273,3 +273,23 @@ def test_bounded_option_combinations(native, dtype, d, k, spherical, frozen):
     assert eb.inertia() == pytest.approx(ea.inertia(), rel=1e-3)
     if frozen:
         assert torch.equal(eb.centers[::5], C0[::5])
+
+
+def test_bounded_incremental_mstep_bitwise(native):
+    """Bounded E-step + incremental M-step (its changed-row list built over the candidates
+    only, label_delta_rows) gives bitwise the bounded E-step + full M-step engine's centres
+    and labels, across a centre reset too."""
+    X = B.make_blobs(250_000, 64, 40, seed=8, dtype=torch.bfloat16, device=DEV)
+    C0 = X[:48].float()
+    ea = LloydEngine(X, 48, bounded=True, incremental=False).set_centers(C0)
+    eb = LloydEngine(X, 48, bounded=True, incremental=True).set_centers(C0)
+    assert eb.delta is not None
+    for it in range(12):
+        if it == 7:
+            ea.set_centers(X[1000:1048].float())
+            eb.set_centers(X[1000:1048].float())
+        ea.step()
+        eb.step()
+        torch.cuda.synchronize()
+        assert torch.equal(ea.labels, eb.labels), it
+        assert torch.equal(ea.centers, eb.centers), it
