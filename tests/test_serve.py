@@ -126,3 +126,23 @@ def test_cli_serve_process(tmp_path):
     finally:
         p.terminate()
         p.wait(timeout=20)
+
+
+def test_concurrent_room_edits_are_serialised():
+    """Many clients adding cards at once: every edit lands exactly once (one lock around the
+    room, as the reference's single-threaded page has no concurrent handlers)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    room = Room(seed=6)
+    c = _client(room)
+    n0 = len(room.cards)
+
+    def add(i):
+        return c.post("/api/cards", json={"title": f"card {i}", "traits": ["T"]}).status_code
+
+    with ThreadPoolExecutor(8) as ex:
+        codes = list(ex.map(add, range(64)))
+    assert codes == [200] * 64
+    titles = sorted(x["title"] for x in room.cards[n0:])
+    assert titles == sorted(f"card {i}" for i in range(64))
+    assert len({x["id"] for x in room.cards}) == len(room.cards)
