@@ -179,7 +179,13 @@ def main(argv=None):
         eng = LloydEngine(X, K, comm=comm, incremental=args.incremental).set_centers(C0)
         use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
         extra["graph"] = _capture(eng, use_graph)
-        elapsed = _timed_steps(eng, comm, args.warmup, args.steps, sync)
+        tel = {}
+        elapsed = _timed_steps(eng, comm, args.warmup, args.steps, sync, telemetry=tel)
+        # the timed steps' mean GFX clock and socket power on rank 0 (null without amdsmi):
+        # value / clock_mhz separates a kernel change from a slower box
+        extra["clock_mhz"] = tel.get("clock_mhz")
+        extra["power_w"] = tel.get("power_w")
+        extra["telemetry"] = tel or None
         ms = elapsed * 1e3 / args.steps
         value = args.steps / elapsed
         unit = "iter/s"
@@ -209,8 +215,8 @@ def main(argv=None):
             }
             if args.also_bounded:
                 # KMeans(algorithm="hamerly"): the bounded E-step re-assigns only the rows its
-                # bounds cannot vouch for (the same Lloyd iterates up to bf16 near-ties).  From
-                # the same start, same warm-up and step count; an extra field, not the headline.
+                # bounds cannot vouch for -- bitwise the full E-step's iterates.  From the same
+                # start, same warm-up and step count; an extra field, not the headline.
                 C_inc = inc.centers.clone()
                 del inc
                 bnd = LloydEngine(X, K, comm=comm, incremental=True, bounded=True).set_centers(C0)
@@ -220,6 +226,7 @@ def main(argv=None):
                     "value": args.steps / el_b,
                     "ms_per_step": el_b * 1e3 / args.steps,
                     "rows_reassigned_last_step": bnd.reassigned,
+                    "centres_bitwise_equal_to_full": bool(torch.equal(bnd.centers, C_inc)),
                     "max_centre_diff_vs_full": float((bnd.centers - C_inc).abs().max()),
                 }
                 del bnd
@@ -274,19 +281,30 @@ def _capture(eng, want: bool):
     return True
 
 
-def _timed_steps(eng, comm, warmup: int, steps: int, sync) -> float:
+def _timed_steps(eng, comm, warmup: int, steps: int, sync, telemetry: dict | None = None) -> float:
     """W untimed iterations, then exactly ``steps`` bracketed by barrier + device sync on
-    both sides; returns the max elapsed seconds over ranks."""
+    both sides; returns the max elapsed seconds over ranks.  ``telemetry``: filled with this
+    rank's mean GFX clock / socket power over the timed steps (utils/telemetry.py; a
+    background amdsmi reader, no HIP calls, nothing inside the step loop)."""
+    from mikmeans.utils.telemetry import ClockSampler
+
     for _ in range(warmup):
         eng.step()
     comm.barrier()
     sync()
+    sampler = ClockSampler(comm.device.index or 0) if (telemetry is not None and comm.device.type == "cuda") else None
     t0 = time.perf_counter()
+    if sampler is not None:
+        sampler.__enter__()
     for _ in range(steps):
         eng.step()
     sync()
+    t1 = time.perf_counter()
+    if sampler is not None:
+        sampler.__exit__(None, None, None)
+        telemetry.update(sampler.summary() or {"error": sampler.error or "no samples"})
     comm.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=comm.device)
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device=comm.device)
     comm.allreduce_max_(el)
     return float(el.item())
 

@@ -143,15 +143,18 @@ __device__ __forceinline__ float sq16(const u32x4& w, float*) {
 // latency hides under the epilogue instead of opening every workgroup's life; the inertia
 // and changed counts go to the slots once per workgroup.  Same scores, same labels.
 template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false,
-          bool VARG = false, int PMAJ = 0, bool PERSIST = false, bool AST = false, bool TOP2 = false>
+          bool VARG = false, int PMAJ = 0, bool PERSIST = false, bool AST = false, bool TOP2 = false, bool XV = false>
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
-  constexpr bool EXACT = sizeof(T) == 4;  // f32: exact (value, index) epilogue
+  constexpr bool F32 = sizeof(T) == 4;
+  // exact (value, index) epilogue: f32, or bf16 scores where the full pass ranks by value (XV)
+  constexpr bool EXACT = F32 || XV;
   // A fragments streamed one at a time (see the MFMA issue): rows of 384..1024 features, or
   // AST (a lower-register variant of the narrow kernels)
   constexpr bool WIDE = AST || DPAD > 256;
-  static_assert(!(VARG && EXACT), "value-only argmin is the bf16 epilogue");
+  static_assert(!(VARG && F32), "value-only argmin is the bf16 epilogue");
   static_assert(!(TOP2 && (VARG || PERSIST)), "bounded E-step: keys / exact epilogues, one pass per block");
+  static_assert(!XV || (TOP2 && !F32), "the bf16 exact epilogue stands in for VARG in the bounded E-step");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -194,6 +197,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   int64_t pbase = blk * C::PTS + (int64_t)wid * (C::P * 16);
   u32x4 xr[C::P][C::NQ];
   float xnr[C::P];
+  float osr[C::P];   // (a.oseed) the rows' full-pass seed offsets, at their X rows
   // The P blocks' fragment loads go out back to back: one memory round trip (two for a
   // gathered batch: the row indices first).  vmcnt retires in order, so a block whose
   // address waited on a load issued after the previous block's fragments (the row index,
@@ -219,15 +223,23 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       __builtin_amdgcn_sched_barrier(0);   // all index loads in flight before the first use
 #pragma unroll
       for (int p = 0; p < C::P; ++p) load_frags(p, src[p]);
-      if (!EXACT && a.xn && a.scatter) {   // (scattering: the caller's norms sit at the X rows)
+      if (!F32 && a.xn && a.scatter) {   // (scattering: the caller's norms sit at the X rows)
 #pragma unroll
         for (int p = 0; p < C::P; ++p) xnr[p] = a.xn[src[p]];
+      }
+      if (!F32 && a.oseed) {
+#pragma unroll
+        for (int p = 0; p < C::P; ++p) osr[p] = a.oseed[src[p]];
       }
     } else {
 #pragma unroll
       for (int p = 0; p < C::P; ++p) load_frags(p, row_of(p));
+      if (!F32 && a.oseed) {
+#pragma unroll
+        for (int p = 0; p < C::P; ++p) osr[p] = a.oseed[row_of(p)];
+      }
     }
-    if (!EXACT && a.xn) {
+    if (!F32 && a.xn) {
       if (!(a.rows && a.scatter)) {
 #pragma unroll
         for (int p = 0; p < C::P; ++p) xnr[p] = a.xn[row_of(p)];
@@ -265,7 +277,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     bool ppo = false;
     float* opt = (float*)(bufs + C::NBUF * C::CHUNK_BYTES + 16 * C::NW);  // [NW][16][PP] offsets
     float* xnl = opt + C::NW * 16 * C::PP;                                 // [NW][16][PP] |x|^2
-    if (!a.xn && (!EXACT || a.slots)) {
+    if (!a.xn && (!F32 || a.slots)) {
 #pragma unroll
       for (int p = 0; p < C::P; ++p) {
         float s = 0.f;
@@ -280,7 +292,17 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         for (int p = 0; p < C::P; ++p) xnl[(wid * 16 + r) * C::PP + p] = xnr[p];
       }
     }
-    if constexpr (!EXACT) {
+    if constexpr (!F32) {
+     if (a.oseed) {
+      // the offsets the full pass gives these rows (launch_seed_offsets), per point: the scores
+      // -- and so the labels and near-tie decisions -- are bitwise the full pass's, whichever
+      // workgroup a gathered row lands in (the bounded E-step's exactness)
+      ppo = true;
+      if (g == 0) {
+#pragma unroll
+        for (int p = 0; p < C::P; ++p) opt[(wid * 16 + r) * C::PP + p] = osr[p];
+      }
+     } else {
       float m = 0.f, mn = 3.0e38f;
 #pragma unroll
       for (int p = 0; p < C::P; ++p) { m = fmaxf(m, xnr[p]); mn = fminf(mn, xnr[p]); }
@@ -307,6 +329,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
           for (int p = 0; p < C::P; ++p) opt[(wid * 16 + r) * C::PP + p] = __builtin_fmaf(xnr[p], 2.44140625e-04f, xnr[p]);
         }
       }
+     }
       // (published by the main loop's first wait_lgkm0 + barrier)
     }
 
@@ -356,7 +379,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         // EARLY (bf16 D=64): the next tile's fragments are read right after this tile's
         // MFMAs are issued, so their LDS latency hides under the argmin epilogue (+2 % at D=64
         // in one-process A/B, profiles/r2_08_assign_clock_study.md; no gain at D=128)
-        constexpr bool EARLY = !EXACT && DPAD == 64;
+        constexpr bool EARLY = !F32 && DPAD == 64;
         u32x4 awe[C::NQ];
         f32x4 cie;
         if constexpr (EARLY) load_a(0, awe, cie);
@@ -394,7 +417,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
           // (profiles/r2_29_assign_setprio_ab.log, one process each: the harness copy -2.2 % at
           // D=128 K=1024 and -1.4 % at D=64 K=4096; this kernel against that copy +0.8 % at D=128,
           // +0.3 % at D=64, about +5 % at D=256 K=512)
-          if constexpr (!EXACT) {
+          if constexpr (!F32) {
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_setprio(1);
             __builtin_amdgcn_sched_barrier(0);
@@ -466,7 +489,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
               for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aw[q], xr[p][q], acc[p]);
             }
           }
-          if constexpr (!EXACT) {
+          if constexpr (!F32) {
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
@@ -771,29 +794,29 @@ static int assign16_splits(int64_t nblk, int nch) {
 // Variant V_ASSIGN_VARG = 0/1 forces it off / on (A/B, tests).
 
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST,
-          bool TOP2>
+          bool TOP2, bool XV>
 static void set_lds_attr() {
   static bool done = false;
   if (done) return;
   (void)hipFuncSetAttribute(
-      (const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST, TOP2>,
+      (const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST, TOP2, XV>,
       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute(
-      (const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST, TOP2>,
+      (const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST, TOP2, XV>,
       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   done = true;
 }
 
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST,
-          bool TOP2>
+          bool TOP2, bool XV>
 static void launch16_kt(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, TOP2>();
+  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, TOP2, XV>();
   if (b.D == DPAD)
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST, TOP2>), grid,
-                       dim3(NW_ * 64), lds, s, b);
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST, TOP2, XV>),
+                       grid, dim3(NW_ * 64), lds, s, b);
   else
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST, TOP2>), grid,
-                       dim3(NW_ * 64), lds, s, b);
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST, TOP2, XV>),
+                       grid, dim3(NW_ * 64), lds, s, b);
 }
 
 // The geometries that run the bounded E-step's TOP2 epilogue (launch16_d routes every call
@@ -811,14 +834,21 @@ constexpr bool top2_geom() {
   return false;
 }
 
+// With bounds (b.ub) the VARG flag says how the FULL pass of this shape ranks: by value (the
+// value-only argmin) -> the TOP2 kernel takes the exact (value, index) epilogue (XV), else the
+// packed keys; with the full pass's seed offsets (b.oseed) its labels are then the full pass's.
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST>
 static void launch16_kpp(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  if constexpr (!VARG && !PERSIST && top2_geom<T, DPAD, P, OCC, NW_, AST>()) {
-    // bounded E-step: the second-smallest score too
-    if (b.ub) return launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, true>(b, grid, lds, s);
+  if (b.ub) {
+    if constexpr (!PERSIST && top2_geom<T, DPAD, P, OCC, NW_, AST>()) {
+      if constexpr (VARG && sizeof(T) == 2)
+        return launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, PMAJ, PERSIST, AST, true, true>(b, grid, lds, s);
+      else
+        return launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, PMAJ, PERSIST, AST, true, false>(b, grid, lds, s);
+    }
+    return;   // (unreachable: launch16_d sends bounds to a top2_geom geometry, one-pass grid)
   }
-  if (b.ub) return;   // (unreachable: launch16_d sends bounds to a top2_geom geometry)
-  launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, false>(b, grid, lds, s);
+  launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, false, false>(b, grid, lds, s);
 }
 
 // Resident workgroups the whole chip holds for a launch geometry: the smaller of the
@@ -881,7 +911,8 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   constexpr bool VARG_OK = sizeof(T) == 2 && DPAD <= 64;   // D=128: -12 % at K=1024, -4 % at 2048 (r3_11)
   if constexpr (VARG_OK) {
     const int e = variant(V_ASSIGN_VARG);
-    varg = (e >= 0 ? e != 0 : a.Kpad >= (DPAD == 64 ? 2048 : 1024)) && !a.ub;
+    // (with bounds: whether the full pass would, see launch16_kpp)
+    varg = e >= 0 ? e != 0 : a.Kpad >= (DPAD == 64 ? 2048 : 1024);
   }
   if constexpr (VARG_OK) {
     if (varg) launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, AST>(b, grid, lds, s);
@@ -892,6 +923,16 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if (splits > 1)
     hipLaunchKernelGGL(split_finish_kernel, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, s, b);
   return hipGetLastError();
+}
+
+// Point blocks per wave of the default geometries (launch16_d / launch16_w, see there).
+template <typename T, int DPAD>
+constexpr int p_narrow() {
+  return sizeof(T) == 2 ? (DPAD == 64 ? 8 : DPAD == 256 ? 3 : 4) : (DPAD / 4 / Elem<T>::V >= 8 ? 2 : 4);
+}
+template <typename T, int DPAD>
+constexpr int p_wide() {
+  return sizeof(T) == 2 ? (DPAD <= 512 ? 4 : 2) : (DPAD <= 512 ? 2 : 1);
 }
 
 // The workgroup's point count (NW*P*16) must divide parallel/shard.py ROW_ALIGN (1536).
@@ -909,7 +950,8 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   //    2 waves 1-10 % slower (profiles/r3_10_assign_p64_ab.log);
   //  * bf16 D=256: 3 point blocks at 3 waves/SIMD, -4 % against 2 at 4;
   //  * f32: the register file sets 4 (D <= 64) or 2 blocks at one wave per SIMD minimum.
-  constexpr int P = sizeof(T) == 2 ? (DPAD == 64 ? 8 : DPAD == 256 ? 3 : 4) : (NQ >= 8 ? 2 : 4);
+  constexpr int P = p_narrow<T, DPAD>();
+  (void)NQ;
   constexpr int OCC = sizeof(T) == 2 ? ((DPAD == 64 || DPAD == 256) ? 3 : 4) : 1;
   static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
   if (a.ub) {   // bounded E-step (TOP2): the geometries of top2_geom
@@ -967,9 +1009,56 @@ template <typename T, int DPAD>
 static hipError_t launch16_w(const AssignArgs& a, hipStream_t s) {
   constexpr int CT = chunk_tiles16(sizeof(T), DPAD);
   static_assert(CT == 1, "wide rows: one tile per chunk");
-  constexpr int P = sizeof(T) == 2 ? (DPAD <= 512 ? 4 : 2) : (DPAD <= 512 ? 2 : 1);
+  constexpr int P = p_wide<T, DPAD>();
   static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
   return launch16_t<T, DPAD, P, CT, 2, 1>(a, s);
+}
+
+// NW * P * 16 of the geometry launch16_d / launch16_w pick for a call without bounds (the A/B
+// switch V_ASSIGN_GEOM included): the row block each bf16 seed offset is taken over.  The
+// bounded E-step's exactness rests on this (tests/test_gpu_bounded.py, bitwise trajectories).
+template <typename T, int DPAD>
+static int block_rows_t(int kpad) {
+  if constexpr (DPAD > 256) return 4 * p_wide<T, DPAD>() * 16;
+  const int gm = variant(V_ASSIGN_GEOM);
+  if constexpr (sizeof(T) == 2 && DPAD == 256) {
+    if (gm == 1) return 8 * 3 * 16;
+    if (gm == 2) return 8 * 2 * 16;
+  }
+  if constexpr (sizeof(T) == 2 && DPAD == 128) {
+    if ((gm == 1 && kpad % (16 * 8) == 0) || gm == 2) return 8 * 4 * 16;
+    if (gm == 3) return 4 * 6 * 16;
+    if (gm == 4) return 4 * 8 * 16;
+  }
+  return 4 * p_narrow<T, DPAD>() * 16;
+}
+
+int assign16_block_rows(int dtype, int dpad, int kpad) {
+  if (dtype == DT_BF16) {
+    switch (dpad) {
+      case 32: return block_rows_t<uint16_t, 32>(kpad);
+      case 64: return block_rows_t<uint16_t, 64>(kpad);
+      case 128: return block_rows_t<uint16_t, 128>(kpad);
+      case 256: return block_rows_t<uint16_t, 256>(kpad);
+      case 384: return block_rows_t<uint16_t, 384>(kpad);
+      case 512: return block_rows_t<uint16_t, 512>(kpad);
+      case 768: return block_rows_t<uint16_t, 768>(kpad);
+      case 1024: return block_rows_t<uint16_t, 1024>(kpad);
+    }
+  } else {
+    switch (dpad) {
+      case 16: return block_rows_t<float, 16>(kpad);
+      case 32: return block_rows_t<float, 32>(kpad);
+      case 64: return block_rows_t<float, 64>(kpad);
+      case 128: return block_rows_t<float, 128>(kpad);
+      case 256: return block_rows_t<float, 256>(kpad);
+      case 384: return block_rows_t<float, 384>(kpad);
+      case 512: return block_rows_t<float, 512>(kpad);
+      case 768: return block_rows_t<float, 768>(kpad);
+      case 1024: return block_rows_t<float, 1024>(kpad);
+    }
+  }
+  return 0;
 }
 
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s) {

@@ -77,7 +77,7 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
             const c10::optional<Tensor>& slots, int64_t Kpad, int64_t dpad, bool track_changed,
             const c10::optional<Tensor>& keys, const c10::optional<Tensor>& rows,
             const c10::optional<Tensor>& ub, const c10::optional<Tensor>& lb, bool scatter,
-            const c10::optional<Tensor>& count) {
+            const c10::optional<Tensor>& count, const c10::optional<Tensor>& oseed) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   // gathered batch: N logical rows, row i = X[rows[i]] (indices from sample_index: in range
@@ -139,6 +139,11 @@ void assign(const Tensor& X, const Tensor& pack, const Tensor& cn, const c10::op
     TORCH_CHECK(gathered && !(keys.has_value() && keys->defined()),
                 "mikmeans: a device row count takes a gathered batch on the one-pass grid");
     a.n_dev = count->data_ptr<int64_t>();
+  }
+  if (oseed.has_value() && oseed->defined()) {   // per-row seed offsets at the X rows (bf16 keys)
+    TORCH_CHECK(dt == mk::DT_BF16, "mikmeans: seed offsets are the bf16 keys'");
+    check_f32(*oseed, "oseed", X.size(0));
+    a.oseed = oseed->data_ptr<float>();
   }
   hip_check(mk::launch_assign16(dt, (int)dpad, a, stream()), "assign");
 }
@@ -621,7 +626,8 @@ void kpar_select(const Tensor& d2, int64_t start, const Tensor& psi, double ell,
 }
 
 void tighten(const Tensor& X, int64_t D, const Tensor& labels, const Tensor& C, const Tensor& rows,
-             const Tensor& count, const Tensor& ub, const Tensor& lb, const Tensor& cand) {
+             const Tensor& count, const Tensor& ub, const Tensor& lb, const Tensor& cand, const Tensor& xn,
+             const Tensor& work, double qeps) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   const int64_t n = X.size(0);
@@ -639,10 +645,23 @@ void tighten(const Tensor& X, int64_t D, const Tensor& labels, const Tensor& C, 
   check_cuda(cand, "cand");
   TORCH_CHECK(cand.scalar_type() == at::kByte && cand.is_contiguous() && cand.numel() >= n,
               "mikmeans: cand must be contiguous uint8 [n]");
+  check_f32(xn, "xn", n);
+  check_f32(work, "work", 4);
   hip_check(mk::launch_tighten(dt, X.data_ptr(), ldx, (int)D, labels.data_ptr<int32_t>(), C.data_ptr<float>(),
                                C.stride(0), rows.data_ptr<int64_t>(), count.data_ptr<int64_t>(), rows.numel(),
-                               ub.data_ptr<float>(), lb.data_ptr<float>(), cand.data_ptr<uint8_t>(), stream()),
+                               ub.data_ptr<float>(), lb.data_ptr<float>(), cand.data_ptr<uint8_t>(),
+                               xn.data_ptr<float>(), work.data_ptr<float>(), (float)qeps, stream()),
             "tighten");
+}
+
+// oseed = the full assign's per-row seed offsets (bf16 keys) for rows with norms xn
+void seed_offsets(const Tensor& xn, const Tensor& oseed, int64_t block_rows) {
+  const int64_t n = xn.numel();
+  check_f32(xn, "xn", n);
+  check_f32(oseed, "oseed", n);
+  TORCH_CHECK(block_rows > 0 && block_rows <= 4096, "mikmeans: bad block_rows ", block_rows);
+  hip_check(mk::launch_seed_offsets(xn.data_ptr<float>(), n, (int)block_rows, oseed.data_ptr<float>(), stream()),
+            "seed_offsets");
 }
 
 void bounds_update(const Tensor& labels, const Tensor& ub, const Tensor& lb, const Tensor& shift2, const Tensor& cn,
@@ -722,7 +741,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("xn"), py::arg("labels"), py::arg("mind"), py::arg("slots"), py::arg("Kpad"), py::arg("dpad"),
         py::arg("track_changed"), py::arg("keys") = py::none(), py::arg("rows") = py::none(),
         py::arg("ub") = py::none(), py::arg("lb") = py::none(), py::arg("scatter") = false,
-        py::arg("count") = py::none());
+        py::arg("count") = py::none(), py::arg("oseed") = py::none());
+  m.def("seed_offsets", &seed_offsets, "the full assign's per-row bf16 seed offsets (bounded E-step)");
+  m.def("assign_block_rows", [](int64_t dt, int64_t dpad, int64_t kpad) {
+    return mk::assign16_block_rows((int)dt, (int)dpad, (int)kpad);
+  }, "rows per workgroup of the full assign (its seed-offset block)");
   m.def("update", &update, "LDS-privatised per-cluster sums/counts (K3)", py::arg("X"), py::arg("labels"),
         py::arg("K"), py::arg("slab"), py::arg("cnt_slab"), py::arg("n_chunks"), py::arg("weights"),
         py::arg("col_exp"), py::arg("cnt_exp"), py::arg("clamp"), py::arg("clamp_count") = py::none(),
@@ -775,8 +798,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     for (int i = 0; i < mk::V_COUNT; ++i) n.emplace_back(mk::kVariantEnv[i] + 9);   // strip "MIKMEANS_"
     return n;
   }, "A/B switch names (lower-cased by mikmeans.ops.native)");
-  m.def("get_variant", [](int64_t i) { return mk::variant((mk::Variant)i); });
-  m.def("set_variant", [](int64_t i, int64_t v) { mk::set_variant((mk::Variant)i, (int)v); },
+  m.def("get_variant", [](int64_t i) {
+    TORCH_CHECK(i >= 0 && i < mk::V_COUNT, "mikmeans: no A/B switch ", i);
+    return mk::variant((mk::Variant)i);
+  });
+  m.def("set_variant", [](int64_t i, int64_t v) {
+    TORCH_CHECK(i >= 0 && i < mk::V_COUNT, "mikmeans: no A/B switch ", i);
+    mk::set_variant((mk::Variant)i, (int)v);
+  },
         "set an A/B switch (-1 = built-in rule); launchers never read the environment");
   (void)mk::variant(mk::V_ASSIGN_VARG);   // snapshot the environment now, at load
   m.def("bounds_update", &bounds_update, "Hamerly bounds moved by the centre shifts; flags the rows to re-assign");

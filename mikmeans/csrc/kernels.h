@@ -66,8 +66,17 @@ struct AssignArgs {
   // min(N, *n_dev) -- a compacted batch whose size only the device knows (no host sync, so
   // the bounded E-step captures into a graph); workgroups past it exit at once
   const int64_t* n_dev = nullptr;
+  // optional per-row seed offsets (bf16, indexed by X row): every row's scores are seeded with
+  // oseed[row] -- the offset the full (ungathered) pass gives it, from launch_seed_offsets -- so a
+  // gathered batch ranks each row bitwise as the full pass does (the bounded E-step)
+  const float* oseed = nullptr;
 };
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
+// Rows per workgroup of the full (ungathered, unbounded) assign for this shape: the block its
+// bf16 seed offset is taken over (mirrors launch16_d / launch16_w)
+int assign16_block_rows(int dtype, int dpad, int kpad);
+// oseed[i] = the full pass's seed offset of row i (block_rows from assign16_block_rows; bf16)
+hipError_t launch_seed_offsets(const float* xn, int64_t n, int block_rows, float* oseed, hipStream_t s);
 
 // ---- transform: every row's distance to every centre (csrc/transform.hip) --------------
 struct TransformArgs {
@@ -84,7 +93,9 @@ hipError_t launch_transform(int dtype, int dpad, const TransformArgs& a, hipStre
 // lb -= the largest |dc_k| over k != label) and flags the points whose bounds no longer prove
 // their label (cand[i] = 1): shift2 = squared shifts [K], cn = |c|^2 of the packed centres
 // and xn = |x|^2 size the rounding slack of the kernel's distances, qeps the relative
-// rounding of the stored centres (bf16 2^-8, f32 2^-23); work: 4 floats scratch.
+// rounding of the stored centres (bf16 2^-8, f32 2^-23); work: 4 floats scratch.  A row
+// stays unflagged only where the full assign's keys provably keep its label (the slack
+// counted on both sides of the test), so skipping it changes nothing.
 hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, const float* shift2, const float* cn,
                                 int K, const float* xn, int64_t n, uint8_t* cand, float* work, float qeps,
                                 hipStream_t s);
@@ -92,10 +103,12 @@ hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, con
 // bscratch: int64 [compact_blocks(n)]
 int64_t compact_blocks(int64_t n);
 // Hamerly's tightening over the compacted candidates rows[0..*count): ub = |x - c_label| (f32
-// centres C [K][ldc]); cand = 0 where that is below lb.  n_max bounds *count (grid sizing)
+// centres C [K][ldc]); cand = 0 where the bounds test of launch_bounds_update passes with it
+// (xn, work and qeps as there: work holds that step's slack terms).  n_max bounds *count
 hipError_t launch_tighten(int dtype, const void* X, int64_t ldx, int D, const int32_t* labels, const float* C,
                           int64_t ldc, const int64_t* rows, const int64_t* count, int64_t n_max, float* ub,
-                          const float* lb, uint8_t* cand, hipStream_t s);
+                          const float* lb, uint8_t* cand, const float* xn, const float* work, float qeps,
+                          hipStream_t s);
 // k-means|| round: cand[i] = u(start + i) < ell * d2[i] / psi[0] (philox uniform keyed by the global row)
 hipError_t launch_kpar_select(const float* d2, int64_t n, int64_t start, const double* psi, double ell,
                               uint64_t seed, uint32_t round, uint8_t* cand, hipStream_t s);

@@ -216,7 +216,20 @@ hipError_t launch_wdot(const float* a, const float* b, int64_t n, double* out, d
 // (bf16 keys; f32 is finer), so d^2 moves by at most delta = 2^-14 (2|x|^2 + |c|max^2) --
 // sqrt(d^2 +- delta), which costs delta / 2d, not sqrt(delta) -- and the quantised centre
 // sits within q = qeps |c|max of the f32 one.  Every later step only adds the f32 shifts.
+//
+// Skipping a row must leave the label the FULL assign would give it (models/lloyd.py: the
+// bounded E-step's iterates are bitwise the full E-step's), not merely the true nearest centre:
+// the full pass ranks scores against the quantised centres, with rounding and 6-bit key
+// truncation.  Its score for the label is at most (u + q)^2 + delta and every other score at
+// least (l - q)^2 - delta, so the row is skipped only where the first is below the second --
+// the slack counted once more, on both sides (delta = 2^-14 (2|x|^2 + |c|max^2) is 8x the
+// key resolution 2^-17 (|x - c|^2 + 3|x|^2) plus the accumulation's rounding at D <= 1024).
 constexpr float BOUND_EPS = 6.103515625e-05f;   // 2^-14
+
+__device__ __forceinline__ bool keys_keep_label(float u, float l, float q, float delta) {
+  const float lq = l - q, uq = u + q;
+  return lq > 0.f && uq * uq + delta < lq * lq - delta;   // (false for u = inf, NaN)
+}
 
 // One workgroup: the largest and second-largest centre shift, the largest's centre, and the
 // largest |c|^2 (the slack's centre term) -> work[0..3].
@@ -278,8 +291,52 @@ __global__ __launch_bounds__(256) void bounds_update_kernel(const int32_t* __res
     l -= (a == a1 ? d2 : d1);
     ub[i] = u;
     lb[i] = l;
-    cand[i] = (u >= l) ? 1 : 0;
+    cand[i] = keys_keep_label(u, l, q, BOUND_EPS * (2.f * xn[i] + cmax2)) ? 0 : 1;
   }
+}
+
+// ---- seed offsets of the full assign ------------------------------------------------------
+// The full assign seeds a bf16 workgroup's scores with o = (1 + 2^-12) max |x|^2 over its block
+// of block_rows rows, or each row's own (1 + 2^-12) |x|^2 where the block's max exceeds 4x its
+// min (assign16.hip, the kernel's prologue: the same fmaxf / fminf folds from 0 / 3e38, the
+// same fma).  The offset is part of every key, so near-ties resolve by it; a gathered assign
+// seeded from this array (AssignArgs::oseed) ranks each row bitwise as the full pass does.
+// One workgroup per block; a tail block's missing rows are the kernel's clamped copies of
+// row n-1, which change neither extreme.
+__global__ __launch_bounds__(256) void seed_offsets_kernel(const float* __restrict__ xn, int64_t n, int block_rows,
+                                                          float* __restrict__ oseed) {
+  const int64_t r0 = (int64_t)blockIdx.x * block_rows;
+  const int64_t r1 = r0 + block_rows < n ? r0 + block_rows : n;
+  float m = 0.f, mn = 3.0e38f;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += 256) {
+    m = fmaxf(m, xn[i]);
+    mn = fminf(mn, xn[i]);
+  }
+  __shared__ float sm[256], sn[256];
+  sm[threadIdx.x] = m;
+  sn[threadIdx.x] = mn;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      sm[threadIdx.x] = fmaxf(sm[threadIdx.x], sm[threadIdx.x + o]);
+      sn[threadIdx.x] = fminf(sn[threadIdx.x], sn[threadIdx.x + o]);
+    }
+    __syncthreads();
+  }
+  const float mx = sm[0];
+  const bool ppo = mx > 4.f * sn[0];
+  const float off = __builtin_fmaf(mx, 2.44140625e-04f, mx);   // * (1 + 2^-12)
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += 256)
+    oseed[i] = ppo ? __builtin_fmaf(xn[i], 2.44140625e-04f, xn[i]) : off;
+}
+
+hipError_t launch_seed_offsets(const float* xn, int64_t n, int block_rows, float* oseed, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (block_rows <= 0) return hipErrorInvalidValue;
+  const int64_t nb = (n + block_rows - 1) / block_rows;
+  if (nb > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(seed_offsets_kernel, dim3((unsigned)nb), dim3(256), 0, s, xn, n, block_rows, oseed);
+  return hipGetLastError();
 }
 
 hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, const float* shift2, const float* cn,
@@ -298,7 +355,7 @@ hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, con
 // ---- Hamerly tightening ----------------------------------------------------------------
 // A row whose moved bounds no longer prove its label first gets the exact distance to its
 // label's f32 centre (Hamerly 2010's second test): ub drops to it, and a row whose tight ub
-// is below lb keeps its label without the full assign.  A wave takes 4 rows per pass, 16
+// passes the bounds test against lb (keys_keep_label) keeps its label without the assign.  A wave takes 4 rows per pass, 16
 // lanes per row in 16-B pieces (one coalesced load per piece), |x - c|^2 summed directly
 // (no |x|^2 + |c|^2 cancellation).  rows[0..*count): the compacted candidates.
 template <typename T>
@@ -307,9 +364,14 @@ __global__ __launch_bounds__(256) void tighten_kernel(const T* __restrict__ X, i
                                                      const float* __restrict__ C, int64_t ldc,
                                                      const int64_t* __restrict__ rows,
                                                      const int64_t* __restrict__ count, float* __restrict__ ub,
-                                                     const float* __restrict__ lb, uint8_t* __restrict__ cand) {
+                                                     const float* __restrict__ lb, uint8_t* __restrict__ cand,
+                                                     const float* __restrict__ xn, const float* __restrict__ work,
+                                                     float qeps) {
   constexpr int V = Elem<T>::V;
   const int64_t m = count[0];
+  // the slack terms of this step's bounds test (bounds_update_kernel)
+  const float cmax = sqrtf(work[3]) + work[0];
+  const float q = qeps * cmax, cmax2 = cmax * cmax;
   const int lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nwave = ((int64_t)gridDim.x * 256) >> 6;
@@ -344,23 +406,24 @@ __global__ __launch_bounds__(256) void tighten_kernel(const T* __restrict__ X, i
     if (gl == 0 && a >= 0) {
       const float u = __builtin_sqrtf(s) * (1.f + 1e-6f);   // (+ the f32 rounding of D terms)
       ub[row] = u;
-      if (u < lb[row]) cand[row] = 0;
+      if (keys_keep_label(u, lb[row], q, BOUND_EPS * (2.f * xn[row] + cmax2))) cand[row] = 0;
     }
   }
 }
 
 hipError_t launch_tighten(int dtype, const void* X, int64_t ldx, int D, const int32_t* labels, const float* C,
                           int64_t ldc, const int64_t* rows, const int64_t* count, int64_t n_max, float* ub,
-                          const float* lb, uint8_t* cand, hipStream_t s) {
+                          const float* lb, uint8_t* cand, const float* xn, const float* work, float qeps,
+                          hipStream_t s) {
   if (n_max <= 0) return hipSuccess;
   int64_t nb = (n_max + 15) / 16;   // 16 rows per block and pass
   if (nb > 8192) nb = 8192;
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(tighten_kernel<uint16_t>, dim3((unsigned)nb), dim3(256), 0, s, (const uint16_t*)X, ldx, D,
-                       labels, C, ldc, rows, count, ub, lb, cand);
+                       labels, C, ldc, rows, count, ub, lb, cand, xn, work, qeps);
   else
     hipLaunchKernelGGL(tighten_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, (const float*)X, ldx, D, labels,
-                       C, ldc, rows, count, ub, lb, cand);
+                       C, ldc, rows, count, ub, lb, cand, xn, work, qeps);
   return hipGetLastError();
 }
 

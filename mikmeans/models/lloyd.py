@@ -79,9 +79,10 @@ class LloydEngine:
         # Bounded E-step (Hamerly 2010): per-point bounds on the distance to the assigned
         # centre (ub) and to the second nearest (lb), moved by each M-step's centre shifts;
         # only points whose bounds no longer prove their label are re-assigned (a gathered
-        # assign over them).  The same Lloyd iterates up to bf16 near-ties (a re-assigned
-        # point's workgroup seed offset differs from the full assign's); per-step inertia is
-        # not tracked (the fit's final inertia is exact).  GPU, keys / exact epilogues.
+        # assign over them).  Bitwise the full E-step's iterates: a re-assigned row is seeded
+        # with the offset the full pass gives it (``oseed``) and ranked by the same epilogue,
+        # and a row is skipped only where the full pass's keys provably keep its label
+        # (csrc/rows.hip keys_keep_label).  The step's inertia comes from the M-step's sums.
         self.bounded = bool(bounded)
         # Hamerly's tightening (exact distance to the label's centre before the full assign):
         # off by default -- here the candidates come from the falling lower bounds, so it
@@ -198,8 +199,8 @@ class LloydEngine:
             self.mind = torch.empty(self.n, dtype=torch.float32, device=dev)
         if self.weights is not None:
             self._wscratch = torch.empty(C.WDOT_SCRATCH, dtype=torch.float64, device=dev)
-        if self.bounded and (self.segments > 1 or self.empty_policy == "farthest" or self.weights is not None):
-            native.warn_once("bounded E-step: not with segment overlap, 'farthest' or sample weights; full E-steps")
+        if self.bounded and self.segments > 1:
+            native.warn_once("bounded E-step: not with segment overlap; full E-steps")
             self.bounded = False
         if self.bounded:
             # per-row bounds (f32), the rows to re-assign (flags, then their compacted indices
@@ -211,6 +212,17 @@ class LloydEngine:
             self._bcount = torch.zeros(1, dtype=torch.int64, device=dev)
             self._bscratch = torch.empty(max(1, C.compact_blocks(self.n)), dtype=torch.int64, device=dev)
             self._bwork = torch.empty(4, dtype=torch.float32, device=dev)
+            # X is static for the fit: every row's full-pass seed offset, once (bf16 keys)
+            self.oseed = self.pk.seed_offsets(self.xn) if self.n else None
+            # sum_i w_i |x_i|^2 over all ranks (f64): with the M-step's sums S_k and counts n_k the
+            # step's inertia is sxx + sum_k (n_k |c_k|^2 - 2 c_k . S_k), no per-row distances
+            sxx = torch.zeros(1, dtype=torch.float64, device=dev)
+            if self.n and self.weights is None:
+                sxx += self.stats.sumsq[: self.Dp].to(device=dev, dtype=torch.float64).sum()
+            elif self.n:
+                C.wdot(self.xn, self.weights, sxx, self._wscratch)
+            self.comm.allreduce_(sxx)
+            self._sxx = sxx
             self._invalidate_bounds()
         self.delta = None
         if self.incremental:
@@ -252,6 +264,8 @@ class LloydEngine:
         if getattr(self, "bounded", False):
             t.update(bound_ub=self.ub, bound_lb=self.lb, bound_cand=self.cand, bound_rows=self._brows,
                      bound_count=self._bcount, bound_scratch=self._bscratch, bound_work=self._bwork)
+            if self.oseed is not None:
+                t["bound_oseed"] = self.oseed
         out = {k: _r(v.numel() * v.element_size()) for k, v in t.items()}
         for name in ("bufs", "stage"):          # streaming: two chunk / staging buffers
             bl = getattr(self, name, None)
@@ -304,6 +318,9 @@ class LloydEngine:
             graphs[2 * self._gphase].replay()
             self._collective()
             if self.empty_policy == "farthest":
+                # (eager: the relocation reads the counts on the host, after the message's
+                # post-collective fix-ups and before it overwrites an empty cluster's sums)
+                self._post_reduce()
                 self._relocate_empty()
             graphs[2 * self._gphase + 1].replay()
             self._gphase ^= 1
@@ -358,7 +375,7 @@ class LloydEngine:
                     if part == "pre":
                         self._pre_collective()
                     else:
-                        self._post_collective(relocate=False)
+                        self._post_collective(relocate=False, reduce_part=self.empty_policy != "farthest")
                 graphs.append(g)
                 if part == "post":   # the next pair: the other centre-buffer parity
                     self.C, self.Cnew = self.Cnew, self.C
@@ -414,13 +431,34 @@ class LloydEngine:
         with _phase("mikmeans.allreduce"):
             self.comm.allreduce_(self.packed)
 
-    def _post_collective(self, relocate: bool = True):
-        """Device work after the all-reduce: wide-column lo sums, (relocation,) finalize,
-        and the sphere projection of the cosine metric."""
+    def _post_reduce(self):
+        """The message's fix-ups right after the all-reduce: the wide columns' lo sums and,
+        for the bounded E-step, the step's inertia from the sums."""
         if self.scales.nw:
             from ..ops import add_wide_lo
 
             add_wide_lo(self.packed, self.K, self.Dp, self.scales)
+        if self.bounded:
+            self._bounded_inertia()
+
+    def _bounded_inertia(self):
+        """packed[inertia] = sum_i w_i |x_i - c_{l_i}|^2 of the step's labels and centres C,
+        as sxx + sum_k (n_k |c_k|^2 - 2 c_k . S_k) from the all-reduced sums S_k and counts n_k
+        (f64; the bounded E-step assigns only some rows, so no per-row distances exist).  Global
+        already: every rank writes the same value."""
+        K, Dp = self.K, self.Dp
+        KD = K * Dp
+        S = self.packed[:KD].view(K, Dp)
+        cnt = self.packed[KD : KD + K]
+        c = self.C.double()
+        t = cnt * (c * c).sum(1) - 2.0 * (c * S).sum(1)
+        self.packed[KD + K : KD + K + 1].copy_(self._sxx + t.sum())
+
+    def _post_collective(self, relocate: bool = True, reduce_part: bool = True):
+        """Device work after the all-reduce: the message fix-ups (``reduce_part``),
+        (relocation,) finalize, and the sphere projection of the cosine metric."""
+        if reduce_part:
+            self._post_reduce()
         with _phase("mikmeans.finalize"):
             if relocate:
                 self._relocate_empty()
@@ -461,7 +499,7 @@ class LloydEngine:
                              self.weights, self.col_exp, self.cnt_exp, False)
                     C.reduce(self.slab, self.cnt_slab, self.n_chunks, self.K, self.Dp, self.slots,
                              self.packed, self.col_exp, self.cnt_exp)
-            if self.weights is not None:
+            if self.weights is not None and not self.bounded:
                 self._weighted_inertia()
         else:
             self.packed.zero_()
@@ -487,10 +525,10 @@ class LloydEngine:
             # Hamerly's second test: the exact distance to the label's centre; rows it clears
             # keep their label, the rest are compacted again for the full assign
             self._C.tighten(self.X, self.D, self.labels, self.C, self._brows, self._bcount, self.ub, self.lb,
-                            self.cand)
+                            self.cand, self.xn, self._bwork, qeps)
             self._C.compact(self.cand, self._brows, self._bcount, self._bscratch)
         self.pk.assign(self.X, self.xn, self.labels, None, self.slots, True, rows=self._brows, ub=self.ub,
-                       lb=self.lb, scatter=True, count=self._bcount)
+                       lb=self.lb, scatter=True, count=self._bcount, oseed=self.oseed)
 
     @property
     def reassigned(self) -> int:
@@ -575,11 +613,13 @@ class LloydEngine:
         empty = torch.nonzero(cnt <= 0).flatten().tolist()
         if not empty:
             return
-        if self.mind is None:
-            # (GPU engines with this policy allocate mind up front and every step's assign
-            # writes it under the step's centres, graph replays included: nothing to redo)
-            self.mind = torch.empty(self.n, dtype=torch.float32, device=self.device)
-            if self.gpu:
+        if self.mind is None or getattr(self, "bounded", False):
+            # (GPU engines with this policy allocate mind up front and every full step's assign
+            # writes it under the step's centres, graph replays included: nothing to redo.  The
+            # bounded E-step writes no distances: the full pass's, under the same packed centres)
+            if self.mind is None:
+                self.mind = torch.empty(self.n, dtype=torch.float32, device=self.device)
+            if self.gpu and self.n:
                 self._assign_into(self.mind)
         # global farthest points: every rank proposes its top-|empty| candidates
         m = len(empty)
@@ -613,9 +653,7 @@ class LloydEngine:
         K, KD = self.K, self.K * self.Dp
         s = torch.stack([self.packed[KD + K], self.packed[KD + K + 1], self.shift.double().sum(),
                          self.shift.double().max()]).cpu().tolist()
-        # (bounded E-step: the slots hold only the re-assigned rows' distances)
-        inertia = math.nan if getattr(self, "bounded", False) else s[0]
-        return IterStats(self.iteration, inertia, int(round(s[1])), s[2], s[3])
+        return IterStats(self.iteration, s[0], int(round(s[1])), s[2], s[3])
 
     def run(self, max_iter: int, tol: float = 0.0, *, check_every: int = 1, callback=None):
         """Iterate until ``shift <= tol`` (absolute), no label changes, or ``max_iter``.

@@ -97,15 +97,17 @@ class CentroidPack:
                          self.dpad, self.Kpad)
 
     def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False, rows=None,
-               ub=None, lb=None, scatter: bool = False, count=None):
+               ub=None, lb=None, scatter: bool = False, count=None, oseed=None):
         """K2 on these centres (``X`` column-padded, 16-B rows).  ``rows`` (int64, device):
         assign the gathered batch X[rows] without materialising it (labels etc. logical, or
         at the rows themselves with ``scatter``).  ``ub`` / ``lb``: also write every point's
         distance to its nearest and second-nearest centre (the bounded E-step's bounds).
-        ``count`` (int64 [1], device): assign only ``rows[:count]`` (a compacted batch)."""
+        ``count`` (int64 [1], device): assign only ``rows[:count]`` (a compacted batch).
+        ``oseed`` (bf16, f32 [X rows]): every row's seed offset, from :func:`seed_offsets` --
+        a gathered row then gets bitwise the scores (and label) of the full pass over ``X``."""
         if rows is not None:
             self._C.assign(X, self.pack, self.cn, xn, labels, mind, slots, self.Kpad, self.dpad,
-                           track_changed, None, rows, ub, lb, scatter, count)
+                           track_changed, None, rows, ub, lb, scatter, count, oseed)
             return
         keys = None
         if 0 < X.shape[0] <= SPLIT_MAX_ROWS and ub is None:
@@ -117,7 +119,17 @@ class CentroidPack:
             if xn is not None and mind is None:   # the splits park each point's seed offset there
                 mind = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)
         self._C.assign(X, self.pack, self.cn, xn, labels, mind, slots, self.Kpad, self.dpad,
-                       track_changed, keys, None, ub, lb, False)
+                       track_changed, keys, None, ub, lb, False, None, oseed)
+
+    def seed_offsets(self, xn: torch.Tensor) -> "torch.Tensor | None":
+        """Per-row seed offsets the full assign over rows with norms ``xn`` gives its bf16
+        keys (its workgroup's, or the row's own; csrc/rows.hip seed_offsets); None for f32,
+        whose scores carry no offset."""
+        if self.dtype != torch.bfloat16:
+            return None
+        out = torch.empty(xn.numel(), dtype=torch.float32, device=xn.device)
+        self._C.seed_offsets(xn, out, self._C.assign_block_rows(self.dt, self.dpad, self.Kpad))
+        return out
 
 
 def pack_centers(centers: torch.Tensor, D: int, dtype: torch.dtype, device):

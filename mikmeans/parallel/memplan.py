@@ -275,7 +275,8 @@ def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = 
                   src_itemsize: int | None = None) -> MemoryPlan:
     """Device-resident Lloyd fit of an ``n``-row shard (``KMeans.fit``): the engine's buffers
     (models/lloyd.py ``LloydEngine._init_gpu``), the seeding workspace and the final E-step.
-    ``bounded``: the Hamerly E-step's per-row bounds, flags and compacted rows (17 B/row)."""
+    ``bounded``: the Hamerly E-step's per-row bounds, flags and compacted rows (17 B/row; bf16
+    adds the rows' seed offsets, 4 B/row)."""
     es = esize_of(dtype)
     Dp = padded_cols(D, es)
     wted = weighted
@@ -305,9 +306,11 @@ def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = 
         cap = max(1, min(n, int(n * 0.125)))
         p.update(delta_prev=_r(n * 4), delta_list=_r(cap * 8), delta_count=_r(4),
                  delta_tot=_r((K * Dp + K) * 8))
-    if bounded and not weighted and empty_policy != "farthest":
+    if bounded:
         p.update(bound_ub=_r(n * 4), bound_lb=_r(n * 4), bound_cand=_r(n), bound_rows=_r(n * 8),
                  bound_count=_r(8), bound_scratch=_r(max(1, -(-n // COMPACT_ROWS)) * 8), bound_work=_r(16))
+        if es == 2 and n:
+            p["bound_oseed"] = _r(n * 4)   # every row's full-pass seed offset (bf16 keys)
     tr = {"init": _init_items(init, n, Dp, D, K, n_local_trials or 0), "final_assign": final}
     if copy_x and (src_itemsize or es) != es:
         tr["load"] = staging_items(n, D, src_itemsize or es, es, "x")
