@@ -347,7 +347,7 @@ void finalize(int64_t mode, const c10::optional<Tensor>& packed, const Tensor& C
               const c10::optional<Tensor>& Cnew, const c10::optional<Tensor>& frozen,
               const c10::optional<Tensor>& mb_counts, const Tensor& pack, const Tensor& cn,
               const c10::optional<Tensor>& shift, const c10::optional<Tensor>& counts,
-              int64_t dpad, int64_t Kpad) {
+              int64_t dpad, int64_t Kpad, const c10::optional<Tensor>& qshift) {
   check_f32(Cold, "C");
   TORCH_CHECK(Cold.dim() == 2, "mikmeans: C must be [K, D]");
   const int K = (int)Cold.size(0), D = (int)Cold.size(1);
@@ -368,6 +368,7 @@ void finalize(int64_t mode, const c10::optional<Tensor>& packed, const Tensor& C
   if (Cnew.has_value()) check_f32(*Cnew, "Cnew", (int64_t)K * D);
   if (shift.has_value()) check_f32(*shift, "shift", K);
   if (counts.has_value()) check_f32(*counts, "counts", K);
+  if (qshift.has_value()) check_f32(*qshift, "qshift", K);
   if (frozen.has_value())
     TORCH_CHECK(frozen->is_cuda() && frozen->scalar_type() == at::kByte && frozen->numel() >= K,
                 "mikmeans: frozen must be uint8 [K]");
@@ -379,6 +380,7 @@ void finalize(int64_t mode, const c10::optional<Tensor>& packed, const Tensor& C
   a.dtype = dt; a.dpad = (int)dpad; a.Kpad = (int)Kpad;
   a.pack = pack.data_ptr(); a.cn = cn.data_ptr<float>();
   a.shift = opt_ptr<float>(shift); a.counts_out = opt_ptr<float>(counts);
+  a.qshift = opt_ptr<float>(qshift);
   a.mode = (int)mode;
   hip_check(mk::launch_finalize(a, stream()), "finalize");
 }
@@ -627,7 +629,7 @@ void kpar_select(const Tensor& d2, int64_t start, const Tensor& psi, double ell,
 
 void tighten(const Tensor& X, int64_t D, const Tensor& labels, const Tensor& C, const Tensor& rows,
              const Tensor& count, const Tensor& ub, const Tensor& lb, const Tensor& cand, const Tensor& xn,
-             const Tensor& work, double qeps) {
+             const Tensor& work, const c10::optional<Tensor>& oseed) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   const int64_t n = X.size(0);
@@ -647,10 +649,11 @@ void tighten(const Tensor& X, int64_t D, const Tensor& labels, const Tensor& C, 
               "mikmeans: cand must be contiguous uint8 [n]");
   check_f32(xn, "xn", n);
   check_f32(work, "work", 4);
+  if (oseed.has_value()) check_f32(*oseed, "oseed", n);
   hip_check(mk::launch_tighten(dt, X.data_ptr(), ldx, (int)D, labels.data_ptr<int32_t>(), C.data_ptr<float>(),
                                C.stride(0), rows.data_ptr<int64_t>(), count.data_ptr<int64_t>(), rows.numel(),
                                ub.data_ptr<float>(), lb.data_ptr<float>(), cand.data_ptr<uint8_t>(),
-                               xn.data_ptr<float>(), work.data_ptr<float>(), (float)qeps, stream()),
+                               xn.data_ptr<float>(), work.data_ptr<float>(), opt_ptr<const float>(oseed), stream()),
             "tighten");
 }
 
@@ -665,7 +668,8 @@ void seed_offsets(const Tensor& xn, const Tensor& oseed, int64_t block_rows) {
 }
 
 void bounds_update(const Tensor& labels, const Tensor& ub, const Tensor& lb, const Tensor& shift2, const Tensor& cn,
-                   const Tensor& xn, const Tensor& cand, const Tensor& work, double qeps) {
+                   const Tensor& xn, const Tensor& cand, const Tensor& work, const c10::optional<Tensor>& oseed,
+                   int64_t nterms) {
   const int64_t n = labels.numel();
   const int K = (int)shift2.numel();
   check_i32(labels, "labels", n);
@@ -675,12 +679,15 @@ void bounds_update(const Tensor& labels, const Tensor& ub, const Tensor& lb, con
   check_f32(shift2, "shift2", 1);
   check_f32(cn, "cn", K);
   check_f32(work, "work", 4);
+  if (oseed.has_value()) check_f32(*oseed, "oseed", n);
+  TORCH_CHECK(nterms >= 1 && nterms <= 1 << 20, "mikmeans: bad nterms");
   check_cuda(cand, "cand");
   TORCH_CHECK(cand.scalar_type() == at::kByte && cand.is_contiguous() && cand.numel() >= n,
               "mikmeans: cand must be contiguous uint8 [n]");
   hip_check(mk::launch_bounds_update(labels.data_ptr<int32_t>(), ub.data_ptr<float>(), lb.data_ptr<float>(),
                                      shift2.data_ptr<float>(), cn.data_ptr<float>(), K, xn.data_ptr<float>(), n,
-                                     cand.data_ptr<uint8_t>(), work.data_ptr<float>(), (float)qeps, stream()),
+                                     cand.data_ptr<uint8_t>(), work.data_ptr<float>(), opt_ptr<const float>(oseed),
+                                     (int)nterms, stream()),
             "bounds_update");
 }
 
@@ -759,7 +766,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("label_delta_rows", &label_delta_rows, "changed-row list over a candidate list (bounded E-step)");
   m.def("update_delta", &update_delta, "incremental M-step scatter-add (+new / -old label)");
   m.def("reduce_delta", &reduce_delta, "slab reduction into running totals + packed message");
-  m.def("finalize", &finalize, "new centroids, shift, fragment re-pack (K4)");
+  m.def("finalize", &finalize, "new centroids, shift, fragment re-pack (K4)", py::arg("mode"), py::arg("packed"),
+        py::arg("Cold"), py::arg("Cnew"), py::arg("frozen"), py::arg("mb_counts"), py::arg("pack"), py::arg("cn"),
+        py::arg("shift"), py::arg("counts"), py::arg("dpad"), py::arg("Kpad"), py::arg("qshift") = py::none());
   m.def("row_sqnorm", &row_sqnorm, "row squared norms (K1)");
   m.def("col_absmax", &col_absmax,
         "per-column max |x| as f32 bit patterns (+ optional sum |x|, nonzero count, lowest-bit exponent)",

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
   const int kk = threadIdx.x >> 3, part = threadIdx.x & 7;
   const int k = blockIdx.x * 32 + kk;
   const int64_t KD = (int64_t)a.K * a.D;
-  float shift = 0.f, cn = 0.f, cnt = 0.f;
+  float shift = 0.f, cn = 0.f, cnt = 0.f, qs = 0.f;
   if (k < a.K) {
     double c = 0.0;
     bool upd = false;
@@ -61,6 +61,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
       shift += diff * diff;
       const float q = (a.dtype == DT_BF16) ? round_bf16(nv) : nv;
       cn += q * q;
+      const float dq = q - ((a.dtype == DT_BF16) ? round_bf16(old) : old);
+      qs += dq * dq;
       if (a.dtype == DT_BF16) store_pack<uint16_t>(a.pack, a.dpad, k, d, -2.f * q);
       else store_pack<float>(a.pack, a.dpad, k, d, -2.f * q);
     }
@@ -80,11 +82,13 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinalizeArgs a) {
   for (int o = 1; o < 8; o <<= 1) {
     shift += __shfl_xor(shift, o, 64);
     cn += __shfl_xor(cn, o, 64);
+    qs += __shfl_xor(qs, o, 64);
   }
   if (part == 0 && k < a.Kpad) {
     a.cn[k] = (k < a.K) ? cn : PAD_SCORE;
     if (k < a.K) {
       if (a.shift) a.shift[k] = shift;
+      if (a.qshift) a.qshift[k] = qs;
       if (a.counts_out) a.counts_out[k] = cnt;
     }
   }

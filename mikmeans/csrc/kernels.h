@@ -91,23 +91,24 @@ hipError_t launch_transform(int dtype, int dpad, const TransformArgs& a, hipStre
 // ---- Hamerly bounds (csrc/rows.hip) ----------------------------------------------------
 // Moves every point's bounds by the last M-step's centre shifts (ub += |dc_label|,
 // lb -= the largest |dc_k| over k != label) and flags the points whose bounds no longer prove
-// their label (cand[i] = 1): shift2 = squared shifts [K], cn = |c|^2 of the packed centres
-// and xn = |x|^2 size the rounding slack of the kernel's distances, qeps the relative
-// rounding of the stored centres (bf16 2^-8, f32 2^-23); work: 4 floats scratch.  A row
-// stays unflagged only where the full assign's keys provably keep its label (the slack
-// counted on both sides of the test), so skipping it changes nothing.
+// their label (cand[i] = 1): shift2 = squared shifts [K] of the centres the assign ranks
+// (finalize qshift); cn = |c|^2 of the packed centres, xn = |x|^2, oseed (bf16: the rows'
+// full-pass seed offsets, else null) and nterms (the features) size the rounding slack of the
+// kernel's scores; work: 4 floats scratch.  A row stays unflagged only where the full
+// assign's keys provably keep its label (the slack counted on both sides of the test), so
+// skipping it changes nothing.
 hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, const float* shift2, const float* cn,
-                                int K, const float* xn, int64_t n, uint8_t* cand, float* work, float qeps,
-                                hipStream_t s);
+                                int K, const float* xn, int64_t n, uint8_t* cand, float* work, const float* oseed,
+                                int nterms, hipStream_t s);
 // rows[0..*count) = indices of the nonzero flags, ascending (deterministic, no host sync);
 // bscratch: int64 [compact_blocks(n)]
 int64_t compact_blocks(int64_t n);
 // Hamerly's tightening over the compacted candidates rows[0..*count): ub = |x - c_label| (f32
-// centres C [K][ldc]); cand = 0 where the bounds test of launch_bounds_update passes with it
-// (xn, work and qeps as there: work holds that step's slack terms).  n_max bounds *count
+// centres C [K][ldc], bf16-rounded for bf16 points: the centres the assign ranks); cand = 0 where the bounds test of launch_bounds_update passes with it
+// (xn, work, oseed as there, nterms = D: work holds that step's slack terms).  n_max bounds *count
 hipError_t launch_tighten(int dtype, const void* X, int64_t ldx, int D, const int32_t* labels, const float* C,
                           int64_t ldc, const int64_t* rows, const int64_t* count, int64_t n_max, float* ub,
-                          const float* lb, uint8_t* cand, const float* xn, const float* work, float qeps,
+                          const float* lb, uint8_t* cand, const float* xn, const float* work, const float* oseed,
                           hipStream_t s);
 // k-means|| round: cand[i] = u(start + i) < ell * d2[i] / psi[0] (philox uniform keyed by the global row)
 hipError_t launch_kpar_select(const float* d2, int64_t n, int64_t start, const double* psi, double ell,
@@ -185,6 +186,9 @@ struct FinalizeArgs {
   float* shift;           // optional [K]
   float* counts_out;      // optional [K]
   int mode;
+  // optional [K]: |q(C_new) - q(C_old)|^2, the move of the quantised centres the assign ranks
+  // (q = bf16 rounding; the f32 shift for f32 points) -- the bounded E-step's shifts
+  float* qshift = nullptr;
 };
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 

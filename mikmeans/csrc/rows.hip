@@ -209,26 +209,40 @@ hipError_t launch_wdot(const float* a, const float* b, int64_t n, double* out, d
 }
 
 // ---- Hamerly bounds ----------------------------------------------------------------------
-// ub / lb bound the TRUE distances of a row to its label's f32 centre and to every other f32
-// centre.  The assign writes raw kernel distances (sqrt of scores against the quantised
-// pack); the step after, while cand[i] still marks the row as freshly assigned, they are
-// widened once: the scores carry at most ~2^-17 of (|x|^2 + |c|^2 + seed offset) of rounding
-// (bf16 keys; f32 is finer), so d^2 moves by at most delta = 2^-14 (2|x|^2 + |c|max^2) --
-// sqrt(d^2 +- delta), which costs delta / 2d, not sqrt(delta) -- and the quantised centre
-// sits within q = qeps |c|max of the f32 one.  Every later step only adds the f32 shifts.
+// ub / lb bound the distances of a row to its label's centre and to every other centre -- the
+// QUANTISED centres the assign ranks (bf16 rounding of the f32 centres; the f32 centres
+// themselves for f32 points), moved each step by the quantised centres' own shifts (finalize
+// qshift), so the bounds carry no quantisation term.  The assign writes raw kernel distances
+// (sqrt of its scores); the step after, while cand[i] still marks the row as freshly assigned,
+// they are widened once by the scores' rounding slack (score_slack) -- sqrt(d^2 +- slack),
+// which costs slack / 2d, not sqrt(slack).  Every later step only adds the shifts.
 //
 // Skipping a row must leave the label the FULL assign would give it (models/lloyd.py: the
-// bounded E-step's iterates are bitwise the full E-step's), not merely the true nearest centre:
-// the full pass ranks scores against the quantised centres, with rounding and 6-bit key
-// truncation.  Its score for the label is at most (u + q)^2 + delta and every other score at
-// least (l - q)^2 - delta, so the row is skipped only where the first is below the second --
-// the slack counted once more, on both sides (delta = 2^-14 (2|x|^2 + |c|max^2) is 8x the
-// key resolution 2^-17 (|x - c|^2 + 3|x|^2) plus the accumulation's rounding at D <= 1024).
-constexpr float BOUND_EPS = 6.103515625e-05f;   // 2^-14
+// bounded E-step's iterates are bitwise the full E-step's), not merely the nearest centre: the
+// full pass ranks rounded scores with 6-bit key truncation.  Its score for the label is at most
+// u^2 + slack and every other score at least l^2 - slack, so the row is skipped only where the
+// first is below the second -- the slack counted once more, on both sides (keys_keep_label).
+//
+// The slack of a score of row i (squared-distance units): its accumulation -- the seed
+// |c|^2 + o_i and `nterms` exact bf16 (f32: rounded-once) products -- errs by at most
+// 2 (nterms + 8) 2^-24 of the sum of the terms' magnitudes |c|^2 + o_i + 2|x||c| (recursive
+// summation in any order, directed rounding allowed, plus the store's own roundings); the key
+// truncation by 2^-17 of the key d^2 + o_i - |x_i|^2, counted twice.  o_i is the row's
+// full-pass seed offset (AssignArgs::oseed; 0 for f32).
+struct RowSlack {
+  float acc, ex;   // accumulation term, |o_i - |x_i|^2|
+  __device__ __forceinline__ float operator()(float d2) const { return acc + 1.52587890625e-05f * (d2 + ex); }
+};
 
-__device__ __forceinline__ bool keys_keep_label(float u, float l, float q, float delta) {
-  const float lq = l - q, uq = u + q;
-  return lq > 0.f && uq * uq + delta < lq * lq - delta;   // (false for u = inf, NaN)
+__device__ __forceinline__ RowSlack row_slack(float xn, float o, float cmax, float eacc) {
+  return RowSlack{eacc * (cmax * cmax + o + 2.f * sqrtf(xn) * cmax), fabsf(o - xn)};
+}
+
+__device__ __forceinline__ float slack_eacc(int nterms) { return 2.f * (float)(nterms + 8) * 5.9604645e-08f; }
+
+__device__ __forceinline__ bool keys_keep_label(float u, float l, const RowSlack& sl) {
+  const float uu = u * u, ll = l * l;
+  return l > 0.f && uu + sl(uu) < ll - sl(ll);   // (false for u = inf, NaN)
 }
 
 // One workgroup: the largest and second-largest centre shift, the largest's centre, and the
@@ -272,26 +286,28 @@ __global__ __launch_bounds__(256) void bounds_update_kernel(const int32_t* __res
                                                            const float* __restrict__ shift2,
                                                            const float* __restrict__ xn, int64_t n,
                                                            uint8_t* __restrict__ cand,
-                                                           const float* __restrict__ work, float qeps) {
+                                                           const float* __restrict__ work,
+                                                           const float* __restrict__ oseed, int nterms) {
   const float d1 = work[0], d2 = work[1];
   const int a1 = __float_as_int(work[2]);
-  // |c|max of the centres the last E-step ranked (the pack now holds the moved ones)
+  // |c|max over the centres the last E-step ranked and the moved ones the pack now holds
   const float cmax = sqrtf(work[3]) + d1;
-  const float q = qeps * cmax, cmax2 = cmax * cmax;
+  const float eacc = slack_eacc(nterms);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int a = labels[i];
     if (a < 0) { cand[i] = 1; continue; }       // unassigned: a full assign decides
+    const RowSlack sl = row_slack(xn[i], oseed ? oseed[i] : 0.f, cmax, eacc);
     float u = ub[i], l = lb[i];
     if (cand[i]) {                               // raw kernel distances: widen them once
-      const float delta = BOUND_EPS * (2.f * xn[i] + cmax2);
-      u = sqrtf(u * u + delta) + q;
-      l = sqrtf(fmaxf(l * l - delta, 0.f)) - q;
+      const float uu = u * u, ll = l * l;
+      u = sqrtf(uu + sl(uu));
+      l = sqrtf(fmaxf(ll - sl(ll), 0.f));
     }
     u += sqrtf(fmaxf(shift2[a], 0.f));
     l -= (a == a1 ? d2 : d1);
     ub[i] = u;
     lb[i] = l;
-    cand[i] = keys_keep_label(u, l, q, BOUND_EPS * (2.f * xn[i] + cmax2)) ? 0 : 1;
+    cand[i] = keys_keep_label(u, l, sl) ? 0 : 1;
   }
 }
 
@@ -340,21 +356,21 @@ hipError_t launch_seed_offsets(const float* xn, int64_t n, int block_rows, float
 }
 
 hipError_t launch_bounds_update(const int32_t* labels, float* ub, float* lb, const float* shift2, const float* cn,
-                                int K, const float* xn, int64_t n, uint8_t* cand, float* work, float qeps,
-                                hipStream_t s) {
+                                int K, const float* xn, int64_t n, uint8_t* cand, float* work, const float* oseed,
+                                int nterms, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (K < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(shift_top2_kernel, dim3(1), dim3(1024), 0, s, shift2, cn, K, work);
   int64_t nb = (n + 255) / 256;
   if (nb > 8192) nb = 8192;
   hipLaunchKernelGGL(bounds_update_kernel, dim3((unsigned)nb), dim3(256), 0, s, labels, ub, lb, shift2, xn, n,
-                     cand, work, qeps);
+                     cand, work, oseed, nterms);
   return hipGetLastError();
 }
 
 // ---- Hamerly tightening ----------------------------------------------------------------
 // A row whose moved bounds no longer prove its label first gets the exact distance to its
-// label's f32 centre (Hamerly 2010's second test): ub drops to it, and a row whose tight ub
+// label's (quantised) centre (Hamerly 2010's second test): ub drops to it, and a row whose tight ub
 // passes the bounds test against lb (keys_keep_label) keeps its label without the assign.  A wave takes 4 rows per pass, 16
 // lanes per row in 16-B pieces (one coalesced load per piece), |x - c|^2 summed directly
 // (no |x|^2 + |c|^2 cancellation).  rows[0..*count): the compacted candidates.
@@ -366,12 +382,12 @@ __global__ __launch_bounds__(256) void tighten_kernel(const T* __restrict__ X, i
                                                      const int64_t* __restrict__ count, float* __restrict__ ub,
                                                      const float* __restrict__ lb, uint8_t* __restrict__ cand,
                                                      const float* __restrict__ xn, const float* __restrict__ work,
-                                                     float qeps) {
+                                                     const float* __restrict__ oseed, int nterms) {
   constexpr int V = Elem<T>::V;
   const int64_t m = count[0];
   // the slack terms of this step's bounds test (bounds_update_kernel)
   const float cmax = sqrtf(work[3]) + work[0];
-  const float q = qeps * cmax, cmax2 = cmax * cmax;
+  const float eacc = slack_eacc(nterms);
   const int lane = threadIdx.x & 63, grp = lane >> 4, gl = lane & 15;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nwave = ((int64_t)gridDim.x * 256) >> 6;
@@ -395,7 +411,9 @@ __global__ __launch_bounds__(256) void tighten_kernel(const T* __restrict__ X, i
         for (int q = 0; q < V; ++q) {
           const int col = p * V + q;
           if (col < D) {
-            const float d = f[q] - cp[col];
+            // (bf16 points: the bf16-rounded centre the assign ranks, as the bounds are)
+            const float c = sizeof(T) == 2 ? round_bf16(cp[col]) : cp[col];
+            const float d = f[q] - c;
             s = __builtin_fmaf(d, d, s);
           }
         }
@@ -406,24 +424,24 @@ __global__ __launch_bounds__(256) void tighten_kernel(const T* __restrict__ X, i
     if (gl == 0 && a >= 0) {
       const float u = __builtin_sqrtf(s) * (1.f + 1e-6f);   // (+ the f32 rounding of D terms)
       ub[row] = u;
-      if (keys_keep_label(u, lb[row], q, BOUND_EPS * (2.f * xn[row] + cmax2))) cand[row] = 0;
+      if (keys_keep_label(u, lb[row], row_slack(xn[row], oseed ? oseed[row] : 0.f, cmax, eacc))) cand[row] = 0;
     }
   }
 }
 
 hipError_t launch_tighten(int dtype, const void* X, int64_t ldx, int D, const int32_t* labels, const float* C,
                           int64_t ldc, const int64_t* rows, const int64_t* count, int64_t n_max, float* ub,
-                          const float* lb, uint8_t* cand, const float* xn, const float* work, float qeps,
+                          const float* lb, uint8_t* cand, const float* xn, const float* work, const float* oseed,
                           hipStream_t s) {
   if (n_max <= 0) return hipSuccess;
   int64_t nb = (n_max + 15) / 16;   // 16 rows per block and pass
   if (nb > 8192) nb = 8192;
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(tighten_kernel<uint16_t>, dim3((unsigned)nb), dim3(256), 0, s, (const uint16_t*)X, ldx, D,
-                       labels, C, ldc, rows, count, ub, lb, cand, xn, work, qeps);
+                       labels, C, ldc, rows, count, ub, lb, cand, xn, work, oseed, D);
   else
     hipLaunchKernelGGL(tighten_kernel<float>, dim3((unsigned)nb), dim3(256), 0, s, (const float*)X, ldx, D, labels,
-                       C, ldc, rows, count, ub, lb, cand, xn, work, qeps);
+                       C, ldc, rows, count, ub, lb, cand, xn, work, oseed, D);
   return hipGetLastError();
 }
 

@@ -212,6 +212,9 @@ class LloydEngine:
             self._bcount = torch.zeros(1, dtype=torch.int64, device=dev)
             self._bscratch = torch.empty(max(1, C.compact_blocks(self.n)), dtype=torch.int64, device=dev)
             self._bwork = torch.empty(4, dtype=torch.float32, device=dev)
+            # the bounds are distances to the centres the assign ranks (bf16-rounded for bf16
+            # points), moved by those centres' own shifts: finalize writes them beside the f32 ones
+            self.qshift = torch.zeros(self.K, dtype=torch.float32, device=dev)
             # X is static for the fit: every row's full-pass seed offset, once (bf16 keys)
             self.oseed = self.pk.seed_offsets(self.xn) if self.n else None
             # sum_i w_i |x_i|^2 over all ranks (f64): with the M-step's sums S_k and counts n_k the
@@ -263,7 +266,8 @@ class LloydEngine:
                      delta_count=self.delta["count"], delta_tot=self.delta["tot"])
         if getattr(self, "bounded", False):
             t.update(bound_ub=self.ub, bound_lb=self.lb, bound_cand=self.cand, bound_rows=self._brows,
-                     bound_count=self._bcount, bound_scratch=self._bscratch, bound_work=self._bwork)
+                     bound_count=self._bcount, bound_scratch=self._bscratch, bound_work=self._bwork,
+                     bound_qshift=self.qshift)
             if self.oseed is not None:
                 t["bound_oseed"] = self.oseed
         out = {k: _r(v.numel() * v.element_size()) for k, v in t.items()}
@@ -410,7 +414,8 @@ class LloydEngine:
         if self.delta is not None:
             st.update({k: v.clone() for k, v in self.delta.items()})
         if self.bounded:
-            st.update(ub=self.ub.clone(), lb=self.lb.clone(), cand=self.cand.clone(), shift=self.shift.clone())
+            st.update(ub=self.ub.clone(), lb=self.lb.clone(), cand=self.cand.clone(), shift=self.shift.clone(),
+                      qshift=self.qshift.clone())
         return st
 
     def _restore_capture_state(self, st: dict):
@@ -419,7 +424,7 @@ class LloydEngine:
             for k, v in self.delta.items():
                 v.copy_(st[k])
         if self.bounded:
-            for k in ("ub", "lb", "cand", "shift"):
+            for k in ("ub", "lb", "cand", "shift", "qshift"):
                 getattr(self, k).copy_(st[k])
 
     def _step_gpu(self):
@@ -462,7 +467,8 @@ class LloydEngine:
         with _phase("mikmeans.finalize"):
             if relocate:
                 self._relocate_empty()
-            self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts)
+            self.pk.finalize(1, self.packed, self.C, self.Cnew, self.frozen, None, self.shift, self.counts,
+                             self.qshift if self.bounded else None)
         if self.spherical:
             self._project_sphere()
 
@@ -516,16 +522,16 @@ class LloydEngine:
         compacted in ascending order (count on the device) -> their exact distance to the
         label's centre (tightening) -> the rows still flagged compacted again -> a gathered
         assign that scatters labels and fresh bounds back to those rows.  No host read."""
-        # (distance of a quantised centre from its f32 copy, relative to |c|: bf16 RNE)
-        qeps = 2.0 ** -8 if self.dtype == torch.bfloat16 else 2.0 ** -22
-        self._C.bounds_update(self.labels, self.ub, self.lb, self.shift, self.pk.cn, self.xn, self.cand,
-                              self._bwork, qeps)
+        # (the bounds and shifts are the ranked centres' own: no quantisation term; the scores'
+        # rounding slack is sized per row from |x|^2, its seed offset and D)
+        self._C.bounds_update(self.labels, self.ub, self.lb, self.qshift, self.pk.cn, self.xn, self.cand,
+                              self._bwork, self.oseed, self.D)
         self._C.compact(self.cand, self._brows, self._bcount, self._bscratch)
         if self.tighten:
             # Hamerly's second test: the exact distance to the label's centre; rows it clears
             # keep their label, the rest are compacted again for the full assign
             self._C.tighten(self.X, self.D, self.labels, self.C, self._brows, self._bcount, self.ub, self.lb,
-                            self.cand, self.xn, self._bwork, qeps)
+                            self.cand, self.xn, self._bwork, self.oseed)
             self._C.compact(self.cand, self._brows, self._bcount, self._bscratch)
         self.pk.assign(self.X, self.xn, self.labels, None, self.slots, True, rows=self._brows, ub=self.ub,
                        lb=self.lb, scatter=True, count=self._bcount, oseed=self.oseed)
@@ -550,6 +556,9 @@ class LloydEngine:
         Cn = self.Cnew[:, : self.D]
         Cn.div_(Cn.norm(dim=1, keepdim=True).clamp_min(1e-30))
         torch.sum((self.Cnew - self.C) ** 2, dim=1, out=self.shift)
+        if getattr(self, "bounded", False):   # the ranked (quantised) centres' move
+            q = self.dtype if self.dtype == torch.bfloat16 else torch.float32
+            torch.sum((self.Cnew.to(q).float() - self.C.to(q).float()) ** 2, dim=1, out=self.qshift)
         if self.gpu:
             self.pk.finalize(0, None, self.Cnew)
 

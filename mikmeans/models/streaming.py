@@ -58,6 +58,7 @@ class StreamingLloydEngine(LloydEngine):
         self.incremental = False
         self.spherical = bool(spherical)
         self.delta = None
+        self.bounded = False      # (every chunk is assigned in full each pass)
         self.segments = 1
         self.empty_policy = empty_policy
         self.K = int(n_clusters)

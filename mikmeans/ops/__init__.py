@@ -90,11 +90,12 @@ class CentroidPack:
         return self
 
     def finalize(self, mode: int, packed, Cold, Cnew=None, frozen=None, mb_counts=None, shift=None,
-                 counts=None):
+                 counts=None, qshift=None):
         """K4: new centres from the all-reduced message (mode 1 Lloyd, 2 mini-batch) or
-        pack-only (mode 0); always re-packs ``-2c`` / ``|c|^2`` for the next assign."""
+        pack-only (mode 0); always re-packs ``-2c`` / ``|c|^2`` for the next assign.
+        ``qshift``: the squared move of the quantised centres the assign ranks."""
         self._C.finalize(mode, packed, Cold, Cnew, frozen, mb_counts, self.pack, self.cn, shift, counts,
-                         self.dpad, self.Kpad)
+                         self.dpad, self.Kpad, qshift)
 
     def assign(self, X, xn, labels, mind=None, slots=None, track_changed: bool = False, rows=None,
                ub=None, lb=None, scatter: bool = False, count=None, oseed=None):

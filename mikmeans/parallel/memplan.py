@@ -308,7 +308,8 @@ def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = 
                  delta_tot=_r((K * Dp + K) * 8))
     if bounded:
         p.update(bound_ub=_r(n * 4), bound_lb=_r(n * 4), bound_cand=_r(n), bound_rows=_r(n * 8),
-                 bound_count=_r(8), bound_scratch=_r(max(1, -(-n // COMPACT_ROWS)) * 8), bound_work=_r(16))
+                 bound_count=_r(8), bound_scratch=_r(max(1, -(-n // COMPACT_ROWS)) * 8), bound_work=_r(16),
+                 bound_qshift=_r(K * 4))
         if es == 2 and n:
             p["bound_oseed"] = _r(n * 4)   # every row's full-pass seed offset (bf16 keys)
     tr = {"init": _init_items(init, n, Dp, D, K, n_local_trials or 0), "final_assign": final}

@@ -136,7 +136,7 @@ def test_bounded_trajectory_bitwise(native, dtype, d, k, init, spread):
     from mikmeans.parallel import Comm
 
     n = 400_000
-    X = _spread_rows(n, d, k, dtype) if spread else B.make_blobs(n, d, k // 2, seed=k, dtype=dtype, device=DEV)
+    X = _spread_rows(n, d, k, dtype) if spread else B.make_blobs(n, d, k, seed=k, dtype=dtype, device=DEV)
     comm = Comm.local(torch.device(DEV))
     if init == "random":
         C0 = init_random(X, d, k, n, 0, comm, 3)
@@ -154,7 +154,10 @@ def test_bounded_trajectory_bitwise(native, dtype, d, k, init, spread):
         assert sa.n_changed == sb.n_changed, it
         assert sb.inertia == pytest.approx(sa.inertia, rel=1e-4), it
         re.append(eb.reassigned)
-    assert re[0] == n and min(re) < n // 2, re
+    print("reassigned per step", re)
+    assert re[0] == n
+    if not spread:      # (structureless rows keep every centre moving: no bound settles)
+        assert min(re) < 0.6 * n, re
 
 
 def test_kmeans_hamerly_fit(native):
@@ -298,11 +301,12 @@ def test_tighten_exact_distance(native, dtype, d):
     cand = torch.ones(n, dtype=torch.uint8, device=DEV)
     xn = ops.row_sqnorm(X)
     work = torch.zeros(4, device=DEV)        # (no shifts, |c|max 0: the slack is the rows' own)
-    native.tighten(X, d, lab, C, rows, count, ub, lb, cand, xn, work, 2.0 ** -8)
+    native.tighten(X, d, lab, C, rows, count, ub, lb, cand, xn, work, None)
     torch.cuda.synchronize()
     listed = rows[: int(count)]
     listed = listed[lab[listed] >= 0]
-    ref = (X[listed, :d].double() - C[lab[listed].long(), :d].double()).norm(dim=1)
+    Cq = C.to(dtype).double() if dtype == torch.bfloat16 else C.double()   # (the centres the assign ranks)
+    ref = (X[listed, :d].double() - Cq[lab[listed].long(), :d]).norm(dim=1)
     torch.testing.assert_close(ub[listed].double(), ref, rtol=2e-6, atol=1e-6)
     even = (listed % 2 == 0)
     assert bool((cand[listed[even]] == 0).all()) and bool((cand[listed[~even]] == 1).all())
