@@ -763,6 +763,9 @@ class MiniBatchKMeans(_Serving):
                 raise memplan.HBMCapacityError(f"MiniBatchKMeans.fit: {plan.summary()} does not fit; "
                                                "use a smaller batch_size or more ranks")
             self.memory_plan_ = plan.as_dict()
+        # (sizes only: the fit's device copies are freed when it returns; a refit allocates
+        # its own before anything of this one could still be referenced)
+        self._fit_buffer_bytes = {}
         if not gpu or resident:
             Xt = _device_rows(X, device, self.dtype, gpu)
             Xh = None
@@ -781,17 +784,19 @@ class MiniBatchKMeans(_Serving):
             eng.set_bound(bound)
         # the fit's own device buffers, allocated before the seeding so the plan's phases
         # (persistent + the largest transient) bound the real peak
+        from .parallel.memplan import _r
+
         buf = rows = None
-        self._fit_buffers = {}
+        fb = self._fit_buffer_bytes
         if eng.gpu and Xt is not None and Xt.data_ptr() != getattr(X, "data_ptr", lambda: None)():
-            self._fit_buffers["X"] = Xt          # the fit's device copy of the shard
+            fb["X"] = _r(Xt.numel() * Xt.element_size())     # the fit's device copy of the shard
         if eng.gpu and b:
             if Xt is not None:    # device shard: the step reads X[rows] in place, nothing gathered
                 rows = torch.empty(b, dtype=torch.int64, device=device)
-                self._fit_buffers["rows"] = rows
+                fb["rows"] = _r(rows.numel() * rows.element_size())
             else:                 # host shard: the batch's rows are gathered on the host
                 buf = torch.zeros((b, eng.Dp), dtype=self.dtype, device=device)
-                self._fit_buffers["batch"] = buf
+                fb["batch"] = _r(buf.numel() * buf.element_size())
         if resume_from is not None:
             ck = load_checkpoint(resume_from, comm=comm)
             if ck.get("kind") != "minibatch" or int(ck["n_features"]) != D:
@@ -952,11 +957,8 @@ class MiniBatchKMeans(_Serving):
     def device_buffers(self) -> dict:
         """Allocator bytes of the last ``fit``'s persistent device buffers (engine + the fit's
         shard copy / row list / batch buffer), named as ``memplan.plan_minibatch`` plans them."""
-        from .parallel.memplan import _r
-
         out = dict(self._eng.device_buffers()) if self._eng is not None else {}
-        for k, v in getattr(self, "_fit_buffers", {}).items():
-            out[k] = _r(v.numel() * v.element_size())
+        out.update(getattr(self, "_fit_buffer_bytes", {}))
         return out
 
     def _finish(self, eng):

@@ -502,6 +502,29 @@ void kpp_cc(const Tensor& centers, int64_t k, const Tensor& cnew, const Tensor& 
             "kpp_cc");
 }
 
+// Weighted k-means++ draws over a candidate set (csrc/kpp.hip wkpp): `steps` draws into out
+void wkpp(const Tensor& Ct, const Tensor& w, const Tensor& d2, const Tensor& cum, const Tensor& part,
+          const Tensor& u, const Tensor& state, const Tensor& out, int64_t steps) {
+  check_cuda(Ct, "Ct");
+  TORCH_CHECK(Ct.scalar_type() == at::kFloat && Ct.dim() == 2 && Ct.is_contiguous(),
+              "mikmeans: Ct must be contiguous f32 [D, M]");
+  const int64_t D = Ct.size(0), M = Ct.size(1);
+  TORCH_CHECK(M >= 1 && D >= 1 && D <= 8192, "mikmeans: bad candidate set [", D, ", ", M, "]");
+  check_f64(w, "w", M);
+  check_f64(d2, "d2", M);
+  check_f64(cum, "cum", M);
+  check_f64(part, "part", (M + 255) / 256);
+  check_f64(u, "u", 1);
+  check_i64(state, "state", 2);
+  check_f32(out, "out", 1);
+  TORCH_CHECK(out.dim() == 2 && out.size(1) >= D && out.stride(1) == 1, "mikmeans: out must be f32 [K, >=D]");
+  TORCH_CHECK(steps >= 0 && steps <= out.size(0) && steps <= u.numel(), "mikmeans: more steps than draws");
+  hip_check(mk::launch_wkpp(Ct.data_ptr<float>(), M, (int)D, w.data_ptr<double>(), d2.data_ptr<double>(),
+                            cum.data_ptr<double>(), part.data_ptr<double>(), u.data_ptr<double>(),
+                            state.data_ptr<int64_t>(), out.data_ptr<float>(), out.stride(0), (int)steps, stream()),
+            "wkpp");
+}
+
 void kpp_sample(const Tensor& block_sums, const Tensor& d2, int64_t rows_per_block,
                 const Tensor& target, const Tensor& X, const Tensor& crow,
                 const c10::optional<Tensor>& idx_out, int64_t mode,
@@ -785,6 +808,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("X"), py::arg("c"), py::arg("first"), py::arg("d2"), py::arg("block_sums"),
         py::arg("rows_per_block"), py::arg("owner") = py::none(), py::arg("cc") = py::none(),
         py::arg("kcc") = 0, py::arg("knew") = -1);
+  m.def("wkpp", &wkpp, "weighted k-means++ draws over a candidate set (k-means|| recluster)");
   m.def("kpp_cc", &kpp_cc, "centre-centre squared distances for the pruned K5 pass");
   m.def("kpp_sample", &kpp_sample, "k-means++ D^2 sampling (K6)");
   m.def("blob_centers", &blob_centers, "Philox blob centres");

@@ -236,6 +236,13 @@ hipError_t launch_kpp_sample(int dtype, const double* block_sums, int nblocks, c
                              int D, int64_t ldx, float* crow, int64_t* idx_out, int mode,
                              const double* totals_all, int world, int rank, hipStream_t s);
 
+// Weighted k-means++ over M candidates (the k-means|| recluster): Ct f32 [D][M] (column-major),
+// w f64 [M], u f64 [K]; d2 f64 [M] (= +inf before the first step), cum f64 [M] and part f64
+// [ceil(M/256)] scratch, state int64 {previous pick (-1 first), next k}.  Enqueues `steps`
+// draws, each writing out[k][0..D) (row stride ldo); no host read.
+hipError_t launch_wkpp(const float* Ct, int64_t M, int D, const double* w, double* d2, double* cum, double* part,
+                       const double* u, int64_t* state, float* out, int64_t ldo, int steps, hipStream_t s);
+
 // ---- synthetic Gaussian blobs (counter-based Philox, deterministic by index) --
 hipError_t launch_blob_centers(float* centers, int n_centers, int D, float box, uint64_t seed,
                                hipStream_t s);

@@ -383,6 +383,157 @@ hipError_t launch_kpp_sample(int dtype, const double* block_sums, int nblocks, c
 }
 
 // ---------------------------------------------------------------------------
+// Weighted k-means++ over a small candidate set (the k-means|| recluster, models/init.py):
+// M candidates (Ct: f32, column-major [D][M], so a wave's candidate loads coalesce), weights
+// w (f64), K draws u (f64).  Step k is two launches, with no host read in between:
+//   wkpp_d2    d2[i] = min(d2[i], |c_i - c_j|^2) against the previous pick j (f64 sums of the
+//              exact f64 differences), then p_i = w_i d2[i] scanned inside each 256-candidate
+//              block (cum[i]: the block's inclusive prefix, part[b]: its total);
+//   wkpp_pick  one workgroup: the block prefixes P_b (a chunked scan of part), the target
+//              t = u[k] * total, the first block with P_b + part[b] > t and in it the first
+//              candidate with P_b + cum[i] > t (torch.searchsorted(..., right=True) on the
+//              cumulative weights; none: the last candidate) -> out[k] and state {j, k+1}.
+// Every sum has a fixed order, so every rank draws the same centres from the same inputs.
+// Step 0 (state j = -1) draws by weight alone; d2 starts at +inf.
+constexpr int WK_NT = 256;
+
+__device__ __forceinline__ double wave_incl_scan(double v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// Inclusive scan over the 256 threads of a block (4 waves), fixed order; returns the thread's
+// prefix and (all threads) the block total.
+__device__ __forceinline__ double block_incl_scan(double v, double* red, double& total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  v = wave_incl_scan(v, lane);
+  if (lane == 63) red[wv] = v;
+  __syncthreads();
+  double off = 0.0;
+  for (int q = 0; q < wv; ++q) off += red[q];
+  total = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();   // (red is reused by the caller's next scan)
+  return v + off;
+}
+
+__global__ __launch_bounds__(WK_NT) void wkpp_d2_kernel(const float* __restrict__ Ct, int64_t M, int D,
+                                                       const double* __restrict__ w, double* __restrict__ d2,
+                                                       double* __restrict__ cum, double* __restrict__ part,
+                                                       const int64_t* __restrict__ state) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* red = (double*)smem;
+  float* cj = (float*)(smem + 64);
+  const int64_t j = state[0];
+  if (j >= 0)
+    for (int d = threadIdx.x; d < D; d += WK_NT) cj[d] = Ct[(int64_t)d * M + j];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * WK_NT + threadIdx.x;
+  double p = 0.0;
+  if (i < M) {
+    double dd = d2[i];
+    if (j >= 0) {
+      double s = 0.0;
+      for (int d = 0; d < D; ++d) {
+        const double t = (double)Ct[(int64_t)d * M + i] - (double)cj[d];
+        s = __builtin_fma(t, t, s);
+      }
+      dd = s < dd ? s : dd;
+      d2[i] = dd;
+    }
+    p = j >= 0 ? w[i] * dd : w[i];   // (step 0: by weight alone)
+  }
+  double total;
+  const double c = block_incl_scan(p, red, total);
+  if (i < M) cum[i] = c;
+  if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(WK_NT) void wkpp_pick_kernel(const float* __restrict__ Ct, int64_t M, int D,
+                                                         const double* __restrict__ cum,
+                                                         const double* __restrict__ part, int nb,
+                                                         const double* __restrict__ u, int64_t* __restrict__ state,
+                                                         float* __restrict__ out, int64_t ldo) {
+  __shared__ double red[4];
+  __shared__ double sh_carry, sh_pb;
+  __shared__ int sh_b;
+  __shared__ int64_t sh_j;
+  const int64_t k = state[1];
+  // P_b, the exclusive prefix of the block totals, chunk by chunk in a fixed order (an
+  // inclusive scan of the totals shifted by one: no subtraction); with t >= 0, the first block
+  // with P_b + part[b] > t is found in pass 2.  Pass 1 computes the grand total the same way.
+  auto chunks = [&](double t, bool search) -> bool {
+    double carry = 0.0;
+    for (int b0 = 0; b0 < nb; b0 += WK_NT) {
+      const int b = b0 + (int)threadIdx.x;
+      const double prev = (b < nb && threadIdx.x > 0) ? part[b - 1] : 0.0;
+      double tot;
+      const double excl = block_incl_scan(prev, red, tot) + carry;
+      const double own = b < nb ? part[b] : 0.0;
+      const int last = b0 + WK_NT - 1 < nb ? b0 + WK_NT - 1 : nb - 1;
+      if (b == last) sh_carry = excl + own;   // (one writer: the chunk's last block)
+      if (search) {
+        if (threadIdx.x == 0) sh_b = nb;
+        __syncthreads();
+        if (b < nb && excl + own > t) atomicMin(&sh_b, b);   // (LDS atomic)
+        __syncthreads();
+        const int f = sh_b;
+        if (f < nb) {
+          if (b == f) sh_pb = excl;
+          __syncthreads();
+          return true;
+        }
+      }
+      __syncthreads();
+      carry = sh_carry;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) sh_pb = carry;
+    __syncthreads();
+    return false;
+  };
+  (void)chunks(0.0, false);
+  const double t = u[k] * sh_pb;   // u * total
+  __syncthreads();
+  const bool hit = chunks(t, true);
+  const int found = hit ? sh_b : nb;
+  const double pb = sh_pb;
+  // inside the block: the first candidate with P_b + cum[i] > t (its last candidate's cum is
+  // the block total bitwise, so the block test guarantees a hit); no block: the last candidate
+  if (threadIdx.x == 0) sh_j = hit ? (int64_t)found * WK_NT + WK_NT - 1 : M - 1;
+  __syncthreads();
+  if (hit) {
+    const int64_t i = (int64_t)found * WK_NT + threadIdx.x;
+    if (i < M && pb + cum[i] > t) atomicMin((unsigned long long*)&sh_j, (unsigned long long)i);
+  }
+  __syncthreads();
+  const int64_t jj = sh_j < M ? sh_j : M - 1;
+  for (int d = threadIdx.x; d < D; d += WK_NT) out[k * ldo + d] = Ct[(int64_t)d * M + jj];
+  if (threadIdx.x == 0) {
+    state[0] = jj;
+    state[1] = k + 1;
+  }
+}
+
+hipError_t launch_wkpp(const float* Ct, int64_t M, int D, const double* w, double* d2, double* cum, double* part,
+                       const double* u, int64_t* state, float* out, int64_t ldo, int steps, hipStream_t s) {
+  if (M <= 0 || steps <= 0) return M <= 0 && steps > 0 ? hipErrorInvalidValue : hipSuccess;
+  const int64_t nb = (M + WK_NT - 1) / WK_NT;
+  if (nb > (1 << 24)) return hipErrorInvalidValue;
+  const size_t lds = 64 + (size_t)D * 4;
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  for (int st = 0; st < steps; ++st) {
+    hipLaunchKernelGGL(wkpp_d2_kernel, dim3((unsigned)nb), dim3(WK_NT), lds, s, Ct, M, D, w, d2, cum, part, state);
+    hipLaunchKernelGGL(wkpp_pick_kernel, dim3(1), dim3(WK_NT), 0, s, Ct, M, D, cum, part, (int)nb, u, state, out,
+                       ldo);
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 constexpr uint32_t TAG_CID = 0xC1D0u, TAG_CTR = 0xCE27u, TAG_NRM = 0x4E52u;
 
 __global__ void blob_centers_kernel(float* centers, int n_centers, int D, float box, uint32_t k0,

@@ -349,7 +349,8 @@ def resolve_init(init, X, D, K, n_global, start, comm: Comm, seed: int, n_local_
             return init_kmeanspp(X, D, K, n_global, start, comm, seed,
                                  n_local_trials or default_local_trials(K), sampling=sampling)
         if name in ("k-means||", "kmeans||", "scalable-k-means++"):
-            return init_kmeans_parallel(X, D, K, n_global, start, comm, seed)
+            return init_kmeans_parallel(X, D, K, n_global, start, comm, seed, n_local_trials=n_local_trials,
+                                        sampling=sampling)
         raise ValueError(f"unknown init {init!r}")
     c = torch.as_tensor(np.asarray(init) if not torch.is_tensor(init) else init, dtype=torch.float32)
     if c.shape != (K, D):
@@ -407,12 +408,43 @@ def _gather_varlen(rows: torch.Tensor, comm: Comm) -> torch.Tensor:
     return torch.cat([allr[r, : counts[r]] for r in range(comm.world)]).to(rows.device)
 
 
-def weighted_kmeanspp(C: torch.Tensor, w: torch.Tensor, K: int, u: torch.Tensor, *, graph_steps: int = 64) -> torch.Tensor:
+def weighted_kmeanspp(C: torch.Tensor, w: torch.Tensor, K: int, u: torch.Tensor, *, graph_steps: int = 64,
+                      native_kernels: bool | None = None) -> torch.Tensor:
     """k-means++ over the rows of ``C`` [M, D] weighted by ``w`` (D^2 x weight sampling),
-    ``u`` [K] uniforms (``u[0]`` draws the first centre by weight).  Device ops only, no
-    host read; identical inputs give identical centres on every rank.  On a GPU the steps
-    replay as a hipGraph of ``graph_steps`` steps each (the step index lives on the device),
-    so K = 4096 seeding steps cost a few hundred graph launches instead of ~40k op launches."""
+    ``u`` [K] uniforms (``u[0]`` draws the first centre by weight); identical inputs give
+    identical centres on every rank.
+
+    On a GPU the draws run on the framework's kernels (csrc/kpp.hip ``wkpp``): per draw one
+    pass lowers the candidates' f64 d2 against the previous pick and scans w * d2 per block,
+    one workgroup turns u * total into the pick -- two launches, no host read, fixed summation
+    orders.  Elsewhere (and with ``native_kernels=False``, the test oracle) the same draws as
+    PyTorch ops (cumsum / searchsorted, replayed as hipGraphs of ``graph_steps`` steps on a
+    GPU).  The two agree draw for draw unless a target falls within f64 rounding of a
+    cumulative-weight boundary (their prefix sums associate differently)."""
+    if native_kernels is None:
+        native_kernels = C.is_cuda
+    if native_kernels:
+        return _weighted_kmeanspp_native(C, w, K, u)
+    return _weighted_kmeanspp_torch(C, w, K, u, graph_steps=graph_steps)
+
+
+def _weighted_kmeanspp_native(C: torch.Tensor, w: torch.Tensor, K: int, u: torch.Tensor) -> torch.Tensor:
+    Cn = native.require()
+    M, D = C.shape
+    dev = C.device
+    Ct = C.to(torch.float32).t().contiguous()            # [D, M]: a wave's candidate loads coalesce
+    d2 = torch.full((M,), float("inf"), dtype=torch.float64, device=dev)  # (step 0 draws by weight alone)
+    cum = torch.empty(M, dtype=torch.float64, device=dev)
+    part = torch.empty(-(-M // 256), dtype=torch.float64, device=dev)
+    state = torch.tensor([-1, 0], dtype=torch.int64, device=dev)
+    out = torch.empty((K, D), dtype=torch.float32, device=dev)
+    Cn.wkpp(Ct, w.to(device=dev, dtype=torch.float64).contiguous(), d2, cum, part,
+            u.to(device=dev, dtype=torch.float64).contiguous(), state, out, K)
+    return out
+
+
+def _weighted_kmeanspp_torch(C: torch.Tensor, w: torch.Tensor, K: int, u: torch.Tensor, *,
+                             graph_steps: int = 64) -> torch.Tensor:
     M = C.shape[0]
     Cd = C.double()
     wd = w.double()
@@ -455,7 +487,8 @@ def weighted_kmeanspp(C: torch.Tensor, w: torch.Tensor, K: int, u: torch.Tensor,
 
 
 def init_kmeans_parallel(X: torch.Tensor, D: int, K: int, n_global: int, start: int, comm: Comm, seed: int,
-                         *, rounds: int = 5, oversampling: float = 2.0, xn: torch.Tensor | None = None) -> torch.Tensor:
+                         *, rounds: int = 5, oversampling: float = 2.0, xn: torch.Tensor | None = None,
+                         n_local_trials: int | None = None, sampling: str = "exact") -> torch.Tensor:
     """k-means|| seeding (Bahmani et al. 2012); returns replicated f32 centres [K, D].
 
     Per round: psi = the global potential (one all-reduce), every row g kept with probability
@@ -465,7 +498,8 @@ def init_kmeans_parallel(X: torch.Tensor, D: int, K: int, n_global: int, start: 
     (rows nearest to it, one all-reduce) and a weighted k-means++ recluster run alike on
     every rank.  About 2 collectives per round plus 3 -- against 2 per centre for exact
     k-means++ -- and the candidates do not depend on the sharding (up to the f64 association
-    of psi)."""
+    of psi).  Data with fewer than K distinct candidates (tiny or duplicated rows) falls back
+    to k-means++ with the caller's ``n_local_trials`` and ``sampling``."""
     rng = np.random.default_rng(seed)
     first = int(rng.integers(0, n_global))
     C = gather_rows(X, D, np.array([first]), start, comm)
@@ -510,7 +544,7 @@ def init_kmeans_parallel(X: torch.Tensor, D: int, K: int, n_global: int, start: 
     if M <= K:
         # (tiny data: every candidate is a centre; the rest by exact k-means++)
         if M < K:
-            return init_kmeanspp(X, D, K, n_global, start, comm, seed)
+            return init_kmeanspp(X, D, K, n_global, start, comm, seed, n_local_trials or 1, sampling=sampling)
         return C
     # candidate weights: rows nearest to each candidate (integer counts, exact in f64)
     if n:

@@ -117,6 +117,9 @@ class ElasticRoomReplica(RoomReplica):
         self.left = False
         self._user = user
         self._joins_seen = 0
+        # join slots counted (join/n) but not written yet -- a newcomer slow or dead between its
+        # add and its set: re-checked every round instead of blocking rank 0 on a get
+        self._join_holes: list[int] = []
 
     # ------------------------------------------------------------ lifecycle
     @classmethod
@@ -137,15 +140,11 @@ class ElasticRoomReplica(RoomReplica):
         rep = cls(store, member, **kw)
         i = store.add(_PREFIX + "join/n", 1) - 1
         store.set(_PREFIX + f"join/{i}", member)
-        # find the epoch that admits us: epochs are written in order, so poll forward
-        e = 1
-        while True:
-            key = _PREFIX + f"epoch/{e}"
-            store.wait([key], rep.timeout)
-            members = json.loads(store.get(key).decode())
-            if member in members:
-                break
-            e += 1
+        # the admitting round names its epoch under this join's own slot (a member id that
+        # left and rejoins must not take an old epoch that listed it)
+        store.wait([_PREFIX + f"admit/{i}"], rep.timeout)
+        e = int(store.get(_PREFIX + f"admit/{i}").decode())
+        members = json.loads(store.get(_PREFIX + f"epoch/{e}").decode())
         rep._form(e, members)
         rep._receive_state()
         return rep
@@ -181,7 +180,7 @@ class ElasticRoomReplica(RoomReplica):
         """The epoch's rank 0 sends room code, round and export JSON to every member."""
         if self.comm.rank == 0:
             blob = json.dumps({"room": self.room.room, "round": self.round, "joins_seen": self._joins_seen,
-                               "state": self.room.export_json()}).encode()
+                               "join_holes": self._join_holes, "state": self.room.export_json()}).encode()
         else:
             blob = None
         return json.loads(self.comm.broadcast_bytes(blob, 0).decode())
@@ -190,16 +189,28 @@ class ElasticRoomReplica(RoomReplica):
         init = self._full_state()
         self._set_room(init["state"], init["room"], init["round"])
         self._joins_seen = init["joins_seen"]
+        self._join_holes = list(init.get("join_holes", []))
 
     def _pending_change(self) -> dict | None:
         """(epoch rank 0) the next epoch's member list, if anyone asked to join or leave."""
         n = self.store.add(_PREFIX + "join/n", 0)
-        joins = [self.store.get(_PREFIX + f"join/{i}").decode() for i in range(self._joins_seen, n)]
+        joins, holes, slots = [], [], []
+        for i in [*self._join_holes, *range(self._joins_seen, n)]:
+            key = _PREFIX + f"join/{i}"
+            if self.store.check([key]):
+                joins.append(self.store.get(key).decode())
+                slots.append(i)
+            else:
+                holes.append(i)
         leaves = [m for m in self.members if self.store.check([_PREFIX + f"leave/{m}"])]
         if not joins and not leaves:
+            if holes != self._join_holes or n != self._joins_seen:
+                # (only new holes: nobody to admit yet; remember them through the next round)
+                return {"epoch": None, "members": None, "joins_seen": n, "join_holes": holes}
             return None
         members = [m for m in self.members if m not in leaves] + [m for m in joins if m not in self.members]
-        return {"epoch": self.epoch + 1, "members": members, "joins_seen": n}
+        return {"epoch": self.epoch + 1, "members": members, "joins_seen": n, "join_holes": holes,
+                "leaves": leaves, "admit": slots}
 
     # ---------------------------------------------------------- replication
     def sync(self) -> list[dict]:
@@ -221,8 +232,18 @@ class ElasticRoomReplica(RoomReplica):
         change = parts[0]["change"]
         if change is not None:
             self._joins_seen = change["joins_seen"]
+            self._join_holes = list(change.get("join_holes", []))
+            if change["epoch"] is None:   # bookkeeping only (unwritten join slots), same members
+                return applied
             if self.comm.rank == 0:       # publish before anyone forms the new group
                 self.store.set(_PREFIX + f"epoch/{change['epoch']}", json.dumps(change["members"]))
+                for i in change.get("admit", []):
+                    self.store.set(_PREFIX + f"admit/{i}", str(change["epoch"]))
+                for m in change.get("leaves", []):   # applied: a member id may rejoin later
+                    try:
+                        self.store.delete_key(_PREFIX + f"leave/{m}")
+                    except Exception:  # noqa: BLE001 -- a store without deletes keeps the notice
+                        pass
             self.comm.close()
             if self.member not in change["members"]:
                 self.left = True          # the reference's peerclose, seen from this side

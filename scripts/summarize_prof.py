@@ -11,13 +11,13 @@ import sys
 from collections import defaultdict
 
 
-def kernel_stats(d):
+def kernel_stats(d, limit=20):
     fs = sorted(glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True), key=os.path.getmtime)
     if not fs:
         return None
     rows = list(csv.DictReader(open(fs[-1])))
     out = ["| kernel | calls | avg ms | total ms | % |", "|---|---:|---:|---:|---:|"]
-    for r in rows[:20]:
+    for r in rows[:limit] if limit else rows:
         out.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | "
                    f"{float(r['TotalDurationNs'])/1e6:.2f} | {float(r['Percentage']):.2f} |")
     return "\n".join(out)
@@ -49,9 +49,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--title", default="rocprofv3 summary")
+    ap.add_argument("--all", action="store_true", help="every kernel, not the top 20")
     a = ap.parse_args()
     parts = [f"# {a.title}\n"]
-    ks = kernel_stats(a.dir)
+    ks = kernel_stats(a.dir, 0 if a.all else 20)
     if ks:
         parts += ["## Kernel time (rocprofv3 --kernel-trace --stats)\n", ks, ""]
     pm = pmc(a.dir)

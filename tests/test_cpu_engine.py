@@ -299,3 +299,30 @@ def test_kmeans_parallel_init_quality_and_weights():
     a = kpar_uniform(100, 50, 9, 2)
     b = kpar_uniform(0, 200, 9, 2)[100:150]
     assert np.array_equal(a, b) and ((a >= 0) & (a < 1)).all()
+
+
+def test_kmeans_parallel_too_few_candidates_keeps_caller_options(monkeypatch):
+    """ Data with fewer distinct rows than K: k-means|| collects fewer than K
+    candidates and falls back to k-means++ -- with the caller's n_local_trials and sampling,
+    not the defaults -- and still returns K data rows."""
+    from mikmeans.models import init as I
+    from mikmeans.parallel import Comm
+
+    # 2 distinct rows (small integers: duplicates sit at d2 = 0 exactly): the first pick is
+    # row 0, round 1 adds row 9, and psi = 0 ends the rounds with 2 < K candidates
+    base = torch.tensor([[1.0, 2.0, 3.0, 4.0], [5.0, 6.0, 7.0, 9.0]])
+    X = base[torch.tensor([0] * 9 + [1])]
+    seen = {}
+    real = I.init_kmeanspp
+
+    def spy(*a, **kw):
+        seen["trials"] = a[7] if len(a) > 7 else kw.get("n_local_trials")
+        seen["sampling"] = kw.get("sampling")
+        return real(*a, **kw)
+
+    monkeypatch.setattr(I, "init_kmeanspp", spy)
+    assert int(np.random.default_rng(1).integers(0, 10)) < 9          # (seed 1: the first pick is row 0)
+    C = I.resolve_init("k-means||", X, 4, 3, 10, 0, Comm.local(), 1, n_local_trials=4, sampling="two-stage")
+    assert seen == {"trials": 4, "sampling": "two-stage"}
+    assert C.shape == (3, 4)
+    assert bool((C[:, None, :] == X[None]).all(-1).any(1).all())

@@ -114,3 +114,60 @@ def test_cli_session_found_and_join(tmp_path):
     assert "Mango" in titles and "Lime" in titles
     last_b = json.loads(out_b.strip().splitlines()[-1])
     assert last_b["round"] == 40 and last_b["peers"] == 1 and sorted(last_b["roster"]) == ["Ann", "Bob"]
+
+
+def _rejoiner(port, member, rounds):
+    """A member that joins, leaves, then joins again under the same id."""
+    from mikmeans.parallel.elastic import ElasticRoomReplica
+
+    store = _store(port)
+    for visit in range(2):
+        rep = ElasticRoomReplica.join(store, member, user=member, seed=3)
+        store.set(f"visit/{member}/{visit}", json.dumps({"epoch": rep.epoch, "round": rep.round}))
+        rep.add_card(f"{member}-visit{visit}", ["Tart"])
+        for _ in range(rounds):
+            rep.sync()
+            time.sleep(0.05)
+        rep.leave()
+        while not rep.left:
+            rep.sync()
+    store.set(f"done/{member}", "1")
+
+
+def _host(port, rounds):
+    from mikmeans.parallel.elastic import _PREFIX, ElasticRoomReplica
+
+    store = _store(port)
+    rep = ElasticRoomReplica.found(store, "A", "ROOM2", user="A", seed=3)
+    # a join slot counted but never written (a newcomer that died between its add and its set)
+    store.add(_PREFIX + "join/n", 1)
+    while not store.check(["done/R"]) and rep.round < rounds:
+        rep.sync()
+        time.sleep(0.05)
+    store.set("done/A", json.dumps({"round": rep.round, "cards": [c["title"] for c in rep.room.cards],
+                                    "holes": rep._join_holes}))
+
+
+@pytest.mark.timeout(240)
+def test_member_rejoins_and_dead_join_slot_does_not_block():
+    """ A member id that left can join again: its leave notice was deleted once
+    applied and it is admitted through its own join slot, not an old epoch that listed it.  A
+    join slot counted but never written does not block the session: it stays a hole that is
+    re-checked each round."""
+    port = free_port()
+    store = _store(port, master=True)
+    ctx = mp.get_context("spawn")
+    host = ctx.Process(target=_host, args=(port, 400))
+    host.start()
+    time.sleep(0.5)
+    r = ctx.Process(target=_rejoiner, args=(port, "R", 4))
+    r.start()
+    for p in (r, host):
+        p.join(200)
+    assert host.exitcode == 0 and r.exitcode == 0, (host.exitcode, r.exitcode)
+    v0 = json.loads(store.get("visit/R/0").decode())
+    v1 = json.loads(store.get("visit/R/1").decode())
+    assert v1["epoch"] > v0["epoch"] + 1 and v1["round"] > v0["round"]
+    done = json.loads(store.get("done/A").decode())
+    assert "R-visit0" in done["cards"] and "R-visit1" in done["cards"]
+    assert done["holes"] == [0]

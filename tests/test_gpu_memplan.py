@@ -204,3 +204,28 @@ def test_fit_peak_memory_within_plan_other_engines(native, monkeypatch, mode):
     assert plan["mode"] == mode
     assert 0.9 * plan["peak"] <= peak <= 1.1 * plan["peak"], (peak, plan["peak"], plan["persistent"],
                                                               plan["transient"])
+
+
+def test_minibatch_fit_frees_its_shard_copy_and_refits_within_plan(native):
+    """ A mini-batch fit keeps no reference to its device copy of the shard, row
+    list or batch buffer once it returns -- only their sizes, for device_buffers() -- so the
+    allocation drops back to the engine and the labels, and a second fit of the same model
+    peaks within its plan instead of holding two shard copies."""
+    n, D, K, b = 2_000_000, 64, 64, 262_144
+    X = B.make_blobs(n, D, K, seed=4, dtype=torch.float32, device="cpu")
+    kw = dict(batch_size=b, max_steps=4, init="random", seed=2, dtype="bfloat16", device=DEV)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    base = torch.cuda.memory_allocated()
+    km = mikmeans.MiniBatchKMeans(K, **kw).fit(X)
+    torch.cuda.synchronize()
+    held = torch.cuda.memory_allocated() - base
+    shard = n * D * 2
+    assert held < shard // 4, (held, shard)                 # the shard copy is gone
+    assert km.device_buffers()["X"] >= shard                 # ... but still accounted for
+    torch.cuda.reset_peak_memory_stats()
+    again = torch.cuda.memory_allocated()
+    km.fit(X)
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - again
+    assert peak <= 1.1 * km.memory_plan_["peak"], (peak, km.memory_plan_["peak"])
