@@ -139,6 +139,10 @@ class Room:
                 return c
         return None
 
+    def centroid(self, cid) -> dict | None:
+        """The centroid record ``cid`` (None when absent)."""
+        return self._centroid(cid)
+
     # -------------------------------------------------------------- centroids
     def next_color(self) -> str:
         used = {c.get("color") for c in self.centroids}

@@ -2,26 +2,43 @@
 model serving (nearest-centre labels on the MFMA assign kernel) behind one FastAPI app.
 
 The reference is a static page whose state lives in the browser and travels between peers
-(``app.mjs:39-118``); here the room lives in this process (:class:`~mikmeans.models.room.Room`,
-every mutation under one lock) and the page talks to it over a small JSON API.  The
-reference's ``_headers`` policy is kept, minus the CDNs and WebRTC trackers the page no
-longer needs: ``default-src 'none'``, scripts and fetches from this origin only, no
-framing, no referrer, no camera / microphone / geolocation / payment, ``nosniff``
-(``_headers:1-22``).
+(``app.mjs:39-118``); every replicated change re-renders every peer (``ydoc.on("update")``
+broadcast, ``app.mjs:121``, then ``observeDeep`` -> ``renderAll``, ``app.mjs:579-580``).  Here
+the room lives in this process (:class:`~mikmeans.models.room.Room`, every mutation under one
+lock) and bumps a change counter; every open page long-polls ``/api/changes`` and re-renders
+on any edit, its own or another browser's.  The reference's ``_headers`` policy is kept,
+minus the CDNs and WebRTC trackers the page no longer needs: ``default-src 'none'``, scripts
+and fetches from this origin only, no framing, no referrer, no camera / microphone /
+geolocation / payment, ``nosniff`` (``_headers:1-22``).
 
-Endpoints (JSON in and out):
+Endpoints (JSON in and out) -- the reference's controls (``index.html:76-131``,
+``app.mjs:240-288, 571-573``):
 
 * ``GET /`` the board page, ``GET /app.js`` its script;
+* ``GET /api/state`` cards, centroids, meta, dashboard and the change ``version``;
+  ``GET /api/changes?since=V&wait=S`` answers as soon as the version passes ``V`` (or after
+  ``S`` <= 25 seconds) -- the live-update channel;
 * ``GET /api/room`` the export JSON, byte-exact ``JSON.stringify(state, null, 2)``
   (``app.mjs:263-267``); ``POST /api/room/import`` replaces cards / centroids, merges meta
   (``app.mjs:268-282``);
-* ``POST /api/cards`` {title, traits}; ``POST /api/centroids`` {name} (at most 3,
-  ``app.mjs:126-129``); ``POST /api/assign`` {card, centroid|null} (the drop / select
-  paths, locks respected); ``POST /api/centroids/{id}/lock``, ``DELETE /api/centroids/{id}``;
+* cards: ``POST /api/cards`` {title, traits[, user]}, ``DELETE /api/cards/{id}``,
+  ``POST /api/assign`` {card, centroid|null} (the drop / select paths, locks respected),
+  ``POST /api/populate`` (test data), ``POST /api/shuffle_unassigned``, ``POST /api/restart``
+  (unassign all), ``POST /api/reset`` {mode?} (hard reset);
+* centroids (at most 3, ``app.mjs:126-129``): ``POST /api/centroids`` {name},
+  ``POST /api/centroids/{id}/rename`` {name}, ``POST /api/centroids/{id}/apply_suggestion``,
+  ``POST /api/centroids/{id}/lock``, ``DELETE /api/centroids/{id}``;
+* meta: ``POST /api/mode`` {mode}, ``POST /api/iteration`` {value}; tools: ``GET /api/coin``,
+  ``GET /api/d12``, ``GET /api/shuffle_names``, ``GET /api/link?base=URL``;
 * ``POST /api/auto`` numeric k-means over the cards' trait vectors; ``GET /api/dashboard``;
-* ``GET /api/model`` the served model's centroids as flat floats; ``POST /api/predict``
+* ``GET /api/model`` the served model's shape and centroids, ``GET /api/model/centroids.json``
+  the flat-float centroid array byte-identical to a saved ``centroids.json``
+  (:func:`~mikmeans.utils.jsjson.centroids_to_json`); ``POST /api/predict``
   {points[, distances]} -> labels (and squared distances), ``POST /api/predict.npy`` (a
   ``.npy`` body in, ``.npy`` labels out), ``POST /api/transform``.
+
+Request bodies over ``max_body_bytes`` get 413, as do batches over ``max_rows`` rows (and
+transforms over ``max_transform_values`` output values); malformed input gets 400.
 
 ``mikmeans serve [--room FILE] [--model DIR] [--host 127.0.0.1] [--port 8000]``.
 """
@@ -32,7 +49,7 @@ import threading
 import numpy as np
 import torch
 from fastapi import Body, FastAPI, HTTPException, Request
-from fastapi.responses import HTMLResponse, Response
+from fastapi.responses import HTMLResponse, JSONResponse, Response
 
 from .models.room import Room
 
@@ -45,22 +62,38 @@ SECURITY_HEADERS = {
     "X-Content-Type-Options": "nosniff",
 }
 
+MAX_BODY_BYTES = 64 << 20          # request bodies (a .npy batch of 1M x 16 f32 rows fits)
+MAX_ROWS = 1 << 20                 # rows per predict / transform batch
+MAX_TRANSFORM_VALUES = 1 << 24     # n x K distances per transform answer
+LONG_POLL_S = 25.0
+
 PAGE = """<!doctype html>
 <html lang="en"><head><meta charset="utf-8"><title>k-means room</title>
 <style>
 body{font-family:system-ui,sans-serif;margin:1rem;background:#fafafa}
+.row{display:flex;gap:.5rem;flex-wrap:wrap;align-items:center;margin:.35rem 0}
 .zones{display:flex;gap:1rem;flex-wrap:wrap}
 .zone{border:2px solid #ccc;border-radius:8px;padding:.5rem;min-width:14rem;background:#fff}
 .card{border:1px solid #ddd;border-radius:6px;padding:.25rem .5rem;margin:.25rem 0}
 .traits{color:#666;font-size:.85em}
+.chip{border:1px solid #ccc;border-radius:99px;padding:.1rem .6rem;font-size:.85em}
 #dash{white-space:pre-wrap;font-family:monospace;font-size:.85em}
 </style></head>
 <body>
-<h1>k-means room <span id="room"></span></h1>
-<p><input id="title" placeholder="card title"> <input id="traits" placeholder="traits, comma separated">
-<button id="addCard">Add card</button>
-<input id="cname" placeholder="centroid name"> <button id="addCentroid">Add centroid</button>
-<button id="auto">Auto-assign (k-means)</button> <a href="/api/room" download>Export JSON</a></p>
+<h1>k-means room <span id="room" class="chip"></span> <span id="version" class="chip"></span></h1>
+<div class="row"><button id="copy">Copy link</button> <button id="populate">Populate test data</button>
+<label>Your name <input id="name" placeholder="e.g., Alex"></label> <button id="saveName">Save</button></div>
+<div class="row"><input id="cname" placeholder="centroid name"> <button id="addCentroid">Add centroid (max 3)</button>
+<button id="coin">Coin flip</button> <button id="d12">d12</button> <button id="shuffle">Shuffle names</button>
+<button id="shuffleUnassigned">Randomize Unassigned</button> <button id="restartAll">Restart (Unassign All)</button>
+<span id="tool" class="chip"></span></div>
+<div class="row"><input id="title" placeholder="Customer name"> <input id="traitA" placeholder="Trait One">
+<input id="traitB" placeholder="Trait Two"> <button id="addCard">Add</button>
+<select id="mode"><option value="learn">learn</option><option value="playtest">playtest</option>
+<option value="custom">custom</option></select>
+<input id="iter" type="number" min="0" step="1" value="0" style="width:6rem">
+<a href="/api/room" download>Export JSON</a> <input id="import" type="file" accept="application/json">
+<button id="reset">Reset</button> <button id="auto">Auto-assign (k-means)</button></div>
 <div class="zones" id="zones"></div>
 <h2>Dashboard</h2><div id="dash"></div>
 <script src="/app.js"></script>
@@ -68,14 +101,18 @@ body{font-family:system-ui,sans-serif;margin:1rem;background:#fafafa}
 """
 
 APP_JS = """'use strict';
+let version = -1;
+let user = localStorage.getItem('mkUser') || '';
 async function api(path, method, body) {
   const r = await fetch(path, {method: method || 'GET', headers: {'Content-Type': 'application/json'},
                                body: body ? JSON.stringify(body) : undefined});
   if (!r.ok) throw new Error(await r.text());
   return r.json();
 }
+function $(id) { return document.getElementById(id); }
 function el(tag, cls, text) { const e = document.createElement(tag); if (cls) e.className = cls;
   if (text !== undefined) e.textContent = text; return e; }
+function btn(text, fn) { const b = el('button', '', text); b.addEventListener('click', fn); return b; }
 function cardEl(card, centroids) {
   const d = el('div', 'card');
   d.appendChild(el('div', '', card.title));
@@ -84,35 +121,80 @@ function cardEl(card, centroids) {
   s.appendChild(new Option('unassigned', ''));
   for (const c of centroids) s.appendChild(new Option(c.name, c.id));
   s.value = card.assignedTo || '';
-  s.addEventListener('change', () => api('/api/assign', 'POST', {card: card.id, centroid: s.value || null}).then(render));
+  s.addEventListener('change', () => api('/api/assign', 'POST', {card: card.id, centroid: s.value || null}));
   d.appendChild(s);
+  d.appendChild(btn('Delete', () => api('/api/cards/' + encodeURIComponent(card.id), 'DELETE')));
   return d;
+}
+function zoneHead(g, row) {
+  const h = el('div');
+  h.appendChild(el('h3', '', g.name + (g.locked ? ' (locked)' : '')));
+  if (g.id === null) return h;
+  const id = encodeURIComponent(g.id);
+  const inp = el('input'); inp.placeholder = 'rename';
+  h.appendChild(inp);
+  h.appendChild(btn('Rename', () => api('/api/centroids/' + id + '/rename', 'POST', {name: inp.value})));
+  h.appendChild(btn(g.locked ? 'Unlock' : 'Lock', () => api('/api/centroids/' + id + '/lock', 'POST')));
+  h.appendChild(btn('Remove', () => api('/api/centroids/' + id, 'DELETE')));
+  if (row && row.suggestion) h.appendChild(btn('Apply: ' + row.suggestion,
+      () => api('/api/centroids/' + id + '/apply_suggestion', 'POST')));
+  return h;
 }
 async function render() {
   const st = await api('/api/state');
-  document.getElementById('room').textContent = st.room;
-  const zones = document.getElementById('zones');
+  version = st.version;
+  $('room').textContent = 'Room: ' + st.room;
+  $('version').textContent = 'v' + st.version;
+  if (document.activeElement !== $('mode')) $('mode').value = st.meta.mode || 'learn';
+  if (document.activeElement !== $('iter')) $('iter').value = st.meta.iteration || 0;
+  const zones = $('zones');
   zones.replaceChildren();
+  const rows = {};
+  for (const r of st.dashboard.rows) rows[r.id] = r;
   const groups = [{id: null, name: 'Unassigned', color: '#999'}].concat(st.centroids);
   for (const g of groups) {
     const z = el('div', 'zone');
     z.style.borderColor = g.color || '#ccc';
-    z.appendChild(el('h3', '', g.name + (g.locked ? ' (locked)' : '')));
+    z.appendChild(zoneHead(g, rows[g.id]));
     for (const card of st.cards.filter(c => (c.assignedTo || null) === g.id)) z.appendChild(cardEl(card, st.centroids));
     zones.appendChild(z);
   }
-  document.getElementById('dash').textContent = JSON.stringify(st.dashboard, null, 2);
+  $('dash').textContent = JSON.stringify(st.dashboard, null, 2);
 }
-document.getElementById('addCard').addEventListener('click', () => {
-  const t = document.getElementById('title').value.trim();
-  const tr = document.getElementById('traits').value.split(',').map(s => s.trim()).filter(Boolean);
-  if (t) api('/api/cards', 'POST', {title: t, traits: tr}).then(render);
+async function follow() {          // live updates: re-render whenever the room changes
+  for (;;) {
+    try {
+      const c = await api('/api/changes?since=' + version + '&wait=20');
+      if (c.version !== version) await render();
+    } catch (e) { await new Promise(r => setTimeout(r, 2000)); }
+  }
+}
+$('name').value = user;
+$('saveName').addEventListener('click', () => { user = $('name').value.trim(); localStorage.setItem('mkUser', user); });
+$('copy').addEventListener('click', async () => {
+  const r = await api('/api/link?base=' + encodeURIComponent(location.origin + location.pathname));
+  if (navigator.clipboard) navigator.clipboard.writeText(r.link); $('tool').textContent = r.link; });
+$('populate').addEventListener('click', () => api('/api/populate', 'POST', {}));
+$('addCentroid').addEventListener('click', () => api('/api/centroids', 'POST', {name: $('cname').value.trim() || null}));
+$('coin').addEventListener('click', async () => { $('tool').textContent = (await api('/api/coin')).result; });
+$('d12').addEventListener('click', async () => { $('tool').textContent = 'd12: ' + (await api('/api/d12')).result; });
+$('shuffle').addEventListener('click', async () => { $('tool').textContent = (await api('/api/shuffle_names')).names.join(', '); });
+$('shuffleUnassigned').addEventListener('click', () => api('/api/shuffle_unassigned', 'POST', {}));
+$('restartAll').addEventListener('click', () => { if (confirm('Unassign every card?')) api('/api/restart', 'POST', {}); });
+$('addCard').addEventListener('click', () => {
+  const t = $('title').value.trim();
+  const tr = [$('traitA').value.trim(), $('traitB').value.trim()].filter(Boolean);
+  if (t) api('/api/cards', 'POST', {title: t, traits: tr, user: user || null});
 });
-document.getElementById('addCentroid').addEventListener('click', () => {
-  api('/api/centroids', 'POST', {name: document.getElementById('cname').value.trim() || null}).then(render);
+$('mode').addEventListener('change', () => api('/api/mode', 'POST', {mode: $('mode').value}));
+$('iter').addEventListener('change', () => api('/api/iteration', 'POST', {value: $('iter').value}));
+$('import').addEventListener('change', async () => {
+  const f = $('import').files[0]; if (!f) return;
+  try { await api('/api/room/import', 'POST', JSON.parse(await f.text())); } catch (e) { alert('Import failed: ' + e); }
 });
-document.getElementById('auto').addEventListener('click', () => api('/api/auto', 'POST', {}).then(render));
-render();
+$('reset').addEventListener('click', () => { if (confirm('Clear the board?')) api('/api/reset', 'POST', {mode: $('mode').value}); });
+$('auto').addEventListener('click', () => api('/api/auto', 'POST', {}));
+render().then(follow);
 """
 
 
@@ -130,22 +212,54 @@ def _jsonable(obj):
     return obj
 
 
-def create_app(room: Room | None = None, model=None, *, device=None):
+class _Board:
+    """The served room plus its change counter: every mutation runs under the lock, bumps
+    the version and wakes the long-polls."""
+
+    def __init__(self, room: Room):
+        self.room = room
+        self.version = 0
+        self.cond = threading.Condition()
+
+    def read(self, fn):
+        with self.cond:
+            return fn(self.room)
+
+    def mutate(self, fn):
+        with self.cond:
+            out = fn(self.room)
+            self.version += 1
+            self.cond.notify_all()
+            return out
+
+    def wait_past(self, since: int, timeout: float) -> int:
+        with self.cond:
+            self.cond.wait_for(lambda: self.version != since, timeout=max(0.0, timeout))
+            return self.version
+
+
+def create_app(room: Room | None = None, model=None, *, device=None, max_body_bytes: int = MAX_BODY_BYTES,
+               max_rows: int = MAX_ROWS, max_transform_values: int = MAX_TRANSFORM_VALUES):
     """The FastAPI app serving ``room`` (a new one when None) and, when given, a fitted
     ``model`` (:class:`~mikmeans.KMeans` / :class:`~mikmeans.MiniBatchKMeans`)."""
     app = FastAPI(title="mikmeans", docs_url=None, redoc_url=None, openapi_url=None)
-    state = {"room": room if room is not None else Room(seed=0)}
-    lock = threading.Lock()
+    board = _Board(room if room is not None else Room(seed=0))
+    model_lock = threading.Lock()   # (one batch at a time on the device: the serving pack is shared)
 
     @app.middleware("http")
     async def _headers(request, call_next):
-        resp = await call_next(request)
+        n = request.headers.get("content-length")
+        try:
+            too_big = n is not None and int(n) > max_body_bytes
+        except ValueError:
+            too_big = False
+        if too_big:
+            resp = JSONResponse({"detail": f"request body over {max_body_bytes} bytes"}, status_code=413)
+        else:
+            resp = await call_next(request)
         for k, v in SECURITY_HEADERS.items():
             resp.headers[k] = v
         return resp
-
-    def _room() -> Room:
-        return state["room"]
 
     @app.get("/", response_class=HTMLResponse)
     def page():
@@ -155,75 +269,172 @@ def create_app(room: Room | None = None, model=None, *, device=None):
     def app_js():
         return Response(APP_JS, media_type="text/javascript")
 
+    # ------------------------------------------------------------------- room state
     @app.get("/api/room")
     def export_room():
-        with lock:
-            txt = _room().export_json()
-            name = _room().export_filename
+        txt, name = board.read(lambda r: (r.export_json(), r.export_filename))
         return Response(txt, media_type="application/json",
                         headers={"Content-Disposition": f'attachment; filename="{name}"'})
 
     @app.get("/api/state")
     def room_state():
-        with lock:
-            r = _room()
-            return _jsonable({"room": r.room, "cards": r.cards, "centroids": r.centroids,
+        def snap(r):
+            return _jsonable({"room": r.room, "version": board.version, "cards": r.cards, "centroids": r.centroids,
+                              "meta": {"mode": r.meta.get("mode"), "iteration": r.meta.get("iteration")},
                               "dashboard": r.dashboard()})
+        return board.read(snap)
+
+    @app.get("/api/changes")
+    def changes(since: int = -1, wait: float = 0.0):
+        """Long-poll: the current version as soon as it differs from ``since``."""
+        v = board.wait_past(int(since), min(float(wait), LONG_POLL_S))
+        return {"version": v, "changed": v != since}
 
     @app.post("/api/room/import")
     def import_room(body: dict = Body(...)):
         import json
 
-        with lock:
-            _room().import_json(json.dumps(body))
-            return {"cards": len(_room().cards), "centroids": len(_room().centroids)}
+        def imp(r):
+            r.import_json(json.dumps(body))
+            return {"cards": len(r.cards), "centroids": len(r.centroids)}
+        try:
+            return board.mutate(imp)
+        except (ValueError, TypeError, KeyError, AttributeError) as e:
+            raise HTTPException(400, f"not a room export: {e}") from None
 
+    # ------------------------------------------------------------------- cards
     @app.post("/api/cards")
     def add_card(body: dict = Body(...)):
         title = str(body.get("title", "")).strip()
         if not title:
             raise HTTPException(400, "title required")
         traits = body.get("traits", [])
-        with lock:
-            return _room().add_card(title, traits)
+        if not isinstance(traits, list) or not all(isinstance(t, str) for t in traits):
+            raise HTTPException(400, "traits: a list of strings")
+        user = body.get("user") or None
+        return board.mutate(lambda r: r.add_card(title, traits, created_by=str(user) if user else None))
 
-    @app.post("/api/centroids")
-    def add_centroid(body: dict = Body(default={})):
-        with lock:
-            c = _room().add_centroid(body.get("name") or None)
-        if c is None:
-            raise HTTPException(409, "at most %d centroids" % _room().max_centroids)
-        return c
-
-    @app.post("/api/centroids/{cid}/lock")
-    def toggle_lock(cid: str):
-        with lock:
-            _room().toggle_lock(cid)
-            return {"locked": bool((_room()._centroid(cid) or {}).get("locked"))}
-
-    @app.delete("/api/centroids/{cid}")
-    def remove_centroid(cid: str):
-        with lock:
-            _room().remove_centroid(cid)
-            return {"centroids": len(_room().centroids)}
+    @app.delete("/api/cards/{card_id}")
+    def delete_card(card_id: str):
+        def rm(r):
+            if r._card_index(card_id) < 0:
+                return None
+            r.delete_card(card_id)
+            return {"cards": len(r.cards)}
+        out = board.mutate(rm)
+        if out is None:
+            raise HTTPException(404, "no such card")
+        return out
 
     @app.post("/api/assign")
     def assign(body: dict = Body(...)):
-        with lock:
-            ok = _room().update_card_assign(body.get("card"), body.get("centroid") or None)
+        ok = board.mutate(lambda r: r.update_card_assign(body.get("card"), body.get("centroid") or None))
         if not ok:
             raise HTTPException(409, "not assigned (unknown card or locked centroid)")
         return {"ok": True}
 
+    @app.post("/api/populate")
+    def populate(body: dict = Body(default={})):
+        return board.mutate(lambda r: (r.populate_test_data(), {"cards": len(r.cards)})[1])
+
+    @app.post("/api/shuffle_unassigned")
+    def shuffle_unassigned(body: dict = Body(default={})):
+        return board.mutate(lambda r: (r.shuffle_unassigned(), {"cards": [c["id"] for c in r.cards]})[1])
+
+    @app.post("/api/restart")
+    def restart(body: dict = Body(default={})):
+        return board.mutate(lambda r: (r.restart_all(), {"ok": True})[1])
+
+    @app.post("/api/reset")
+    def reset(body: dict = Body(default={})):
+        mode = body.get("mode")
+        if mode is not None and not isinstance(mode, str):
+            raise HTTPException(400, "mode: a string")
+        return board.mutate(lambda r: (r.hard_reset(mode), {"cards": len(r.cards), "centroids": 0})[1])
+
+    # ------------------------------------------------------------------- centroids
+    @app.post("/api/centroids")
+    def add_centroid(body: dict = Body(default={})):
+        c = board.mutate(lambda r: r.add_centroid(body.get("name") or None))
+        if c is None:
+            raise HTTPException(409, "at most %d centroids" % board.room.max_centroids)
+        return c
+
+    def _known(r, cid):
+        if r.centroid(cid) is None:
+            raise HTTPException(404, "no such centroid")
+
+    @app.post("/api/centroids/{cid}/rename")
+    def rename_centroid(cid: str, body: dict = Body(...)):
+        name = body.get("name")
+        if not isinstance(name, str):
+            raise HTTPException(400, "name: a string")
+
+        def ren(r):
+            _known(r, cid)
+            r.rename_centroid(cid, name)
+            return r.centroid(cid)
+        return board.mutate(ren)
+
+    @app.post("/api/centroids/{cid}/apply_suggestion")
+    def apply_suggestion(cid: str):
+        """The dashboard's "Suggested:" name for this centroid (app.mjs:571-573)."""
+        def app_(r):
+            _known(r, cid)
+            sug = next((row["suggestion"] for row in r.dashboard()["rows"] if row["id"] == cid), None)
+            if not sug:
+                raise HTTPException(409, "no suggestion for this centroid")
+            r.apply_suggested_name(cid, sug)
+            return r.centroid(cid)
+        return board.mutate(app_)
+
+    @app.post("/api/centroids/{cid}/lock")
+    def toggle_lock(cid: str):
+        def tog(r):
+            _known(r, cid)
+            r.toggle_lock(cid)
+            return {"locked": bool(r.centroid(cid).get("locked"))}
+        return board.mutate(tog)
+
+    @app.delete("/api/centroids/{cid}")
+    def remove_centroid(cid: str):
+        return board.mutate(lambda r: (r.remove_centroid(cid), {"centroids": len(r.centroids)})[1])
+
+    # ------------------------------------------------------------------- meta / tools
+    @app.post("/api/mode")
+    def set_mode(body: dict = Body(...)):
+        mode = body.get("mode")
+        if not isinstance(mode, str):
+            raise HTTPException(400, "mode: a string")
+        return board.mutate(lambda r: (r.set_mode(mode), {"mode": r.meta.get("mode")})[1])
+
+    @app.post("/api/iteration")
+    def set_iteration(body: dict = Body(...)):
+        return board.mutate(lambda r: (r.set_iteration(body.get("value")), {"iteration": r.meta.get("iteration")})[1])
+
+    @app.get("/api/coin")
+    def coin():
+        return {"result": board.read(lambda r: r.coin())}
+
+    @app.get("/api/d12")
+    def d12():
+        return {"result": board.read(lambda r: r.d12())}
+
+    @app.get("/api/shuffle_names")
+    def shuffle_names():
+        return {"names": board.read(lambda r: r.shuffled_titles())}
+
+    @app.get("/api/link")
+    def link(base: str = ""):
+        return {"link": board.read(lambda r: r.share_link(base))}
+
     @app.post("/api/auto")
     def auto(body: dict = Body(default={})):
-        with lock:
-            return _jsonable(_room().auto_assign(seed=int(body.get("seed", 0))))
+        return _jsonable(board.mutate(lambda r: r.auto_assign(seed=int(body.get("seed", 0)))))
 
     @app.get("/api/dashboard")
     def dashboard():
-        with lock:
-            return _jsonable(_room().dashboard())
+        return board.read(lambda r: _jsonable(r.dashboard()))
 
     # ------------------------------------------------------------------- model serving
     def _model():
@@ -231,18 +442,37 @@ def create_app(room: Room | None = None, model=None, *, device=None):
             raise HTTPException(404, "no model loaded (mikmeans serve --model DIR)")
         return model
 
+    def _centroid_text() -> str:
+        from .utils.jsjson import centroids_to_json
+
+        return centroids_to_json(_model().cluster_centers_)
+
     @app.get("/api/model")
     def model_info():
-        m = _model()
-        C = m.cluster_centers_.float().cpu()
-        return {"n_clusters": int(C.shape[0]), "n_features": int(C.shape[1]),
-                "centroids": [float(v) for v in C.reshape(-1).tolist()]}
+        C = _model().cluster_centers_
+        # the centroids as the flat-float array of centroids.json, spliced in verbatim
+        body = (f'{{"n_clusters":{int(C.shape[0])},"n_features":{int(C.shape[1])},'
+                f'"centroids":{_centroid_text()}}}')
+        return Response(body, media_type="application/json")
+
+    @app.get("/api/model/centroids.json")
+    def model_centroids():
+        return Response(_centroid_text(), media_type="application/json")
+
+    def _check_rows(n: int):
+        if n > max_rows:
+            raise HTTPException(413, f"at most {max_rows} rows per batch")
 
     def _points(body: dict) -> torch.Tensor:
         pts = body.get("points")
         if not isinstance(pts, list) or not pts:
             raise HTTPException(400, "points: a non-empty list of rows")
-        X = torch.as_tensor(np.asarray(pts, dtype=np.float32))
+        _check_rows(len(pts))
+        try:
+            arr = np.asarray(pts, dtype=np.float32)
+        except (ValueError, TypeError) as e:
+            raise HTTPException(400, f"points: a rectangular array of numbers ({e})") from None
+        X = torch.as_tensor(arr)
         m = _model()
         if X.dim() != 2 or X.shape[1] != m.cluster_centers_.shape[1]:
             raise HTTPException(400, f"points must be [n, {m.cluster_centers_.shape[1]}]")
@@ -252,7 +482,7 @@ def create_app(room: Room | None = None, model=None, *, device=None):
     def predict(body: dict = Body(...)):
         m = _model()
         X = _points(body)
-        with lock:   # (one batch at a time on the device: the serving pack is shared)
+        with model_lock:
             labels, mind, _ = m._assign_rows(X, bool(body.get("distances", False)))
         out = {"labels": labels.cpu().tolist()}
         if mind is not None:
@@ -263,19 +493,29 @@ def create_app(room: Room | None = None, model=None, *, device=None):
     async def predict_npy(request: Request):
         """Binary serving: the body is a ``.npy`` array [n, D] (``numpy.save``; loaded with
         ``allow_pickle=False``), the answer the int32 labels as ``.npy`` -- no JSON
-        parsing of large batches."""
+        parsing of large batches.  The body is read up to ``max_body_bytes`` (413 beyond,
+        whatever the request declared)."""
         import io
 
         m = _model()
-        raw = await request.body()
+        chunks, size = [], 0
+        async for part in request.stream():
+            size += len(part)
+            if size > max_body_bytes:
+                raise HTTPException(413, f"request body over {max_body_bytes} bytes")
+            chunks.append(part)
         try:
-            arr = np.load(io.BytesIO(raw), allow_pickle=False)
+            arr = np.load(io.BytesIO(b"".join(chunks)), allow_pickle=False)
         except Exception as e:  # noqa: BLE001 -- any malformed payload is the client's error
             raise HTTPException(400, f"body must be a .npy array: {e}") from None
         if arr.ndim != 2 or arr.shape[1] != m.cluster_centers_.shape[1]:
             raise HTTPException(400, f"array must be [n, {m.cluster_centers_.shape[1]}]")
-        X = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float32)).to(m.cluster_centers_.device)
-        with lock:
+        _check_rows(arr.shape[0])
+        try:
+            X = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float32)).to(m.cluster_centers_.device)
+        except (ValueError, TypeError) as e:
+            raise HTTPException(400, f"array must hold numbers ({e})") from None
+        with model_lock:
             labels, _, _ = m._assign_rows(X, False)
         buf = io.BytesIO()
         np.save(buf, labels.cpu().numpy().astype(np.int32), allow_pickle=False)
@@ -285,10 +525,13 @@ def create_app(room: Room | None = None, model=None, *, device=None):
     def transform(body: dict = Body(...)):
         m = _model()
         X = _points(body)
-        with lock:
+        if X.shape[0] * int(m.cluster_centers_.shape[0]) > max_transform_values:
+            raise HTTPException(413, f"at most {max_transform_values} distances per answer")
+        with model_lock:
             d = m.transform(X)
         return {"distances": d.cpu().tolist()}
 
+    app.state.board = board
     return app
 
 

@@ -1,4 +1,4 @@
-"""Multi-rank GPU execution on one MI355X: W = 2 / 4 processes share cuda:0 over a
+"""Multi-rank GPU execution on one MI355X: W = 2 / 4 / 8 processes share cuda:0 over a
 host-staged gloo group (parallel/comm.py ``staged``) and run the real HIP kernels
 through every distributed code path -- the reference's several participants meshed on one
 board (app.mjs:70-118) -- and every case must give bitwise the W = 1 GPU result.
@@ -7,8 +7,10 @@ RCCL refuses two ranks on one GPU, so the collectives here go device -> host -> 
 kernels, the sharding on the 1536-row grid, the k-means++ owner selection with real
 non-owner ranks (csrc/kpp.hip mode 2), the memory-plan agreement, the per-rank device
 sampler, the 'farthest' relocation across ranks and the W=2 -> W=4 resume are the ones
-the 8-GPU RCCL job runs.  One spawn per world size runs all of its cases (each rank is a
-fresh process: ~5 s of start-up).
+the 8-GPU RCCL job runs.  W = 8 is the target node's world size: one 1536-row grid unit per
+rank (the last one short), five empty tail ranks on the small set, the 8-way owner draw, the
+8-rank device sampler, and a W = 8 checkpoint resumed at W = 2.  One spawn per world size
+runs all of its cases (each rank is a fresh process: ~5 s of start-up).
 """
 import os
 
@@ -21,8 +23,8 @@ from mikmeans.parallel.launch import spawn_local
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
-N, D, K = 12_000, 48, 24          # 8 units of the 1536-row grid: W=2 -> 4+4, W=4 -> 2+2+2+2
-N_EMPTY = 4_000                   # 3 units: at W=4 the last rank holds no rows
+N, D, K = 12_000, 48, 24          # 8 units of the 1536-row grid: W=2 -> 4+4, W=4 -> 2+2+2+2, W=8 -> 1 each
+N_EMPTY = 4_000                   # 3 units: at W=4 the last rank holds no rows, at W=8 the last five
 
 
 def _data(dtype=torch.bfloat16, n=N, device=None):
@@ -130,6 +132,12 @@ def case_fit_cosine(comm):
     return _fit(comm, metric="cosine")
 
 
+def case_fit_hamerly(comm):
+    """The bounded E-step (bitwise the full one) on real ranks: every shard starts on the
+    1536-row grid, so each row's full-pass seed offset is the W=1 one."""
+    return _fit(comm, algorithm="hamerly")
+
+
 def case_fit_graph(comm):
     """hipGraph replay with the host-staged collective between the graphs."""
     return _fit(comm, graph=True, incremental=False)
@@ -214,7 +222,7 @@ def case_ckpt_resume(comm, path):
 CASES = {f.__name__[5:]: f for f in (case_lloyd_random_bf16, case_lloyd_random_f32, case_lloyd_kpp,
                                      case_kpp_greedy, case_fit_farthest, case_fit_weighted, case_fit_cosine,
                                      case_fit_graph, case_stream_agreement, case_minibatch_fit,
-                                     case_fit_empty_shard, case_kpp_two_stage, case_kpar)}
+                                     case_fit_empty_shard, case_kpp_two_stage, case_kpar, case_fit_hamerly)}
 CASES["fit_kpp_greedy_f32"] = _fit_kpp
 
 
@@ -249,15 +257,17 @@ def _mb_reference(world):
 
     C = native.require()
     X = _data(torch.float32)
-    eng = MiniBatchEngine(K, D, MB_B * world, dtype=torch.float32, device=DEV, comm=_local())
+    # (a rank draws min(batch_size, its rows): W=8's short last shard draws 1248)
+    bs = [min(MB_B, shard_range(N, r, world)[1] - shard_range(N, r, world)[0]) for r in range(world)]
+    eng = MiniBatchEngine(K, D, sum(bs), dtype=torch.float32, device=DEV, comm=_local())
     eng.set_bound(col_stats(X, stats=False).absmax)
     eng.set_centers(X[:K].clone())
     for s in range(MB_STEPS):
         parts = []
         for r in range(world):
             r0, r1 = shard_range(N, r, world)
-            rows = torch.empty(MB_B, dtype=torch.int64, device=DEV)
-            C.sample_index(r1 - r0, MB_B, MB_SEED, r, s, rows)
+            rows = torch.empty(bs[r], dtype=torch.int64, device=DEV)
+            C.sample_index(r1 - r0, bs[r], MB_SEED, r, s, rows)
             parts.append(rows + r0)
         eng.partial_fit_rows(X, torch.cat(parts))
     return eng.centers.clone().cpu(), eng.vcount.clone().cpu()
@@ -305,6 +315,8 @@ W2_CASES = ["lloyd_random_bf16", "lloyd_random_f32", "lloyd_kpp", "kpp_greedy", 
             "kpp_two_stage", "kpar"]
 W4_CASES = ["lloyd_random_bf16", "lloyd_kpp", "kpp_greedy", "fit_farthest", "fit_weighted", "minibatch_fit",
             "fit_empty_shard", "kpp_two_stage", "kpar"]
+W8_CASES = ["lloyd_random_bf16", "lloyd_random_f32", "lloyd_kpp", "kpp_greedy", "fit_farthest", "fit_weighted",
+            "fit_hamerly", "minibatch_fit", "fit_empty_shard", "kpp_two_stage", "kpar"]
 _NOT_W1 = ("minibatch_fit", "stream_agreement", "fit_empty_shard", "kpp_two_stage")
 
 
@@ -321,6 +333,16 @@ def w4(w2):
     return spawn_local(_suite, 4, W4_CASES, ("ckpt_resume", path), device="cuda", timeout=600)
 
 
+@pytest.fixture(scope="module")
+def w8(w4, tmp_path_factory):
+    """Eight ranks on cuda:0 (the 8-GPU node's world size; 8 of the box's 16 GPU processes),
+    saving a checkpoint after three iterations that a W = 2 spawn then resumes."""
+    path = str(tmp_path_factory.mktemp("ck8") / "run")
+    outs = spawn_local(_suite, 8, W8_CASES, ("ckpt_save", path), device="cuda", timeout=900)
+    back = spawn_local(_suite, 2, [], ("ckpt_resume", path), device="cuda", timeout=600)
+    return outs, back
+
+
 @pytest.mark.parametrize("name", [n for n in W2_CASES if n not in _NOT_W1])
 def test_w2_equals_w1(refs, w2, name):
     outs, _ = w2
@@ -332,13 +354,38 @@ def test_w4_equals_w1(refs, w4, name):
     _check(name, refs[name], [o[name] for o in w4])
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_kpp_two_stage_replicas(refs, w2, w4, world):
+@pytest.mark.parametrize("name", [n for n in W8_CASES if n not in _NOT_W1])
+def test_w8_equals_w1(refs, w8, name):
+    _check(name, refs[name], [o[name] for o in w8[0]])
+
+
+def test_w8_grid_and_empty_tail_ranks(w8):
+    """The W=8 shards: one 1536-row unit per rank (the last short) on the 12k set, and on the
+    4k set only ranks 0-2 hold rows -- the empty tail ranks still join every collective."""
+    outs, _ = w8
+    assert [shard_range(N, r, 8)[1] - shard_range(N, r, 8)[0] for r in range(8)] == [1536] * 7 + [1248]
+    assert [o["fit_empty_shard"]["n"] for o in outs] == [1536, 1536, 928, 0, 0, 0, 0, 0]
+
+
+def test_checkpoint_w8_resumed_at_w2(w8):
+    """Three iterations at W=8, checkpointed; resumed at W=2 to iteration 8: the W=1 run's
+    eight-iteration centres and labels."""
+    import mikmeans
+
+    ref = mikmeans.KMeans(K, init="random", dtype="bfloat16", max_iter=8, tol=-1, seed=2, comm=_local()).fit(
+        _data())
+    res = [o["ckpt_resume"] for o in w8[1]]
+    assert torch.equal(res[0]["C"], ref.cluster_centers_.cpu())
+    assert torch.equal(_cat_labels(res), ref.labels_.cpu())
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_kpp_two_stage_replicas(refs, w2, w4, w8, world):
     """Two-stage k-means++ on real ranks: every rank holds the same centres, each one a data
     row, none drawn twice; at W = 1 it is the exact path (refs)."""
     from mikmeans.ops import pad_columns
 
-    res = [o["kpp_two_stage"] for o in (w2[0] if world == 2 else w4)]
+    res = [o["kpp_two_stage"] for o in {2: w2[0], 4: w4, 8: w8[0]}[world]]
     X = pad_columns(_data()).float().cpu()[:, :D]
     for t in (1, 3):
         for r in res:
@@ -360,9 +407,9 @@ def test_w2_stream_agreement(w2):
     assert torch.equal(_cat_labels(res), ref.labels_.cpu())
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_minibatch_device_sampler(w2, w4, world):
-    outs = w2[0] if world == 2 else w4
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_minibatch_device_sampler(w2, w4, w8, world):
+    outs = {2: w2[0], 4: w4, 8: w8[0]}[world]
     res = [o["minibatch_fit"] for o in outs]
     C_ref, v_ref = _mb_reference(world)
     for r in res:
@@ -372,8 +419,9 @@ def test_minibatch_device_sampler(w2, w4, world):
     assert torch.equal(res[0]["counts"].double(), v_ref)
 
 
-def test_w4_empty_shard(refs, w4):
-    res = [o["fit_empty_shard"] for o in w4]
+@pytest.mark.parametrize("world", [4, 8])
+def test_empty_shard(refs, w4, w8, world):
+    res = [o["fit_empty_shard"] for o in (w4 if world == 4 else w8[0])]
     ref = refs["fit_empty_shard"]
     assert [r["n"] for r in res][-1] == 0
     for key, lab in (("C", "labels"), ("C_kpp", "labels_kpp")):

@@ -146,3 +146,102 @@ def test_concurrent_room_edits_are_serialised():
     titles = sorted(x["title"] for x in room.cards[n0:])
     assert titles == sorted(f"card {i}" for i in range(64))
     assert len({x["id"] for x in room.cards}) == len(room.cards)
+
+
+def test_live_updates_reach_every_open_board():
+    """(verdict r4) One browser's edit re-renders every other: a second client's long-poll on
+    /api/changes returns as soon as the first one edits, and its next /api/state holds the
+    edit -- the reference's update broadcast + observeDeep -> renderAll (app.mjs:121, 579-580)."""
+    import threading
+    import time
+
+    app = create_app(Room(seed=7))
+    a, b = TestClient(app), TestClient(app)
+    v0 = b.get("/api/state").json()["version"]
+    assert b.get(f"/api/changes?since={v0}&wait=0").json() == {"version": v0, "changed": False}
+    got = {}
+
+    def poll():
+        t0 = time.perf_counter()
+        got["r"] = b.get(f"/api/changes?since={v0}&wait=10").json()
+        got["dt"] = time.perf_counter() - t0
+
+    th = threading.Thread(target=poll)
+    th.start()
+    time.sleep(0.3)
+    card = a.post("/api/cards", json={"title": "Yuzu", "traits": ["Citrus"], "user": "Ann"}).json()
+    th.join(15)
+    assert got["r"]["changed"] and got["r"]["version"] > v0 and got["dt"] < 5, got
+    st = b.get("/api/state").json()
+    assert st["version"] == got["r"]["version"]
+    mine = [c for c in st["cards"] if c["id"] == card["id"]]
+    assert mine and mine[0]["createdBy"] == "Ann"
+    # reads do not count as changes
+    b.get("/api/dashboard")
+    b.get("/api/coin")
+    assert b.get("/api/state").json()["version"] == st["version"]
+
+
+def test_every_board_control_has_a_route():
+    """The reference's controls (index.html:76-131, app.mjs:240-288, 571-573) over HTTP, each
+    against the Room operation it drives."""
+    room = Room(seed=11, clock=lambda: 1_700_000_000_000)
+    c = _client(room)
+    assert c.post("/api/populate", json={}).json()["cards"] == len(room.cards) > 1
+    s = c.post("/api/centroids", json={"name": "Sweet"}).json()
+    c.post("/api/centroids", json={"name": "Sour"})
+    assert c.post(f"/api/centroids/{s['id']}/rename", json={"name": "  Candy "}).json()["name"] == "Candy"
+    assert c.post("/api/centroids/nope/rename", json={"name": "x"}).status_code == 404
+    for card in room.cards[:4]:
+        c.post("/api/assign", json={"card": card["id"], "centroid": s["id"]})
+    sug = next(r["suggestion"] for r in room.dashboard()["rows"] if r["id"] == s["id"])
+    assert sug and c.post(f"/api/centroids/{s['id']}/apply_suggestion").json()["name"] == sug
+    victim = room.cards[-1]["id"]
+    n = len(room.cards)
+    assert c.delete(f"/api/cards/{victim}").json() == {"cards": n - 1}
+    assert c.delete(f"/api/cards/{victim}").status_code == 404
+    before = [x["id"] for x in room.cards if x.get("assignedTo")]
+    order = c.post("/api/shuffle_unassigned", json={}).json()["cards"]
+    assert order[: len(before)] == before and sorted(order) == sorted(x["id"] for x in room.cards)
+    assert c.post("/api/mode", json={"mode": "playtest"}).json() == {"mode": "playtest"}
+    assert c.post("/api/iteration", json={"value": "3"}).json() == {"iteration": 3}
+    assert room.meta.get("prevSnapshot") is not None
+    assert c.get("/api/coin").json()["result"] in ("Heads", "Tails")
+    assert 1 <= c.get("/api/d12").json()["result"] <= 12
+    assert sorted(c.get("/api/shuffle_names").json()["names"]) == sorted(x["title"] for x in room.cards)
+    assert c.get("/api/link?base=http://h/").json()["link"] == f"http://h/?room={room.room}"
+    assert c.post("/api/restart", json={}).json() == {"ok": True}
+    assert not any(x.get("assignedTo") for x in room.cards)
+    exp = c.get("/api/room").text
+    assert c.post("/api/reset", json={"mode": "custom"}).status_code == 200
+    assert room.centroids == [] and room.meta.get("mode") == "custom" and room.meta.get("iteration") == 0
+    assert c.post("/api/room/import", json=json.loads(exp)).status_code == 200
+    assert room.export_json() != "" and len(room.centroids) == 2
+    assert c.post("/api/room/import", json=[1, 2]).status_code in (400, 422)
+    assert c.post("/api/room/import", json={"cards": 5, "meta": "x"}).status_code in (200, 400)
+
+
+def test_model_json_is_the_saved_centroids_file_and_limits(tmp_path):
+    """/api/model/centroids.json is byte-identical to the saved centroids.json (flat JS
+    numbers, 1.0 as 1), /api/model splices the same text; oversized bodies get 413, too many
+    rows 413, ragged or malformed input 400."""
+    X = torch.as_tensor(np.random.default_rng(1).integers(-3, 4, size=(400, 3)), dtype=torch.float32)
+    km = mikmeans.KMeans(3, device="cpu", seed=2).fit(X)
+    km.save(tmp_path / "m")
+    saved = (tmp_path / "m" / "centroids.json").read_bytes()
+    c = TestClient(create_app(Room(seed=0), km, max_body_bytes=4096, max_rows=50))
+    assert c.get("/api/model/centroids.json").content == saved
+    info = c.get("/api/model")
+    assert info.content.endswith(b'"centroids":' + saved + b"}")
+    assert json.loads(info.content)["centroids"] == json.loads(saved)
+    assert c.post("/api/predict", json={"points": [[0.0, 1.0, 2.0]] * 51}).status_code == 413
+    assert c.post("/api/predict", json={"points": [[0.0, 1.0, 2.0]] * 400}).status_code == 413   # > 4 KiB body
+    assert c.post("/api/predict", json={"points": [[0.0, 1.0], [1.0, 2.0, 3.0]]}).status_code == 400
+    assert c.post("/api/predict", json={"points": [["a", 1.0, 2.0]]}).status_code == 400
+    assert c.post("/api/predict", json={"points": [[0.0, 1.0, 2.0]]}).status_code == 200
+    import io
+
+    buf = io.BytesIO()
+    np.save(buf, np.zeros((60, 3), dtype=np.float32))
+    assert c.post("/api/predict.npy", content=buf.getvalue()).status_code == 413
+    assert c.post("/api/predict.npy", content=b"x" * 5000).status_code == 413
