@@ -398,7 +398,8 @@ void row_sqnorm(const Tensor& X, const Tensor& out) {
 // Optional column statistics (all three or none): fstats f64 [3, D] (sum |x|, sum x,
 // sum x^2) and nnz int64 [D] zero-filled, lowbit int32 [D] filled with INT_MAX.
 void col_absmax(const Tensor& X, const Tensor& out, const c10::optional<Tensor>& fstats,
-                const c10::optional<Tensor>& nnz, const c10::optional<Tensor>& lowbit) {
+                const c10::optional<Tensor>& nnz, const c10::optional<Tensor>& lowbit,
+                const c10::optional<Tensor>& xn) {
   const int dt = dtype_of(X);
   const int64_t ldx = check_points(X, dt);
   check_cuda(out, "out");
@@ -411,10 +412,19 @@ void col_absmax(const Tensor& X, const Tensor& out, const c10::optional<Tensor>&
     check_i64(*nnz, "nnz", X.size(1));
     check_i32(*lowbit, "lowbit", X.size(1));
   }
+  if (xn.has_value()) {
+    check_f32(*xn, "xn", X.size(0));
+    TORCH_CHECK(X.size(1) <= 64 * (dt == mk::DT_BF16 ? 8 : 4), "mikmeans: fused row norms up to 64 pieces per row");
+  }
+  // per-block partial sums, summed in a fixed order by the launcher (bitwise reproducible)
+  Tensor fpart;
+  if (fstats.has_value())
+    fpart = at::zeros({(int64_t)mk::colstat_blocks() * 3 * X.size(1)}, X.options().dtype(at::kDouble));
   hip_check(mk::launch_col_absmax(dt, X.data_ptr(), X.size(0), (int)X.size(1), ldx,
                                   reinterpret_cast<uint32_t*>(out.data_ptr<int32_t>()), stream(),
                                   opt_ptr<double>(fstats), opt_ptr<unsigned long long>(nnz),
-                                  opt_ptr<int>(lowbit)),
+                                  opt_ptr<int>(lowbit), fstats.has_value() ? fpart.data_ptr<double>() : nullptr,
+                                  opt_ptr<float>(xn)),
             "col_absmax");
 }
 
@@ -796,7 +806,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("col_absmax", &col_absmax,
         "per-column max |x| as f32 bit patterns (+ optional sum |x|, nonzero count, lowest-bit exponent)",
         py::arg("X"), py::arg("out"), py::arg("fstats") = py::none(), py::arg("nnz") = py::none(),
-        py::arg("lowbit") = py::none());
+        py::arg("lowbit") = py::none(), py::arg("xn") = py::none());
+  m.attr("COLSTAT_FUSED_PIECES") = 64;
   m.def("sample_rows", &sample_rows, "mini-batch rows X[philox(seed; j, step, rank) * n] (+ norms, indices)",
         py::arg("X"), py::arg("out"), py::arg("b"), py::arg("seed"), py::arg("rank"), py::arg("step"),
         py::arg("xn") = py::none(), py::arg("idx_out") = py::none());

@@ -102,7 +102,10 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// K1: xn[i] = sum_d x[i,d]^2 (f32 accumulate).  16 lanes per row, 16-B loads.
+// K1: xn[i] = sum_d x[i,d]^2 (f32).  16 lanes per row, 16-B loads.  The order is canonical --
+// lane s chains fmas over the elements of pieces s, s+16, s+32, ... in turn, then a 16-lane
+// butterfly (1, 2, 4, 8) -- and shared with every other producer of row norms (the fused
+// column-statistics pass below, csrc/rows.hip sample_rows), so all of them give the same bits.
 template <typename T>
 __global__ __launch_bounds__(256) void row_sqnorm_kernel(const T* __restrict__ X, int64_t N, int D,
                                                          int64_t ldx, float* __restrict__ out) {
@@ -118,10 +121,10 @@ __global__ __launch_bounds__(256) void row_sqnorm_kernel(const T* __restrict__ X
         float f[V];
         unpack16(w, f, (T*)nullptr);
 #pragma unroll
-        for (int e = 0; e < V; ++e) acc += f[e] * f[e];
+        for (int e = 0; e < V; ++e) acc = __builtin_fmaf(f[e], f[e], acc);
       }
     } else {
-      for (int c = sub; c < D; c += 16) { const float f = Elem<T>::to_f32(row[c]); acc += f * f; }
+      for (int c = sub; c < D; c += 16) { const float f = Elem<T>::to_f32(row[c]); acc = __builtin_fmaf(f, f, acc); }
     }
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
@@ -148,14 +151,19 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
 // independent row loads in flight per lane; |x| compared as bit patterns (non-negative
 // floats order like unsigned integers, and a NaN's pattern exceeds +inf's, so NaN
 // propagates like torch.aminmax).  One global atomicMax per (block, column).  STATS: also,
-// per column, the sums of |x|, x and x^2 (f32 per lane, one f64 atomicAdd per (block,
-// column) each: fstats = [sum |x| | sum x | sum x^2], the last two give the tol scale's
-// variance without an f32 copy of X), the count of nonzero values and the exponent of the lowest set bit over all nonzero finite
-// values (x is an integer multiple of 2^lowbit).  From these the engine flags wide-range
-// columns for the residual M-step pass: a column whose values all sit on the hi pass's
-// grid (lowbit >= -col_exp: one-hot, small integers, coarse bf16) never needs it, and
-// otherwise the max is compared with the mean of the NONZERO |x| (sparse columns stay
-// single-pass).
+// per column, the sums of |x|, x and x^2 (f64 per lane; every block writes its partial sums
+// to its own row of fpart [COLSTAT_BLOCKS][3][D], which colstat_reduce_kernel then sums in a
+// fixed order -- no f64 atomics, so the statistics are bitwise the same on every launch:
+// fstats = [sum |x| | sum x | sum x^2], the last two give the tol scale's variance without
+// an f32 copy of X), the count of nonzero values and the exponent of the lowest set bit over
+// all nonzero finite values (x is an integer multiple of 2^lowbit; integer atomics, order-free).
+// From these the engine flags wide-range columns for the residual M-step pass: a column whose
+// values all sit on the hi pass's grid (lowbit >= -col_exp: one-hot, small integers, coarse
+// bf16) never needs it, and otherwise the max is compared with the mean of the NONZERO |x|
+// (sparse columns stay single-pass).  NORMS (the launch covers whole rows, <= 64 pieces): also
+// every row's |x|^2 in row_sqnorm_kernel's canonical order -- the fit's setup reads X once.
+constexpr int COLSTAT_BLOCKS = 2048;
+
 __device__ __forceinline__ int lowbit_exp(float f) {
   const uint32_t b = __float_as_uint(f) & 0x7fffffffu;
   const uint32_t e = b >> 23, m = b & 0x7fffffu;
@@ -163,25 +171,26 @@ __device__ __forceinline__ int lowbit_exp(float f) {
   return e == 0u ? -149 + (int)__builtin_ctz(m) : (int)e - 150 + (int)__builtin_ctz(m | 0x800000u);
 }
 
-// One launch covers up to 64 16-B pieces of a row (a column block: X, out, fstats, nnz and
-// lowbit point at its first column; fstats rows are fstride columns apart).
-template <typename T, bool STATS>
+// One launch covers up to 64 16-B pieces of a row (a column block: X, out, fpart, nnz and
+// lowbit point at its first column; fpart rows are fstride columns apart).
+template <typename T, bool STATS, bool NORMS>
 __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X, int64_t N, int NP,
                                                          int L, int64_t ldx, uint32_t* __restrict__ out,
-                                                         double* __restrict__ fstats, int64_t fstride,
+                                                         double* __restrict__ fpart, int64_t fstride,
                                                          unsigned long long* __restrict__ nnz,
-                                                         int* __restrict__ lowbit) {
+                                                         int* __restrict__ lowbit, float* __restrict__ xn) {
   constexpr int V = Elem<T>::V;
   const int p = threadIdx.x & (L - 1);
   const int R = 256 / L;
   const int64_t step = (int64_t)gridDim.x * R;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t m[V];
   double q[V], sx[V], sxx[V];   // f64 per lane: chunked / sharded passes agree to ~1e-16
   uint32_t nz[V];
   int lb[V];
 #pragma unroll
   for (int e = 0; e < V; ++e) { m[e] = 0u; q[e] = 0.0; sx[e] = 0.0; sxx[e] = 0.0; nz[e] = 0u; lb[e] = 1 << 30; }
-  auto take = [&](const u32x4& w) {
+  auto take = [&](const u32x4& w, int64_t row) {
     float f[V];
     unpack16(w, f, (T*)nullptr);
 #pragma unroll
@@ -196,18 +205,42 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
         lb[e] = min(lb[e], lowbit_exp(f[e]));
       }
     }
+    if constexpr (NORMS) {
+      // the row's |x|^2 as row_sqnorm_kernel chains it: lane s < 16 takes its own piece, then
+      // pieces s+16, s+32, s+48 (from the lanes holding them), then the 16-lane butterfly
+      float acc = 0.f;
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc = __builtin_fmaf(f[e], f[e], acc);
+      for (int g = 16; g < L; g += 16) {   // (L > 16: every lane of the row group runs it)
+        const int src = (lane & ~(L - 1)) + ((p + g) & (L - 1));
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const float o = __shfl(f[e], src, 64);
+          if (p + g < NP) acc = __builtin_fmaf(o, o, acc);
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1)
+        if (o < L) acc += __shfl_xor(acc, o, 64);
+      if (p == 0) xn[row] = acc;
+    }
   };
-  if (p < NP) {
+  // (NORMS: a row group's lanes all run the loop -- lanes past the row's pieces take zeros --
+  // so the shuffles above see every lane of the group)
+  if (NORMS || p < NP) {
     int64_t i = (int64_t)blockIdx.x * R + threadIdx.x / L;
     const T* base = X + (int64_t)p * V;
+    auto load = [&](int64_t row) -> u32x4 {
+      return p < NP ? *(const u32x4*)(base + row * ldx) : u32x4{0u, 0u, 0u, 0u};
+    };
     for (; i + 3 * step < N; i += 4 * step) {
       u32x4 w[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) w[u] = *(const u32x4*)(base + (i + u * step) * ldx);
+      for (int u = 0; u < 4; ++u) w[u] = load(i + u * step);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) take(w[u]);
+      for (int u = 0; u < 4; ++u) take(w[u], i + u * step);
     }
-    for (; i < N; i += step) take(*(const u32x4*)(base + i * ldx));
+    for (; i < N; i += step) take(load(i), i);
   }
   for (int o = L; o < 64; o <<= 1)
 #pragma unroll
@@ -222,8 +255,7 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
       }
     }
   __shared__ uint32_t red[4][64 * V];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (lane < L)
+  if (lane < L && p < NP)
 #pragma unroll
     for (int e = 0; e < V; ++e) red[wv][lane * V + e] = m[e];
   __syncthreads();
@@ -233,20 +265,19 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
   }
   if constexpr (STATS) {
     __shared__ double rd[4][64 * 8];
+    double* mine = fpart + (int64_t)blockIdx.x * 3 * fstride;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       __syncthreads();
-      if (lane < L)
+      if (lane < L && p < NP)
 #pragma unroll
         for (int e = 0; e < V; ++e) rd[wv][lane * V + e] = k == 0 ? q[e] : k == 1 ? sx[e] : sxx[e];
       __syncthreads();
-      for (int j = threadIdx.x; j < NP * V; j += 256) {
-        const double v = (rd[0][j] + rd[1][j]) + (rd[2][j] + rd[3][j]);
-        if (v != 0.0) atomicAdd(fstats + (int64_t)k * fstride + j, v);
-      }
+      for (int j = threadIdx.x; j < NP * V; j += 256)
+        mine[(int64_t)k * fstride + j] = (rd[0][j] + rd[1][j]) + (rd[2][j] + rd[3][j]);
     }
     __syncthreads();
-    if (lane < L)
+    if (lane < L && p < NP)
 #pragma unroll
       for (int e = 0; e < V; ++e) red[wv][lane * V + e] = nz[e];
     __syncthreads();
@@ -256,7 +287,7 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
     }
     __syncthreads();
     int* ri = (int*)&red[0][0];
-    if (lane < L)
+    if (lane < L && p < NP)
 #pragma unroll
       for (int e = 0; e < V; ++e) ri[wv * 64 * V + lane * V + e] = lb[e];
     __syncthreads();
@@ -267,13 +298,37 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
   }
 }
 
+// fstats[j] = sum over the COLSTAT_BLOCKS rows of fpart[.][j] (j < n = 3 D), in one fixed order:
+// each of 256 threads sums 8 consecutive rows, then a fixed LDS tree.  One workgroup per j.
+__global__ __launch_bounds__(256) void colstat_reduce_kernel(const double* __restrict__ fpart, int64_t n,
+                                                            double* __restrict__ fstats) {
+  constexpr int PER = COLSTAT_BLOCKS / 256;
+  const int64_t j = blockIdx.x;
+  double v = 0.0;
+#pragma unroll
+  for (int r = 0; r < PER; ++r) v += fpart[((int64_t)threadIdx.x * PER + r) * n + j];
+  __shared__ double t[256];
+  t[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) t[threadIdx.x] += t[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) fstats[j] = t[0];
+}
+
+int colstat_blocks() { return COLSTAT_BLOCKS; }
+
 hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
-                             hipStream_t s, double* fstats, unsigned long long* nnz, int* lowbit) {
+                             hipStream_t s, double* fstats, unsigned long long* nnz, int* lowbit, double* fpart,
+                             float* xn) {
   const int V = dtype == DT_BF16 ? 8 : 4;
   const int NPT = D / V;
   if (N <= 0 || D % V || NPT < 1) return N <= 0 ? hipSuccess : hipErrorInvalidValue;
-  if ((fstats != nullptr) != (nnz != nullptr) || (fstats != nullptr) != (lowbit != nullptr))
+  if ((fstats != nullptr) != (nnz != nullptr) || (fstats != nullptr) != (lowbit != nullptr) ||
+      (fstats != nullptr) != (fpart != nullptr))
     return hipErrorInvalidValue;  // the statistics come together
+  if (xn && NPT > 64) return hipErrorInvalidValue;   // (row norms: one launch must cover the row)
   // wide rows: one launch per block of 64 pieces (512 bf16 / 256 f32 columns)
   for (int p0 = 0; p0 < NPT; p0 += 64) {
     const int NP = NPT - p0 < 64 ? NPT - p0 : 64;
@@ -282,21 +337,26 @@ hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t
     while (L < NP) L *= 2;
     const int R = 256 / L;
     int64_t nb = (N + R - 1) / R;
-    if (nb > 2048) nb = 2048;  // 8 per CU; each streams its rows with 4 loads in flight per lane
+    if (nb > COLSTAT_BLOCKS) nb = COLSTAT_BLOCKS;  // 8 per CU; each streams its rows with 4 loads in flight per lane
     const dim3 g((unsigned)nb), b(256);
-    double* fs = fstats ? fstats + c0 : nullptr;
+    double* fp = fpart ? fpart + c0 : nullptr;
     unsigned long long* nz = nnz ? nnz + c0 : nullptr;
     int* lb = lowbit ? lowbit + c0 : nullptr;
+#define MK_COLSTAT(TT, ST, NR)                                                                              \
+  hipLaunchKernelGGL((col_absmax_kernel<TT, ST, NR>), g, b, 0, s, (const TT*)X + c0, N, NP, L, ldx, out + c0, \
+                     fp, (int64_t)D, nz, lb, xn)
     if (dtype == DT_BF16) {
-      const uint16_t* Xb = (const uint16_t*)X + c0;
-      if (fstats) hipLaunchKernelGGL((col_absmax_kernel<uint16_t, true>), g, b, 0, s, Xb, N, NP, L, ldx, out + c0, fs, (int64_t)D, nz, lb);
-      else hipLaunchKernelGGL((col_absmax_kernel<uint16_t, false>), g, b, 0, s, Xb, N, NP, L, ldx, out + c0, fs, (int64_t)D, nz, lb);
+      if (fstats) { if (xn) MK_COLSTAT(uint16_t, true, true); else MK_COLSTAT(uint16_t, true, false); }
+      else { if (xn) MK_COLSTAT(uint16_t, false, true); else MK_COLSTAT(uint16_t, false, false); }
     } else {
-      const float* Xf = (const float*)X + c0;
-      if (fstats) hipLaunchKernelGGL((col_absmax_kernel<float, true>), g, b, 0, s, Xf, N, NP, L, ldx, out + c0, fs, (int64_t)D, nz, lb);
-      else hipLaunchKernelGGL((col_absmax_kernel<float, false>), g, b, 0, s, Xf, N, NP, L, ldx, out + c0, fs, (int64_t)D, nz, lb);
+      if (fstats) { if (xn) MK_COLSTAT(float, true, true); else MK_COLSTAT(float, true, false); }
+      else { if (xn) MK_COLSTAT(float, false, true); else MK_COLSTAT(float, false, false); }
     }
+#undef MK_COLSTAT
   }
+  if (fstats)
+    hipLaunchKernelGGL(colstat_reduce_kernel, dim3((unsigned)(3 * D)), dim3(256), 0, s, fpart, (int64_t)3 * D,
+                       fstats);
   return hipGetLastError();
 }
 

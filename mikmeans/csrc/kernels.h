@@ -197,9 +197,13 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 // together, fstats = [sum |x| | sum x | sum x^2] (f64 [3][D], zeroed), the nonzero count
 // (u64 [D], zeroed) and the lowest set bit's exponent over nonzero finite values (int [D],
 // initialised to INT_MAX by the caller).
+// The f64 sums are bitwise reproducible: each block writes its partials to its row of fpart
+// (f64 [colstat_blocks()][3][D], zeroed by the caller) and one fixed-order pass sums them.
+// xn (optional, D <= 64 pieces): every row's |x|^2 from the same pass, bitwise row_sqnorm's.
+int colstat_blocks();
 hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
                              hipStream_t s, double* fstats = nullptr, unsigned long long* nnz = nullptr,
-                             int* lowbit = nullptr);
+                             int* lowbit = nullptr, double* fpart = nullptr, float* xn = nullptr);
 hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t ldx, float* out,
                              hipStream_t s);
 

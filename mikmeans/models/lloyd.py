@@ -175,16 +175,16 @@ class LloydEngine:
         self.slab = torch.empty(self.n_chunks * self.K * self.Dp, dtype=torch.int64, device=dev)
         self.cnt_slab = torch.empty(self.n_chunks * self.K, dtype=torch.int64, device=dev)
         self.xn = torch.empty(self.n, dtype=torch.float32, device=dev)
-        if self.n:
-            C.row_sqnorm(self.X, self.xn)
         # fixed-point scale of the M-step accumulators (X is static for the fit)
-        from ..ops import MStepScales, mstep_scales
+        from ..ops import MStepScales, col_stats, fused_norms_ok, mstep_scales
 
         # (global column statistics: every rank uses the same scale -> exact, world-size independent
         # sums; columns with inexact values far above their nonzero mean also get a residual lo pass)
-        from ..ops import col_stats
-
-        self.stats = col_stats(self.X)             # (also the tol scale's column sums: api.fit)
+        # One pass over X: the statistics and, rows of <= 64 pieces, the row norms with them
+        fused = bool(self.n) and fused_norms_ok(self.X)
+        if self.n and not fused:
+            C.row_sqnorm(self.X, self.xn)
+        self.stats = col_stats(self.X, xn=self.xn if fused else None)   # (also the tol scale's sums: api.fit)
         self.scales = mstep_scales(self.X, self.weights, comm=self.comm, stats=self.stats)
         if self.scales.nw and C.update_slice_width(self.dt, self.K, self.Dp, self.weights is not None) == 0:
             self.scales = MStepScales(self.scales.col_exp, self.scales.cnt_exp, [], dev)

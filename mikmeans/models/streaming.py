@@ -15,7 +15,9 @@ policy.
 Same options as the resident engine, with the same numerics (bitwise the resident fit
 from the same start -- up to a column whose statistics sit within f64 rounding of the
 wide-column threshold or the tol scale: those are f64 sums, merged chunk by chunk here and
-accumulated by atomics in one pass there, so their last bits differ): sample weights, the cosine metric (each chunk is normalised on the
+in one pass there (each bitwise reproducible: fixed-order per-block partials,
+csrc/finalize.hip), so for inexact values their last bits can differ between the two;
+tests/test_gpu_mstep.py pins a column exactly at the threshold): sample weights, the cosine metric (each chunk is normalised on the
 device by the same kernel as the resident rows), empty_policy 'farthest' (the farthest
 rows are fetched from host memory), wide-range columns (residual lo pass per chunk, from
 column statistics merged over chunks).  Host rows of another dtype or an unpadded width
@@ -44,7 +46,7 @@ class StreamingLloydEngine(LloydEngine):
                  comm: Comm | None = None, device=None, frozen=None, n_features: int | None = None,
                  dtype: torch.dtype | None = None, sample_weight: torch.Tensor | None = None,
                  empty_policy: str = "keep", spherical: bool = False):
-        from ..ops import CentroidPack, ColStats, col_stats, mstep_scales, MStepScales
+        from ..ops import CentroidPack, ColStats, col_stats, fused_norms_ok, mstep_scales, MStepScales
         from ..parallel.memplan import padded_cols, stream_chunk_rows
 
         if X_host.device.type != "cpu":
@@ -116,8 +118,11 @@ class StreamingLloydEngine(LloydEngine):
         st = ColStats.empty(self.Dp, dev)
         for Xc, r0, r1 in self._chunks():
             if r1 > r0:
-                C.row_sqnorm(Xc, self.xn[r0:r1])
-                st = st.merge(col_stats(Xc))
+                if fused_norms_ok(Xc):       # (one pass over the chunk: statistics + row norms)
+                    st = st.merge(col_stats(Xc, xn=self.xn[r0:r1]))
+                else:
+                    C.row_sqnorm(Xc, self.xn[r0:r1])
+                    st = st.merge(col_stats(Xc))
         self.stats = st
         self.scales = mstep_scales(self.bufs[0][:0], self.weights, comm=self.comm, stats=st)
         if self.scales.nw and C.update_slice_width(self.dt, self.K, self.Dp, self.weights is not None) == 0:

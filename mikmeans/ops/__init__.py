@@ -259,21 +259,31 @@ def _lowbit_torch(Xb: torch.Tensor) -> torch.Tensor:
     return torch.where((b == 0) | (e == 255), torch.full_like(lb, ColStats.LOWBIT_NONE), lb)
 
 
-def col_stats(X: torch.Tensor, stats: bool = True) -> ColStats:
+def fused_norms_ok(X: torch.Tensor) -> bool:
+    """Whether :func:`col_stats` can also write the row norms (a row of <= 64 16-B pieces)."""
+    return _native_colstats_ok(X) and X.shape[1] <= 64 * (16 // X.element_size())
+
+
+def col_stats(X: torch.Tensor, stats: bool = True, xn: torch.Tensor | None = None) -> ColStats:
     """One pass over ``X``: per-column max |x| and, with ``stats``, sum |x|, sum x, sum x^2,
-    the nonzero count and the lowest-bit exponent (native kernel on the GPU; torch elsewhere)."""
+    the nonzero count and the lowest-bit exponent (native kernel on the GPU, whose f64 sums
+    are per-block partials summed in a fixed order: bitwise the same on every launch; torch
+    elsewhere).  ``xn`` (GPU, :func:`fused_norms_ok`): also every row's |x|^2 into it, bitwise
+    :func:`row_sqnorm`'s -- the fit's setup then reads X once."""
     D = X.shape[1]
     if X.shape[0] == 0:
         return ColStats.empty(D, X.device, stats)
+    if xn is not None and not fused_norms_ok(X):
+        raise ValueError("col_stats: fused row norms need a native-layout GPU X of <= 64 pieces per row")
     if _native_colstats_ok(X):
         out = torch.zeros(D, dtype=torch.int32, device=X.device)
         if not stats:
-            require().col_absmax(X, out)
+            require().col_absmax(X, out, None, None, None, xn)
             return ColStats(out.view(torch.float32).double())
         fs = torch.zeros((3, D), dtype=torch.float64, device=X.device)
         nz = torch.zeros(D, dtype=torch.int64, device=X.device)
         lb = torch.full((D,), ColStats.LOWBIT_NONE, dtype=torch.int32, device=X.device)
-        require().col_absmax(X, out, fs, nz, lb)
+        require().col_absmax(X, out, fs, nz, lb, xn)
         return ColStats(out.view(torch.float32).double(), fs[0], nz, lb, fs[1], fs[2])
     mn, mx = torch.aminmax(X, dim=0)
     m = torch.maximum(mn.double().abs(), mx.double().abs())
