@@ -4,8 +4,11 @@ rounds, on the bench's blob data a few Lloyd iterations in.
 
 usage: assign_ab.py [--n N] [--d D] [--k K] [--dtype bf16|f32] [--rounds R] [--reps M]
                     --arms "assign_persist=0;assign_persist=1;assign_geom=4,assign_persist=1"
-Prints one JSON line per shape: median / min ms per arm, TF/s, and whether every arm's labels
-equal the first arm's (bitwise).
+Prints one JSON line per shape: median / min ms per arm, TF/s, whether every arm's labels
+equal the first arm's (bitwise), and -- from the GFX clock sampled during each arm's timed
+launches (mikmeans/utils/telemetry.py, amdsmi) -- the mean clock and the cycles per MFMA per
+SIMD (16 for a v_mfma_f32_16x16x32_bf16 issued back to back): a clock-normalised cost, so
+an A/B across boxes or power states compares work per cycle, not wall time.
 """
 import argparse
 import json
@@ -70,17 +73,26 @@ def main():
     times = {n: [] for n in names}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
-    def run(arm):
+    from mikmeans.utils.telemetry import ClockSampler
+
+    clocks = {n: [] for n in names}
+
+    def run(arm, name):
         old = {k: native.get_variant(k) for k in arm}
         for k, v in arm.items():
             native.set_variant(k, v)
         try:
             call()   # warm / attributes
-            ev[0].record()
-            for _ in range(a.reps):
-                call()
-            ev[1].record()
             torch.cuda.synchronize()
+            with ClockSampler(0, period_s=0.01) as cs:
+                ev[0].record()
+                for _ in range(a.reps):
+                    call()
+                ev[1].record()
+                torch.cuda.synchronize()
+            sm = cs.summary()
+            if sm and sm.get("clock_mhz"):
+                clocks[name].append(sm["clock_mhz"])
             return ev[0].elapsed_time(ev[1]) / a.reps, (glab if a.gather else eng.labels).clone()
         finally:
             for k, v in old.items():
@@ -89,18 +101,26 @@ def main():
     for rd in range(a.rounds):
         order = list(zip(names, arms)) if rd % 2 == 0 else list(zip(names, arms))[::-1]
         for n, arm in order:
-            t, lab = run(arm)
+            t, lab = run(arm, n)
             times[n].append(t)
             labels.setdefault(n, lab)
     ref = labels[names[0]]
     res = {"n": a.n, "d": a.d, "k": a.k, "dtype": a.dtype, "rounds": a.rounds, "reps": a.reps,
            "gathered_rows": a.gather}
     m = a.gather or a.n
+    kpad = eng.pk.Kpad
+    # MFMA instructions per SIMD: 16-point blocks x 16-centre tiles x K-steps of 32 (bf16) / 4 x 4 (f32)
+    ksteps = eng.pk.dpad // 32 if dt == torch.bfloat16 else eng.pk.dpad // 4
+    mfma_per_simd = (m / 16) * (kpad / 16) * ksteps / 1024
     for n in names:
         med = statistics.median(times[n])
         res[n] = {"median_ms": round(med, 4), "min_ms": round(min(times[n]), 4),
                   "tflops": round(2.0 * m * a.k * a.d / (med * 1e-3) / 1e12, 1),
                   "labels_equal": bool(torch.equal(labels[n], ref))}
+        if clocks[n]:
+            clk = statistics.fmean(clocks[n])
+            res[n]["clock_mhz"] = round(clk, 1)
+            res[n]["cycles_per_mfma"] = round(med * 1e-3 * clk * 1e6 / mfma_per_simd, 2)
     print(json.dumps(res), flush=True)
 
 

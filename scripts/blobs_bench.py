@@ -41,6 +41,18 @@ def main():
         ms = statistics.median(ts)
         res[name] = {"median_ms": round(ms, 4), "min_ms": round(min(ts), 4),
                      "write_TBps": round(X.numel() * 2 / (ms * 1e-3) / 1e12, 3)}
+    # the write floor: torch's vectorised fill of the same bytes
+    ts = []
+    for r in range(a.reps + 2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        X.fill_(float(r))
+        e1.record()
+        torch.cuda.synchronize()
+        if r >= 2:
+            ts.append(e0.elapsed_time(e1))
+    ms = statistics.median(ts)
+    res["fill"] = {"median_ms": round(ms, 4), "write_TBps": round(X.numel() * 2 / (ms * 1e-3) / 1e12, 3)}
     print(json.dumps(res), flush=True)
 
 
