@@ -161,7 +161,11 @@ def cmd_serve(a) -> int:
     """`mikmeans serve`: the room board and model serving over HTTP (mikmeans/serve.py)."""
     from .serve import serve
 
-    serve(a.room, a.model, host=a.host, port=a.port, device=a.device)
+    session = None
+    if a.found is not None or a.join:
+        session = {"store_host": a.store_host, "store_port": a.store_port,
+                   "found": a.found if a.found is not None else None, "member": a.member, "user": a.user}
+    serve(a.room, a.model, host=a.host, port=a.port, device=a.device, session=session)
     return 0
 
 
@@ -387,6 +391,15 @@ def build_parser():
     sv.add_argument("--host", default="127.0.0.1")
     sv.add_argument("--port", type=int, default=8000)
     sv.add_argument("--device", default=None)
+    # serve one member of a live replicated room session (parallel/elastic.py)
+    sg = sv.add_mutually_exclusive_group()
+    sg.add_argument("--found", nargs="?", const="", metavar="ROOM",
+                    help="start a live session (hosts its rendezvous store) and serve it")
+    sg.add_argument("--join", action="store_true", help="join a running session and serve it")
+    sv.add_argument("--store-host", default="127.0.0.1", help="session rendezvous (TCPStore) host")
+    sv.add_argument("--store-port", type=int, default=29555, help="session rendezvous port")
+    sv.add_argument("--member", help="unique member id (default host-pid)")
+    sv.add_argument("--user", help="this member's display name")
     se = sub.add_parser("session", help="one participant of a live replicated room session")
     se.add_argument("--host", default="127.0.0.1", help="rendezvous (TCPStore) host")
     se.add_argument("--port", type=int, required=True)

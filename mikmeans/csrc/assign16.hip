@@ -979,6 +979,10 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
     // 3: streamed A fragments (the wide-row issue), 3 blocks at 3 waves/SIMD in 151-157
     // VGPRs without the 4 spilled registers of the default (4 blocks spill hundreds)
     if (gm == 3) return launch16_t<T, DPAD, 3, CT, 2, 3, 4, true>(a, s);
+    // 4: streamed A fragments with 6 point blocks at 2 waves/SIMD (each A fragment feeds 6
+    // MFMAs, half the LDS reads and chunk barriers per MFMA of the default); 5: 4 blocks
+    if (gm == 4) return launch16_t<T, DPAD, 6, CT, 2, 2, 4, true>(a, s);
+    if (gm == 5) return launch16_t<T, DPAD, 4, CT, 2, 2, 4, true>(a, s);
   }
   if constexpr (sizeof(T) == 2 && DPAD == 128) {
     // A/B switch V_ASSIGN_GEOM: 1 = 8 waves share a ring of 32 KiB chunks (a barrier
@@ -1024,6 +1028,8 @@ static int block_rows_t(int kpad) {
   if constexpr (sizeof(T) == 2 && DPAD == 256) {
     if (gm == 1) return 8 * 3 * 16;
     if (gm == 2) return 8 * 2 * 16;
+    if (gm == 4) return 4 * 6 * 16;
+    if (gm == 5) return 4 * 4 * 16;
   }
   if constexpr (sizeof(T) == 2 && DPAD == 128) {
     if ((gm == 1 && kpad % (16 * 8) == 0) || gm == 2) return 8 * 4 * 16;

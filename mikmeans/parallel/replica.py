@@ -114,7 +114,16 @@ class RoomReplica:
         raise AttributeError(name)
 
     # ---------------------------------------------------------- replication
-    def _apply(self, rec: dict):
+    def _apply(self, rec: dict) -> bool:
+        """Apply one op; an op that raises (a malformed import, say) raises on every replica
+        alike -- same state, same op -- so it is skipped everywhere and the round goes on."""
+        try:
+            self._apply_op(rec)
+            return True
+        except (ValueError, TypeError, KeyError, AttributeError, IndexError):
+            return False
+
+    def _apply_op(self, rec: dict):
         r = self.room
         op, args, kw = rec["op"], rec["args"], rec["kw"]
         if op == "shuffle_unassigned":

@@ -40,7 +40,13 @@ Endpoints (JSON in and out) -- the reference's controls (``index.html:76-131``,
 Request bodies over ``max_body_bytes`` get 413, as do batches over ``max_rows`` rows (and
 transforms over ``max_transform_values`` output values); malformed input gets 400.
 
-``mikmeans serve [--room FILE] [--model DIR] [--host 127.0.0.1] [--port 8000]``.
+Session mode (``--found [ROOM]`` / ``--join``, ``--store-host/--store-port``): the served
+room is one member of a live replicated session (:class:`~mikmeans.parallel.elastic.
+ElasticRoomReplica`, the reference's peer mesh, ``app.mjs:70-118``): edits are queued (202)
+and every member applies them in the same order at the next round, so boards served by
+different processes -- and scripted ``mikmeans session`` members -- stay byte-identical.
+
+``mikmeans serve [--room FILE] [--model DIR] [--host 127.0.0.1] [--port 8000] [--found|--join]``.
 """
 from __future__ import annotations
 
@@ -216,6 +222,8 @@ class _Board:
     """The served room plus its change counter: every mutation runs under the lock, bumps
     the version and wakes the long-polls."""
 
+    queued = False    # (mutations apply at once)
+
     def __init__(self, room: Room):
         self.room = room
         self.version = 0
@@ -238,12 +246,102 @@ class _Board:
             return self.version
 
 
+class _QueuedRoom:
+    """What the route handlers see in session mode: the replica's room for reads, and every
+    replicated Room operation (parallel/replica.py OPS) queued for the next round instead of
+    applied (the reference broadcasts each transaction, app.mjs:121; here every member
+    applies the same ops in the same order)."""
+
+    def __init__(self, replica):
+        self._rep = replica
+
+    def __getattr__(self, name):
+        from .parallel.replica import OPS
+
+        if name in OPS:
+            op = getattr(self._rep, name)
+
+            def queue(*args, **kw):
+                kw.pop("created_by", None)     # (the member's own name is the author)
+                if name == "import_json":
+                    kw.pop("compat", None)
+                out = op(*args, **kw)
+                return out if out is not None else True
+            return queue
+        return getattr(self._rep.room, name)
+
+
+class _ReplicaBoard(_Board):
+    """The served room as one member of a live replicated session
+    (:class:`~mikmeans.parallel.elastic.ElasticRoomReplica`): edits are queued and applied by
+    every member at the next round; a background thread runs the rounds and bumps the version
+    whenever one applied an op or changed the roster, so every browser on every member's
+    server re-renders."""
+
+    queued = True
+
+    def __init__(self, replica, interval: float = 0.2):
+        self.replica = replica
+        self.version = 0
+        self.cond = threading.Condition()
+        self.interval = float(interval)
+        self.error = None
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._rounds, name="mikmeans-session", daemon=True)
+        self._thread.start()
+
+    @property
+    def room(self):
+        return self.replica.room
+
+    def read(self, fn):
+        with self.cond:
+            return fn(self.replica.room)
+
+    def mutate(self, fn):
+        with self.cond:
+            return fn(_QueuedRoom(self.replica))
+
+    def _rounds(self):
+        roster = None
+        while not self._stop.is_set() and not self.replica.left:
+            try:
+                with self.cond:      # (a round applies ops to the room the handlers read)
+                    applied = self.replica.sync()
+                    if applied or self.replica.roster != roster:
+                        roster = list(self.replica.roster)
+                        self.version += 1
+                        self.cond.notify_all()
+            except Exception as e:  # noqa: BLE001 -- a dead session: keep serving the last state
+                self.error = f"{type(e).__name__}: {e}"
+                return
+            self._stop.wait(self.interval)
+
+    def close(self, leave: bool = True):
+        if leave and not self.replica.left:
+            with self.cond:
+                self.replica.leave()
+        deadline = 50
+        while leave and not self.replica.left and self._thread.is_alive() and deadline:
+            self._stop.wait(self.interval)
+            deadline -= 1
+        self._stop.set()
+        self._thread.join(timeout=5)
+
+
 def create_app(room: Room | None = None, model=None, *, device=None, max_body_bytes: int = MAX_BODY_BYTES,
-               max_rows: int = MAX_ROWS, max_transform_values: int = MAX_TRANSFORM_VALUES):
+               max_rows: int = MAX_ROWS, max_transform_values: int = MAX_TRANSFORM_VALUES, replica=None,
+               session_interval: float = 0.2):
     """The FastAPI app serving ``room`` (a new one when None) and, when given, a fitted
-    ``model`` (:class:`~mikmeans.KMeans` / :class:`~mikmeans.MiniBatchKMeans`)."""
+    ``model`` (:class:`~mikmeans.KMeans` / :class:`~mikmeans.MiniBatchKMeans`).  ``replica``
+    (an :class:`~mikmeans.parallel.elastic.ElasticRoomReplica`): serve that member's room of a
+    live session instead -- edits are queued (HTTP 202) and appear on every member's board
+    after the next round."""
     app = FastAPI(title="mikmeans", docs_url=None, redoc_url=None, openapi_url=None)
-    board = _Board(room if room is not None else Room(seed=0))
+    if replica is not None:
+        board = _ReplicaBoard(replica, session_interval)
+    else:
+        board = _Board(room if room is not None else Room(seed=0))
     model_lock = threading.Lock()   # (one batch at a time on the device: the serving pack is shared)
 
     @app.middleware("http")
@@ -257,6 +355,10 @@ def create_app(room: Room | None = None, model=None, *, device=None, max_body_by
             resp = JSONResponse({"detail": f"request body over {max_body_bytes} bytes"}, status_code=413)
         else:
             resp = await call_next(request)
+            # session mode: a room edit is queued for the next round, not applied yet
+            if (board.queued and resp.status_code == 200 and request.method in ("POST", "DELETE")
+                    and request.url.path.startswith("/api/") and request.url.path not in _READ_POSTS):
+                resp.status_code = 202
         for k, v in SECURITY_HEADERS.items():
             resp.headers[k] = v
         return resp
@@ -279,9 +381,14 @@ def create_app(room: Room | None = None, model=None, *, device=None, max_body_by
     @app.get("/api/state")
     def room_state():
         def snap(r):
-            return _jsonable({"room": r.room, "version": board.version, "cards": r.cards, "centroids": r.centroids,
-                              "meta": {"mode": r.meta.get("mode"), "iteration": r.meta.get("iteration")},
-                              "dashboard": r.dashboard()})
+            out = {"room": r.room, "version": board.version, "cards": r.cards, "centroids": r.centroids,
+                   "meta": {"mode": r.meta.get("mode"), "iteration": r.meta.get("iteration")},
+                   "dashboard": r.dashboard()}
+            if board.queued:    # the session's presence (the reference's roster, app.mjs:66-67, :94-95)
+                rep = board.replica
+                out["session"] = {"round": rep.round, "epoch": rep.epoch, "peers": rep.peers,
+                                  "roster": rep.roster, "error": board.error}
+            return _jsonable(out)
         return board.read(snap)
 
     @app.get("/api/changes")
@@ -293,6 +400,11 @@ def create_app(room: Room | None = None, model=None, *, device=None, max_body_by
     @app.post("/api/room/import")
     def import_room(body: dict = Body(...)):
         import json
+
+        try:                     # (validated before it reaches the room -- or a session's queue)
+            Room.from_json(json.dumps(body))
+        except (ValueError, TypeError, KeyError, AttributeError) as e:
+            raise HTTPException(400, f"not a room export: {e}") from None
 
         def imp(r):
             r.import_json(json.dumps(body))
@@ -532,20 +644,58 @@ def create_app(room: Room | None = None, model=None, *, device=None, max_body_by
         return {"distances": d.cpu().tolist()}
 
     app.state.board = board
+    if board.queued:
+        app.router.on_shutdown.append(board.close)
     return app
 
 
-def serve(room_path=None, model_path=None, host: str = "127.0.0.1", port: int = 8000, device=None):
-    """Run the app with uvicorn (blocking)."""
+# POST routes that change nothing in the room (model serving)
+_READ_POSTS = ("/api/predict", "/api/predict.npy", "/api/transform")
+
+
+def serve(room_path=None, model_path=None, host: str = "127.0.0.1", port: int = 8000, device=None,
+          session: dict | None = None):
+    """Run the app with uvicorn (blocking).  ``session``: serve a member of a live room
+    session -- ``{"store_host", "store_port", "found": ROOM or None (join), "member", "user"}``
+    (the founder hosts the rendezvous store; ``room_path`` seeds a founded room)."""
     import uvicorn
 
     room = None
+    text = None
     if room_path:
         with open(room_path) as f:
-            room = Room.from_json(f.read())
+            text = f.read()
+        room = Room.from_json(text)
     model = None
     if model_path:
         from .api import KMeans
 
         model = KMeans.load(model_path, device=device)
-    uvicorn.run(create_app(room, model), host=host, port=port, log_level="warning")
+    replica = None
+    if session is not None:
+        replica = open_session(text, **session)
+    uvicorn.run(create_app(room, model, replica=replica), host=host, port=port, log_level="warning")
+
+
+def open_session(state_json=None, *, store_host: str = "127.0.0.1", store_port: int, found=None,
+                 member: str | None = None, user: str | None = None, timeout_s: float = 120.0, seed: int = 0):
+    """Found (``found`` = room code, "" for a new one) or join a live room session over a
+    TCPStore at ``store_host:store_port`` and return this member's ElasticRoomReplica."""
+    import datetime
+    import os
+    import socket
+
+    import torch.distributed as dist
+
+    from .parallel.elastic import ElasticRoomReplica
+
+    store = dist.TCPStore(store_host, int(store_port), is_master=found is not None, wait_for_workers=False,
+                          timeout=datetime.timedelta(seconds=timeout_s))
+    member = member or f"{socket.gethostname()}-{os.getpid()}-serve"
+    kw = dict(user=user, seed=seed, timeout_s=timeout_s)
+    if found is not None:
+        rep = ElasticRoomReplica.found(store, member, found or None, state_json=state_json, **kw)
+    else:
+        rep = ElasticRoomReplica.join(store, member, **kw)
+    rep._store_ref = store          # (the master store lives as long as the replica)
+    return rep

@@ -245,3 +245,48 @@ def test_model_json_is_the_saved_centroids_file_and_limits(tmp_path):
     np.save(buf, np.zeros((60, 3), dtype=np.float32))
     assert c.post("/api/predict.npy", content=buf.getvalue()).status_code == 413
     assert c.post("/api/predict.npy", content=b"x" * 5000).status_code == 413
+
+
+@pytest.mark.timeout(240)
+def test_served_board_is_a_live_session_member(tmp_path):
+    """(verdict r4) `mikmeans serve --found` serves one member of a live replicated session
+    (parallel/elastic.py): an edit through HTTP is queued (202) and reaches a peer member in
+    another process, the peer's edit appears on the served board, and the board's state
+    carries the session's roster."""
+    import os
+    import subprocess
+    import sys
+    import time
+
+    from mikmeans.parallel.launch import free_port
+    from mikmeans.serve import open_session
+
+    port = free_port()
+    rep = open_session(None, store_port=port, found="LIVE", member="server", user="Srv")
+    app = create_app(replica=rep, session_interval=0.1)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    peer = subprocess.Popen([sys.executable, "-m", "mikmeans", "session", "--join", "--port", str(port),
+                             "--user", "Peer", "--card", "PeerCard:Sweet,Sour", "--until-round", "400",
+                             "--leave-at", "60", "--interval", "0.1", "--export", str(tmp_path / "peer.json")],
+                            cwd=root, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        with TestClient(app) as c:
+            r = c.post("/api/cards", json={"title": "ServerCard", "traits": ["Mint"]})
+            assert r.status_code == 202
+            seen, roster = False, []
+            for _ in range(300):
+                st = c.get("/api/state").json()
+                titles = [x["title"] for x in st["cards"]]
+                roster = st["session"]["roster"]
+                if "PeerCard" in titles and "ServerCard" in titles and sorted(roster) == ["Peer", "Srv"]:
+                    seen = True
+                    break
+                time.sleep(0.1)
+            assert seen, (titles, roster, st["session"])
+            out, err = peer.communicate(timeout=120)
+            assert peer.returncode == 0, err[-2000:]
+            peer_titles = [x["title"] for x in json.loads((tmp_path / "peer.json").read_text())["cards"]]
+            assert "ServerCard" in peer_titles and "PeerCard" in peer_titles
+    finally:
+        if peer.poll() is None:
+            peer.kill()
