@@ -37,9 +37,11 @@ def _member(port, member, delay, leave_at):
         rep = ElasticRoomReplica.join(store, member, user=member, seed=3)
     store.set(f"joined/{member}", str(rep.round))
     asked = False
+    first = True
     while rep.round < ROUNDS and not rep.left:
-        if rep.round % 3 == 0:
+        if rep.round % 3 == 0 or first:     # (a late joiner under load still leaves a card)
             rep.add_card(f"{member}-{rep.round}", ["Mint", "Choc"])
+            first = False
         if member == "A" and rep.round == 5:
             rep.add_centroid("Fresh")
         if leave_at is not None and rep.round >= leave_at and not asked:
