@@ -168,6 +168,14 @@ __device__ __forceinline__ unsigned key6_mask() {
 // blobs (kpp.hip) and the mini-batch row sampler (rows.hip); NumPy mirror in
 // mikmeans/data/blobs.py.
 struct U4 { uint32_t x, y, z, w; };
+// a ^ b ^ k in one VALU instruction: gfx950's three-input v_bitop3_b32 with the XOR3 truth
+// table 0x96 (the compiler emits two v_xor_b32 for the round's key mix; the round keys are
+// wave-uniform, so k is the SGPR operand).  Plain VALU asm.
+__device__ __forceinline__ uint32_t xor3_sk(uint32_t a, uint32_t b, uint32_t k) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %3, %1, %2 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+}
 __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -177,7 +185,7 @@ __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
     const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    c = U4{xor3_sk(hi1, c.y, k0), lo1, xor3_sk(hi0, c.w, k1), lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
