@@ -110,7 +110,10 @@ def main(argv=None):
     from mikmeans.parallel import Comm, shard_range
 
     cfg = dict(CONFIGS[args.config])
-    if args.n:
+    if args.n and args.n != cfg["n"]:
+        # (a rehearsal size: the model label says so, not the config's own N)
+        m, e = f"{args.n:.0e}".split("e")
+        cfg["model"] = cfg["model"].replace(cfg["model"].split()[1], f"N={m}e{int(e)}", 1)
         cfg["n"] = args.n
     comm = Comm.from_env(args.device, timeout_s=args.timeout)
     world = comm.world

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--d", type=int, default=256)
     ap.add_argument("--k", type=int, default=512)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--tpr", default="", help="comma list of lanes-per-row A/B arms (variant blobs_tpr)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     c = blob_centers(a.k, a.d, 10.0, 0, device=dev)
@@ -41,6 +42,24 @@ def main():
         ms = statistics.median(ts)
         res[name] = {"median_ms": round(ms, 4), "min_ms": round(min(ts), 4),
                      "write_TBps": round(X.numel() * 2 / (ms * 1e-3) / 1e12, 3)}
+    if a.tpr:
+        from mikmeans.ops import native
+
+        ref = X.clone()
+        for tv in [int(t) for t in a.tpr.split(",")]:
+            native.set_variant("blobs_tpr", tv)
+            ts = []
+            for r in range(a.reps + 2):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                make_blobs(a.n, a.d, a.k, seed=a.reps + 1, i0=(a.reps + 1) * a.n, dtype=torch.bfloat16,
+                           device=dev, centers=c, out=X, norms=xn)
+                e1.record()
+                torch.cuda.synchronize()
+                if r >= 2:
+                    ts.append(e0.elapsed_time(e1))
+            res[f"tpr{tv}"] = {"median_ms": round(statistics.median(ts), 4), "same_rows": bool(torch.equal(X, ref))}
+        native.set_variant("blobs_tpr", -1)
     # the write floor: torch's vectorised fill of the same bytes
     ts = []
     for r in range(a.reps + 2):
