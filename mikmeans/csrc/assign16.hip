@@ -82,18 +82,6 @@ struct Assign16Cfg {
   static_assert(PIECES % NW == 0, "chunk pieces must split evenly over waves");
 };
 
-// An MFMA seed plus a per-point offset, as four scalar v_add_f32.  Never a packed
-// v_pk_add_f32: seeds built that way (op_sel broadcasts of the offset) intermittently
-// reached the next MFMA wrong on gfx950 -- one point block of a per-point-offset
-// workgroup got labels from a corrupted seed in 5 of 12 launches
-// (scripts/debug/keys_d32_repro.py, profiles/r3_15_ppo_seed_race.md).  The file is built
-// with -fno-slp-vectorize (mikmeans/_build.py), so these stay scalar.
-__device__ __forceinline__ void seed_add(f32x4& acc, float o) {
-  float a0 = acc[0], a1 = acc[1], a2 = acc[2], a3 = acc[3];
-  a0 += o; a1 += o; a2 += o; a3 += o;
-  acc = f32x4{a0, a1, a2, a3};
-}
-
 template <typename T> struct Mfma16;
 template <> struct Mfma16<uint16_t> {
   __device__ static __forceinline__ f32x4 run(const u32x4& a, const u32x4& b, const f32x4& c) {
@@ -983,6 +971,9 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
     // MFMAs, half the LDS reads and chunk barriers per MFMA of the default); 5: 4 blocks
     if (gm == 4) return launch16_t<T, DPAD, 6, CT, 2, 2, 4, true>(a, s);
     if (gm == 5) return launch16_t<T, DPAD, 4, CT, 2, 2, 4, true>(a, s);
+    // 6: the default with a 3-slot ring (two chunks in flight: a 2-tile chunk is only ~1 us of
+    // MFMA work per wave at 3 waves/SIMD, about one L2 round trip); 50 KiB LDS, 3 per CU
+    if (gm == 6) return launch16_t<T, DPAD, 3, CT, 3, 3>(a, s);
   }
   if constexpr (sizeof(T) == 2 && DPAD == 128) {
     // A/B switch V_ASSIGN_GEOM: 1 = 8 waves share a ring of 32 KiB chunks (a barrier
@@ -1040,6 +1031,7 @@ static int block_rows_t(int kpad) {
 }
 
 int assign16_block_rows(int dtype, int dpad, int kpad) {
+  if (variant(V_ASSIGN_CS) > 0 && assign_cs_eligible(dtype, dpad, kpad)) return 64;   // its super-block
   if (dtype == DT_BF16) {
     switch (dpad) {
       case 32: return block_rows_t<uint16_t, 32>(kpad);
@@ -1068,6 +1060,7 @@ int assign16_block_rows(int dtype, int dpad, int kpad) {
 }
 
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s) {
+  if (variant(V_ASSIGN_CS) > 0 && assign_cs_takes(dtype, dpad, a)) return launch_assign_cs(dpad, a, s);
   if (dtype == DT_BF16) {
     switch (dpad) {
       case 32: return launch16_d<uint16_t, 32>(a, s);

@@ -614,7 +614,8 @@ namespace mk {
 static const char* const kVariantEnv[V_COUNT] = {"MIKMEANS_ASSIGN_VARG", "MIKMEANS_ASSIGN_PMAJ",
                                                  "MIKMEANS_ASSIGN_GEOM", "MIKMEANS_UPDATE_KS",
                                                  "MIKMEANS_UPDATE_KS_GM", "MIKMEANS_BLOBS_TPR",
-                                                 "MIKMEANS_ASSIGN_PERSIST", "MIKMEANS_ASSIGN_TOP2_GEOM"};
+                                                 "MIKMEANS_ASSIGN_PERSIST", "MIKMEANS_ASSIGN_TOP2_GEOM",
+                                                 "MIKMEANS_ASSIGN_CS"};
 static int* variant_table() {
   static int t[V_COUNT] = {};
   static const bool init = [] {

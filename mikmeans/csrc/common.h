@@ -100,6 +100,18 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// An MFMA seed plus a per-point offset, as four scalar v_add_f32.  Never a packed
+// v_pk_add_f32: seeds built that way (op_sel broadcasts of the offset) intermittently
+// reached the next MFMA wrong on gfx950 -- one point block of a per-point-offset
+// workgroup got labels from a corrupted seed in 5 of 12 launches
+// (scripts/debug/keys_d32_repro.py, profiles/r3_15_ppo_seed_race.md).  Files that use it are
+// built with -fno-slp-vectorize (mikmeans/_build.py), so these stay scalar.
+__device__ __forceinline__ void seed_add(f32x4& acc, float o) {
+  float a0 = acc[0], a1 = acc[1], a2 = acc[2], a3 = acc[3];
+  a0 += o; a1 += o; a2 += o; a3 += o;
+  acc = f32x4{a0, a1, a2, a3};
+}
+
 // Volatile form: also a scheduling barrier, which keeps MFMA groups contiguous.
 __device__ __forceinline__ float min3f_v(float a, float b, float c) {
   float d;

@@ -33,7 +33,7 @@ constexpr int SLOT_STRIDE = 8;
 // changed only through set_variant (mikmeans.ops.native.variant); -1 = the built-in rule.
 // A captured hipGraph keeps the geometry that was in force when it was recorded.
 enum Variant { V_ASSIGN_VARG = 0, V_ASSIGN_PMAJ, V_ASSIGN_GEOM, V_UPDATE_KS, V_UPDATE_KS_GM, V_BLOBS_TPR,
-               V_ASSIGN_PERSIST, V_ASSIGN_TOP2_GEOM, V_COUNT };
+               V_ASSIGN_PERSIST, V_ASSIGN_TOP2_GEOM, V_ASSIGN_CS, V_COUNT };
 int variant(Variant v);
 void set_variant(Variant v, int value);
 
@@ -75,6 +75,11 @@ hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t
 // Rows per workgroup of the full (ungathered, unbounded) assign for this shape: the block its
 // bf16 seed offset is taken over (mirrors launch16_d / launch16_w)
 int assign16_block_rows(int dtype, int dpad, int kpad);
+// The centre-stationary bf16 assign (assign_cs.hip; A/B switch V_ASSIGN_CS = 1): whether it
+// handles a shape, and its launcher (plain full passes with row norms only).
+bool assign_cs_eligible(int dtype, int dpad, int kpad);
+bool assign_cs_takes(int dtype, int dpad, const AssignArgs& a);
+hipError_t launch_assign_cs(int dpad, const AssignArgs& a, hipStream_t s);
 // oseed[i] = the full pass's seed offset of row i (block_rows from assign16_block_rows; bf16)
 hipError_t launch_seed_offsets(const float* xn, int64_t n, int block_rows, float* oseed, hipStream_t s);
 

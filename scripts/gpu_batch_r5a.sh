@@ -2,7 +2,7 @@
 # round-5 GPU batch: D=256 geometry A/B, setup-pass timing, W=2/4/8 multi-rank tests, cfg5 with prefetch
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
 timeout -k 10 300 python -u scripts/assign_ab.py --n 16777216 --d 256 --k 512 --rounds 4 --reps 10 \
-  --arms "default;assign_geom=3;assign_geom=4;assign_geom=5" > gpurun_out/r5_13_ab_d256_ast.log 2>&1 || exit $?
+  --arms "default;assign_geom=3;assign_geom=4;assign_geom=5;assign_geom=6" > gpurun_out/r5_13_ab_d256_ast.log 2>&1 || exit $?
 timeout -k 10 300 python -u scripts/setup_pass_bench.py > gpurun_out/r5_14_setup_pass.log 2>&1 || exit $?
 timeout -k 10 600 python -u -m pytest tests/test_gpu_multirank.py -q --timeout 600 --timeout-method thread \
   > gpurun_out/r5_15_multirank.log 2>&1 || exit $?

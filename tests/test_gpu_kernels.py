@@ -899,3 +899,46 @@ def test_kmeans_transform_uses_kernel(native):
     assert torch.equal(top2.indices[:, 0][clear].int(), lab[clear])
     Dn = km.transform(X[:100].cpu().float().numpy())
     assert Dn.shape == (100, 12)
+
+
+@pytest.mark.parametrize("n,d,k,outlier", [(20_000, 128, 256, False), (9000, 128, 1024, False),
+                                           (3000, 256, 512, False), (255, 100, 70, False),
+                                           (70_001, 256, 77, True), (300_007, 128, 1000, True),
+                                           (1, 128, 16, False), (65, 256, 33, False)])
+def test_assign_centre_stationary(native, kvariant, n, d, k, outlier):
+    """The centre-stationary kernel (csrc/assign_cs.hip, switch ``assign_cs``): near-optimal
+    labels and distances against the f64 reference, the inertia and changed count of its
+    outputs, and -- its exactness contract -- bitwise the labels and distances of the streaming
+    kernel run row by row with the 64-row seed offsets it reports (a gathered pass with
+    ``oseed``); with an outlier row its super-block takes per-point offsets."""
+    from mikmeans.ops import pad_columns
+
+    g = torch.Generator().manual_seed(n + d + k)
+    X = torch.randn(n, d, generator=g)
+    if outlier:
+        X[n // 3] *= 500.0
+    Xb = pad_columns(X.to(torch.bfloat16).to(DEV))
+    C = torch.randn(k, d, generator=g) * 0.8
+    pk = ops.pack_centers(C.to(DEV), Xb.shape[1], torch.bfloat16, DEV)
+    xn = ops.row_sqnorm(Xb)
+    kvariant("assign_cs", 1)
+    assert native.assign_block_rows(pk.dt, pk.dpad, pk.Kpad) == 64
+    lab = torch.full((n,), 5, dtype=torch.int32, device=DEV)
+    mind = torch.empty(n, device=DEV)
+    slots = torch.zeros(native.NSLOT * native.SLOT_STRIDE, dtype=torch.float64, device=DEV)
+    pk.assign(Xb, xn, lab, mind, slots, True)
+    oseed = pk.seed_offsets(xn)
+    rows = torch.arange(n, device=DEV)
+    lab_g = torch.empty(n, dtype=torch.int32, device=DEV)
+    mind_g = torch.empty(n, device=DEV)
+    pk.assign(Xb, xn, lab_g, mind_g, rows=rows, oseed=oseed)   # (gathered: the streaming kernel)
+    torch.cuda.synchronize()
+    assert torch.equal(lab, lab_g) and torch.equal(mind, mind_g)
+    _check_assign(X.to(torch.bfloat16), C, lab, mind, rel=3e-5)
+    tot = slots.view(-1, native.SLOT_STRIDE)[:, :2].sum(0)
+    assert float(tot[1]) == int((lab != 5).sum())
+    assert float(tot[0]) == pytest.approx(float(mind.double().sum()), rel=1e-9)
+    # no change tracking, no distances: same labels
+    lab2 = torch.zeros(n, dtype=torch.int32, device=DEV)
+    pk.assign(Xb, xn, lab2)
+    assert torch.equal(lab2, lab)
