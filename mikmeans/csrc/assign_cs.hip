@@ -41,16 +41,16 @@ struct CsCfg {
   static constexpr int SPTS = SB * 16;             // points per super-block
   static constexpr int SLOT = SB * NQ * 1024;      // ring slot bytes
   static constexpr int NB = 3;                     // ring slots (two super-blocks in flight)
-  static constexpr int NXB = 4;                    // |x|^2 ring (read by the finisher one step late)
+  static constexpr int NXB = 8;                    // |x|^2 ring (fetched a step ahead of the rows,
+                                                   // read by the finisher a step behind)
   static constexpr int NDMA = SB * NQ;             // 1-KiB DMA instructions per super-block
   static constexpr int FIN = NW - 1;               // the finisher wave (no DMA duty)
   static constexpr int NDW = NW - 1;               // waves sharing the DMA
-  // DMA instructions of wave w per super-block (fragments d = w, w + NDW, ...; wave NDW-1 also
-  // fetches the 64 row norms)
-  static constexpr int dma_of(int w) {
+  // row DMA instructions of wave w per super-block (fragments d = w, w + NDW, ...)
+  static constexpr __device__ int dma_x(int w) {
     int c = 0;
     for (int d = w; d < NDMA; d += NDW) ++c;
-    return c + (w == NDW - 1 ? 1 : 0);
+    return c;
   }
 };
 
@@ -84,7 +84,8 @@ __global__ __launch_bounds__(1024, 1) void assign_cs_kernel(AssignArgs a) {
   float* xnr = (float*)(smem + C::NB * C::SLOT);                         // [NXB][SPTS]
   uint32_t* mrg = (uint32_t*)(xnr + C::NXB * C::SPTS);                   // [2][NW][SPTS] wave winners
   f32x4* sdl = (f32x4*)(mrg + 2 * C::NW * C::SPTS);                      // [NW][T][64] seeds
-  float* cnl = (float*)(sdl + C::NW * T * 64);                           // [Kpad]
+  float* offl = (float*)(sdl + C::NW * T * 64);                          // [4] super-block offsets
+  float* cnl = offl + 4;                                                 // [Kpad]
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, g = lane >> 4;
@@ -96,7 +97,8 @@ __global__ __launch_bounds__(1024, 1) void assign_cs_kernel(AssignArgs a) {
   const int tw = min(max(ntiles - wid * T, 0), T);   // this wave's tiles (wave-uniform)
   const size_t rowb = (size_t)a.ldx * 2;             // bytes per X row
 
-  // centres: A fragments into registers for the fit of the kernel's life, |c|^2 into LDS
+  // centres: A fragments into registers for the kernel's life (tiles past Kpad: zeros, seeded
+  // with PAD_SCORE below, so they never win and the MFMA loop needs no per-tile guard)
   const uint16_t* pack = (const uint16_t*)a.Cpack;
   u32x4 af[T][NQ];
 #pragma unroll
@@ -108,13 +110,15 @@ __global__ __launch_bounds__(1024, 1) void assign_cs_kernel(AssignArgs a) {
   }
   for (int k = threadIdx.x; k < a.Kpad; k += 1024) cnl[k] = a.cn[k];
 
-  // LDS-DMA of super-block s (its i-th) into ring slot i % NB and |x|^2 slot i % NXB; rows past
-  // N read as zeros (buffer bounds)
-  const int my_dma = C::dma_of(wid);
-  auto issue = [&](int64_t i) {
-    const int64_t sb = blockIdx.x + i * gridDim.x;
-    const int64_t r0 = sb * C::SPTS;
-    const int64_t nv = N - r0 < C::SPTS ? N - r0 : C::SPTS;
+  // LDS-DMA of the i-th super-block's rows into ring slot i % NB (rows past N read as zeros:
+  // buffer bounds), and -- one step further ahead -- of its row norms into |x|^2 slot i % NXB
+  auto sb_rows = [&](int64_t i, int64_t& r0) {   // (rows of the i-th super-block; <= 0 past the end)
+    r0 = (blockIdx.x + i * gridDim.x) * (int64_t)C::SPTS;
+    return N - r0 < C::SPTS ? N - r0 : (int64_t)C::SPTS;
+  };
+  auto issue_x = [&](int64_t i) {
+    int64_t r0;
+    const int64_t nv = sb_rows(i, r0);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc((const char*)a.X + (size_t)r0 * rowb, (uint32_t)(nv * rowb));
     char* slot = ring + (int)(i % C::NB) * C::SLOT;
 #pragma unroll
@@ -128,17 +132,21 @@ __global__ __launch_bounds__(1024, 1) void assign_cs_kernel(AssignArgs a) {
         blds16(rx, (MK_LDS void*)(slot + d * 1024), voff, 0u);
       }
     }
-    if (wid == C::NDW - 1) {
-      const __amdgpu_buffer_rsrc_t rn = make_rsrc(a.xn + r0, (uint32_t)(nv * 4));
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (MK_LDS void*)(xnr + (int)(i % C::NXB) * C::SPTS), 4,
-                                               (uint32_t)lane * 4u, 0u, 0, 0);
-    }
   };
+  auto issue_xn = [&](int64_t i) {   // (wave NDW-1; past the last super-block: an empty buffer)
+    int64_t r0;
+    const int64_t nv = sb_rows(i, r0);
+    const __amdgpu_buffer_rsrc_t rn = make_rsrc(nv > 0 ? a.xn + r0 : a.xn, (uint32_t)(nv > 0 ? nv * 4 : 0));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (MK_LDS void*)(xnr + (int)(i % C::NXB) * C::SPTS), 4,
+                                             (uint32_t)lane * 4u, 0u, 0, 0);
+  };
+  constexpr int XNW = C::NDW - 1;   // the wave that fetches the row norms
   if (wid != C::FIN) {
-    issue(0);
-    if (cnt > 1) issue(1);
+    issue_x(0);
+    if (cnt > 1) issue_x(1);
+    if (wid == XNW) { issue_xn(0); issue_xn(1); issue_xn(2); }
   }
-  __syncthreads();   // (cn, merge slots and the centre fragments' loads: vmcnt(0) drains the DMA too)
+  __syncthreads();   // (cn and the centre fragments' loads: vmcnt(0) drains the DMA too)
 
   const unsigned kmask = key6_mask();
   const int nwt = (ntiles + T - 1) / T;   // waves holding centres
@@ -149,23 +157,22 @@ __global__ __launch_bounds__(1024, 1) void assign_cs_kernel(AssignArgs a) {
   int changed = 0;
   const bool want_mind = a.mind != nullptr;
 
-  // the super-block's seed offset(s) from its row norms in LDS (every wave computes them)
-  auto offsets = [&](int64_t i, float& off, bool& ppo, float& xs) {
-    const int64_t sb = blockIdx.x + i * gridDim.x;
-    const int64_t nv = N - sb * C::SPTS < C::SPTS ? N - sb * C::SPTS : C::SPTS;
-    const float* xb = xnr + (int)(i % C::NXB) * C::SPTS;
-    xs = xb[lane < nv ? lane : (int)nv - 1];      // (past the end: the last row's, as assign16 clamps)
+  // (finisher) the i-th super-block's seed offset from its row norms, into LDS slot i % 4 for
+  // every wave: the shared offset, or -1 for per-point offsets (max > 4 min)
+  auto offsets = [&](int64_t i) {
+    int64_t r0;
+    const int64_t nv = sb_rows(i, r0);
+    if (nv <= 0) return;
+    const float xs = xnr[(int)(i % C::NXB) * C::SPTS + (lane < nv ? lane : (int)nv - 1)];   // (assign16 clamps)
     const float m = wave_max_f(fmaxf(0.f, xs)), mn = wave_min_f(fminf(3.0e38f, xs));
-    ppo = m > 4.f * mn;
-    off = ppo ? 0.f : __builtin_fmaf(m, 2.44140625e-04f, m);
+    if (lane == 0) offl[(int)(i & 3)] = m > 4.f * mn ? -1.f : __builtin_fmaf(m, 2.44140625e-04f, m);
   };
 
-  auto finish = [&](int64_t i, int old) {   // (finisher) super-block i's outputs; its merge slots reset
-    const int64_t sb = blockIdx.x + i * gridDim.x;
-    const int64_t row = sb * C::SPTS + lane;
-    float off, xs;
-    bool ppo;
-    offsets(i, off, ppo, xs);
+  auto finish = [&](int64_t i, int old) {   // (finisher) super-block i's outputs
+    int64_t r0;
+    const int64_t nv = sb_rows(i, r0);
+    const float xs = xnr[(int)(i % C::NXB) * C::SPTS + lane];
+    const float off = offl[(int)(i & 3)];
     // the 16 waves' winners of each point: lexicographic (truncated score, wave, local index) --
     // the waves' centre ranges ascend, so that is (score, centre index)
     const uint32_t* ms = mrg + (int)(i & 1) * C::NW * C::SPTS + lane;
@@ -175,97 +182,112 @@ __global__ __launch_bounds__(1024, 1) void assign_cs_kernel(AssignArgs a) {
       const uint32_t kw = ms[w * C::SPTS];
       if ((kw & ~63u) < (best & ~63u)) { best = kw; bw = w; }
     }
-    if (row < N) {
-      const float offp = ppo ? __builtin_fmaf(xs, 2.44140625e-04f, xs) : off;
+    if (lane < nv) {
+      const float offp = off < 0.f ? __builtin_fmaf(xs, 2.44140625e-04f, xs) : off;
       const int k = bw * T * 16 + (int)(best & 63u);
       const float v = __uint_as_float(best & ~63u) - offp;
       const float d = fmaxf(xs + v, 0.f);
       if (a.track_changed) changed += (old != k);
-      a.labels[row] = k;
-      if (want_mind) a.mind[row] = d;
+      a.labels[r0 + lane] = k;
+      if (want_mind) a.mind[r0 + lane] = d;
       inert += (double)d;
     }
   };
 
+  // one 16-point block against this wave's T tiles: seeds from LDS (+ the point's own offset
+  // under PPO), NQ K-steps, the lane's 6-bit key minimum, then the 4 lane groups' via two
+  // shuffles; the winner (truncated score | local index 16t + 4g + reg) parked for the finisher
+  auto block = [&](auto ppo_tag, const char* slot, const float* xb, const f32x4* sdw, uint32_t* ms, int j) {
+    constexpr bool PPO = decltype(ppo_tag)::value;
+    const char* blk = slot + j * NQ * 1024 + lane * 16;
+    f32x4 acc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[t] = sdw[t * 64];
+    if constexpr (PPO) {
+      const float xv = xb[16 * j + r];
+      const float op = __builtin_fmaf(xv, 2.44140625e-04f, xv);
+#pragma unroll
+      for (int t = 0; t < T; ++t) seed_add(acc[t], op);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_sched_barrier(0);
+    u32x4 b0 = *(const u32x4*)blk;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      u32x4 b1;
+      if (q + 1 < NQ) b1 = *(const u32x4*)(blk + (q + 1) * 1024);
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(short8, af[t][q]),
+                                                         __builtin_bit_cast(short8, b0), acc[t], 0, 0, 0);
+      if (q + 1 < NQ) b0 = b1;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    // keys: truncated score | (16 t + reg) -- wave-uniform index bits (lane group g added after
+    // the lane's minimum, bits 2-3), so each key is one v_and_or_b32
+    float kb = 3.0e38f;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float k0 = pack_key6(acc[t][0], kmask, (unsigned)(16 * t + 0));
+      const float k1 = pack_key6(acc[t][1], kmask, (unsigned)(16 * t + 1));
+      const float k2 = pack_key6(acc[t][2], kmask, (unsigned)(16 * t + 2));
+      const float k3 = pack_key6(acc[t][3], kmask, (unsigned)(16 * t + 3));
+      kb = min3f(min3f(k0, k1, k2), k3, kb);
+    }
+    uint32_t kbits = __float_as_uint(kb) | ((uint32_t)g << 2);     // local index 16t + 4g + reg
+    kbits = lane_min_x32(lane_min_x16(kbits));                      // (positive floats: integer order)
+    if (g == 0) ms[16 * j + r] = kbits;
+  };
+
+  if (wid == C::FIN) offsets(0);
   for (int64_t i = 0; i < cnt; ++i) {
-    // super-block i landed: each DMA wave waits for its own instructions of i (those of i+1 may
-    // stay in flight), then the barrier publishes all of them and the merge-slot resets
+    // super-block i landed: each DMA wave waits for its own instructions of i (those issued a
+    // step ago may stay in flight), then the barrier publishes them, the merge slots and offsets
     if (wid != C::FIN) {
-      if (i + 1 < cnt) wait_vm_n<3>(my_dma); else wait_vmcnt<0>();
+      const int ahead = (i + 1 < cnt ? C::dma_x(wid) : 0) + (wid == XNW ? 1 : 0);
+      wait_vm_n<3>(ahead);
     }
     wait_lgkm0();
     raw_barrier();
     if (wid != C::FIN) {
-      if (i + 2 < cnt) issue(i + 2);   // (slot (i+2) % NB was last read at step i-1)
+      if (i + 2 < cnt) issue_x(i + 2);   // (slot (i+2) % NB was last read at step i-1)
+      if (wid == XNW) issue_xn(i + 3);   // (slot (i+3) % NXB: none of i-1 .. i+2)
     } else {
-      // the finisher: old labels of super-block i for the next step, then super-block i-1's outputs
-      const int64_t row_i = (blockIdx.x + i * gridDim.x) * C::SPTS + lane;
+      // the finisher: old labels of super-block i for the next step, super-block i-1's outputs,
+      // super-block i+1's offsets (its norms landed with this step's wait)
+      int64_t r0;
+      const int64_t nv = sb_rows(i, r0);
       const int prev_old = oldl;
-      oldl = row_i < N ? a.labels[row_i] : -2;
+      oldl = lane < nv ? a.labels[r0 + lane] : -2;
       if (i > 0) finish(i - 1, prev_old);
+      if (i + 1 < cnt) offsets(i + 1);
     }
-    float off, xs;
-    bool ppo;
-    offsets(i, off, ppo, xs);
-    const char* slot = ring + (int)(i % C::NB) * C::SLOT;
-    uint32_t* ms = mrg + (int)(i & 1) * C::NW * C::SPTS + wid * C::SPTS;
-    const float* xb = xnr + (int)(i % C::NXB) * C::SPTS;
     if (tw > 0) {
+      const char* slot = ring + (int)(i % C::NB) * C::SLOT;
+      uint32_t* ms = mrg + (int)(i & 1) * C::NW * C::SPTS + wid * C::SPTS;
+      const float* xb = xnr + (int)(i % C::NXB) * C::SPTS;
+      const float off = offl[(int)(i & 3)];
       // this wave's seeds per tile in LDS (not registers: the centre fragments fill those):
-      // fl(|c|^2 + o) with the super-block's shared offset, or |c|^2 for per-point offsets
+      // fl(|c|^2 + o) with the shared offset, |c|^2 for per-point offsets, PAD past Kpad
       f32x4* sdw = sdl + wid * T * 64 + lane;
 #pragma unroll
       for (int t = 0; t < T; ++t) {
-        f32x4 c = *(const f32x4*)(cnl + (wid * T + t) * 16 + 4 * g);
-        if (!ppo) seed_add(c, off);
+        f32x4 c = f32x4{PAD_SCORE, PAD_SCORE, PAD_SCORE, PAD_SCORE};
+        if (t < tw) {
+          c = *(const f32x4*)(cnl + (wid * T + t) * 16 + 4 * g);
+          if (off >= 0.f) seed_add(c, off);
+        }
         sdw[t * 64] = c;
       }
+      if (off >= 0.f) {
 #pragma unroll
-      for (int j = 0; j < C::SB; ++j) {
-        const char* blk = slot + j * NQ * 1024 + lane * 16;
-        f32x4 acc[T];
-        const float op = ppo ? __builtin_fmaf(xb[16 * j + r], 2.44140625e-04f, xb[16 * j + r]) : 0.f;
+        for (int j = 0; j < C::SB; ++j) block(std::false_type{}, slot, xb, sdw, ms, j);
+      } else {
 #pragma unroll
-        for (int t = 0; t < T; ++t) {
-          acc[t] = sdw[t * 64];
-          if (ppo) seed_add(acc[t], op);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-        __builtin_amdgcn_sched_barrier(0);
-        u32x4 b0 = *(const u32x4*)blk;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          u32x4 b1;
-          if (q + 1 < NQ) b1 = *(const u32x4*)(blk + (q + 1) * 1024);
-#pragma unroll
-          for (int t = 0; t < T; ++t) {
-            if (t < tw)
-              acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(short8, af[t][q]),
-                                                               __builtin_bit_cast(short8, b0), acc[t], 0, 0, 0);
-          }
-          if (q + 1 < NQ) b0 = b1;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        // keys: truncated score | (16 t + reg) -- wave-uniform index bits (lane group g added
-        // after the lane's minimum, bits 2-3), so each key is one v_and_or_b32
-        float kb = 3.0e38f;
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-          if (t < tw) {
-            const float k0 = pack_key6(acc[t][0], kmask, (unsigned)(16 * t + 0));
-            const float k1 = pack_key6(acc[t][1], kmask, (unsigned)(16 * t + 1));
-            const float k2 = pack_key6(acc[t][2], kmask, (unsigned)(16 * t + 2));
-            const float k3 = pack_key6(acc[t][3], kmask, (unsigned)(16 * t + 3));
-            kb = min3f(min3f(k0, k1, k2), k3, kb);
-          }
-        }
-        uint32_t kbits = __float_as_uint(kb) | ((uint32_t)g << 2);   // local index 16t + 4g + reg
-        kbits = min(kbits, (uint32_t)__shfl_xor((int)kbits, 16, 64));  // (positive floats: integer order)
-        kbits = min(kbits, (uint32_t)__shfl_xor((int)kbits, 32, 64));
-        if (g == 0) ms[16 * j + r] = kbits;
+        for (int j = 0; j < C::SB; ++j) block(std::true_type{}, slot, xb, sdw, ms, j);
       }
     }
   }
@@ -290,7 +312,7 @@ template <int DPAD>
 static hipError_t launch_cs_t(const AssignArgs& a, hipStream_t s) {
   using C = CsCfg<DPAD>;
   const size_t lds = (size_t)C::NB * C::SLOT + C::NXB * C::SPTS * 4 + 2 * C::NW * C::SPTS * 4 + C::NW * C::T * 64 * 16 +
-                     (size_t)a.Kpad * 4;
+                     16 + (size_t)a.Kpad * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
@@ -321,8 +343,9 @@ bool assign_cs_eligible(int dtype, int dpad, int kpad) {
 }
 
 bool assign_cs_takes(int dtype, int dpad, const AssignArgs& a) {
+  // (a split_keys scratch is only an offer: the streaming launcher splits small batches)
   return assign_cs_eligible(dtype, dpad, a.Kpad) && a.Kpad % 16 == 0 && a.xn && a.labels && !a.rows && !a.ub &&
-         !a.split_keys && !a.n_dev && !a.oseed && !a.scatter;
+         !a.n_dev && !a.oseed && !a.scatter;
 }
 
 hipError_t launch_assign_cs(int dpad, const AssignArgs& a, hipStream_t s) {

@@ -139,6 +139,19 @@ __device__ __forceinline__ float split_value(unsigned long long key) {
 }
 
 // ---------------------------------------------------------------------------
+// Unsigned minimum over lanes l and l ^ 16 / l ^ 32 with the gfx950 lane swaps (one VALU op
+// each, no LDS traffic and no address arithmetic, unlike a ds_bpermute shuffle): swapping a
+// value with itself leaves each lane holding itself in one result and its partner in the other.
+__device__ __forceinline__ uint32_t lane_min_x16(uint32_t x) {
+  const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  return min((uint32_t)p[0], (uint32_t)p[1]);
+}
+__device__ __forceinline__ uint32_t lane_min_x32(uint32_t x) {
+  const auto p = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return min((uint32_t)p[0], (uint32_t)p[1]);
+}
+
+// ---------------------------------------------------------------------------
 // 64-lane reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

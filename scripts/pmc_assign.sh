@@ -14,6 +14,6 @@ for i in 1 2 3; do
   rm -rf gpurun_out/pmca_$name$i
   timeout -s KILL 120 rocprofv3 --pmc $P --kernel-trace --output-format csv -d gpurun_out/pmca_$name$i -- \
     python3 scripts/assign_ab.py --rounds 1 --reps 3 --arms default "$@" > gpurun_out/pmca_$name$i.log 2>&1 || exit $?
-  python3 scripts/summarize_pmc.py gpurun_out/pmca_$name$i --match assign16 >> gpurun_out/pmca_$name.md
+  python3 scripts/summarize_pmc.py gpurun_out/pmca_$name$i --match ${MATCH:-assign16} >> gpurun_out/pmca_$name.md
 done
 echo pmc-done
