@@ -54,8 +54,9 @@ def main(argv=None):
     ap.add_argument("--shard-rows", type=int, default=None,
                     help="cfg5 --resident: rows per rank (default N/8: the W=8 shard of N=1e9, 64 GB)")
     ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=False,
-                    help="cfg5: generate the next batch on a side stream while the current one is fitted "
-                         "(measured no faster: profiles/r1_18_blobstream_prefetch_ab.json)")
+                    help="cfg5: generate the next batch on a side stream, started between the "
+                         "current batch's assign and its M-step (mikmeans/data/blobs.py kick); measured "
+                         "no faster: the M-step's workgroups hold the CUs (profiles/r5_27_cfg5_*.log)")
     ap.add_argument("--incremental", action="store_true",
                     help="incremental M-step (re-scatter changed rows only; not the headline mode)")
     ap.add_argument("--also-incremental", action=argparse.BooleanOptionalAction, default=True,
@@ -392,6 +393,8 @@ def _bench_minibatch(args, cfg, comm, dtype):
                             prefetch=args.prefetch)  # batch j+1 generated on a side stream during step j
         # the generator's value bound fixes the fixed-point scales up front (no per-step clamp check)
         eng = MiniBatchEngine(K, D, b, dtype=dtype, device=dev, comm=comm, value_bound=stream.value_bound)
+        if args.prefetch:
+            eng.after_assign = stream.kick   # batch j+1's generator overlaps batch j's M-step
 
         def gen():
             Xb = next(stream)

@@ -161,6 +161,7 @@ class BlobStream:
         # (event recorded when the next batch is requested) before overwriting it.
         self.prefetch = bool(prefetch) and self.device.type == "cuda"
         self._pf = None          # (X, norms, ready event) of the batch generated ahead
+        self._pending = None     # step whose generation waits for kick()
         self._pool = []
         self._side = torch.cuda.Stream(device=self.device) if self.prefetch else None
 
@@ -178,7 +179,7 @@ class BlobStream:
     def seek(self, pos: int) -> "BlobStream":
         """Continue the global row sequence at ``pos`` -- with any world size: a resumed
         job with the same global batch (``batch * world``) sees the same rows per step."""
-        if self.prefetch and self._pf is not None:
+        if self.prefetch and (self._pf is not None or self._pending is not None):
             raise RuntimeError("seek() before the first batch of a prefetching stream")
         self.offset, self.step = int(pos), 0
         return self
@@ -207,24 +208,40 @@ class BlobStream:
                        device=self.device, centers=self.centers, out=Xb[:n], norms=nrm)
         return X, nrm
 
+    def kick(self) -> None:
+        """Start generating the next batch now (prefetch streams; no-op otherwise).  The side
+        stream starts once the caller's stream reaches this point, so a consumer that calls
+        it between its matrix-core assign and its memory-bound M-step (``MiniBatchEngine.
+        after_assign``) overlaps the VALU-bound generator with the M-step instead of racing
+        the assign for the CUs.  Without a kick, the next batch starts when this one is taken."""
+        if self._pending is None:
+            return
+        j = self._pending
+        self._pending = None
+        cur = torch.cuda.current_stream(self.device)
+        # everything the caller enqueued on batch j-2 (slot j % 2) precedes this point
+        freed = torch.cuda.Event()
+        freed.record(cur)
+        self._side.wait_event(freed)
+        with torch.cuda.stream(self._side):
+            Xn, nn = self._gen(j, j % 2)
+            ready = torch.cuda.Event()
+            ready.record(self._side)
+        self._pf = (Xn, nn, ready)
+
     def _next_prefetch(self) -> torch.Tensor:
         cur = torch.cuda.current_stream(self.device)
         j = self.step
+        self.kick()                               # (a batch not kicked yet starts now)
         if self._pf is None:                      # first batch: generate in order
             X, nrm = self._gen(j, j % 2)
         else:
             X, nrm, ev = self._pf
             cur.wait_event(ev)
-        # the caller has enqueued all its work on batch j-1 (slot (j+1) % 2): the side
-        # stream may overwrite that slot once the caller's stream gets past this point
-        freed = torch.cuda.Event()
-        freed.record(cur)
-        self._side.wait_event(freed)
-        with torch.cuda.stream(self._side):
-            Xn, nn = self._gen(j + 1, (j + 1) % 2)
-            ready = torch.cuda.Event()
-            ready.record(self._side)
-        self._pf = (Xn, nn, ready)
+        # batch j+1 goes to slot (j+1) % 2, batch j-1's: generated at the next kick(), when
+        # the caller has enqueued all its work on batch j-1
+        self._pending = j + 1
+        self._pf = None
         self.step += 1
         self.last_norms = nrm
         return X

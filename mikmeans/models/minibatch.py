@@ -43,6 +43,10 @@ class MiniBatchEngine:
             self.frozen = torch.as_tensor(frozen, dtype=torch.uint8).reshape(-1).to(self.device)
         self.steps = 0
         self.batch_inertia = 0.0
+        # optional host callback between a step's assign and its M-step (enqueue time), e.g.
+        # a prefetching BlobStream's kick(): the next batch's generator then overlaps the
+        # memory-bound M-step rather than the matrix-core assign
+        self.after_assign = None
         if self.gpu and native.dpad_for(self.Dp, dtype) == 0:
             native.warn_once(f"D={self.D} > 1024: mini-batch steps use the PyTorch GEMM path")
             self.gpu = False
@@ -192,6 +196,8 @@ class MiniBatchEngine:
         lab = self.labels[:b]
         if b:
             self.pk.assign(Xp, None, lab, None, self.slots, False, rows=rows)
+        if self.after_assign is not None:
+            self.after_assign()
         self._mstep(Xp, lab, rows)
         self.pk.finalize(2, self.packed, self.C, self.Cnew, self.frozen, self.vcount, self.shift, self.counts)
         self.C, self.Cnew = self.Cnew, self.C
@@ -210,6 +216,8 @@ class MiniBatchEngine:
             # key offsets and the inertia from the row fragments (no caller norms): the
             # gathered-row path (partial_fit_rows) computes them the same way, bit for bit
             self.pk.assign(Xb, None, lab, None, self.slots, False)
+        if self.after_assign is not None:
+            self.after_assign()
         self._mstep(Xb, lab)
         if not self.bounded:
             # one host read per step: the all-reduced clamp count is the same on every rank,

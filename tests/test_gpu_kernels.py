@@ -213,14 +213,17 @@ def test_blobs_match_numpy_mirror(native, dtype):
 
 
 def test_blob_stream_prefetch_is_identical(native):
-    """Side-stream prefetch (bench cfg5) yields the same batches and the same mini-batch fit."""
+    """Side-stream prefetch (bench cfg5) yields the same batches and the same mini-batch fit --
+    also when the engine kicks the next batch's generation between its assign and M-step."""
     from mikmeans.models.minibatch import MiniBatchEngine
 
     D, K, b = 64, 32, 4096
     res = []
-    for pf in (False, True):
+    for pf, kick in ((False, False), (True, False), (True, True)):
         s = B.BlobStream(10**6, D, K, b, seed=5, dtype=torch.bfloat16, device=DEV, with_norms=True, prefetch=pf)
         eng = MiniBatchEngine(K, D, b, dtype=torch.bfloat16, device=DEV)
+        if kick:
+            eng.after_assign = s.kick
         X0 = next(s)
         eng.set_centers(X0[:K].float())
         batches = [X0.clone()]
@@ -230,9 +233,10 @@ def test_blob_stream_prefetch_is_identical(native):
             eng.partial_fit(Xb, s.last_norms)
         torch.cuda.synchronize()
         res.append((batches, eng.C.clone()))
-    for a, c in zip(res[0][0], res[1][0]):
-        assert torch.equal(a, c)
-    assert torch.equal(res[0][1], res[1][1])
+    for r in res[1:]:
+        for a, c in zip(res[0][0], r[0]):
+            assert torch.equal(a, c)
+        assert torch.equal(res[0][1], r[1])
 
 
 def _resolvable_argmin(X, C, rel=1e-5):
