@@ -19,7 +19,7 @@ N, D, K = 10_000_000, 64, 4096
 dev = torch.device("cuda")
 comm = Comm.local(dev)
 X = make_blobs(N, D, K, seed=0, dtype=torch.bfloat16, device=dev, centers=blob_centers(K, D, 10.0, 0, device=dev))
-for rep in range(2):
+for rep in range(int(os.environ.get("KPAR_REPS", "2"))):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     C = init_kmeans_parallel(X, D, K, N, 0, comm, seed=0)
