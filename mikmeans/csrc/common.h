@@ -152,6 +152,25 @@ __device__ __forceinline__ uint32_t lane_min_x32(uint32_t x) {
 }
 
 // ---------------------------------------------------------------------------
+// The canonical row-norm butterfly: v += v[lane ^ o] for o = 1, 2, 4, 8 inside each aligned
+// group of 16 lanes (only the steps o < lim), as DPP lane moves (one v_add_f32_dpp per step,
+// no ds_bpermute and no address VALU).  xor 1 / 2 are quad permutes; for o = 4 / 8 the partner
+// quad / half-row is reached by a mirror instead, which reads the same values: after the
+// steps before it every lane of a quad (half-row) holds the same partial sum, and a + b == b + a
+// in IEEE arithmetic, so the sums are bitwise the xor butterfly's.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum16_xor(float v, int lim = 16) {
+  if (lim > 1) v += dpp_f32<0xB1>(v);    // quad_perm [1,0,3,2]: lane ^ 1
+  if (lim > 2) v += dpp_f32<0x4E>(v);    // quad_perm [2,3,0,1]: lane ^ 2
+  if (lim > 4) v += dpp_f32<0x141>(v);   // row_half_mirror: the other quad of the half-row
+  if (lim > 8) v += dpp_f32<0x140>(v);   // row_mirror: the other half of the row
+  return v;
+}
+
+// ---------------------------------------------------------------------------
 // 64-lane reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -104,7 +104,7 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 // K1: xn[i] = sum_d x[i,d]^2 (f32).  16 lanes per row, 16-B loads.  The order is canonical --
 // lane s chains fmas over the elements of pieces s, s+16, s+32, ... in turn, then a 16-lane
-// butterfly (1, 2, 4, 8) -- and shared with every other producer of row norms (the fused
+// butterfly (1, 2, 4, 8; common.h sum16_xor) -- and shared with every other producer of row norms (the fused
 // column-statistics pass below, csrc/rows.hip sample_rows), so all of them give the same bits.
 template <typename T>
 __global__ __launch_bounds__(256) void row_sqnorm_kernel(const T* __restrict__ X, int64_t N, int D,
@@ -126,8 +126,7 @@ __global__ __launch_bounds__(256) void row_sqnorm_kernel(const T* __restrict__ X
     } else {
       for (int c = sub; c < D; c += 16) { const float f = Elem<T>::to_f32(row[c]); acc = __builtin_fmaf(f, f, acc); }
     }
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    acc = sum16_xor(acc);
     if (sub == 0) out[i] = acc;
   }
 }
@@ -164,11 +163,15 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
 // every row's |x|^2 in row_sqnorm_kernel's canonical order -- the fit's setup reads X once.
 constexpr int COLSTAT_BLOCKS = 2048;
 
+// Branch-free (it runs once per element of the pass; the branchy form cost ~20 VALU + SALU
+// exec-mask instructions per element and made the statistics pass VALU-bound): with y = |f|'s
+// bits, ctz(y | 2^23) is the mantissa's trailing-zero count capped at 23 (the hidden bit), and
+// max(e, 1) covers subnormals (-149 + ctz(m) = max(0, 1) + ctz(m) - 150).  Zero, inf and NaN
+// (y - 1 >= 0x7f7fffff unsigned) give "no constraint".
 __device__ __forceinline__ int lowbit_exp(float f) {
-  const uint32_t b = __float_as_uint(f) & 0x7fffffffu;
-  const uint32_t e = b >> 23, m = b & 0x7fffffu;
-  if (b == 0u || e == 255u) return 1 << 30;            // zero / inf / NaN: no constraint
-  return e == 0u ? -149 + (int)__builtin_ctz(m) : (int)e - 150 + (int)__builtin_ctz(m | 0x800000u);
+  const uint32_t y = __float_as_uint(f) & 0x7fffffffu;
+  const int v = (int)(__builtin_ctz(y | 0x800000u) + max(y >> 23, 1u)) - 150;
+  return y - 1u < 0x7f7fffffu ? v : 1 << 30;
 }
 
 // One launch covers up to 64 16-B pieces of a row (a column block: X, out, fpart, nnz and
@@ -219,9 +222,7 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
           if (p + g < NP) acc = __builtin_fmaf(o, o, acc);
         }
       }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1)
-        if (o < L) acc += __shfl_xor(acc, o, 64);
+      acc = sum16_xor(acc, L);
       if (p == 0) xn[row] = acc;
     }
   };

@@ -132,8 +132,7 @@ __global__ __launch_bounds__(256) void row_normalize_kernel(T* X, int64_t N, int
 #pragma unroll
       for (int q = 0; q < V; ++q) s = __builtin_fmaf(f[q], f[q], s);
     }
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+  s = sum16_xor(s);
   const float nrm = fmaxf(sqrtf(s), 1e-30f);
   float s2 = 0.f;
   if (ok)
@@ -150,8 +149,7 @@ __global__ __launch_bounds__(256) void row_normalize_kernel(T* X, int64_t N, int
       *(u32x4*)(row + p * V) = *(const u32x4*)h;
     }
   if (xn) {
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) s2 += __shfl_xor(s2, o, 64);
+    s2 = sum16_xor(s2);
     if (ok && sub == 0) xn[i] = s2;
   }
 }
