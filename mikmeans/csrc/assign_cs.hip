@@ -24,6 +24,13 @@
 // Layout of a super-block in the ring: for 16-point block j and 16-B piece q, 1 KiB where
 // lane l = r + 16g holds point 16j + r's features [(4q+g)8, +8) -- the B fragments, read
 // with one conflict-free ds_read_b128 per lane (the centroid pack's layout, kernels.h).
+//
+// Measured (profiles/r5_24_ab_d*_cs_v2.log, r5_25_pmc_cs256_v2.md): slower than the streaming
+// kernel -- 4.55 vs 3.83 ms at D=256 K=512, 5.44 vs 3.93 ms at D=128 K=1024 -- so it stays an
+// opt-in A/B switch.  Each 16-point block is merged across its 4 lane groups and parked per
+// wave, a cost the streaming kernel pays once per segment of 16 tiles but this one once per
+// T = 2 / 4 tiles (1.9 non-MFMA VALU per MFMA against 1.3), and its B-fragment + seed reads per
+// MFMA exceed the streaming kernel's A-fragment reads shared by 3-4 point blocks.
 #include <type_traits>
 
 #include "common.h"
