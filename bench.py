@@ -206,37 +206,12 @@ def main(argv=None):
             phase_ms=_phase_breakdown(eng) if (eng.gpu and not args.incremental) else None,
         )
         if args.config == "cfg3" and args.also_incremental and not args.incremental and eng.gpu:
-            # The library default (KMeans(incremental=True)) from the same start: identical
-            # E-step, the M-step re-scatters only rows whose label changed into exact int64
-            # running totals.  Reported beside the headline, which stays the full M-step.
-            C_full = eng.centers.clone()
-            del eng
-            inc = LloydEngine(X, K, comm=comm, incremental=True).set_centers(C0)
-            _capture(inc, use_graph)
-            el_inc = _timed_steps(inc, comm, args.warmup, args.steps, sync)
-            extra["incremental_mstep"] = {
-                "value": args.steps / el_inc,
-                "ms_per_step": el_inc * 1e3 / args.steps,
-                "assignments_per_s": args.steps / el_inc * N,
-                "centres_bitwise_equal_to_full": bool(torch.equal(inc.centers, C_full)),
-            }
-            if args.also_bounded:
-                # KMeans(algorithm="hamerly"): the bounded E-step re-assigns only the rows its
-                # bounds cannot vouch for -- bitwise the full E-step's iterates.  From the same
-                # start, same warm-up and step count; an extra field, not the headline.
-                C_inc = inc.centers.clone()
-                del inc
-                bnd = LloydEngine(X, K, comm=comm, incremental=True, bounded=True).set_centers(C0)
-                _capture(bnd, use_graph)
-                el_b = _timed_steps(bnd, comm, args.warmup, args.steps, sync)
-                extra["bounded_estep"] = {
-                    "value": args.steps / el_b,
-                    "ms_per_step": el_b * 1e3 / args.steps,
-                    "rows_reassigned_last_step": bnd.reassigned,
-                    "centres_bitwise_equal_to_full": bool(torch.equal(bnd.centers, C_inc)),
-                    "max_centre_diff_vs_full": float((bnd.centers - C_inc).abs().max()),
-                }
-                del bnd
+            # extras from the same start (untimed for the headline): a failure there is recorded
+            # in the line instead of costing the headline its JSON
+            try:
+                _headline_extras(args, eng, X, K, C0, comm, sync, use_graph, N, extra)
+            except Exception as exc:   # noqa: BLE001
+                extra["extras_error"] = f"{type(exc).__name__}: {exc}"[:300]
     if comm.rank == 0:
         out = {
             "metric": METRIC if args.config == "cfg3" else f"{cfg['model']} ({unit})",
@@ -286,6 +261,44 @@ def _capture(eng, want: bool):
             print(f"[bench] graph capture failed ({err}); eager steps", file=sys.stderr, flush=True)
         return {"captured": False, "error": err} if err else False
     return True
+
+
+
+def _headline_extras(args, eng, X, K, C0, comm, sync, use_graph, N, extra):
+    """The incremental M-step and bounded E-step runs reported beside the headline."""
+    from mikmeans.models.lloyd import LloydEngine
+
+    # The library default (KMeans(incremental=True)) from the same start: identical
+    # E-step, the M-step re-scatters only rows whose label changed into exact int64
+    # running totals.  Reported beside the headline, which stays the full M-step.
+    C_full = eng.centers.clone()
+    del eng
+    inc = LloydEngine(X, K, comm=comm, incremental=True).set_centers(C0)
+    _capture(inc, use_graph)
+    el_inc = _timed_steps(inc, comm, args.warmup, args.steps, sync)
+    extra["incremental_mstep"] = {
+        "value": args.steps / el_inc,
+        "ms_per_step": el_inc * 1e3 / args.steps,
+        "assignments_per_s": args.steps / el_inc * N,
+        "centres_bitwise_equal_to_full": bool(torch.equal(inc.centers, C_full)),
+    }
+    if args.also_bounded:
+        # KMeans(algorithm="hamerly"): the bounded E-step re-assigns only the rows its
+        # bounds cannot vouch for -- bitwise the full E-step's iterates.  From the same
+        # start, same warm-up and step count; an extra field, not the headline.
+        C_inc = inc.centers.clone()
+        del inc
+        bnd = LloydEngine(X, K, comm=comm, incremental=True, bounded=True).set_centers(C0)
+        _capture(bnd, use_graph)
+        el_b = _timed_steps(bnd, comm, args.warmup, args.steps, sync)
+        extra["bounded_estep"] = {
+            "value": args.steps / el_b,
+            "ms_per_step": el_b * 1e3 / args.steps,
+            "rows_reassigned_last_step": bnd.reassigned,
+            "centres_bitwise_equal_to_full": bool(torch.equal(bnd.centers, C_inc)),
+            "max_centre_diff_vs_full": float((bnd.centers - C_inc).abs().max()),
+        }
+        del bnd
 
 
 def _timed_steps(eng, comm, warmup: int, steps: int, sync, telemetry: dict | None = None) -> float:
