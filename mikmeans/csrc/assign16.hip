@@ -180,6 +180,13 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   // a workgroup past it leaves before any barrier)
   const int64_t N = a.n_dev ? min(a.N, *a.n_dev) : a.N;
   if (a.n_dev && (int64_t)blockIdx.x * C::PTS >= N) return;
+  if (a.stagger > 0) {   // (first resident wave only; see AssignArgs::stagger)
+    const int sl = (int)(blockIdx.x / (unsigned)a.stagger_cus);
+    if (sl > 0 && sl < a.stagger_slots) {
+      const uint64_t until = __builtin_amdgcn_s_memrealtime() + (uint64_t)sl * (uint64_t)a.stagger;
+      while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(8);
+    }
+  }
   const int64_t nblk = (N + C::PTS - 1) / C::PTS;
   int64_t blk = blockIdx.x;
   int64_t pbase = blk * C::PTS + (int64_t)wid * (C::P * 16);
@@ -895,6 +902,18 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if ((a.ub != nullptr) != (a.lb != nullptr) || (a.scatter && !a.rows)) return hipErrorInvalidValue;
   if (splits == 1) b.split_keys = nullptr;
   const dim3 grid((unsigned)nblk, (unsigned)splits);
+  {
+    // A/B switch V_ASSIGN_STAGGER (microseconds per CU slot): start the first resident wave's
+    // workgroups of slot s s * step late (AssignArgs::stagger)
+    const int st = variant(V_ASSIGN_STAGGER);
+    if (st > 0 && splits == 1) {
+      const int64_t res = resident_workgroups(C::NW, OCC, lds);
+      const int cus = resident_workgroups(4, 1, 0) / 1;   // (4 waves at 1/SIMD: one per CU)
+      b.stagger = st * 100;
+      b.stagger_cus = cus;
+      b.stagger_slots = (int)(res / cus);
+    }
+  }
   bool varg = false;
   constexpr bool VARG_OK = sizeof(T) == 2 && DPAD <= 64;   // D=128: -12 % at K=1024, -4 % at 2048 (r3_11)
   if constexpr (VARG_OK) {

@@ -33,7 +33,7 @@ constexpr int SLOT_STRIDE = 8;
 // changed only through set_variant (mikmeans.ops.native.variant); -1 = the built-in rule.
 // A captured hipGraph keeps the geometry that was in force when it was recorded.
 enum Variant { V_ASSIGN_VARG = 0, V_ASSIGN_PMAJ, V_ASSIGN_GEOM, V_UPDATE_KS, V_UPDATE_KS_GM, V_BLOBS_TPR,
-               V_ASSIGN_PERSIST, V_ASSIGN_TOP2_GEOM, V_ASSIGN_CS, V_COUNT };
+               V_ASSIGN_PERSIST, V_ASSIGN_TOP2_GEOM, V_ASSIGN_CS, V_ASSIGN_STAGGER, V_COUNT };
 int variant(Variant v);
 void set_variant(Variant v, int value);
 
@@ -70,6 +70,10 @@ struct AssignArgs {
   // oseed[row] -- the offset the full (ungathered) pass gives it, from launch_seed_offsets -- so a
   // gathered batch ranks each row bitwise as the full pass does (the bounded E-step)
   const float* oseed = nullptr;
+  // first-wave stagger (launcher-set): a workgroup of the launch's first resident wave in CU
+  // slot s > 0 (blockIdx.x / stagger_cus, < stagger_slots) starts s * stagger real-time ticks
+  // (10 ns) late, so the co-resident workgroups' row loads and MFMA phases do not line up
+  int stagger = 0, stagger_cus = 0, stagger_slots = 0;
 };
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 // Rows per workgroup of the full (ungathered, unbounded) assign for this shape: the block its
