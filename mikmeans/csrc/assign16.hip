@@ -180,6 +180,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   // a workgroup past it leaves before any barrier)
   const int64_t N = a.n_dev ? min(a.N, *a.n_dev) : a.N;
   if (a.n_dev && (int64_t)blockIdx.x * C::PTS >= N) return;
+  const unsigned long long t_entry = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
   if (a.stagger > 0) {   // (first resident wave only; see AssignArgs::stagger)
     const int sl = (int)(blockIdx.x / (unsigned)a.stagger_cus);
     if (sl > 0 && sl < a.stagger_slots) {
@@ -256,6 +257,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       blds16(rN, (MK_LDS void*)(cn_lds + p * 1024), loff, (uint32_t)p * 1024u);
     if (!PERSIST || first) issue_chunk(0, ring % C::NBUF);
     wait_vmcnt<0>();  // retire the fragments before the LDS-DMA loop (its vmcnt waits count chunks)
+    const unsigned long long t_landed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (C::NBUF == 3 && ncl > 1) issue_chunk(1, (ring + 1) % C::NBUF);
     const int64_t nxt = blk + (int64_t)gridDim.x;
     const bool has_next = PERSIST && nxt < nblk;   // (wave-uniform)
@@ -526,8 +528,18 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         }
       }
     };
+    const unsigned long long t_loop = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (ppo) chunk_loop(std::true_type{});
     else chunk_loop(std::false_type{});
+    if (a.timeline && threadIdx.x == 0 && first && blockIdx.y == 0) {
+      unsigned long long* tl = a.timeline + (int64_t)blockIdx.x * 8;
+      tl[0] = t_entry;
+      tl[1] = t_loop;
+      tl[2] = __builtin_amdgcn_s_memrealtime();
+      tl[4] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_ID
+      tl[5] = (unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));   // XCC_ID
+      tl[6] = t_landed;   // fragments, |c|^2 and the first chunk landed (wave 0)
+    }
 
     // VARG: merge the 4 lane groups of each point on (value, tile, group) -- the centre index
     // 16 t + 4 g + e orders like that triple -- then recover e: for the points 4m..4m+3 the
@@ -724,6 +736,8 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     raw_barrier();
     ring += ncl;
   }  // block loop
+  if (a.timeline && threadIdx.x == 0 && blockIdx.y == 0)
+    a.timeline[(int64_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();
   if (a.slots && !a.split_keys) {
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -846,6 +860,13 @@ static void launch16_kpp(const AssignArgs& b, const dim3& grid, size_t lds, hipS
   launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, false, false>(b, grid, lds, s);
 }
 
+static unsigned long long* g_timeline = nullptr;
+static int64_t g_timeline_cap = 0;
+void set_assign_timeline(unsigned long long* buf, int64_t capacity) {
+  g_timeline = buf;
+  g_timeline_cap = buf ? capacity : 0;
+}
+
 // Resident workgroups the whole chip holds for a launch geometry: the smaller of the
 // wave-slot and the LDS limit per CU, times the CU count (the persistent grid).
 static int64_t resident_workgroups(int waves_per_wg, int occ_per_simd, size_t lds) {
@@ -902,6 +923,7 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if ((a.ub != nullptr) != (a.lb != nullptr) || (a.scatter && !a.rows)) return hipErrorInvalidValue;
   if (splits == 1) b.split_keys = nullptr;
   const dim3 grid((unsigned)nblk, (unsigned)splits);
+  if (g_timeline && nblk <= g_timeline_cap && splits == 1) b.timeline = g_timeline;
   {
     // A/B switch V_ASSIGN_STAGGER (microseconds per CU slot): start the first resident wave's
     // workgroups of slot s s * step late (AssignArgs::stagger)

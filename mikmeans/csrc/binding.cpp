@@ -843,6 +843,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     for (int i = 0; i < mk::V_COUNT; ++i) n.emplace_back(mk::kVariantEnv[i] + 9);   // strip "MIKMEANS_"
     return n;
   }, "A/B switch names (lower-cased by mikmeans.ops.native)");
+  m.def("set_assign_timeline", [](c10::optional<torch::Tensor> buf) {
+    if (!buf.has_value()) { mk::set_assign_timeline(nullptr, 0); return; }
+    TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == torch::kInt64 && buf->is_contiguous(),
+                "mikmeans: timeline buffer must be a contiguous int64 CUDA tensor");
+    mk::set_assign_timeline((unsigned long long*)buf->data_ptr<int64_t>(), buf->numel() / 8);
+  }, py::arg("buf"));
   m.def("get_variant", [](int64_t i) {
     TORCH_CHECK(i >= 0 && i < mk::V_COUNT, "mikmeans: no A/B switch ", i);
     return mk::variant((mk::Variant)i);

@@ -74,7 +74,14 @@ struct AssignArgs {
   // slot s > 0 (blockIdx.x / stagger_cus, < stagger_slots) starts s * stagger real-time ticks
   // (10 ns) late, so the co-resident workgroups' row loads and MFMA phases do not line up
   int stagger = 0, stagger_cus = 0, stagger_slots = 0;
+  // optional timeline (profiling, launcher-set from set_assign_timeline): per workgroup 8 u64 --
+  // real-time ticks (10 ns) at entry, chunk-loop start, epilogue start and exit, then HW_ID
+  // and XCC_ID (which CU ran it), then the tick wave 0's prologue loads had all landed
+  unsigned long long* timeline = nullptr;
 };
+// Profiling hook: every assign16 launch writes its workgroups' timelines to buf (nullptr: off;
+// the caller sizes it for the grid, 8 u64 per workgroup, capacity in workgroups)
+void set_assign_timeline(unsigned long long* buf, int64_t capacity);
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 // Rows per workgroup of the full (ungathered, unbounded) assign for this shape: the block its
 // bf16 seed offset is taken over (mirrors launch16_d / launch16_w)
