@@ -246,6 +246,33 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     }
   };
   load_block();
+  // (one pass) the epilogue's per-row inputs, fetched with the fragments so their memory round
+  // trip hides under the prologue's instead of opening the epilogue (~2 us of a workgroup's
+  // ~50 us at D=128, scripts/assign_timeline.py): lane (r, g) stores the rows of the blocks
+  // p = 4j + g, so it keeps their old label and caller norm -- two registers per 4 blocks
+  constexpr int EJ = (C::P + 3) / 4;
+  int eold[EJ];
+  float exn[EJ];
+  const bool eread = !PERSIST && !a.split_keys && a.epi_prefetch;
+  if (eread) {
+#pragma unroll
+    for (int j = 0; j < EJ; ++j) {
+      const int pg = 4 * j + g;
+      const int64_t i = pbase + pg * 16 + r;
+      const bool mine = pg < C::P && i < N;
+      const int64_t oi = mine && a.scatter ? a.rows[i] : i;
+      eold[j] = mine && a.track_changed ? a.labels[oi] : -2;
+      if (F32 || !a.xn) {
+        exn[j] = mine && a.xn ? a.xn[oi] : 0.f;
+      } else {   // (bf16: the prologue loaded them, xnr[p] = xn at block p's rows)
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (4 * j + q < C::P && q == g) v = xnr[4 * j + q];
+        exn[j] = v;
+      }
+    }
+  }
   // per-wave (inertia, changed) totals over the workgroup's passes, in LDS after the offsets
   double* wacc = (double*)(bufs + C::NBUF * C::CHUNK_BYTES + 16 * C::NW + C::OPT_BYTES);
   for (bool first = true;; first = false) {
@@ -687,9 +714,10 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         if constexpr (TOP2) sec = second(p);
         const int64_t i = pcur + p * 16 + r;
         if ((p & 3) == g && i < N) {
-          const bool rd = !a.split_keys;
           const int64_t oi = a.scatter ? a.rows[i] : i;
-          store(p, oi, k, v, rd && a.track_changed ? a.labels[oi] : -2, rd && a.xn ? a.xn[oi] : 0.f, sec);
+          const bool rd = !a.split_keys;
+          store(p, oi, k, v, eread ? eold[p >> 2] : (rd && a.track_changed ? a.labels[oi] : -2),
+                eread ? exn[p >> 2] : (rd && a.xn ? a.xn[oi] : 0.f), sec);
         }
       }
     } else {
@@ -924,6 +952,7 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if (splits == 1) b.split_keys = nullptr;
   const dim3 grid((unsigned)nblk, (unsigned)splits);
   if (g_timeline && nblk <= g_timeline_cap && splits == 1) b.timeline = g_timeline;
+  b.epi_prefetch = variant(V_ASSIGN_EPI) != 0;
   {
     // A/B switch V_ASSIGN_STAGGER (microseconds per CU slot): start the first resident wave's
     // workgroups of slot s s * step late (AssignArgs::stagger)

@@ -33,7 +33,7 @@ constexpr int SLOT_STRIDE = 8;
 // changed only through set_variant (mikmeans.ops.native.variant); -1 = the built-in rule.
 // A captured hipGraph keeps the geometry that was in force when it was recorded.
 enum Variant { V_ASSIGN_VARG = 0, V_ASSIGN_PMAJ, V_ASSIGN_GEOM, V_UPDATE_KS, V_UPDATE_KS_GM, V_BLOBS_TPR,
-               V_ASSIGN_PERSIST, V_ASSIGN_TOP2_GEOM, V_ASSIGN_CS, V_ASSIGN_STAGGER, V_COUNT };
+               V_ASSIGN_PERSIST, V_ASSIGN_TOP2_GEOM, V_ASSIGN_CS, V_ASSIGN_STAGGER, V_ASSIGN_EPI, V_COUNT };
 int variant(Variant v);
 void set_variant(Variant v, int value);
 
@@ -78,6 +78,9 @@ struct AssignArgs {
   // real-time ticks (10 ns) at entry, chunk-loop start, epilogue start and exit, then HW_ID
   // and XCC_ID (which CU ran it), then the tick wave 0's prologue loads had all landed
   unsigned long long* timeline = nullptr;
+  // launcher-set (A/B switch V_ASSIGN_EPI, default on): the epilogue's old labels and caller
+  // norms are fetched with the prologue's fragments instead of in the epilogue
+  int epi_prefetch = 1;
 };
 // Profiling hook: every assign16 launch writes its workgroups' timelines to buf (nullptr: off;
 // the caller sizes it for the grid, 8 u64 per workgroup, capacity in workgroups)
