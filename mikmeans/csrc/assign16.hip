@@ -283,6 +283,11 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     for (int p = wid; p < cn_bytes / 1024; p += C::NW)
       blds16(rN, (MK_LDS void*)(cn_lds + p * 1024), loff, (uint32_t)p * 1024u);
     if (!PERSIST || first) issue_chunk(0, ring % C::NBUF);
+    unsigned long long t_frag = 0ull;
+    if (a.timeline) {   // (diagnostic: the fragments alone, the younger DMAs (<= 5 at Kpad <= 1024) may fly)
+      wait_vmcnt<5>();
+      t_frag = __builtin_amdgcn_s_memrealtime();
+    }
     wait_vmcnt<0>();  // retire the fragments before the LDS-DMA loop (its vmcnt waits count chunks)
     const unsigned long long t_landed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (C::NBUF == 3 && ncl > 1) issue_chunk(1, (ring + 1) % C::NBUF);
@@ -566,6 +571,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       tl[4] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_ID
       tl[5] = (unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));   // XCC_ID
       tl[6] = t_landed;   // fragments, |c|^2 and the first chunk landed (wave 0)
+      tl[7] = t_frag;     // (Kpad <= 1024, CT * 16 * DPAD * 2 / 1024 / NW <= 4) the fragments alone
     }
 
     // VARG: merge the 4 lane groups of each point on (value, tile, group) -- the centre index

@@ -62,10 +62,13 @@ def main():
     pro, lp, ep = (loop - ent) * us, (epi - loop) * us, (ext - epi) * us
     land = (t[:, 6] - t0 - ent) * us       # entry -> the prologue's loads landed
     out_land = {"median": float(np.median(land)), "p90": float(np.percentile(land, 90))}
+    frag = (t[:, 7] - t0 - ent) * us
+    out_frag = {"median": float(np.median(frag)), "p90": float(np.percentile(frag, 90))}
     out = {"n": a.n, "d": a.d, "k": a.k, "arm": a.arm, "workgroups": int(len(t)),
            "kernel_us": float((ext.max()) * us),
            "prologue_us": {"median": float(np.median(pro)), "p90": float(np.percentile(pro, 90))},
            "loads_landed_us": out_land,
+           "fragments_landed_us": out_frag,
            "loop_us": {"median": float(np.median(lp)), "p90": float(np.percentile(lp, 90))},
            "epilogue_us": {"median": float(np.median(ep)), "p90": float(np.percentile(ep, 90))},
            "distinct_cus": int(len(np.unique(cu_id)))}
@@ -74,6 +77,11 @@ def main():
     order = np.argsort(ent)
     first = order[: min(len(order), 1024)]
     out["first_wave_start_spread_us"] = float((ent[first].max() - ent[first].min()) * us)
+    # the first resident wave runs with idle neighbours: its prologue is the unloaded latency
+    out["first_wave_loads_landed_us"] = float(np.median(land[first]))
+    out["first_wave_prologue_us"] = float(np.median(pro[first]))
+    late = order[len(order) // 2:]
+    out["steady_loads_landed_us"] = float(np.median(land[late]))
     # how aligned are co-resident workgroups: for each CU, the gaps between consecutive starts
     gaps = []
     for c in np.unique(cu_id):
