@@ -245,12 +245,30 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       for (int p = 0; p < C::P; ++p) xnr[p] = 0.f;
     }
   };
-  load_block();
+  // Early prologue (one pass over plain full bf16 rows with caller norms): the |c|^2 DMA and
+  // the norms go out first, then the fragments, the epilogue's reads and the first chunk, and
+  // the seed-offset reduction waits for the norms alone -- its barrier runs while the fragments
+  // are still in flight (the chunk loop's first wait retires them).  A/B switch V_ASSIGN_EARLY.
+  constexpr int EJ = (C::P + 3) / 4;
+  constexpr bool EARLY_OK = !F32 && !PERSIST && FULLD && C::P * C::NQ + EJ + C::NPW < 64;   // (vmcnt range)
+  const bool early = EARLY_OK && a.xn && !a.rows && !a.oseed && !a.split_keys && a.epi_prefetch &&
+                     a.early_prologue;
+  if (early) {
+    for (int pc = wid; pc < cn_bytes / 1024; pc += C::NW)
+      blds16(rN, (MK_LDS void*)(cn_lds + pc * 1024), loff, (uint32_t)pc * 1024u);
+#pragma unroll
+    for (int p = 0; p < C::P; ++p) xnr[p] = a.xn[row_of(p)];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int p = 0; p < C::P; ++p) load_frags(p, row_of(p));
+    __builtin_amdgcn_sched_barrier(0);
+  } else {
+    load_block();
+  }
   // (one pass) the epilogue's per-row inputs, fetched with the fragments so their memory round
   // trip hides under the prologue's instead of opening the epilogue (~2 us of a workgroup's
   // ~50 us at D=128, scripts/assign_timeline.py): lane (r, g) stores the rows of the blocks
   // p = 4j + g, so it keeps their old label and caller norm -- two registers per 4 blocks
-  constexpr int EJ = (C::P + 3) / 4;
   int eold[EJ];
   float exn[EJ];
   const bool eread = !PERSIST && !a.split_keys && a.epi_prefetch;
@@ -261,7 +279,12 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       const int64_t i = pbase + pg * 16 + r;
       const bool mine = pg < C::P && i < N;
       const int64_t oi = mine && a.scatter ? a.rows[i] : i;
-      eold[j] = mine && a.track_changed ? a.labels[oi] : -2;
+      if (early) {   // (one load per j whatever the lane: the prologue's wait counts them)
+        const int v = a.labels[i < N ? i : N - 1];
+        eold[j] = mine && a.track_changed ? v : -2;
+      } else {
+        eold[j] = mine && a.track_changed ? a.labels[oi] : -2;
+      }
       if (F32 || !a.xn) {
         exn[j] = mine && a.xn ? a.xn[oi] : 0.f;
       } else {   // (bf16: the prologue loaded them, xnr[p] = xn at block p's rows)
@@ -280,15 +303,22 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     // fragment address (the gathered row indices) also waits for them.  (PERSIST: after the
     // first pass the chunk is already in flight, issued at the previous pass's last barrier.)
     __builtin_amdgcn_sched_barrier(0);
-    for (int p = wid; p < cn_bytes / 1024; p += C::NW)
-      blds16(rN, (MK_LDS void*)(cn_lds + p * 1024), loff, (uint32_t)p * 1024u);
+    if (!early)
+      for (int p = wid; p < cn_bytes / 1024; p += C::NW)
+        blds16(rN, (MK_LDS void*)(cn_lds + p * 1024), loff, (uint32_t)p * 1024u);
     if (!PERSIST || first) issue_chunk(0, ring % C::NBUF);
     unsigned long long t_frag = 0ull;
-    if (a.timeline) {   // (diagnostic: the fragments alone, the younger DMAs (<= 5 at Kpad <= 1024) may fly)
-      wait_vmcnt<5>();
-      t_frag = __builtin_amdgcn_s_memrealtime();
+    if (early) {
+      // the norms and |c|^2 landed; younger: the fragments, one label load per 4 blocks and
+      // the first chunk (all issued unconditionally)
+      if constexpr (EARLY_OK) wait_vmcnt<C::P * C::NQ + EJ + C::NPW>();
+    } else {
+      if (a.timeline) {   // (diagnostic: the fragments alone, the younger DMAs (<= 5 at Kpad <= 1024) may fly)
+        wait_vmcnt<5>();
+        t_frag = __builtin_amdgcn_s_memrealtime();
+      }
+      wait_vmcnt<0>();  // retire the fragments before the LDS-DMA loop (its vmcnt waits count chunks)
     }
-    wait_vmcnt<0>();  // retire the fragments before the LDS-DMA loop (its vmcnt waits count chunks)
     const unsigned long long t_landed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (C::NBUF == 3 && ncl > 1) issue_chunk(1, (ring + 1) % C::NBUF);
     const int64_t nxt = blk + (int64_t)gridDim.x;
@@ -342,7 +372,10 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       }
       float* red = (float*)(bufs + C::NBUF * C::CHUNK_BYTES);
       if (lane == 0) { red[2 * wid] = m; red[2 * wid + 1] = mn; }
-      __syncthreads();  // (every wave's cn / chunk-0 DMA has landed: vmcnt(0) above)
+      // every wave's |c|^2 DMA has landed (its wait above); a raw barrier, so an early
+      // prologue's fragments and first chunk stay in flight (__syncthreads drains vmcnt)
+      wait_lgkm0();
+      raw_barrier();
       float mnw = 3.0e38f;
 #pragma unroll
       for (int w = 0; w < C::NW; ++w) { off = fmaxf(off, red[2 * w]); mnw = fminf(mnw, red[2 * w + 1]); }
@@ -959,6 +992,7 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)nblk, (unsigned)splits);
   if (g_timeline && nblk <= g_timeline_cap && splits == 1) b.timeline = g_timeline;
   b.epi_prefetch = variant(V_ASSIGN_EPI) != 0;
+  b.early_prologue = variant(V_ASSIGN_EARLY) != 0;
   {
     // A/B switch V_ASSIGN_STAGGER (microseconds per CU slot): start the first resident wave's
     // workgroups of slot s s * step late (AssignArgs::stagger)
