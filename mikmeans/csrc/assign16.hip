@@ -806,7 +806,10 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   if (a.timeline && threadIdx.x == 0 && blockIdx.y == 0)
     a.timeline[(int64_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();
   if (a.slots && !a.split_keys) {
-    __syncthreads();
+    // the waves' LDS totals are published by a raw barrier: __syncthreads would first drain
+    // vmcnt, i.e. wait for every label / distance store of the epilogue to be acknowledged
+    wait_lgkm0();
+    raw_barrier();
     if (threadIdx.x == 0) {
       double si = 0, sc = 0;
 #pragma unroll
