@@ -57,6 +57,10 @@ def main(argv=None):
                     help="cfg5: generate the next batch on a side stream, started between the "
                          "current batch's assign and its M-step (mikmeans/data/blobs.py kick); measured "
                          "no faster: the M-step's workgroups hold the CUs (profiles/r5_27_cfg5_*.log)")
+    ap.add_argument("--gen-norms", action=argparse.BooleanOptionalAction, default=False,
+                    help="cfg5 streamed: the generator also writes the rows' |x|^2 (fused) and the "
+                         "assign takes them (early prologue) instead of summing its fragments; "
+                         "measured slower: assign -0.14 ms, generator +0.20 ms (profiles/r5_52_*)")
     ap.add_argument("--incremental", action="store_true",
                     help="incremental M-step (re-scatter changed rows only; not the headline mode)")
     ap.add_argument("--also-incremental", action=argparse.BooleanOptionalAction, default=True,
@@ -405,12 +409,14 @@ def _bench_minibatch(args, cfg, comm, dtype):
         extra["data_bytes_per_rank"] = S * D * X.element_size()
     else:
         stream = BlobStream(N, D, K, b, seed=args.seed, dtype=dtype, device=dev, rank=comm.rank,
-                            world=comm.world, with_norms=False,  # (the assign takes |x|^2 from its fragments)
+                            world=comm.world, with_norms=args.gen_norms,  # (fused |x|^2 for the assign)
                             prefetch=args.prefetch)  # batch j+1 generated on a side stream during step j
         # the generator's value bound fixes the fixed-point scales up front (no per-step clamp check)
         eng = MiniBatchEngine(K, D, b, dtype=dtype, device=dev, comm=comm, value_bound=stream.value_bound)
         if args.prefetch:
             eng.after_assign = stream.kick   # batch j+1's generator overlaps batch j's M-step
+
+        extra["gen_norms"] = bool(args.gen_norms)
 
         def gen():
             Xb = next(stream)

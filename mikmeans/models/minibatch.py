@@ -101,9 +101,11 @@ class MiniBatchEngine:
         return {k: _r(v.numel() * v.element_size()) for k, v in t.items()}
 
     def partial_fit(self, Xb: torch.Tensor, norms: torch.Tensor | None = None):
-        """One mini-batch step on this rank's batch ``Xb`` (may be empty).  ``norms`` is
-        accepted for API compatibility and unused: the GPU assign takes |x|^2 from the row
-        fragments it loads anyway (key offsets and the batch inertia)."""
+        """One mini-batch step on this rank's batch ``Xb`` (may be empty).  ``norms``
+        (optional, f32 [rows], e.g. a BlobStream's fused norms): the GPU assign then takes the
+        rows' |x|^2 from them (key offsets, batch inertia) and can start its matrix-core work
+        while the row fragments are still in flight (the early prologue); without them it
+        computes |x|^2 from the fragments -- as :meth:`partial_fit_rows` does, bit for bit."""
         if self.gpu:
             self._step_gpu(Xb, norms)
         else:
@@ -213,9 +215,12 @@ class MiniBatchEngine:
             self._set_bound(Xb)
         lab = self.labels[:b]
         if b:
-            # key offsets and the inertia from the row fragments (no caller norms): the
-            # gathered-row path (partial_fit_rows) computes them the same way, bit for bit
-            self.pk.assign(Xb, None, lab, None, self.slots, False)
+            # key offsets and the inertia from the caller's norms when given, else from the row
+            # fragments (as the gathered-row path, partial_fit_rows, computes them)
+            xn = None
+            if norms is not None and norms.is_cuda and norms.numel() >= b and norms.dtype == torch.float32:
+                xn = norms[:b]
+            self.pk.assign(Xb, xn, lab, None, self.slots, False)
         if self.after_assign is not None:
             self.after_assign()
         self._mstep(Xb, lab)
