@@ -265,6 +265,9 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   } else {
     load_block();
   }
+  // (timeline) every row load issued: issue time vs landing time separates a full request
+  // queue from memory latency
+  const unsigned long long t_issued = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // (one pass) the epilogue's per-row inputs, fetched with the fragments so their memory round
   // trip hides under the prologue's instead of opening the epilogue (~2 us of a workgroup's
   // ~50 us at D=128, scripts/assign_timeline.py): lane (r, g) stores the rows of the blocks
@@ -604,7 +607,8 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       tl[4] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_ID
       tl[5] = (unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));   // XCC_ID
       tl[6] = t_landed;   // fragments, |c|^2 and the first chunk landed (wave 0)
-      tl[7] = t_frag;     // (Kpad <= 1024, CT * 16 * DPAD * 2 / 1024 / NW <= 4) the fragments alone
+      tl[7] = early ? t_issued : t_frag;   // early prologue: the loads' issue completed; else
+                                           // (Kpad <= 1024, 4 chunk pieces per wave) the fragments landed
     }
 
     // VARG: merge the 4 lane groups of each point on (value, tile, group) -- the centre index

@@ -68,7 +68,7 @@ def main():
            "kernel_us": float((ext.max()) * us),
            "prologue_us": {"median": float(np.median(pro)), "p90": float(np.percentile(pro, 90))},
            "loads_landed_us": out_land,
-           "fragments_landed_us": out_frag,
+           "fragments_landed_or_issued_us": out_frag,   # (early prologue: issued)
            "loop_us": {"median": float(np.median(lp)), "p90": float(np.percentile(lp, 90))},
            "epilogue_us": {"median": float(np.median(ep)), "p90": float(np.percentile(ep, 90))},
            "distinct_cus": int(len(np.unique(cu_id)))}
