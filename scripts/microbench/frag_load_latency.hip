@@ -63,6 +63,17 @@ __global__ __launch_bounds__(256) void frag_load_contended(const unsigned short*
         __syncthreads();
         off = (off + 16384u) & (262144u - 1u);
       }
+    } else if (stream == 3) {   // LDS-DMA at full rate: 8 KiB per wave in flight, no barrier
+      const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, 262144, 0x00020000);
+      unsigned off = 0;
+      for (int it = 0; it < stream_us * 8; ++it) {
+        for (int i = 0; i < 4; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (__attribute__((address_space(3))) void*)(ring + (wid * 4 + i) * 1024), 16,
+                                                   (unsigned)lane * 16u, off + (unsigned)(wid * 4 + i) * 1024u, 0, 0);
+        __builtin_amdgcn_s_waitcnt((8 & 15) | (7 << 4) | (15 << 8));   // vmcnt(8): two batches in flight
+        off = (off + 16384u) & (262144u - 1u);
+      }
+      __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (15 << 8));
     } else if (stream == 2) {   // matrix cores + LDS reads, as the assign's chunk loop (no barrier)
       typedef float f32x4 __attribute__((ext_vector_type(4)));
       typedef short short8 __attribute__((ext_vector_type(8)));
@@ -132,7 +143,7 @@ int main(int argc, char** argv) {
     char* C;
     (void)hipMalloc(&C, 262144);
     (void)hipMemset(C, 2, 262144);
-    for (int stream = 0; stream < 3; ++stream) {
+    for (int stream = 0; stream < 4; ++stream) {
       for (int rep = 0; rep < 3; ++rep) {
         hipLaunchKernelGGL(frag_load_contended, dim3(1024), dim3(256), 0, 0, X, n, C, ts, sink, stream, 60,
                            (long)(stream * 3 + rep + 1) * 1500000L);
@@ -141,7 +152,7 @@ int main(int argc, char** argv) {
       }
       (void)hipMemcpy(h.data(), ts, 256 * 64, hipMemcpyDeviceToHost);
       report(stream == 1 ? "loaders_with_centre_stream" : stream == 2 ? "loaders_with_mfma_neighbours"
-                                                                      : "loaders_idle_neighbours", h, 256, n);
+             : stream == 3 ? "loaders_with_saturating_lds_dma" : "loaders_idle_neighbours", h, 256, n);
     }
     return 0;
   }
