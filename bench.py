@@ -61,6 +61,9 @@ def main(argv=None):
                     help="cfg5 streamed: the generator also writes the rows' |x|^2 (fused) and the "
                          "assign takes them (early prologue) instead of summing its fragments; "
                          "measured slower: assign -0.14 ms, generator +0.20 ms (profiles/r5_52_*)")
+    ap.add_argument("--telemetry", action=argparse.BooleanOptionalAction, default=True,
+                    help="sample the GFX clock and socket power (amdsmi, a background thread) over "
+                         "the timed steps")
     ap.add_argument("--incremental", action="store_true",
                     help="incremental M-step (re-scatter changed rows only; not the headline mode)")
     ap.add_argument("--also-incremental", action=argparse.BooleanOptionalAction, default=True,
@@ -190,8 +193,9 @@ def main(argv=None):
         eng = LloydEngine(X, K, comm=comm, incremental=args.incremental).set_centers(C0)
         use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
         extra["graph"] = _capture(eng, use_graph)
-        tel = {}
+        tel = {} if args.telemetry else None
         elapsed = _timed_steps(eng, comm, args.warmup, args.steps, sync, telemetry=tel)
+        tel = tel or {}
         # the timed steps' mean GFX clock and socket power on rank 0 (null without amdsmi):
         # value / clock_mhz separates a kernel change from a slower box
         extra["clock_mhz"] = tel.get("clock_mhz")
@@ -317,9 +321,11 @@ def _timed_steps(eng, comm, warmup: int, steps: int, sync, telemetry: dict | Non
     comm.barrier()
     sync()
     sampler = ClockSampler(comm.device.index or 0) if (telemetry is not None and comm.device.type == "cuda") else None
-    t0 = time.perf_counter()
     if sampler is not None:
+        # (outside the clock: entering takes the first amdsmi sample synchronously, ~1 ms --
+        # 8 % of cfg2's timed region when it sat inside, profiles/r5_60_cfg2_*.log)
         sampler.__enter__()
+    t0 = time.perf_counter()
     for _ in range(steps):
         eng.step()
     sync()
