@@ -253,11 +253,16 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   constexpr bool EARLY_OK = !F32 && !PERSIST && FULLD && C::P * C::NQ + EJ + C::NPW < 64;   // (vmcnt range)
   const bool early = EARLY_OK && a.xn && !a.rows && !a.oseed && !a.split_keys && a.epi_prefetch &&
                      a.early_prologue;
+  // early: lane (r, g) loads the norm of its epilogue rows only -- block p = 4j + g -- one
+  // instruction per 4 blocks instead of one per block (the prologue's vector-memory issue is
+  // what takes its time, profiles/r5_45_assign_prologue_study.md); lanes past the last block
+  // repeat it (harmless to the max / min)
+  float xg[EJ];
   if (early) {
     for (int pc = wid; pc < cn_bytes / 1024; pc += C::NW)
       blds16(rN, (MK_LDS void*)(cn_lds + pc * 1024), loff, (uint32_t)pc * 1024u);
 #pragma unroll
-    for (int p = 0; p < C::P; ++p) xnr[p] = a.xn[row_of(p)];
+    for (int j = 0; j < EJ; ++j) xg[j] = a.xn[row_of(4 * j + g < C::P ? 4 * j + g : C::P - 1)];
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int p = 0; p < C::P; ++p) load_frags(p, row_of(p));
@@ -290,6 +295,8 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       }
       if (F32 || !a.xn) {
         exn[j] = mine && a.xn ? a.xn[oi] : 0.f;
+      } else if (early) {   // (loaded per lane group above)
+        exn[j] = xg[j];
       } else {   // (bf16: the prologue loaded them, xnr[p] = xn at block p's rows)
         float v = 0.f;
 #pragma unroll
@@ -366,8 +373,17 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       }
      } else {
       float m = 0.f, mn = 3.0e38f;
+      if (early) {   // (one norm per lane and 4 blocks: reduce over the whole wave)
 #pragma unroll
-      for (int p = 0; p < C::P; ++p) { m = fmaxf(m, xnr[p]); mn = fminf(mn, xnr[p]); }
+        for (int j = 0; j < EJ; ++j) { m = fmaxf(m, xg[j]); mn = fminf(mn, xg[j]); }
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        mn = fminf(mn, __shfl_xor(mn, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        mn = fminf(mn, __shfl_xor(mn, 32, 64));
+      } else {
+#pragma unroll
+        for (int p = 0; p < C::P; ++p) { m = fmaxf(m, xnr[p]); mn = fminf(mn, xnr[p]); }
+      }
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
         m = fmaxf(m, __shfl_xor(m, o, 64));
@@ -389,7 +405,11 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         for (int k = threadIdx.x; k < a.Kpad; k += C::NW * 64) ((float*)cn_lds)[k] += off;
       } else {
         off = 0.f;
-        if (g == 0) {
+        if (early) {
+#pragma unroll
+          for (int j = 0; j < EJ; ++j)
+            if (4 * j + g < C::P) opt[(wid * 16 + r) * C::PP + 4 * j + g] = __builtin_fmaf(xg[j], 2.44140625e-04f, xg[j]);
+        } else if (g == 0) {
 #pragma unroll
           for (int p = 0; p < C::P; ++p) opt[(wid * 16 + r) * C::PP + p] = __builtin_fmaf(xnr[p], 2.44140625e-04f, xnr[p]);
         }
