@@ -258,6 +258,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   // what takes its time, profiles/r5_45_assign_prologue_study.md); lanes past the last block
   // repeat it (harmless to the max / min)
   float xg[EJ];
+  if (a.prologue_prio) __builtin_amdgcn_s_setprio(3);
   if (early) {
     for (int pc = wid; pc < cn_bytes / 1024; pc += C::NW)
       blds16(rN, (MK_LDS void*)(cn_lds + pc * 1024), loff, (uint32_t)pc * 1024u);
@@ -317,6 +318,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       for (int p = wid; p < cn_bytes / 1024; p += C::NW)
         blds16(rN, (MK_LDS void*)(cn_lds + p * 1024), loff, (uint32_t)p * 1024u);
     if (!PERSIST || first) issue_chunk(0, ring % C::NBUF);
+    if (a.prologue_prio) __builtin_amdgcn_s_setprio(0);   // (every prologue load issued)
     unsigned long long t_frag = 0ull;
     if (early) {
       // the norms and |c|^2 landed; younger: the fragments, one label load per 4 blocks and
@@ -1020,6 +1022,7 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if (g_timeline && nblk <= g_timeline_cap && splits == 1) b.timeline = g_timeline;
   b.epi_prefetch = variant(V_ASSIGN_EPI) != 0;
   b.early_prologue = variant(V_ASSIGN_EARLY) != 0;
+  b.prologue_prio = variant(V_ASSIGN_PPRIO) > 0;
   {
     // A/B switch V_ASSIGN_STAGGER (microseconds per CU slot): start the first resident wave's
     // workgroups of slot s s * step late (AssignArgs::stagger)

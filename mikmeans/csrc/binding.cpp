@@ -616,7 +616,8 @@ static const char* const kVariantEnv[V_COUNT] = {"MIKMEANS_ASSIGN_VARG", "MIKMEA
                                                  "MIKMEANS_UPDATE_KS_GM", "MIKMEANS_BLOBS_TPR",
                                                  "MIKMEANS_ASSIGN_PERSIST", "MIKMEANS_ASSIGN_TOP2_GEOM",
                                                  "MIKMEANS_ASSIGN_CS", "MIKMEANS_ASSIGN_STAGGER",
-                                                 "MIKMEANS_ASSIGN_EPI", "MIKMEANS_ASSIGN_EARLY"};
+                                                 "MIKMEANS_ASSIGN_EPI", "MIKMEANS_ASSIGN_EARLY",
+                                                 "MIKMEANS_ASSIGN_PPRIO"};
 static int* variant_table() {
   static int t[V_COUNT] = {};
   static const bool init = [] {

@@ -33,7 +33,7 @@ constexpr int SLOT_STRIDE = 8;
 // changed only through set_variant (mikmeans.ops.native.variant); -1 = the built-in rule.
 // A captured hipGraph keeps the geometry that was in force when it was recorded.
 enum Variant { V_ASSIGN_VARG = 0, V_ASSIGN_PMAJ, V_ASSIGN_GEOM, V_UPDATE_KS, V_UPDATE_KS_GM, V_BLOBS_TPR,
-               V_ASSIGN_PERSIST, V_ASSIGN_TOP2_GEOM, V_ASSIGN_CS, V_ASSIGN_STAGGER, V_ASSIGN_EPI, V_ASSIGN_EARLY, V_COUNT };
+               V_ASSIGN_PERSIST, V_ASSIGN_TOP2_GEOM, V_ASSIGN_CS, V_ASSIGN_STAGGER, V_ASSIGN_EPI, V_ASSIGN_EARLY, V_ASSIGN_PPRIO, V_COUNT };
 int variant(Variant v);
 void set_variant(Variant v, int value);
 
@@ -84,6 +84,9 @@ struct AssignArgs {
   // launcher-set (A/B switch V_ASSIGN_EARLY): norms first, fragments in flight across the
   // seed-offset barrier (plain full bf16 rows with caller norms)
   int early_prologue = 1;
+  // launcher-set (A/B switch V_ASSIGN_PPRIO): the prologue's loads issue at raised wave
+  // priority (s_setprio 3), ahead of the co-resident waves' centre-ring DMA
+  int prologue_prio = 0;
 };
 // Profiling hook: every assign16 launch writes its workgroups' timelines to buf (nullptr: off;
 // the caller sizes it for the grid, 8 u64 per workgroup, capacity in workgroups)

@@ -106,7 +106,8 @@ def get_variant(name: str) -> int:
 def set_variant(name: str, value: int) -> None:
     """Set a kernel A/B switch (``assign_varg``, ``assign_pmaj``, ``assign_geom``,
     ``update_ks``, ``update_ks_gm``, ``blobs_tpr``, ``assign_persist``, ``assign_top2_geom``,
-    ``assign_cs``, ``assign_stagger``, ``assign_epi``, ``assign_early``; -1 = built-in rule).  The launchers never
+    ``assign_cs``, ``assign_stagger``, ``assign_epi``, ``assign_early``, ``assign_pprio``; -1 =
+    built-in rule).  The launchers never
     read the environment: ``MIKMEANS_<NAME>`` is read once when the extension loads."""
     require().set_variant(_variant_index(name), int(value))
 
