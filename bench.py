@@ -60,7 +60,7 @@ def main(argv=None):
     ap.add_argument("--gen-norms", action=argparse.BooleanOptionalAction, default=False,
                     help="cfg5 streamed: the generator also writes the rows' |x|^2 (fused) and the "
                          "assign takes them (early prologue) instead of summing its fragments; "
-                         "measured slower: assign -0.14 ms, generator +0.20 ms (profiles/r5_52_*)")
+                         "measured slower: assign -0.10 ms, generator +0.14 ms (profiles/r5_68_*)")
     ap.add_argument("--telemetry", action=argparse.BooleanOptionalAction, default=True,
                     help="sample the GFX clock and socket power (amdsmi, a background thread) over "
                          "the timed steps")

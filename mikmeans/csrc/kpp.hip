@@ -637,10 +637,9 @@ __global__ __launch_bounds__(256) void blobs_kernel(T* X, int64_t i0, int64_t n,
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             w[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{f[2 * j], f[2 * j + 1]}, bf16x2));
-            if constexpr (NORMS) {
-              const float q0 = __uint_as_float(w[j] << 16), q1 = __uint_as_float(w[j] & 0xffff0000u);
-              sq = __builtin_fmaf(q0, q0, sq);
-              sq = __builtin_fmaf(q1, q1, sq);
+            if constexpr (NORMS) {   // both squares of the stored pair in one v_dot2c_f32_bf16
+              const bf16x2 h = __builtin_bit_cast(bf16x2, w[j]);
+              sq = __builtin_amdgcn_fdot2_f32_bf16(h, h, sq, false);
             }
           }
           *(u32x4*)(out + EL * g) = w;
