@@ -946,3 +946,64 @@ def test_assign_centre_stationary(native, kvariant, n, d, k, outlier):
     lab2 = torch.zeros(n, dtype=torch.int32, device=DEV)
     pk.assign(Xb, xn, lab2)
     assert torch.equal(lab2, lab)
+
+
+@pytest.mark.parametrize("n,d,k,outlier", [(300_007, 128, 1024, False), (70_001, 256, 512, True),
+                                           (100_003, 64, 4096, True), (5000, 128, 256, False)])
+def test_assign_prologue_switches_bitwise(native, kvariant, n, d, k, outlier):
+    """The early prologue (norms first, fragments in flight across the seed-offset barrier;
+    one norm load per 4 blocks) and the epilogue-read prefetch change only when loads are
+    issued and waited for: labels, distances, inertia and changed count are bitwise those of
+    the plain prologue -- on ragged N, with an outlier row (per-point-offset workgroups)."""
+    from mikmeans.ops import pad_columns
+
+    g = torch.Generator().manual_seed(n + d)
+    X = torch.randn(n, d, generator=g)
+    if outlier:
+        X[n // 2] *= 300.0
+    Xb = pad_columns(X.to(torch.bfloat16).to(DEV))
+    C = torch.randn(k, d, generator=g) * 0.8
+    pk = ops.pack_centers(C.to(DEV), Xb.shape[1], torch.bfloat16, DEV)
+    xn = ops.row_sqnorm(Xb)
+    out = {}
+    for arm in ((0, 0), (0, 1), (1, 1)):
+        kvariant("assign_early", arm[0])
+        kvariant("assign_epi", arm[1])
+        lab = torch.full((n,), 3, dtype=torch.int32, device=DEV)
+        mind = torch.empty(n, device=DEV)
+        slots = torch.zeros(native.NSLOT * native.SLOT_STRIDE, dtype=torch.float64, device=DEV)
+        pk.assign(Xb, xn, lab, mind, slots, True)
+        torch.cuda.synchronize()
+        out[arm] = (lab, mind, slots.view(-1, native.SLOT_STRIDE)[:, :2].sum(0))
+    ref = out[(0, 0)]
+    for arm, o in out.items():
+        assert torch.equal(o[0], ref[0]) and torch.equal(o[1], ref[1]), arm
+        assert float(o[2][1]) == float(ref[2][1]), arm
+        assert float(o[2][0]) == pytest.approx(float(ref[2][0]), rel=1e-12), arm
+
+
+def test_assign_timeline_hook(native):
+    """set_assign_timeline: every workgroup of the next launches stamps entry <= loop start <=
+    epilogue start <= exit (real-time ticks) and its CU; disarmed, launches write nothing."""
+    from mikmeans.ops import pad_columns
+
+    n, d, k = 300_000, 128, 256    # (one-pass grid: small batches split the centres instead)
+    Xb = pad_columns(torch.randn(n, d, device=DEV).to(torch.bfloat16))
+    pk = ops.pack_centers(torch.randn(k, d, device=DEV), Xb.shape[1], torch.bfloat16, DEV)
+    xn = ops.row_sqnorm(Xb)
+    lab = torch.zeros(n, dtype=torch.int32, device=DEV)
+    buf = torch.zeros((n // 16 + 1) * 8, dtype=torch.int64, device=DEV)
+    native.set_assign_timeline(buf)
+    try:
+        pk.assign(Xb, xn, lab)
+        torch.cuda.synchronize()
+    finally:
+        native.set_assign_timeline(None)
+    t = buf.view(-1, 8).cpu()
+    t = t[t[:, 0] > 0]
+    assert len(t) > 0
+    assert bool((t[:, 0] <= t[:, 1]).all() and (t[:, 1] <= t[:, 2]).all() and (t[:, 2] <= t[:, 3]).all())
+    buf.zero_()
+    pk.assign(Xb, xn, lab)
+    torch.cuda.synchronize()
+    assert int(buf.abs().sum()) == 0
