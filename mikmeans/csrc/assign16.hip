@@ -124,24 +124,20 @@ __device__ __forceinline__ float sq16(const u32x4& w, float*) {
 // per score instead of the packed keys' 1.5); the row inside the winning tile is recovered
 // once per point after the loop by recomputing the winning tile's candidates on the
 // matrix cores (bitwise the main loop's scores), right after the chunk loop.
-// PERSIST: a grid of one workgroup per resident slot (occupancy x CUs) loops over the point
-// blocks (blk += gridDim.x).  Across a block boundary the centre ring keeps streaming (the
-// next pass's first chunk is issued at the last chunk's barrier of this one) and the next
-// block's fragments are loaded before this block's argmin epilogue, so their memory
-// latency hides under the epilogue instead of opening every workgroup's life; the inertia
-// and changed counts go to the slots once per workgroup.  Same scores, same labels.
+// (A persistent grid that carried the next block's fragments across the epilogue measured
+// 13-15 % slower -- the second register set spills at 4 waves/SIMD -- and was removed,
+// profiles/r4_04_persistent_grid_ab.md.)
 template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool FULLD = false,
-          bool VARG = false, int PMAJ = 0, bool PERSIST = false, bool AST = false, bool TOP2 = false, bool XV = false>
+          bool VARG = false, int PMAJ = 0, bool TOP2 = false, bool XV = false>
 __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   constexpr bool F32 = sizeof(T) == 4;
   // exact (value, index) epilogue: f32, or bf16 scores where the full pass ranks by value (XV)
   constexpr bool EXACT = F32 || XV;
-  // A fragments streamed one at a time (see the MFMA issue): rows of 384..1024 features, or
-  // AST (a lower-register variant of the narrow kernels)
-  constexpr bool WIDE = AST || DPAD > 256;
+  // A fragments streamed one at a time (see the MFMA issue): rows of 384..1024 features
+  constexpr bool WIDE = DPAD > 256;
   static_assert(!(VARG && F32), "value-only argmin is the bf16 epilogue");
-  static_assert(!(TOP2 && (VARG || PERSIST)), "bounded E-step: keys / exact epilogues, one pass per block");
+  static_assert(!(TOP2 && VARG), "bounded E-step: keys / exact epilogues");
   static_assert(!XV || (TOP2 && !F32), "the bf16 exact epilogue stands in for VARG in the bounded E-step");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -163,9 +159,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   const uint32_t loff = (uint32_t)lane * 16u;
   const __amdgpu_buffer_rsrc_t rC = make_rsrc(a.Cpack, (uint32_t)a.Kpad * DPAD * sizeof(T));
   const __amdgpu_buffer_rsrc_t rN = make_rsrc(a.cn, (uint32_t)a.Kpad * 4u);
-  // Ring slots: chunk c of the workgroup's p-th pass sits in slot (p * ncl + c) % NBUF
-  // (ring = p * ncl); one pass per workgroup unless PERSIST.
-  int ring = 0;
+  // Ring slots: chunk c sits in slot c % NBUF.
   auto issue_chunk = [&](int c, int slot) {  // c: chunk index within this split
     const uint32_t src = (uint32_t)(c0 + c) * C::CHUNK_BYTES;
     char* dst = bufs + slot * C::CHUNK_BYTES;
@@ -181,16 +175,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   const int64_t N = a.n_dev ? min(a.N, *a.n_dev) : a.N;
   if (a.n_dev && (int64_t)blockIdx.x * C::PTS >= N) return;
   const unsigned long long t_entry = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  if (a.stagger > 0) {   // (first resident wave only; see AssignArgs::stagger)
-    const int sl = (int)(blockIdx.x / (unsigned)a.stagger_cus);
-    if (sl > 0 && sl < a.stagger_slots) {
-      const uint64_t until = __builtin_amdgcn_s_memrealtime() + (uint64_t)sl * (uint64_t)a.stagger;
-      while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(8);
-    }
-  }
-  const int64_t nblk = (N + C::PTS - 1) / C::PTS;
-  int64_t blk = blockIdx.x;
-  int64_t pbase = blk * C::PTS + (int64_t)wid * (C::P * 16);
+  const int64_t pbase = (int64_t)blockIdx.x * C::PTS + (int64_t)wid * (C::P * 16);
   u32x4 xr[C::P][C::NQ];
   float xnr[C::P];
   float osr[C::P];   // (a.oseed) the rows' full-pass seed offsets, at their X rows
@@ -250,7 +235,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   // the seed-offset reduction waits for the norms alone -- its barrier runs while the fragments
   // are still in flight (the chunk loop's first wait retires them).  A/B switch V_ASSIGN_EARLY.
   constexpr int EJ = (C::P + 3) / 4;
-  constexpr bool EARLY_OK = !F32 && !PERSIST && FULLD && C::P * C::NQ + EJ + C::NPW < 64;   // (vmcnt range)
+  constexpr bool EARLY_OK = !F32 && FULLD && C::P * C::NQ + EJ + C::NPW < 64;   // (vmcnt range)
   const bool early = EARLY_OK && a.xn && !a.rows && !a.oseed && !a.split_keys && a.epi_prefetch &&
                      a.early_prologue;
   // early: lane (r, g) loads the norm of its epilogue rows only -- block p = 4j + g -- one
@@ -258,7 +243,6 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   // what takes its time, profiles/r5_45_assign_prologue_study.md); lanes past the last block
   // repeat it (harmless to the max / min)
   float xg[EJ];
-  if (a.prologue_prio) __builtin_amdgcn_s_setprio(3);
   if (early) {
     for (int pc = wid; pc < cn_bytes / 1024; pc += C::NW)
       blds16(rN, (MK_LDS void*)(cn_lds + pc * 1024), loff, (uint32_t)pc * 1024u);
@@ -280,7 +264,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
   // p = 4j + g, so it keeps their old label and caller norm -- two registers per 4 blocks
   int eold[EJ];
   float exn[EJ];
-  const bool eread = !PERSIST && !a.split_keys && a.epi_prefetch;
+  const bool eread = !a.split_keys && a.epi_prefetch;
   if (eread) {
 #pragma unroll
     for (int j = 0; j < EJ; ++j) {
@@ -307,18 +291,16 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       }
     }
   }
-  // per-wave (inertia, changed) totals over the workgroup's passes, in LDS after the offsets
+  // per-wave (inertia, changed) totals, in LDS after the offsets
   double* wacc = (double*)(bufs + C::NBUF * C::CHUNK_BYTES + 16 * C::NW + C::OPT_BYTES);
-  for (bool first = true;; first = false) {
+  {
     // |c|^2 and the first centre chunk by LDS-DMA, issued after the fragments so no wait for a
-    // fragment address (the gathered row indices) also waits for them.  (PERSIST: after the
-    // first pass the chunk is already in flight, issued at the previous pass's last barrier.)
+    // fragment address (the gathered row indices) also waits for them.
     __builtin_amdgcn_sched_barrier(0);
     if (!early)
       for (int p = wid; p < cn_bytes / 1024; p += C::NW)
         blds16(rN, (MK_LDS void*)(cn_lds + p * 1024), loff, (uint32_t)p * 1024u);
-    if (!PERSIST || first) issue_chunk(0, ring % C::NBUF);
-    if (a.prologue_prio) __builtin_amdgcn_s_setprio(0);   // (every prologue load issued)
+    issue_chunk(0, 0);
     unsigned long long t_frag = 0ull;
     if (early) {
       // the norms and |c|^2 landed; younger: the fragments, one label load per 4 blocks and
@@ -332,9 +314,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       wait_vmcnt<0>();  // retire the fragments before the LDS-DMA loop (its vmcnt waits count chunks)
     }
     const unsigned long long t_landed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    if (C::NBUF == 3 && ncl > 1) issue_chunk(1, (ring + 1) % C::NBUF);
-    const int64_t nxt = blk + (int64_t)gridDim.x;
-    const bool has_next = PERSIST && nxt < nblk;   // (wave-uniform)
+    if (C::NBUF == 3 && ncl > 1) issue_chunk(1, 1);
 
     // bf16 seed offset (see the header): o = (1 + 2^-12) max |x|^2 over the workgroup's
     // points, from the caller's row norms when given (loaded with the fragments) or from
@@ -450,9 +430,8 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         // (the next chunk's pieces all go out right after the barrier: spreading them one group
         // per tile after that tile's epilogue measured -2.5 % at D=128, -5 % at D=256 and far
         // slower at D=64, profiles/r3_28_ab_spread_dma.log)
-        if (c + C::NBUF - 1 < ncl) issue_chunk(c + C::NBUF - 1, (ring + c + C::NBUF - 1) % C::NBUF);
-        else if (has_next && c + C::NBUF - 1 == ncl) issue_chunk(0, (ring + ncl) % C::NBUF);  // next pass
-        const char* buf = bufs + ((ring + c) % C::NBUF) * C::CHUNK_BYTES;
+        if (c + C::NBUF - 1 < ncl) issue_chunk(c + C::NBUF - 1, (c + C::NBUF - 1) % C::NBUF);
+        const char* buf = bufs + (c % C::NBUF) * C::CHUNK_BYTES;
         // A fragments + |c|^2 of a tile from the LDS ring
         auto load_a = [&](int tl_i, u32x4* aw_, f32x4& ci_) {
           const int tile = (c0 + c) * C::CT + tl_i;
@@ -621,7 +600,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     const unsigned long long t_loop = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (ppo) chunk_loop(std::true_type{});
     else chunk_loop(std::false_type{});
-    if (a.timeline && threadIdx.x == 0 && first && blockIdx.y == 0) {
+    if (a.timeline && threadIdx.x == 0 && blockIdx.y == 0) {
       unsigned long long* tl = a.timeline + (int64_t)blockIdx.x * 8;
       tl[0] = t_entry;
       tl[1] = t_loop;
@@ -769,66 +748,30 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
         }
       }
     };
-    if constexpr (!PERSIST) {
 #pragma unroll
-      for (int p = 0; p < C::P; ++p) {
-        int k;
-        float v;
-        merged(p, k, v);
-        float sec = 0.f;
-        if constexpr (TOP2) sec = second(p);
-        const int64_t i = pcur + p * 16 + r;
-        if ((p & 3) == g && i < N) {
-          const int64_t oi = a.scatter ? a.rows[i] : i;
-          const bool rd = !a.split_keys;
-          store(p, oi, k, v, eread ? eold[p >> 2] : (rd && a.track_changed ? a.labels[oi] : -2),
-                eread ? exn[p >> 2] : (rd && a.xn ? a.xn[oi] : 0.f), sec);
-        }
+    for (int p = 0; p < C::P; ++p) {
+      int k;
+      float v;
+      merged(p, k, v);
+      float sec = 0.f;
+      if constexpr (TOP2) sec = second(p);
+      const int64_t i = pcur + p * 16 + r;
+      if ((p & 3) == g && i < N) {
+        const int64_t oi = a.scatter ? a.rows[i] : i;
+        const bool rd = !a.split_keys;
+        store(p, oi, k, v, eread ? eold[p >> 2] : (rd && a.track_changed ? a.labels[oi] : -2),
+              eread ? exn[p >> 2] : (rd && a.xn ? a.xn[oi] : 0.f), sec);
       }
-    } else {
-      // merge every block first (frees the running keys), then this block's global reads,
-      // then the next block's fragments -- after those reads, so neither waits on the
-      // other's round trip (vmcnt retires in order) -- whose latency hides under the stores
-      int kk[C::P], oldl[C::P];
-      float vv[C::P], xg[C::P];
-#pragma unroll
-      for (int p = 0; p < C::P; ++p) merged(p, kk[p], vv[p]);
-#pragma unroll
-      for (int p = 0; p < C::P; ++p) {
-        const int64_t i = pcur + p * 16 + r;
-        const bool mine = (p & 3) == g && i < N;
-        oldl[p] = mine && a.track_changed ? a.labels[i] : -2;
-        xg[p] = mine && a.xn ? a.xn[i] : 0.f;
-      }
-      if (has_next) {
-        __builtin_amdgcn_sched_barrier(0);
-        blk = nxt;
-        pbase = blk * C::PTS + (int64_t)wid * (C::P * 16);
-        load_block();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int p = 0; p < C::P; ++p)
-        if ((p & 3) == g && pcur + p * 16 + r < N) store(p, pcur + p * 16 + r, kk[p], vv[p], oldl[p], xg[p], 0.f);
     }
-    if (a.slots && !a.split_keys) {
-      // this pass's wave totals; over several passes (PERSIST) they accumulate in this
-      // wave's LDS slot, so no register stays live across the chunk loop
+    if (a.slots && !a.split_keys) {   // the wave's totals, in its LDS slot
       const double di = wave_sum((double)inert);
       const int dc = wave_sum(changed);
       if (lane == 0) {
-        wacc[2 * wid] = (PERSIST && !first) ? wacc[2 * wid] + di : di;
-        wacc[2 * wid + 1] = (PERSIST && !first) ? wacc[2 * wid + 1] + (double)dc : (double)dc;
+        wacc[2 * wid] = di;
+        wacc[2 * wid + 1] = (double)dc;
       }
     }
-    if (!has_next) break;
-    // (PERSIST) every wave is past its last reads of this pass's |c|^2 copy, offsets and slot
-    // scratch before the next prologue rewrites them; a raw barrier, so the next block's
-    // fragments and first chunk stay in flight (__syncthreads would drain vmcnt)
-    wait_lgkm0();
-    raw_barrier();
-    ring += ncl;
-  }  // block loop
+  }
   if (a.timeline && threadIdx.x == 0 && blockIdx.y == 0)
     a.timeline[(int64_t)blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();
   if (a.slots && !a.split_keys) {
@@ -840,9 +783,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
       double si = 0, sc = 0;
 #pragma unroll
       for (int w = 0; w < C::NW; ++w) { si += wacc[2 * w]; sc += wacc[2 * w + 1]; }
-      double* slot = a.slots + (blockIdx.x % NSLOT) * SLOT_STRIDE;
-      atomicAdd(slot + 0, si);
-      atomicAdd(slot + 1, sc);
+      slot_add((unsigned long long*)(a.slots + (blockIdx.x % NSLOT) * SLOT_STRIDE), si, (long long)sc);
     }
   }
 }
@@ -873,11 +814,9 @@ __global__ __launch_bounds__(256) void split_finish_kernel(AssignArgs a) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (lane == 0) { red[2 * w] = di; red[2 * w + 1] = (double)dc; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      double* slot = a.slots + (blockIdx.x % NSLOT) * SLOT_STRIDE;
-      atomicAdd(slot + 0, red[0] + red[2] + red[4] + red[6]);
-      atomicAdd(slot + 1, red[1] + red[3] + red[5] + red[7]);
-    }
+    if (threadIdx.x == 0)
+      slot_add((unsigned long long*)(a.slots + (blockIdx.x % NSLOT) * SLOT_STRIDE), red[0] + red[2] + red[4] + red[6],
+               (long long)(red[1] + red[3] + red[5] + red[7]));
   }
 }
 
@@ -898,30 +837,26 @@ static int assign16_splits(int64_t nblk, int nch) {
 // D=64 K=2048 +8.5 %, K=1024 -3.7 %; D=32 K=1024 +5.6 %, K=512 -8.8 %).
 // Variant V_ASSIGN_VARG = 0/1 forces it off / on (A/B, tests).
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST,
-          bool TOP2, bool XV>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool TOP2, bool XV>
 static void set_lds_attr() {
   static bool done = false;
   if (done) return;
-  (void)hipFuncSetAttribute(
-      (const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST, TOP2, XV>,
-      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute(
-      (const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST, TOP2, XV>,
-      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, TOP2, XV>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, TOP2, XV>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   done = true;
 }
 
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST,
-          bool TOP2, bool XV>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool TOP2, bool XV>
 static void launch16_kt(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, TOP2, XV>();
+  set_lds_attr<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, TOP2, XV>();
   if (b.D == DPAD)
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, PERSIST, AST, TOP2, XV>),
-                       grid, dim3(NW_ * 64), lds, s, b);
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, VARG, PMAJ, TOP2, XV>), grid,
+                       dim3(NW_ * 64), lds, s, b);
   else
-    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, PERSIST, AST, TOP2, XV>),
-                       grid, dim3(NW_ * 64), lds, s, b);
+    hipLaunchKernelGGL((assign16_kernel<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, VARG, PMAJ, TOP2, XV>), grid,
+                       dim3(NW_ * 64), lds, s, b);
 }
 
 // The geometries that run the bounded E-step's TOP2 epilogue (launch16_d routes every call
@@ -929,10 +864,9 @@ static void launch16_kt(const AssignArgs& b, const dim3& grid, size_t lds, hipSt
 // defaults at D = 64 / 128 / 256 spilled 400-940 VGPRs and ran 5.7x slower
 // (profiles/r4_05_hamerly_ab_top2_spills.log); the state is now the second minimum alone
 // (profiles/r4_16_top2_register_study.md), and D = 256 keeps 3 blocks at 8 waves per ring.
-template <typename T, int DPAD, int P, int OCC, int NW_, bool AST>
+template <typename T, int DPAD, int P, int OCC, int NW_>
 constexpr bool top2_geom() {
   if (sizeof(T) == 4 || DPAD == 32 || DPAD > 256) return true;   // (the defaults hold it, 0 spills)
-  if (AST) return false;
   if (DPAD == 64) return (P == 2 || P == 4) && OCC == 4 && NW_ == 4;
   if (DPAD == 128) return (P == 2 || P == 4) && OCC == 4 && NW_ == 4;
   if (DPAD == 256) return P == 3 && OCC == 2 && NW_ == 8;
@@ -942,18 +876,18 @@ constexpr bool top2_geom() {
 // With bounds (b.ub) the VARG flag says how the FULL pass of this shape ranks: by value (the
 // value-only argmin) -> the TOP2 kernel takes the exact (value, index) epilogue (XV), else the
 // packed keys; with the full pass's seed offsets (b.oseed) its labels are then the full pass's.
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool PERSIST, bool AST>
-static void launch16_kpp(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ>
+static void launch16_kp(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
   if (b.ub) {
-    if constexpr (!PERSIST && top2_geom<T, DPAD, P, OCC, NW_, AST>()) {
+    if constexpr (top2_geom<T, DPAD, P, OCC, NW_>()) {
       if constexpr (VARG && sizeof(T) == 2)
-        return launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, PMAJ, PERSIST, AST, true, true>(b, grid, lds, s);
+        return launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, PMAJ, true, true>(b, grid, lds, s);
       else
-        return launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, PMAJ, PERSIST, AST, true, false>(b, grid, lds, s);
+        return launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, PMAJ, true, false>(b, grid, lds, s);
     }
-    return;   // (unreachable: launch16_d sends bounds to a top2_geom geometry, one-pass grid)
+    return;   // (unreachable: launch16_d sends bounds to a top2_geom geometry)
   }
-  launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, PERSIST, AST, false, false>(b, grid, lds, s);
+  launch16_kt<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, false, false>(b, grid, lds, s);
 }
 
 static unsigned long long* g_timeline = nullptr;
@@ -963,47 +897,19 @@ void set_assign_timeline(unsigned long long* buf, int64_t capacity) {
   g_timeline_cap = buf ? capacity : 0;
 }
 
-// Resident workgroups the whole chip holds for a launch geometry: the smaller of the
-// wave-slot and the LDS limit per CU, times the CU count (the persistent grid).
-static int64_t resident_workgroups(int waves_per_wg, int occ_per_simd, size_t lds) {
-  static int cus = [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    return n;
-  }();
-  const int by_waves = (4 * occ_per_simd) / waves_per_wg;
-  const int by_lds = lds ? (int)((160 * 1024) / lds) : by_waves;
-  const int per_cu = by_waves < by_lds ? by_waves : by_lds;
-  return (int64_t)(per_cu > 0 ? per_cu : 1) * cus;
-}
-
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, int PMAJ, bool AST>
-static void launch16_kp(const AssignArgs& b, dim3 grid, size_t lds, hipStream_t s) {
-  // Persistent grid (variant V_ASSIGN_PERSIST = 1; default off): one-pass grids only (no
-  // centre split), and only where the point blocks outnumber the resident slots.
-  const int64_t slots = resident_workgroups(NW_, OCC, lds);
-  if (variant(V_ASSIGN_PERSIST) > 0 && grid.y == 1 && (int64_t)grid.x > slots && !b.ub && !b.scatter &&
-      !b.n_dev) {
-    grid.x = (unsigned)slots;
-    return launch16_kpp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, true, AST>(b, grid, lds, s);
-  }
-  launch16_kpp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, PMAJ, false, AST>(b, grid, lds, s);
-}
-
-template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG, bool AST>
+template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG>
 static void launch16_k(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
-  if constexpr (AST || DPAD > 256) {   // streamed A fragments: one issue order
-    return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 0, AST>(b, grid, lds, s);
+  if constexpr (DPAD > 256) {   // streamed A fragments: one issue order
+    return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 0>(b, grid, lds, s);
   } else {
     const int e = variant(V_ASSIGN_PMAJ);
     const int pm = e >= 0 ? e : (sizeof(T) == 2 ? 1 : 0);
-    if (pm != 0) return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 1, AST>(b, grid, lds, s);
-    launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 0, AST>(b, grid, lds, s);
+    if (pm != 0) return launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 1>(b, grid, lds, s);
+    launch16_kp<T, DPAD, P, CT_, NBUF_, OCC, NW_, VARG, 0>(b, grid, lds, s);
   }
 }
 
-template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4, bool AST = false>
+template <typename T, int DPAD, int P, int CT_ = 0, int NBUF_ = 2, int OCC = 1, int NW_ = 4>
 static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   using C = Assign16Cfg<T, DPAD, P, CT_, NBUF_, NW_>;
   if (a.Kpad % (16 * C::CT) != 0) return hipErrorInvalidValue;
@@ -1022,31 +928,18 @@ static hipError_t launch16_t(const AssignArgs& a, hipStream_t s) {
   if (g_timeline && nblk <= g_timeline_cap && splits == 1) b.timeline = g_timeline;
   b.epi_prefetch = variant(V_ASSIGN_EPI) != 0;
   b.early_prologue = variant(V_ASSIGN_EARLY) != 0;
-  b.prologue_prio = variant(V_ASSIGN_PPRIO) > 0;
-  {
-    // A/B switch V_ASSIGN_STAGGER (microseconds per CU slot): start the first resident wave's
-    // workgroups of slot s s * step late (AssignArgs::stagger)
-    const int st = variant(V_ASSIGN_STAGGER);
-    if (st > 0 && splits == 1) {
-      const int64_t res = resident_workgroups(C::NW, OCC, lds);
-      const int cus = resident_workgroups(4, 1, 0) / 1;   // (4 waves at 1/SIMD: one per CU)
-      b.stagger = st * 100;
-      b.stagger_cus = cus;
-      b.stagger_slots = (int)(res / cus);
-    }
-  }
   bool varg = false;
   constexpr bool VARG_OK = sizeof(T) == 2 && DPAD <= 64;   // D=128: -12 % at K=1024, -4 % at 2048 (r3_11)
   if constexpr (VARG_OK) {
     const int e = variant(V_ASSIGN_VARG);
-    // (with bounds: whether the full pass would, see launch16_kpp)
+    // (with bounds: whether the full pass would, see launch16_kp)
     varg = e >= 0 ? e != 0 : a.Kpad >= (DPAD == 64 ? 2048 : 1024);
   }
   if constexpr (VARG_OK) {
-    if (varg) launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, true, AST>(b, grid, lds, s);
-    else launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, AST>(b, grid, lds, s);
+    if (varg) launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, true>(b, grid, lds, s);
+    else launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, false>(b, grid, lds, s);
   } else {
-    launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, false, AST>(b, grid, lds, s);
+    launch16_k<T, DPAD, P, CT_, NBUF_, OCC, NW_, false>(b, grid, lds, s);
   }
   if (splits > 1)
     hipLaunchKernelGGL(split_finish_kernel, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, s, b);
@@ -1067,19 +960,18 @@ constexpr int p_wide() {
 template <typename T, int DPAD>
 static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
   constexpr int CT = chunk_tiles16(sizeof(T), DPAD);
-  constexpr int NQ = DPAD / 4 / Elem<T>::V;
   // 16 KiB chunks in a 2-slot ring.  A/B on MI355X (one process, interleaved rounds; round 1
   // profiles/r1_08_*, r1_16_*, r1_17_*, round 2 profiles/r2_04_assign_ab.md):
-  //  * bf16 D=128: 4 point blocks per wave at <= 128 VGPRs (4 waves/SIMD) -- 3 / 5 blocks,
-  //    3 waves/SIMD, 8/16 waves per ring, 4/8 KiB chunks x 3 slots and next-tile fragment
+  //  * bf16 D=128: 4 point blocks per wave at <= 128 VGPRs (4 waves/SIMD) -- 3 / 5 / 6 / 8 blocks,
+  //    2-3 waves/SIMD, 8/16 waves per ring, 4/8 KiB chunks x 3 slots and next-tile fragment
   //    loads under the MFMAs are all slower;
   //  * bf16 D=64: 8 point blocks at 3 waves/SIMD, -5 % against 4 blocks at 4; with the
   //    value-only argmin (K >= 2048) 4 blocks at 4 waves are 4-9 % slower and 12 blocks at
   //    2 waves 1-10 % slower (profiles/r3_10_assign_p64_ab.log);
-  //  * bf16 D=256: 3 point blocks at 3 waves/SIMD, -4 % against 2 at 4;
+  //  * bf16 D=256: 3 point blocks at 3 waves/SIMD, -4 % against 2 at 4; streamed A fragments
+  //    (3, 4 or 6 blocks) and a 3-slot ring were slower too (r4_04, r5_67), and were removed;
   //  * f32: the register file sets 4 (D <= 64) or 2 blocks at one wave per SIMD minimum.
   constexpr int P = p_narrow<T, DPAD>();
-  (void)NQ;
   constexpr int OCC = sizeof(T) == 2 ? ((DPAD == 64 || DPAD == 256) ? 3 : 4) : 1;
   static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
   if (a.ub) {   // bounded E-step (TOP2): the geometries of top2_geom
@@ -1099,21 +991,9 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
     if constexpr (sizeof(T) == 2 && DPAD == 256) return launch16_t<T, DPAD, 3, CT, 2, 2, 8>(a, s);
   }
   if constexpr (sizeof(T) == 2 && DPAD == 256) {
-    // A/B switch V_ASSIGN_GEOM: 8 waves per ring (half the per-point centre stream and
-    // per-workgroup start-up): 1 = 3 point blocks at 2 waves/SIMD, 2 = 2 blocks at 4
-    const int gm = variant(V_ASSIGN_GEOM);
-    if (gm == 1) return launch16_t<T, DPAD, 3, CT, 2, 2, 8>(a, s);
-    if (gm == 2) return launch16_t<T, DPAD, 2, CT, 2, 4, 8>(a, s);
-    // 3: streamed A fragments (the wide-row issue), 3 blocks at 3 waves/SIMD in 151-157
-    // VGPRs without the 4 spilled registers of the default (4 blocks spill hundreds)
-    if (gm == 3) return launch16_t<T, DPAD, 3, CT, 2, 3, 4, true>(a, s);
-    // 4: streamed A fragments with 6 point blocks at 2 waves/SIMD (each A fragment feeds 6
-    // MFMAs, half the LDS reads and chunk barriers per MFMA of the default); 5: 4 blocks
-    if (gm == 4) return launch16_t<T, DPAD, 6, CT, 2, 2, 4, true>(a, s);
-    if (gm == 5) return launch16_t<T, DPAD, 4, CT, 2, 2, 4, true>(a, s);
-    // 6: the default with a 3-slot ring (two chunks in flight: a 2-tile chunk is only ~1 us of
-    // MFMA work per wave at 3 waves/SIMD, about one L2 round trip); 50 KiB LDS, 3 per CU
-    if (gm == 6) return launch16_t<T, DPAD, 3, CT, 3, 3>(a, s);
+    // A/B switch V_ASSIGN_GEOM = 1: 8 waves per ring (half the per-point centre stream and
+    // per-workgroup start-up), 3 point blocks at 2 waves/SIMD -- the bounded E-step's geometry
+    if (variant(V_ASSIGN_GEOM) == 1) return launch16_t<T, DPAD, 3, CT, 2, 2, 8>(a, s);
   }
   if constexpr (sizeof(T) == 2 && DPAD == 128) {
     // A/B switch V_ASSIGN_GEOM: 1 = 8 waves share a ring of 32 KiB chunks (a barrier
@@ -1125,8 +1005,6 @@ static hipError_t launch16_d(const AssignArgs& a, hipStream_t s) {
     const int gm = variant(V_ASSIGN_GEOM);
     if (gm == 1 && a.Kpad % (16 * 8) == 0) return launch16_t<T, DPAD, P, 8, 2, OCC, 8>(a, s);
     if (gm == 2) return launch16_t<T, DPAD, P, CT, 2, OCC, 8>(a, s);
-    if (gm == 3) return launch16_t<T, DPAD, 6, CT, 2, 3>(a, s);   // 6 point blocks at 3 waves/SIMD
-    if (gm == 4) return launch16_t<T, DPAD, 8, CT, 2, 2>(a, s);   // 8 point blocks at 2 waves/SIMD (half the LDS reads)
   }
   return launch16_t<T, DPAD, P, CT, 2, OCC>(a, s);
 }
@@ -1158,20 +1036,14 @@ static int block_rows_t(int kpad) {
   const int gm = variant(V_ASSIGN_GEOM);
   if constexpr (sizeof(T) == 2 && DPAD == 256) {
     if (gm == 1) return 8 * 3 * 16;
-    if (gm == 2) return 8 * 2 * 16;
-    if (gm == 4) return 4 * 6 * 16;
-    if (gm == 5) return 4 * 4 * 16;
   }
   if constexpr (sizeof(T) == 2 && DPAD == 128) {
     if ((gm == 1 && kpad % (16 * 8) == 0) || gm == 2) return 8 * 4 * 16;
-    if (gm == 3) return 4 * 6 * 16;
-    if (gm == 4) return 4 * 8 * 16;
   }
   return 4 * p_narrow<T, DPAD>() * 16;
 }
 
 int assign16_block_rows(int dtype, int dpad, int kpad) {
-  if (variant(V_ASSIGN_CS) > 0 && assign_cs_eligible(dtype, dpad, kpad)) return 64;   // its super-block
   if (dtype == DT_BF16) {
     switch (dpad) {
       case 32: return block_rows_t<uint16_t, 32>(kpad);
@@ -1200,7 +1072,6 @@ int assign16_block_rows(int dtype, int dpad, int kpad) {
 }
 
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s) {
-  if (variant(V_ASSIGN_CS) > 0 && assign_cs_takes(dtype, dpad, a)) return launch_assign_cs(dpad, a, s);
   if (dtype == DT_BF16) {
     switch (dpad) {
       case 32: return launch16_d<uint16_t, 32>(a, s);

@@ -614,10 +614,8 @@ namespace mk {
 static const char* const kVariantEnv[V_COUNT] = {"MIKMEANS_ASSIGN_VARG", "MIKMEANS_ASSIGN_PMAJ",
                                                  "MIKMEANS_ASSIGN_GEOM", "MIKMEANS_UPDATE_KS",
                                                  "MIKMEANS_UPDATE_KS_GM", "MIKMEANS_BLOBS_TPR",
-                                                 "MIKMEANS_ASSIGN_PERSIST", "MIKMEANS_ASSIGN_TOP2_GEOM",
-                                                 "MIKMEANS_ASSIGN_CS", "MIKMEANS_ASSIGN_STAGGER",
-                                                 "MIKMEANS_ASSIGN_EPI", "MIKMEANS_ASSIGN_EARLY",
-                                                 "MIKMEANS_ASSIGN_PPRIO"};
+                                                 "MIKMEANS_ASSIGN_TOP2_GEOM", "MIKMEANS_ASSIGN_EPI",
+                                                 "MIKMEANS_ASSIGN_EARLY"};
 static int* variant_table() {
   static int t[V_COUNT] = {};
   static const bool init = [] {
@@ -846,10 +844,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return n;
   }, "A/B switch names (lower-cased by mikmeans.ops.native)");
   m.def("set_assign_timeline", [](c10::optional<torch::Tensor> buf) {
-    if (!buf.has_value()) { mk::set_assign_timeline(nullptr, 0); return; }
+    // the binding holds a reference while the hook is armed: a caller that drops its buffer
+    // cannot leave later launches writing into memory the caching allocator handed on
+    static torch::Tensor held;
+    if (!buf.has_value()) { mk::set_assign_timeline(nullptr, 0); held = torch::Tensor(); return; }
     TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == torch::kInt64 && buf->is_contiguous(),
                 "mikmeans: timeline buffer must be a contiguous int64 CUDA tensor");
-    mk::set_assign_timeline((unsigned long long*)buf->data_ptr<int64_t>(), buf->numel() / 8);
+    int dev = 0;
+    hip_check(hipGetDevice(&dev), "hipGetDevice");
+    TORCH_CHECK(buf->get_device() == dev, "mikmeans: timeline buffer on device ", buf->get_device(),
+                ", launches run on device ", dev);
+    held = *buf;
+    mk::set_assign_timeline((unsigned long long*)held.data_ptr<int64_t>(), held.numel() / 8);
   }, py::arg("buf"));
   m.def("get_variant", [](int64_t i) {
     TORCH_CHECK(i >= 0 && i < mk::V_COUNT, "mikmeans: no A/B switch ", i);

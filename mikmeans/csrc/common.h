@@ -188,6 +188,42 @@ __device__ __forceinline__ int wave_sum(int v) {
   return v;
 }
 
+// ---------------------------------------------------------------------------
+// Order-free inertia / changed-count slots.  A slot is 8 u64 words: words 0..6 hold
+// signed 32-bit "digits" of a fixed-point sum at scale 2^-64 (word j weighs 2^(32 j - 64),
+// range up to 2^160), word 7 an integer count.  Every addend is truncated to a multiple of
+// 2^-64 by its own value alone and added with integer atomics, so the totals -- and the
+// f64 decoded from them in a fixed order -- are bitwise the same whatever order the
+// workgroups finish in (f64 atomicAdd made the logged inertia vary in its low bits from
+// launch to launch).  A non-finite or >= 2^149 addend marks word 6 with 2^61 (inf).
+constexpr unsigned long long SLOT_OVF = 1ull << 61;
+__device__ __forceinline__ void slot_add(unsigned long long* w, double v, long long cnt) {
+  if (cnt) atomicAdd(w + 7, (unsigned long long)cnt);
+  if (v == 0.0) return;
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+  const bool neg = bits >> 63;
+  const int ex = (int)((bits >> 52) & 0x7ff);
+  if (ex == 0x7ff) { atomicAdd(w + 6, SLOT_OVF); return; }
+  unsigned long long m = (bits & ((1ull << 52) - 1)) | (ex ? (1ull << 52) : 0ull);
+  int s = (ex ? ex : 1) - 1075 + 64;          // v = m * 2^(s - 64)
+  if (s < 0) { m = -s >= 64 ? 0ull : m >> -s; s = 0; }
+  const int j0 = s >> 5, o = s & 31;
+  if (j0 > 4) { atomicAdd(w + 6, SLOT_OVF); return; }
+  const unsigned long long lo = m << o, hi = o ? (m >> (64 - o)) : 0ull;
+  const unsigned long long d[3] = {lo & 0xffffffffull, lo >> 32, hi};
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (d[i]) atomicAdd(w + j0 + i, neg ? (unsigned long long)(-(long long)d[i]) : d[i]);
+}
+// The value of summed digit words W[0..6] (each the int64 total over slots), fixed order.
+__device__ __forceinline__ double slot_decode(const long long* W) {
+  if (W[6] >= (long long)(SLOT_OVF >> 1)) return __builtin_inf();
+  double v = 0.0;
+#pragma unroll
+  for (int j = 6; j >= 0; --j) v += __builtin_ldexp((double)W[j], 32 * j - 64);
+  return v;
+}
+
 // argmin key: a score with a 4-bit index in its low mantissa bits (relative
 // resolution 2^-19), so one v_min3_f32 tree yields (min score, index).
 __device__ __forceinline__ float pack_key(float s, int r) {

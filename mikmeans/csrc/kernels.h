@@ -32,8 +32,10 @@ constexpr int SLOT_STRIDE = 8;
 // environment: the values are taken from MIKMEANS_<NAME> once when the extension loads and
 // changed only through set_variant (mikmeans.ops.native.variant); -1 = the built-in rule.
 // A captured hipGraph keeps the geometry that was in force when it was recorded.
+// (Round 6 removed the measured losers: the persistent grid, the centre-stationary kernel, the
+// first-wave stagger and the prologue priority; their results stay in profiles/.)
 enum Variant { V_ASSIGN_VARG = 0, V_ASSIGN_PMAJ, V_ASSIGN_GEOM, V_UPDATE_KS, V_UPDATE_KS_GM, V_BLOBS_TPR,
-               V_ASSIGN_PERSIST, V_ASSIGN_TOP2_GEOM, V_ASSIGN_CS, V_ASSIGN_STAGGER, V_ASSIGN_EPI, V_ASSIGN_EARLY, V_ASSIGN_PPRIO, V_COUNT };
+               V_ASSIGN_TOP2_GEOM, V_ASSIGN_EPI, V_ASSIGN_EARLY, V_COUNT };
 int variant(Variant v);
 void set_variant(Variant v, int value);
 
@@ -47,7 +49,7 @@ struct AssignArgs {
   const float* xn;      // optional: |x|^2 per row, needed for mind/inertia
   int32_t* labels;      // in/out (old labels read when track_changed)
   float* mind;          // optional: squared distance to the chosen centroid
-  double* slots;        // optional: [NSLOT][SLOT_STRIDE] (+inertia, +changed)
+  double* slots;        // optional: [NSLOT][SLOT_STRIDE] order-free digit slots (common.h slot_add)
   int track_changed;
   // optional u64 [N] all-ones scratch; small N then splits the centre range over
   // grid.y (split_finish_kernel writes labels and restores the all-ones)
@@ -70,10 +72,6 @@ struct AssignArgs {
   // oseed[row] -- the offset the full (ungathered) pass gives it, from launch_seed_offsets -- so a
   // gathered batch ranks each row bitwise as the full pass does (the bounded E-step)
   const float* oseed = nullptr;
-  // first-wave stagger (launcher-set): a workgroup of the launch's first resident wave in CU
-  // slot s > 0 (blockIdx.x / stagger_cus, < stagger_slots) starts s * stagger real-time ticks
-  // (10 ns) late, so the co-resident workgroups' row loads and MFMA phases do not line up
-  int stagger = 0, stagger_cus = 0, stagger_slots = 0;
   // optional timeline (profiling, launcher-set from set_assign_timeline): per workgroup 8 u64 --
   // real-time ticks (10 ns) at entry, chunk-loop start, epilogue start and exit, then HW_ID
   // and XCC_ID (which CU ran it), then the tick wave 0's prologue loads had all landed
@@ -84,9 +82,6 @@ struct AssignArgs {
   // launcher-set (A/B switch V_ASSIGN_EARLY): norms first, fragments in flight across the
   // seed-offset barrier (plain full bf16 rows with caller norms)
   int early_prologue = 1;
-  // launcher-set (A/B switch V_ASSIGN_PPRIO): the prologue's loads issue at raised wave
-  // priority (s_setprio 3), ahead of the co-resident waves' centre-ring DMA
-  int prologue_prio = 0;
 };
 // Profiling hook: every assign16 launch writes its workgroups' timelines to buf (nullptr: off;
 // the caller sizes it for the grid, 8 u64 per workgroup, capacity in workgroups)
@@ -95,11 +90,6 @@ hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t
 // Rows per workgroup of the full (ungathered, unbounded) assign for this shape: the block its
 // bf16 seed offset is taken over (mirrors launch16_d / launch16_w)
 int assign16_block_rows(int dtype, int dpad, int kpad);
-// The centre-stationary bf16 assign (assign_cs.hip; A/B switch V_ASSIGN_CS = 1): whether it
-// handles a shape, and its launcher (plain full passes with row norms only).
-bool assign_cs_eligible(int dtype, int dpad, int kpad);
-bool assign_cs_takes(int dtype, int dpad, const AssignArgs& a);
-hipError_t launch_assign_cs(int dpad, const AssignArgs& a, hipStream_t s);
 // oseed[i] = the full pass's seed offset of row i (block_rows from assign16_block_rows; bf16)
 hipError_t launch_seed_offsets(const float* xn, int64_t n, int block_rows, float* oseed, hipStream_t s);
 

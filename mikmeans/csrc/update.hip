@@ -1014,6 +1014,41 @@ hipError_t launch_update(int dtype, const UpdateArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
+// The assign kernel's slots (common.h slot_add) -> out[0] = inertia, out[1] = changed rows,
+// then re-zeroed.  Integer word totals, decoded in a fixed order: the same bits whatever
+// order the assign's workgroups added in.  One 256-thread workgroup.
+__device__ void slots_collect(double* slots, double* out) {
+  __shared__ long long red[4][SLOT_STRIDE];
+  long long w[SLOT_STRIDE];
+#pragma unroll
+  for (int j = 0; j < SLOT_STRIDE; ++j) w[j] = 0;
+  if (slots) {
+    unsigned long long* s = (unsigned long long*)slots;
+    for (int i = threadIdx.x; i < NSLOT; i += 256) {
+#pragma unroll
+      for (int j = 0; j < SLOT_STRIDE; ++j) {
+        w[j] += (long long)s[i * SLOT_STRIDE + j];
+        s[i * SLOT_STRIDE + j] = 0ull;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < SLOT_STRIDE; ++j) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) w[j] += __shfl_xor(w[j], o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][j] = w[j];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long W[SLOT_STRIDE];
+#pragma unroll
+    for (int j = 0; j < SLOT_STRIDE; ++j) W[j] = red[0][j] + red[1][j] + red[2][j] + red[3][j];
+    out[0] = slot_decode(W);
+    out[1] = (double)W[7];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // launch_reduce: packed[k*D+d] = 2^-exp[d] * sum_c slab[c][k][d] (f64, exact: every
 // partial is an integer below 2^53), counts likewise,
 // plus the assign kernel's inertia / changed slots (which it then re-zeroes).
@@ -1046,26 +1081,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(const long long* __restrict
     }
     packed[e] = acc;
   }
-  if (blockIdx.x == gridDim.x - 1) {
-    __shared__ double red[4][2];
-    double si = 0, sc = 0;
-    if (slots) {
-      for (int i = threadIdx.x; i < NSLOT; i += 256) {
-        si += slots[i * SLOT_STRIDE + 0];
-        sc += slots[i * SLOT_STRIDE + 1];
-        slots[i * SLOT_STRIDE + 0] = 0.0;
-        slots[i * SLOT_STRIDE + 1] = 0.0;
-      }
-    }
-    si = wave_sum(si);
-    sc = wave_sum(sc);
-    if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6][0] = si; red[threadIdx.x >> 6][1] = sc; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      packed[total + 0] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-      packed[total + 1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
-    }
-  }
+  if (blockIdx.x == gridDim.x - 1) slots_collect(slots, packed + total);
 }
 
 hipError_t launch_reduce(const long long* slab, const long long* cnt_slab, int n_chunks, int K,

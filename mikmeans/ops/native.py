@@ -105,10 +105,9 @@ def get_variant(name: str) -> int:
 
 def set_variant(name: str, value: int) -> None:
     """Set a kernel A/B switch (``assign_varg``, ``assign_pmaj``, ``assign_geom``,
-    ``update_ks``, ``update_ks_gm``, ``blobs_tpr``, ``assign_persist``, ``assign_top2_geom``,
-    ``assign_cs``, ``assign_stagger``, ``assign_epi``, ``assign_early``, ``assign_pprio``; -1 =
-    built-in rule).  The launchers never
-    read the environment: ``MIKMEANS_<NAME>`` is read once when the extension loads."""
+    ``update_ks``, ``update_ks_gm``, ``blobs_tpr``, ``assign_top2_geom``, ``assign_epi``,
+    ``assign_early``; -1 = built-in rule).  The launchers never read the environment:
+    ``MIKMEANS_<NAME>`` is read once when the extension loads."""
     require().set_variant(_variant_index(name), int(value))
 
 
@@ -126,6 +125,25 @@ class variant:
     def __exit__(self, *exc):
         set_variant(self.name, self.old)
         return False
+
+
+NSLOT, SLOT_STRIDE = 256, 8   # csrc/kernels.h
+SLOT_OVF = 1 << 61            # csrc/common.h
+
+
+def slot_totals(slots: torch.Tensor) -> tuple[float, int]:
+    """(inertia, changed rows) held by the assign kernel's order-free slots (csrc/common.h
+    ``slot_add``): integer digit words summed over the slots, decoded high word first --
+    the same value ``reduce_kernel`` writes into the packed message."""
+    w = slots.detach().reshape(-1).view(torch.int64).reshape(-1, SLOT_STRIDE).sum(0).tolist()
+    if w[6] >= SLOT_OVF >> 1:
+        return float("inf"), int(w[7])
+    import math
+
+    v = 0.0
+    for j in range(6, -1, -1):
+        v += math.ldexp(float(w[j]), 32 * j - 64)
+    return v, int(w[7])
 
 
 def loaded_path() -> str | None:

@@ -144,6 +144,8 @@ class ElasticRoomReplica(RoomReplica):
         # left and rejoins must not take an old epoch that listed it)
         store.wait([_PREFIX + f"admit/{i}"], rep.timeout)
         e = int(store.get(_PREFIX + f"admit/{i}").decode())
+        if e < 0:
+            raise ValueError(f"member id {member!r} is already in the session")
         members = json.loads(store.get(_PREFIX + f"epoch/{e}").decode())
         rep._form(e, members)
         rep._receive_state()
@@ -208,9 +210,19 @@ class ElasticRoomReplica(RoomReplica):
                 # (only new holes: nobody to admit yet; remember them through the next round)
                 return {"epoch": None, "members": None, "joins_seen": n, "join_holes": holes}
             return None
-        members = [m for m in self.members if m not in leaves] + [m for m in joins if m not in self.members]
+        # A member id that leaves and joins again before this round is both released (its old
+        # process closes) and admitted (its new one takes the id's place).  An id already in the
+        # session and not leaving, or asked for twice, is refused through its own slot (-1).
+        members = [m for m in self.members if m not in leaves]
+        admit, refuse = [], []
+        for m, i in zip(joins, slots):
+            if m in members:
+                refuse.append(i)
+            else:
+                members.append(m)
+                admit.append(i)
         return {"epoch": self.epoch + 1, "members": members, "joins_seen": n, "join_holes": holes,
-                "leaves": leaves, "admit": slots}
+                "leaves": leaves, "admit": admit, "refuse": refuse}
 
     # ---------------------------------------------------------- replication
     def sync(self) -> list[dict]:
@@ -239,13 +251,15 @@ class ElasticRoomReplica(RoomReplica):
                 self.store.set(_PREFIX + f"epoch/{change['epoch']}", json.dumps(change["members"]))
                 for i in change.get("admit", []):
                     self.store.set(_PREFIX + f"admit/{i}", str(change["epoch"]))
+                for i in change.get("refuse", []):
+                    self.store.set(_PREFIX + f"admit/{i}", "-1")
                 for m in change.get("leaves", []):   # applied: a member id may rejoin later
                     try:
                         self.store.delete_key(_PREFIX + f"leave/{m}")
                     except Exception:  # noqa: BLE001 -- a store without deletes keeps the notice
                         pass
             self.comm.close()
-            if self.member not in change["members"]:
+            if self.member in change.get("leaves", []) or self.member not in change["members"]:
                 self.left = True          # the reference's peerclose, seen from this side
                 return applied
             self._form(change["epoch"], change["members"])

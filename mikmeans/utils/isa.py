@@ -160,7 +160,7 @@ def kernel_resources(elf: Path) -> list[KernelResources]:
 
 def assign16_template_args(demangled: str) -> list[str] | None:
     """The template arguments of an assign16_kernel instantiation (T, DPAD, P, CT, NBUF, OCC,
-    NW, FULLD, VARG, PMAJ, PERSIST, AST, TOP2, XV), or None."""
+    NW, FULLD, VARG, PMAJ, TOP2, XV), or None."""
     if "assign16_kernel<" not in demangled:
         return None
     inner = demangled[demangled.index("assign16_kernel<") + len("assign16_kernel<"):]

@@ -3,7 +3,7 @@
 rounds, on the bench's blob data a few Lloyd iterations in.
 
 usage: assign_ab.py [--n N] [--d D] [--k K] [--dtype bf16|f32] [--rounds R] [--reps M]
-                    --arms "assign_persist=0;assign_persist=1;assign_geom=4,assign_persist=1"
+                    --arms "assign_geom=0;assign_geom=1;assign_geom=2"
 Prints one JSON line per shape: median / min ms per arm, TF/s, whether every arm's labels
 equal the first arm's (bitwise), and -- from the GFX clock sampled during each arm's timed
 launches (mikmeans/utils/telemetry.py, amdsmi) -- the mean clock and the cycles per MFMA per
@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--arms", default="assign_persist=0;assign_persist=1")
+    ap.add_argument("--arms", default="assign_early=0;assign_early=1")
     ap.add_argument("--gather", type=int, default=0,
                     help="> 0: time the gathered assign of this many random rows (the mini-batch "
                          "resident path: X[rows] read in place, norms from the fragments)")

@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--n", type=int, default=20_000_000)
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--k", type=int, default=1024)
-    ap.add_argument("--arm", default="", help="kernel switches, e.g. assign_stagger=12")
+    ap.add_argument("--arm", default="", help="kernel switches, e.g. assign_early=0")
     a = ap.parse_args()
     dev = torch.device("cuda")
     comm = Comm.local(dev)

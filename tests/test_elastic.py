@@ -136,14 +136,17 @@ def _rejoiner(port, member, rounds):
     store.set(f"done/{member}", "1")
 
 
-def _host(port, rounds):
+def _host(port, deadline_s):
     from mikmeans.parallel.elastic import _PREFIX, ElasticRoomReplica
 
     store = _store(port)
     rep = ElasticRoomReplica.found(store, "A", "ROOM2", user="A", seed=3)
     # a join slot counted but never written (a newcomer that died between its add and its set)
     store.add(_PREFIX + "join/n", 1)
-    while not store.check(["done/R"]) and rep.round < rounds:
+    # rounds until the rejoiner is done, under a wall-clock deadline (a round cap raced the
+    # rejoiner's two visits on a loaded box)
+    t_end = time.monotonic() + deadline_s
+    while not store.check(["done/R"]) and time.monotonic() < t_end:
         rep.sync()
         time.sleep(0.05)
     store.set("done/A", json.dumps({"round": rep.round, "cards": [c["title"] for c in rep.room.cards],
@@ -159,7 +162,7 @@ def test_member_rejoins_and_dead_join_slot_does_not_block():
     port = free_port()
     store = _store(port, master=True)
     ctx = mp.get_context("spawn")
-    host = ctx.Process(target=_host, args=(port, 400))
+    host = ctx.Process(target=_host, args=(port, 180.0))
     host.start()
     time.sleep(0.5)
     r = ctx.Process(target=_rejoiner, args=(port, "R", 4))
@@ -173,3 +176,22 @@ def test_member_rejoins_and_dead_join_slot_does_not_block():
     done = json.loads(store.get("done/A").decode())
     assert "R-visit0" in done["cards"] and "R-visit1" in done["cards"]
     assert done["holes"] == [0]
+
+
+def test_leave_and_rejoin_in_one_round_and_duplicate_ids():
+    """ A member id whose leave notice and new join request are pending in the
+    same round is released (its old process closes) AND admitted (the new process takes the
+    id); a join under an id still in the session is refused through its own slot."""
+    from mikmeans.parallel.elastic import _PREFIX, ElasticRoomReplica
+
+    port = free_port()
+    store = _store(port, master=True)
+    rep = ElasticRoomReplica.found(store, "A", "ROOM3", user="A", seed=3)
+    rep.members = ["A", "R", "S"]          # (as if R and S had been admitted earlier)
+    store.set(_PREFIX + "leave/R", "1")
+    for m in ("R", "S", "Q"):             # R rejoins, S is a duplicate, Q is new
+        i = store.add(_PREFIX + "join/n", 1) - 1
+        store.set(_PREFIX + f"join/{i}", m)
+    ch = rep._pending_change()
+    assert ch["members"] == ["A", "S", "R", "Q"]
+    assert ch["leaves"] == ["R"] and ch["admit"] == [0, 2] and ch["refuse"] == [1]

@@ -10,6 +10,7 @@ from mikmeans import KMeans, ops
 from mikmeans.data import blobs as B
 from mikmeans.models.lloyd import LloydEngine
 from mikmeans.ops import cpu as ref
+from mikmeans.ops.native import slot_totals
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -82,17 +83,14 @@ def _spread_rows(n, d, seed, dtype):
     return X.to(dtype).to(DEV)
 
 
-@pytest.mark.parametrize("d,k,cs", [(64, 96, 0), (128, 256, 0), (256, 64, 0), (512, 40, 0), (64, 2048, 0),
-                                    (32, 1024, 0), (128, 1024, 1), (256, 512, 1), (100, 77, 1)])
-def test_gathered_assign_with_seed_offsets_is_the_full_pass(native, kvariant, d, k, cs):
+@pytest.mark.parametrize("d,k", [(64, 96), (128, 256), (256, 64), (512, 40), (64, 2048), (32, 1024), (128, 1024),
+                                 (256, 512), (100, 77)])
+def test_gathered_assign_with_seed_offsets_is_the_full_pass(native, d, k):
     """csrc/rows.hip seed_offsets + AssignArgs::oseed: a scattering gathered TOP2 assign over a
     random subset of rows writes bitwise the full pass's distances and labels at those rows --
     also where the full pass ranks by value (VARG: D=64 K>=2048, D=32 K>=1024), which the TOP2
-    kernel then mirrors with its exact epilogue -- and where it is the centre-stationary kernel
-    (``cs``: csrc/assign_cs.hip, 64-row offset blocks).  Without the offsets the distances differ."""
+    kernel then mirrors with its exact epilogue.  Without the offsets the distances differ."""
     from mikmeans.ops import pad_columns
-
-    kvariant("assign_cs", cs)
 
     n = 120_000
     Xb = pad_columns(_spread_rows(n, d, d + k, torch.bfloat16))
@@ -123,25 +121,22 @@ def test_gathered_assign_with_seed_offsets_is_the_full_pass(native, kvariant, d,
     assert not torch.equal(out[False][1][rows], mind_f[rows])
 
 
-@pytest.mark.parametrize("dtype,d,k,init,spread,cs", [
-    (torch.bfloat16, 64, 96, "random", False, 0),
-    (torch.bfloat16, 128, 256, "random", True, 0),
-    (torch.bfloat16, 256, 64, "random", False, 0),
-    (torch.bfloat16, 128, 200, "k-means||", False, 0),
-    (torch.bfloat16, 64, 2048, "random", False, 0),
-    (torch.float32, 64, 100, "random", False, 0),
-    (torch.float32, 128, 64, "k-means||", True, 0),
-    (torch.bfloat16, 128, 256, "random", True, 1),
-    (torch.bfloat16, 256, 64, "random", False, 1),
+@pytest.mark.parametrize("dtype,d,k,init,spread", [
+    (torch.bfloat16, 64, 96, "random", False),
+    (torch.bfloat16, 128, 256, "random", True),
+    (torch.bfloat16, 256, 64, "random", False),
+    (torch.bfloat16, 128, 200, "k-means||", False),
+    (torch.bfloat16, 64, 2048, "random", False),
+    (torch.float32, 64, 100, "random", False),
+    (torch.float32, 128, 64, "k-means||", True),
 ])
-def test_bounded_trajectory_bitwise(native, kvariant, dtype, d, k, init, spread, cs):
+def test_bounded_trajectory_bitwise(native, dtype, d, k, init, spread):
     """30 Lloyd iterations with the bounded E-step and with the full one from the same start:
     labels, centres and changed counts equal bit for bit after every step, the inertia agrees
     (sums formula vs per-row distances), and the bounded engine re-assigns few rows late on."""
     from mikmeans.models.init import init_kmeans_parallel, init_random
     from mikmeans.parallel import Comm
 
-    kvariant("assign_cs", cs)   # (1: the full passes run the centre-stationary kernel)
     n = 400_000
     X = _spread_rows(n, d, k, dtype) if spread else B.make_blobs(n, d, k, seed=k, dtype=dtype, device=DEV)
     comm = Comm.local(torch.device(DEV))
@@ -221,7 +216,7 @@ def test_device_count_assign_matches_host_count(native):
                           count=torch.tensor([m], dtype=torch.int64, device=DEV))
             elif m:
                 pk.assign(X, xn, lab, None, slots, True, rows=rows[:m].contiguous(), ub=ub, lb=lb, scatter=True)
-            out.append((lab, ub, lb, slots.view(-1, native.SLOT_STRIDE)[:, 1].sum()))
+            out.append((lab, ub, lb, slot_totals(slots)[1]))
         a, b = out
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2]), m
         assert float(a[3]) == float(b[3])

@@ -69,8 +69,8 @@ def test_assign_kernels_register_budget(tmp_path):
     res = isa.kernel_resources(isa.device_elf(obj, tmp_path / "dev.o"))
     a16 = [(r, isa.assign16_template_args(r.name)) for r in res]
     a16 = [(r, t) for r, t in a16 if t]
-    assert len(a16) > 50
-    top2 = [(r, t) for r, t in a16 if t[12] == "true"]     # (TOP2; t[13]: its exact epilogue XV)
+    assert len(a16) > 30
+    top2 = [(r, t) for r, t in a16 if t[10] == "true"]     # (TOP2; t[11]: its exact epilogue XV)
     assert top2, "no TOP2 instantiations"
     # TOP2 geometries (top2_geom) spill nothing, except the 4-block D = 128 one (the default
     # since round 4: 14 VGPRs, outside the MFMA loop; profiles/r4_16_top2_register_study.md)
@@ -78,27 +78,5 @@ def test_assign_kernels_register_budget(tmp_path):
            if r.vgpr_spills > (16 if (t[1] in ("64", "128") and t[2] == "4") else 0)]
     assert not bad, bad
     head = [r for r, t in a16 if t[:7] == ["unsigned short", "128", "4", "4", "2", "4", "4"]
-            and t[8:] == ["false", "1", "false", "false", "false", "false"]]
+            and t[8:] == ["false", "1", "false", "false"]]
     assert head and max(r.vgpr_spills for r in head) <= 2, [(r.name[-60:], r.vgpr_spills) for r in head]
-
-
-def test_centre_stationary_kernel_isa(tmp_path):
-    """csrc/assign_cs.hip: built with the same seed flag, no packed seed writes into MFMA
-    srcC, no spills at 1024 threads (128 VGPRs: the centre fragments fill half), and no LDS
-    atomics -- the compiler drains every in-flight LDS-DMA before one (vmcnt(0)), which would
-    serialise the super-block ring."""
-    src = _build.CSRC / "assign_cs.hip"
-    flags = _build.source_flags(src.name)
-    assert "-fno-slp-vectorize" in flags
-    obj = _build._compile(src, flags, verbose=False)
-    dev = isa.device_elf(obj, tmp_path / "dev.o")
-    funcs = isa.functions(isa.disassemble(dev))
-    cs = {f: body for f, body in funcs.items() if "assign_cs_kernel" in f}
-    assert len(cs) == 2, list(funcs)[:5]
-    assert not isa.packed_seed_hazards(cs, name_filter="assign_cs_kernel")
-    for f, body in cs.items():
-        text = "\n".join(body)
-        assert "ds_min_u64" not in text and "ds_min_rtn" not in text, f
-        assert text.count("v_mfma_f32_16x16x32_bf16") >= 16, f
-    res = [r for r in isa.kernel_resources(dev) if "assign_cs_kernel" in r.name]
-    assert len(res) == 2 and all(r.vgpr_spills == 0 for r in res), [(r.name, r.vgpr_spills) for r in res]
