@@ -259,7 +259,7 @@ class KMeans(_Serving):
                  verbose: int = 0, mode: str = "learn", run_id: str | None = None,
                  checkpoint_every: int = 0, checkpoint_dir: str | None = None, metrics_path: str | None = None,
                  graph: bool = False, incremental: bool = True, chunk_rows: int | None = None,
-                 init_size: int | None = None, metric: str = "euclidean", algorithm: str = "lloyd",
+                 init_size: int | None = None, metric: str = "euclidean", algorithm: str = "auto",
                  init_sampling: str = "exact"):
         self.n_clusters = int(n_clusters)
         self.init = init
@@ -290,12 +290,16 @@ class KMeans(_Serving):
         # cosine = spherical k-means: unit rows, centres re-normalised after every M-step
         self.metric = metric
         # 'hamerly' (sklearn's 'elkan' maps here too): the GPU E-step keeps per-row distance
-        # bounds and re-assigns only the rows they cannot vouch for (models/lloyd.py); the
-        # same Lloyd iterates up to bf16 near-ties, far fewer MFMA passes once few rows move
-        algo = {"elkan": "hamerly", "auto": "lloyd", "full": "lloyd"}.get(algorithm, algorithm)
-        if algo not in ("lloyd", "hamerly"):
-            raise ValueError(f"algorithm must be 'lloyd' or 'hamerly' ('elkan'), got {algorithm!r}")
+        # bounds and re-assigns only the rows they cannot vouch for (models/lloyd.py) -- the
+        # full E-step's labels bit for bit (tests/test_gpu_bounded.py), far fewer MFMA passes
+        # once few rows move.  'auto' (default): 'hamerly' wherever the memory plan holds the
+        # bounds resident (~21 B/row) and the options are the bounded path's, else 'lloyd';
+        # the choice is agreed by every rank and reported as ``algorithm_``.
+        algo = {"elkan": "hamerly", "full": "lloyd"}.get(algorithm, algorithm)
+        if algo not in ("auto", "lloyd", "hamerly"):
+            raise ValueError(f"algorithm must be 'auto', 'lloyd' or 'hamerly' ('elkan'), got {algorithm!r}")
         self.algorithm = algo
+        self.algorithm_ = None
         # multi-rank k-means++: 'exact' (world-size invariant, two collectives per centre) or
         # 'two-stage' (one all-gather per centre; models/init.py)
         if init_sampling not in ("exact", "two-stage"):
@@ -329,6 +333,17 @@ class KMeans(_Serving):
                             metric=self.metric, algorithm=self.algorithm, init_sampling=self.init_sampling)
 
     # ------------------------------------------------------------------- fit
+    AUTO_MIN_ROWS = 1 << 16      # per rank: below it the full E-step's pass costs less than the bounds
+    AUTO_MIN_CLUSTERS = 32
+
+    def _auto_bounded_ok(self, n_local: int, weighted: bool) -> bool:
+        """This rank's vote for the bounded E-step under algorithm='auto': the option set the
+        bounded path covers bit for bit (plain Euclidean, unweighted, 'keep' empty clusters, an
+        in-HBM shard) and a problem big enough for the bounds to pay."""
+        return (self.metric == "euclidean" and not weighted and self.empty_cluster == "keep"
+                and self.chunk_rows is None and n_local >= self.AUTO_MIN_ROWS
+                and self.n_clusters >= self.AUTO_MIN_CLUSTERS)
+
     def _memory_plan(self, X, comm, device, D, weighted):
         """Resident or streamed (parallel/memplan.py), agreed by every rank: a rank whose
         shard does not fit makes all of them stream (the init sample and its collectives
@@ -336,6 +351,7 @@ class KMeans(_Serving):
         from .parallel import memplan
 
         n_local = int(X.shape[0])
+        self.algorithm_ = "hamerly" if self.algorithm == "hamerly" else "lloyd"
         es_src = X.element_size() if torch.is_tensor(X) else np.asarray(X).itemsize
         x_dev = torch.is_tensor(X) and X.is_cuda
         kw = dict(weighted=weighted, init=self.init, n_local_trials=self.n_local_trials,
@@ -354,17 +370,31 @@ class KMeans(_Serving):
                     + (plan.summary() if not plan.fits else "another rank's HBM budget")
                     + "; use a smaller chunk_rows or more ranks")
         else:
+            fit_kw = dict(budget=budget, x_on_device=x_dev, incremental=self.incremental, init_rows=self.init_size,
+                          src_itemsize=es_src, copy_x=not self._x_ready(X, device), **kw)
+            auto_b = self.algorithm == "auto" and self._auto_bounded_ok(n_local, weighted)
+            plan = None
+            if auto_b:
+                try:   # the bounds must fit beside a resident shard, else the plain plan decides
+                    plan = memplan.plan_fit(n_local, D, self.n_clusters, self.dtype, bounded=True, **fit_kw)
+                    auto_b = plan.mode == "resident"
+                except memplan.HBMCapacityError:
+                    auto_b = False
+                if not auto_b:
+                    plan = None
             try:
-                plan = memplan.plan_fit(n_local, D, self.n_clusters, self.dtype, budget=budget, x_on_device=x_dev,
-                                        incremental=self.incremental, init_rows=self.init_size,
-                                        src_itemsize=es_src, copy_x=not self._x_ready(X, device),
-                                        bounded=self.algorithm == "hamerly", **kw)
+                if plan is None:
+                    plan = memplan.plan_fit(n_local, D, self.n_clusters, self.dtype,
+                                            bounded=self.algorithm == "hamerly", **fit_kw)
                 err = 0.0
             except memplan.HBMCapacityError as e:
                 plan, err = e, 1.0
-            flags = torch.tensor([err, 1.0 if (err == 0.0 and plan.mode == "streaming") else 0.0],
+            no_b = 0.0 if (auto_b or self.algorithm == "hamerly") else 1.0
+            flags = torch.tensor([err, 1.0 if (err == 0.0 and plan.mode == "streaming") else 0.0, no_b],
                                  dtype=torch.float64, device=comm.device)
             comm.allreduce_max_(flags)
+            if self.algorithm == "auto" and flags[2].item() == 0.0:
+                self.algorithm_ = "hamerly"     # every rank voted for the bounds (and holds them)
             if flags[0].item() > 0:
                 raise plan if isinstance(plan, memplan.HBMCapacityError) else memplan.HBMCapacityError(
                     "KMeans.fit: another rank's shard does not fit its HBM budget")
@@ -436,6 +466,7 @@ class KMeans(_Serving):
                                 else sample_weight, dtype=torch.float32)
         gpu = device.type == "cuda" and native_dpad(D, self.dtype) != 0
         self.memory_plan_ = None
+        self.algorithm_ = "hamerly" if self.algorithm == "hamerly" else "lloyd"
         streaming = False
         if gpu:
             plan = self._memory_plan(X, comm, device, D, w is not None)
@@ -477,7 +508,7 @@ class KMeans(_Serving):
             else:
                 eng = LloydEngine(Xt, self.n_clusters, comm=comm, sample_weight=w, frozen=self.frozen,
                                   empty_policy=self.empty_cluster, n_features=D, incremental=self.incremental,
-                                  spherical=spherical, bounded=self.algorithm == "hamerly")
+                                  spherical=spherical, bounded=self.algorithm_ == "hamerly")
                 if trial == 0:
                     stats = eng.stats if eng.gpu else None
                     tol_abs = tol_to_abs(self.tol, Xt, comm, n_global, D, stats=stats)

@@ -319,9 +319,17 @@ def cmd_plan(a) -> int:
                 pl = memplan.plan_minibatch(n_local, a.d, a.k, a.dtype, batch_rows=a.batch_size, resident=False)
                 pl.budget = budget
         else:
-            pl = memplan.plan_fit(n_local, a.d, a.k, a.dtype, budget=budget, x_on_device=False,
-                                  incremental=not a.full_mstep, init=a.init,
-                                  bounded=a.algorithm in ("hamerly", "elkan"))
+            fkw = dict(budget=budget, x_on_device=False, incremental=not a.full_mstep, init=a.init)
+            pl = None
+            if a.algorithm == "auto":   # (KMeans' default: the bounds when they fit beside a resident shard)
+                try:
+                    pl = memplan.plan_fit(n_local, a.d, a.k, a.dtype, bounded=True, **fkw)
+                    pl = pl if pl.mode == "resident" else None
+                except memplan.HBMCapacityError:
+                    pl = None
+            if pl is None:
+                pl = memplan.plan_fit(n_local, a.d, a.k, a.dtype, bounded=a.algorithm in ("hamerly", "elkan"),
+                                      **fkw)
     except memplan.HBMCapacityError as e:
         print(json.dumps({"error": str(e)}))
         return 1
@@ -442,8 +450,8 @@ def build_parser():
     pl.add_argument("--init", default="k-means++")
     pl.add_argument("--batch-size", type=int, default=0, help="> 0: plan a mini-batch fit")
     pl.add_argument("--full-mstep", action="store_true", help="no incremental M-step buffers")
-    pl.add_argument("--algorithm", default="lloyd", choices=["lloyd", "hamerly", "elkan"],
-                    help="hamerly: the bounded E-step's per-row bounds too")
+    pl.add_argument("--algorithm", default="auto", choices=["auto", "lloyd", "hamerly", "elkan"],
+                    help="hamerly: the bounded E-step's per-row bounds too; auto: them when they fit resident")
     pl.add_argument("--budget-gb", type=float, default=None)
     pl.add_argument("--compact", action="store_true")
     return ap

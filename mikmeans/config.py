@@ -60,7 +60,7 @@ class KMeansConfig:
     incremental: bool = True         # M-step re-scatters only rows whose label changed (exact)
     chunk_rows: int | None = None    # out-of-core: keep X on the host, stream it in chunks of rows
     metric: str = "euclidean"        # euclidean | cosine (spherical k-means on unit rows)
-    algorithm: str = "lloyd"         # lloyd | hamerly (bounded E-step: re-assign only unproven rows)
+    algorithm: str = "auto"          # auto | lloyd | hamerly (bounded E-step: re-assign only unproven rows)
     init_sampling: str = "exact"     # multi-rank k-means++: exact | two-stage (one all-gather per centre)
     timeout_s: float = 60.0          # collective timeout: a lost rank fails the job after this long
     resume: str | None = None        # checkpoint dir to continue from, or "auto" (= checkpoint_dir if present)

@@ -419,7 +419,8 @@ void col_absmax(const Tensor& X, const Tensor& out, const c10::optional<Tensor>&
   // per-block partial sums, summed in a fixed order by the launcher (bitwise reproducible)
   Tensor fpart;
   if (fstats.has_value())
-    fpart = at::zeros({(int64_t)mk::colstat_blocks() * 3 * X.size(1)}, X.options().dtype(at::kDouble));
+    fpart = at::zeros({(int64_t)mk::colstat_rows(dt, X.size(0), (int)X.size(1)) * 3 * X.size(1)},
+                      X.options().dtype(at::kDouble));
   hip_check(mk::launch_col_absmax(dt, X.data_ptr(), X.size(0), (int)X.size(1), ldx,
                                   reinterpret_cast<uint32_t*>(out.data_ptr<int32_t>()), stream(),
                                   opt_ptr<double>(fstats), opt_ptr<unsigned long long>(nnz),
@@ -871,6 +872,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("capture_teardown", &capture_teardown, "end a stream capture an error left open (status found)");
   m.def("js_format", &js_format, "ECMAScript Number::toString of a double");
   m.def("js_array", &js_array, "JSON array of a CPU float tensor with JS number formatting");
+  m.def("colstat_rows", &mk::colstat_rows, "f64 partial rows one column-statistics pass of N rows writes");
   m.attr("NSLOT") = mk::NSLOT;
   m.attr("SLOT_STRIDE") = mk::SLOT_STRIDE;
 }

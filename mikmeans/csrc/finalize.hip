@@ -299,15 +299,19 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
   }
 }
 
-// fstats[j] = sum over the COLSTAT_BLOCKS rows of fpart[.][j] (j < n = 3 D), in one fixed order:
-// each of 256 threads sums 8 consecutive rows, then a fixed LDS tree.  One workgroup per j.
+// fstats[j] = sum over the first `rows` rows of fpart[.][j] (j < n = 3 D; the launched blocks), in
+// one fixed order: each of 256 threads sums its 8 consecutive row slots (rows past `rows` count as
+// zero), then a fixed LDS tree.  One workgroup per j.
 __global__ __launch_bounds__(256) void colstat_reduce_kernel(const double* __restrict__ fpart, int64_t n,
-                                                            double* __restrict__ fstats) {
+                                                            int rows, double* __restrict__ fstats) {
   constexpr int PER = COLSTAT_BLOCKS / 256;
   const int64_t j = blockIdx.x;
   double v = 0.0;
 #pragma unroll
-  for (int r = 0; r < PER; ++r) v += fpart[((int64_t)threadIdx.x * PER + r) * n + j];
+  for (int r = 0; r < PER; ++r) {
+    const int row = (int)threadIdx.x * PER + r;
+    if (row < rows) v += fpart[(int64_t)row * n + j];
+  }
   __shared__ double t[256];
   t[threadIdx.x] = v;
   __syncthreads();
@@ -319,6 +323,23 @@ __global__ __launch_bounds__(256) void colstat_reduce_kernel(const double* __res
 }
 
 int colstat_blocks() { return COLSTAT_BLOCKS; }
+
+// Blocks of the widest launch launch_col_absmax makes for N rows of D columns: the rows of
+// fpart it writes (the caller's allocation; ADVICE r5: sized to N, not to COLSTAT_BLOCKS).
+int colstat_rows(int dtype, int64_t N, int D) {
+  const int V = dtype == DT_BF16 ? 8 : 4;
+  const int NPT = D / V;
+  int64_t rows = 0;
+  for (int p0 = 0; p0 < NPT; p0 += 64) {
+    const int NP = NPT - p0 < 64 ? NPT - p0 : 64;
+    int L = 1;
+    while (L < NP) L *= 2;
+    int64_t nb = (N + 256 / L - 1) / (256 / L);
+    if (nb > COLSTAT_BLOCKS) nb = COLSTAT_BLOCKS;
+    rows = nb > rows ? nb : rows;
+  }
+  return (int)rows;
+}
 
 hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
                              hipStream_t s, double* fstats, unsigned long long* nnz, int* lowbit, double* fpart,
@@ -357,7 +378,7 @@ hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t
   }
   if (fstats)
     hipLaunchKernelGGL(colstat_reduce_kernel, dim3((unsigned)(3 * D)), dim3(256), 0, s, fpart, (int64_t)3 * D,
-                       fstats);
+                       colstat_rows(dtype, N, D), fstats);
   return hipGetLastError();
 }
 

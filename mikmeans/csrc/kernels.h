@@ -213,9 +213,10 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 // (u64 [D], zeroed) and the lowest set bit's exponent over nonzero finite values (int [D],
 // initialised to INT_MAX by the caller).
 // The f64 sums are bitwise reproducible: each block writes its partials to its row of fpart
-// (f64 [colstat_blocks()][3][D], zeroed by the caller) and one fixed-order pass sums them.
+// (f64 [colstat_rows(dtype, N, D)][3][D], zeroed by the caller) and one fixed-order pass sums them.
 // xn (optional, D <= 64 pieces): every row's |x|^2 from the same pass, bitwise row_sqnorm's.
 int colstat_blocks();
+int colstat_rows(int dtype, int64_t N, int D);   // fpart rows one launch_col_absmax call writes
 hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t ldx, uint32_t* out,
                              hipStream_t s, double* fstats = nullptr, unsigned long long* nnz = nullptr,
                              int* lowbit = nullptr, double* fpart = nullptr, float* xn = nullptr);

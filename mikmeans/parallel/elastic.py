@@ -228,12 +228,30 @@ class ElasticRoomReplica(RoomReplica):
     def sync(self) -> list[dict]:
         """One round: exchange queued ops (+ presence and, from rank 0, any membership
         change), apply them in (rank, sequence) order, then move to the next epoch."""
+        parts = self.round_exchange(self.round_begin())
+        applied, change = self.round_apply(parts)
+        if change is not None:
+            self.round_transition(change)
+        return applied
+
+    # A round in four steps, so a server (serve.py) holds its board lock only for the local
+    # ones -- begin (take the queued ops) and apply -- and runs the collectives without it.
+    def round_begin(self) -> bytes:
+        """The round's message: this member's queued ops, its name and (rank 0) the change."""
         if self.left:
             raise RuntimeError(f"member {self.member} has left the session")
         change = self._pending_change() if self.comm.rank == 0 else None
         msg = json.dumps({"user": self.room.user, "ops": self._pending, "change": change}).encode()
         self._pending = []
-        parts = [json.loads(b.decode()) for b in self.comm.all_gather_bytes(msg)]
+        return msg
+
+    def round_exchange(self, msg: bytes) -> list[dict]:
+        """The round's collective: every member's message."""
+        return [json.loads(b.decode()) for b in self.comm.all_gather_bytes(msg)]
+
+    def round_apply(self, parts: list[dict]):
+        """Apply the gathered ops in (rank, sequence) order; returns (applied ops, the
+        membership change to move to, or None)."""
         self.roster = [p["user"] for p in parts]
         applied = []
         for p in parts:
@@ -242,30 +260,36 @@ class ElasticRoomReplica(RoomReplica):
                 applied.append(rec)
         self.round += 1
         change = parts[0]["change"]
-        if change is not None:
-            self._joins_seen = change["joins_seen"]
-            self._join_holes = list(change.get("join_holes", []))
-            if change["epoch"] is None:   # bookkeeping only (unwritten join slots), same members
-                return applied
-            if self.comm.rank == 0:       # publish before anyone forms the new group
-                self.store.set(_PREFIX + f"epoch/{change['epoch']}", json.dumps(change["members"]))
-                for i in change.get("admit", []):
-                    self.store.set(_PREFIX + f"admit/{i}", str(change["epoch"]))
-                for i in change.get("refuse", []):
-                    self.store.set(_PREFIX + f"admit/{i}", "-1")
-                for m in change.get("leaves", []):   # applied: a member id may rejoin later
-                    try:
-                        self.store.delete_key(_PREFIX + f"leave/{m}")
-                    except Exception:  # noqa: BLE001 -- a store without deletes keeps the notice
-                        pass
-            self.comm.close()
-            if self.member in change.get("leaves", []) or self.member not in change["members"]:
-                self.left = True          # the reference's peerclose, seen from this side
-                return applied
-            self._form(change["epoch"], change["members"])
-            st = self._full_state()       # newcomers take it; survivors already hold it
-            assert st["state"] == self.room.export_json() and st["round"] == self.round, "replica diverged"
-        return applied
+        if change is None:
+            return applied, None
+        self._joins_seen = change["joins_seen"]
+        self._join_holes = list(change.get("join_holes", []))
+        if change["epoch"] is None:   # bookkeeping only (unwritten join slots), same members
+            return applied, None
+        return applied, change
+
+    def round_transition(self, change: dict) -> bool:
+        """Move to the change's epoch: publish it (rank 0), close this group, then leave or
+        form the new group and take the full state.  True when this member stays."""
+        if self.comm.rank == 0:       # publish before anyone forms the new group
+            self.store.set(_PREFIX + f"epoch/{change['epoch']}", json.dumps(change["members"]))
+            for i in change.get("admit", []):
+                self.store.set(_PREFIX + f"admit/{i}", str(change["epoch"]))
+            for i in change.get("refuse", []):
+                self.store.set(_PREFIX + f"admit/{i}", "-1")
+            for m in change.get("leaves", []):   # applied: a member id may rejoin later
+                try:
+                    self.store.delete_key(_PREFIX + f"leave/{m}")
+                except Exception:  # noqa: BLE001 -- a store without deletes keeps the notice
+                    pass
+        self.comm.close()
+        if self.member in change.get("leaves", []) or self.member not in change["members"]:
+            self.left = True          # the reference's peerclose, seen from this side
+            return False
+        self._form(change["epoch"], change["members"])
+        st = self._full_state()       # newcomers take it; survivors already hold it
+        assert st["state"] == self.room.export_json() and st["round"] == self.round, "replica diverged"
+        return True
 
     def submit(self, op: str, *args, **kw) -> dict:
         rec = super().submit(op, *args, **kw)

@@ -269,6 +269,28 @@ class MemoryPlan:
         return s
 
 
+COLSTAT_BLOCKS = 2048     # csrc/finalize.hip
+
+
+def colstat_rows(es: int, n: int, Dp: int) -> int:
+    """Rows of the column-statistics partials one setup pass over ``n`` rows writes
+    (csrc/finalize.hip ``colstat_rows``): its widest launch's block count."""
+    V = 16 // es
+    npt, rows = Dp // V, 0
+    for p0 in range(0, npt, 64):
+        L = 1
+        while L < min(64, npt - p0):
+            L *= 2
+        rows = max(rows, min(COLSTAT_BLOCKS, -(-n // (256 // L))))
+    return rows
+
+
+def _setup_items(n: int, Dp: int, es: int) -> dict:
+    """The setup pass's transient (LloydEngine / StreamingLloydEngine ``col_stats``): the
+    per-block f64 partials of the column statistics, zeroed and reduced in a fixed order."""
+    return {"colstat_part": _r(colstat_rows(es, n, Dp) * 3 * Dp * 8)} if n else {}
+
+
 def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = False,
                   incremental: bool = True, init="k-means++", n_local_trials: int | None = None,
                   copy_x: bool = True, empty_policy: str = "keep", bounded: bool = False,
@@ -312,7 +334,8 @@ def plan_resident(n: int, D: int, K: int, dtype="bfloat16", *, weighted: bool = 
                  bound_qshift=_r(K * 4))
         if es == 2 and n:
             p["bound_oseed"] = _r(n * 4)   # every row's full-pass seed offset (bf16 keys)
-    tr = {"init": _init_items(init, n, Dp, D, K, n_local_trials or 0), "final_assign": final}
+    tr = {"init": _init_items(init, n, Dp, D, K, n_local_trials or 0), "final_assign": final,
+          "setup": _setup_items(n, Dp, es)}
     if copy_x and (src_itemsize or es) != es:
         tr["load"] = staging_items(n, D, src_itemsize or es, es, "x")
     return MemoryPlan("resident", n, D, Dp, K, "bfloat16" if es == 2 else "float32", p, tr)
@@ -351,7 +374,8 @@ def plan_streaming(n: int, D: int, K: int, dtype="bfloat16", *, chunk_rows: int,
     else:   # k-means++ seeds on a device-resident init_size-row sample
         m = min(n, init_rows or max(20 * K, 1 << 16))
         init_tr = {"sample": _r(m * Dp * es), **_init_items(init, m, Dp, D, K, n_local_trials or 0)}
-    tr = {"init": init_tr, "final_assign": {"labels_out": _r(n * 4), "mind_out": _r(n * 4)}}
+    tr = {"init": init_tr, "final_assign": {"labels_out": _r(n * 4), "mind_out": _r(n * 4)},
+          "setup": _setup_items(min(R, n), Dp, es)}      # (the statistics pass, one chunk at a time)
     pl = MemoryPlan("streaming", n, D, Dp, K, "bfloat16" if es == 2 else "float32", p, tr)
     pl.chunk_rows = R
     return pl

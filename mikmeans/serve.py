@@ -15,14 +15,17 @@ Endpoints (JSON in and out) -- the reference's controls (``index.html:76-131``,
 ``app.mjs:240-288, 571-573``):
 
 * ``GET /`` the board page, ``GET /app.js`` its script;
-* ``GET /api/state`` cards, centroids, meta, dashboard and the change ``version``;
-  ``GET /api/changes?since=V&wait=S`` answers as soon as the version passes ``V`` (or after
-  ``S`` <= 25 seconds) -- the live-update channel;
+* ``GET /api/state`` cards, centroids, meta, card positions, dashboard, presence and the
+  change ``version``; ``GET /api/changes?since=V&wait=S&user=NAME`` (async) answers as soon as
+  the version passes ``V`` (or after ``S`` <= 25 seconds) -- the live-update channel, whose
+  polling names are the presence list (the reference's Peers chip and avatars, app.mjs:51-65);
 * ``GET /api/room`` the export JSON, byte-exact ``JSON.stringify(state, null, 2)``
   (``app.mjs:263-267``); ``POST /api/room/import`` replaces cards / centroids, merges meta
   (``app.mjs:268-282``);
 * cards: ``POST /api/cards`` {title, traits[, user]}, ``DELETE /api/cards/{id}``,
-  ``POST /api/assign`` {card, centroid|null} (the drop / select paths, locks respected),
+  ``POST /api/assign`` {card, centroid|null} (the ``<select>`` path, app.mjs:398-402),
+  ``POST /api/drop`` {card, centroid|null, x, y} (drag-and-drop: the clamped ``pos:<id>`` with
+  the assignment, locks respected, app.mjs:356-372; null = onto Unassigned, app.mjs:421-433),
   ``POST /api/populate`` (test data), ``POST /api/shuffle_unassigned``, ``POST /api/restart``
   (unassign all), ``POST /api/reset`` {mode?} (hard reset);
 * centroids (at most 3, ``app.mjs:126-129``): ``POST /api/centroids`` {name},
@@ -37,7 +40,8 @@ Endpoints (JSON in and out) -- the reference's controls (``index.html:76-131``,
   {points[, distances]} -> labels (and squared distances), ``POST /api/predict.npy`` (a
   ``.npy`` body in, ``.npy`` labels out), ``POST /api/transform``.
 
-Request bodies over ``max_body_bytes`` get 413, as do batches over ``max_rows`` rows (and
+Request bodies over ``max_body_bytes`` get 413 -- declared or counted as they stream in (chunked) --
+as do batches over ``max_rows`` rows (and
 transforms over ``max_transform_values`` output values); malformed input gets 400.
 
 Session mode (``--found [ROOM]`` / ``--join``, ``--store-host/--store-port``): the served
@@ -50,7 +54,9 @@ different processes -- and scripted ``mikmeans session`` members -- stay byte-id
 """
 from __future__ import annotations
 
+import asyncio
 import threading
+import time
 
 import numpy as np
 import torch
@@ -76,17 +82,32 @@ LONG_POLL_S = 25.0
 PAGE = """<!doctype html>
 <html lang="en"><head><meta charset="utf-8"><title>k-means room</title>
 <style>
-body{font-family:system-ui,sans-serif;margin:1rem;background:#fafafa}
+body{font-family:system-ui,sans-serif;margin:1rem;background:#fafafa;color:#222}
 .row{display:flex;gap:.5rem;flex-wrap:wrap;align-items:center;margin:.35rem 0}
-.zones{display:flex;gap:1rem;flex-wrap:wrap}
-.zone{border:2px solid #ccc;border-radius:8px;padding:.5rem;min-width:14rem;background:#fff}
-.card{border:1px solid #ddd;border-radius:6px;padding:.25rem .5rem;margin:.25rem 0}
+.board{display:grid;grid-template-columns:1fr 18rem;gap:1rem}
+.zones{display:grid;grid-template-columns:repeat(auto-fit,minmax(15rem,1fr));gap:1rem}
+.zone{position:relative;border:2px solid #ccc;border-radius:8px;padding:.5rem;background:#fff;min-height:16rem}
+.zone.over{background:#eef4ff}
+.zone .head{display:flex;gap:.3rem;flex-wrap:wrap;align-items:center;margin-bottom:.3rem}
+.swatch{width:.9rem;height:.9rem;border-radius:3px;display:inline-block}
+.card{border:1px solid #ddd;border-radius:6px;padding:.25rem .5rem;margin:.25rem 0;background:#fff;cursor:grab}
+.card.float{position:absolute;width:11rem;margin:0;box-shadow:0 2px 6px rgba(0,0,0,.15)}
+.card.dragging{opacity:.5}
 .traits{color:#666;font-size:.85em}
-.chip{border:1px solid #ccc;border-radius:99px;padding:.1rem .6rem;font-size:.85em}
-#dash{white-space:pre-wrap;font-family:monospace;font-size:.85em}
+#unassigned{border:2px dashed #bbb;border-radius:8px;padding:.5rem;min-height:16rem;background:#fff}
+#unassigned.over{background:#eef4ff}
+.chip{border:1px solid #ccc;border-radius:99px;padding:.1rem .6rem;font-size:.85em;display:inline-block}
+.chip.ok{background:#e8f7ec;border-color:#8fcf9f}.chip.warn{background:#fdf5e0;border-color:#e0c070}
+.avatar{width:1.7rem;height:1.7rem;border-radius:50%;border:1px solid #bbb;display:inline-grid;place-items:center;font-size:.7em;font-weight:700;background:#eee}
+.kmrow{display:flex;gap:.5rem;align-items:center;margin:.3rem 0;white-space:nowrap}
+.bar{flex:1;min-width:6rem;height:.5rem;border:1px solid #ccc;border-radius:99px;overflow:hidden;background:#f3f3f3}
+.fill{height:100%}
+.delta{font-size:.8em;color:#2b6be0}.delta.bad{color:#c0392b}
+.top{font-size:.8em;color:#555;overflow:hidden;text-overflow:ellipsis}
 </style></head>
 <body>
-<h1>k-means room <span id="room" class="chip"></span> <span id="version" class="chip"></span></h1>
+<h1>k-means room <span id="room" class="chip"></span> <span id="status" class="chip"></span>
+<span id="presence"></span> <span id="version" class="chip"></span></h1>
 <div class="row"><button id="copy">Copy link</button> <button id="populate">Populate test data</button>
 <label>Your name <input id="name" placeholder="e.g., Alex"></label> <button id="saveName">Save</button></div>
 <div class="row"><input id="cname" placeholder="centroid name"> <button id="addCentroid">Add centroid (max 3)</button>
@@ -100,8 +121,9 @@ body{font-family:system-ui,sans-serif;margin:1rem;background:#fafafa}
 <input id="iter" type="number" min="0" step="1" value="0" style="width:6rem">
 <a href="/api/room" download>Export JSON</a> <input id="import" type="file" accept="application/json">
 <button id="reset">Reset</button> <button id="auto">Auto-assign (k-means)</button></div>
-<div class="zones" id="zones"></div>
-<h2>Dashboard</h2><div id="dash"></div>
+<h2>Dashboard</h2><div id="kmeans"></div>
+<div class="board"><div class="zones" id="canvas"></div>
+<div><h3>Unassigned</h3><div id="unassigned"></div></div></div>
 <script src="/app.js"></script>
 </body></html>
 """
@@ -109,6 +131,7 @@ body{font-family:system-ui,sans-serif;margin:1rem;background:#fafafa}
 APP_JS = """'use strict';
 let version = -1;
 let user = localStorage.getItem('mkUser') || '';
+let drag = {id: null, dx: 90, dy: 24};        // the card in flight and where it was grabbed
 async function api(path, method, body) {
   const r = await fetch(path, {method: method || 'GET', headers: {'Content-Type': 'application/json'},
                                body: body ? JSON.stringify(body) : undefined});
@@ -119,32 +142,120 @@ function $(id) { return document.getElementById(id); }
 function el(tag, cls, text) { const e = document.createElement(tag); if (cls) e.className = cls;
   if (text !== undefined) e.textContent = text; return e; }
 function btn(text, fn) { const b = el('button', '', text); b.addEventListener('click', fn); return b; }
-function cardEl(card, centroids) {
-  const d = el('div', 'card');
+function initials(n) { return (n || '??').trim().split(/\\s+/).slice(0, 2).map(s => (s[0] || '').toUpperCase()).join('') || '??'; }
+function cardEl(card, centroids, pos) {
+  const d = el('div', 'card' + (pos ? ' float' : ''));
+  d.draggable = true;
+  if (pos) { d.style.left = (pos.x * 100).toFixed(4) + '%'; d.style.top = (pos.y * 100).toFixed(4) + '%'; }
   d.appendChild(el('div', '', card.title));
-  d.appendChild(el('div', 'traits', (card.traits || []).join(', ')));
+  d.appendChild(el('div', 'traits', (card.traits || []).join(' \\u2022 ')));
   const s = el('select');
-  s.appendChild(new Option('unassigned', ''));
+  s.appendChild(new Option('Unassigned', ''));
   for (const c of centroids) s.appendChild(new Option(c.name, c.id));
   s.value = card.assignedTo || '';
   s.addEventListener('change', () => api('/api/assign', 'POST', {card: card.id, centroid: s.value || null}));
   d.appendChild(s);
-  d.appendChild(btn('Delete', () => api('/api/cards/' + encodeURIComponent(card.id), 'DELETE')));
+  d.appendChild(btn('Delete', () => { if (confirm('Delete "' + card.title + '"?'))
+    api('/api/cards/' + encodeURIComponent(card.id), 'DELETE'); }));
+  d.addEventListener('dragstart', ev => {
+    ev.dataTransfer.setData('text/plain', card.id);
+    const r = d.getBoundingClientRect();
+    drag = {id: card.id, dx: ev.clientX - r.left, dy: ev.clientY - r.top};
+    d.classList.add('dragging');
+  });
+  d.addEventListener('dragend', () => d.classList.remove('dragging'));
   return d;
 }
+function dropTarget(node, onDrop) {
+  node.addEventListener('dragover', ev => { ev.preventDefault(); node.classList.add('over'); });
+  node.addEventListener('dragleave', () => node.classList.remove('over'));
+  node.addEventListener('drop', ev => {
+    ev.preventDefault(); node.classList.remove('over');
+    const id = ev.dataTransfer.getData('text/plain') || drag.id;
+    if (id) onDrop(id, ev);
+  });
+}
 function zoneHead(g, row) {
-  const h = el('div');
-  h.appendChild(el('h3', '', g.name + (g.locked ? ' (locked)' : '')));
-  if (g.id === null) return h;
-  const id = encodeURIComponent(g.id);
-  const inp = el('input'); inp.placeholder = 'rename';
+  const h = el('div', 'head');
+  const sw = el('span', 'swatch'); sw.style.background = g.color; h.appendChild(sw);
+  const inp = el('input'); inp.value = g.name; inp.size = 12;
+  inp.addEventListener('change', () => api('/api/centroids/' + encodeURIComponent(g.id) + '/rename', 'POST',
+                                           {name: inp.value.trim() || g.name}));
   h.appendChild(inp);
-  h.appendChild(btn('Rename', () => api('/api/centroids/' + id + '/rename', 'POST', {name: inp.value})));
+  const id = encodeURIComponent(g.id);
   h.appendChild(btn(g.locked ? 'Unlock' : 'Lock', () => api('/api/centroids/' + id + '/lock', 'POST')));
-  h.appendChild(btn('Remove', () => api('/api/centroids/' + id, 'DELETE')));
-  if (row && row.suggestion) h.appendChild(btn('Apply: ' + row.suggestion,
-      () => api('/api/centroids/' + id + '/apply_suggestion', 'POST')));
+  h.appendChild(btn('Remove', () => { if (confirm('Remove centroid "' + g.name + '"?')) api('/api/centroids/' + id, 'DELETE'); }));
   return h;
+}
+function renderCanvas(st) {
+  const wrap = $('canvas');
+  wrap.replaceChildren();
+  if (!st.centroids.length) {
+    wrap.appendChild(el('div', 'traits', 'Add up to 3 centroids. Each appears here as a section where you can drop cards.'));
+    return;
+  }
+  const minH = Math.max(260, 64 + st.cards.length * 120);
+  for (const g of st.centroids) {
+    const z = el('div', 'zone');
+    z.style.borderColor = g.color || '#ccc';
+    z.style.minHeight = minH + 'px';
+    z.appendChild(zoneHead(g));
+    z.appendChild(el('div', 'traits', g.locked ? 'Locked: drops are refused' : 'Drop cards here'));
+    dropTarget(z, (id, ev) => {
+      if (g.locked) return;
+      const r = z.getBoundingClientRect();
+      api('/api/drop', 'POST', {card: id, centroid: g.id, x: (ev.clientX - r.left - drag.dx) / r.width,
+                                y: (ev.clientY - r.top - drag.dy) / r.height});
+    });
+    for (const card of st.cards.filter(c => c.assignedTo === g.id))
+      z.appendChild(cardEl(card, st.centroids, st.positions[card.id] || {x: 0.05, y: 0.18}));
+    wrap.appendChild(z);
+  }
+}
+function renderUnassigned(st) {
+  const u = $('unassigned');
+  u.replaceChildren();
+  const cards = st.cards.filter(c => !c.assignedTo);
+  if (!cards.length) u.appendChild(el('div', 'traits', 'No unassigned cards.'));
+  for (const card of cards) u.appendChild(cardEl(card, st.centroids, null));
+}
+function deltaSpan(text) {
+  const good = text.indexOf('\\u2191') >= 0 || text.indexOf('+') >= 0 || text.indexOf('\\u00b1') >= 0;
+  return el('span', 'delta' + (good ? '' : ' bad'), text);
+}
+function renderDashboard(d) {
+  const root = $('kmeans');
+  root.replaceChildren();
+  const m = el('div', 'row');
+  for (const c of d.chips) m.appendChild(el('span', 'chip', c));
+  for (const t of d.deltas) m.appendChild(deltaSpan(t));
+  root.appendChild(m);
+  for (const r of d.rows) {
+    const row = el('div', 'kmrow');
+    row.appendChild(el('span', 'chip', r.name));
+    const bar = el('div', 'bar'), fill = el('div', 'fill');
+    fill.style.width = r.bar_pct + '%'; fill.style.background = r.color || '#888';
+    bar.appendChild(fill); row.appendChild(bar);
+    const coh = el('span', 'chip', r.cohesion);
+    if (r.cohesion_delta) coh.appendChild(deltaSpan(r.cohesion_delta));
+    row.appendChild(coh);
+    row.appendChild(el('span', 'top', r.top));
+    const sg = el('span', 'top', r.suggested);
+    if (r.suggestion) sg.appendChild(btn('Use', () => api('/api/centroids/' + encodeURIComponent(r.id) + '/apply_suggestion', 'POST')));
+    row.appendChild(sg);
+    root.appendChild(row);
+  }
+}
+function renderPresence(st) {
+  const p = st.presence || {};
+  const s = $('status');
+  s.textContent = 'Peers: ' + (p.peers || 0) + ' | ' + (p.link || 'local');
+  s.className = 'chip ' + ((p.peers || 0) > 0 ? 'ok' : 'warn');
+  const box = $('presence');
+  box.replaceChildren();
+  const me = user || ('Guest ' + st.room);
+  const names = [me].concat((p.names || []).filter(n => n !== me)).slice(0, 6);
+  for (const n of names) { const a = el('span', 'avatar', initials(n)); a.title = n; box.appendChild(a); }
 }
 async function render() {
   const st = await api('/api/state');
@@ -153,30 +264,22 @@ async function render() {
   $('version').textContent = 'v' + st.version;
   if (document.activeElement !== $('mode')) $('mode').value = st.meta.mode || 'learn';
   if (document.activeElement !== $('iter')) $('iter').value = st.meta.iteration || 0;
-  const zones = $('zones');
-  zones.replaceChildren();
-  const rows = {};
-  for (const r of st.dashboard.rows) rows[r.id] = r;
-  const groups = [{id: null, name: 'Unassigned', color: '#999'}].concat(st.centroids);
-  for (const g of groups) {
-    const z = el('div', 'zone');
-    z.style.borderColor = g.color || '#ccc';
-    z.appendChild(zoneHead(g, rows[g.id]));
-    for (const card of st.cards.filter(c => (c.assignedTo || null) === g.id)) z.appendChild(cardEl(card, st.centroids));
-    zones.appendChild(z);
-  }
-  $('dash').textContent = JSON.stringify(st.dashboard, null, 2);
+  renderPresence(st);
+  renderCanvas(st);
+  renderUnassigned(st);
+  renderDashboard(st.dashboard);
 }
-async function follow() {          // live updates: re-render whenever the room changes
+async function follow() {          // live updates: re-render whenever the room or the presence changes
   for (;;) {
     try {
-      const c = await api('/api/changes?since=' + version + '&wait=20');
+      const c = await api('/api/changes?since=' + version + '&wait=20&user=' + encodeURIComponent(user || ''));
       if (c.version !== version) await render();
     } catch (e) { await new Promise(r => setTimeout(r, 2000)); }
   }
 }
+dropTarget($('unassigned'), id => api('/api/drop', 'POST', {card: id, centroid: null}));
 $('name').value = user;
-$('saveName').addEventListener('click', () => { user = $('name').value.trim(); localStorage.setItem('mkUser', user); });
+$('saveName').addEventListener('click', () => { user = $('name').value.trim(); localStorage.setItem('mkUser', user); render(); });
 $('copy').addEventListener('click', async () => {
   const r = await api('/api/link?base=' + encodeURIComponent(location.origin + location.pathname));
   if (navigator.clipboard) navigator.clipboard.writeText(r.link); $('tool').textContent = r.link; });
@@ -218,9 +321,15 @@ def _jsonable(obj):
     return obj
 
 
+PRESENCE_TTL_S = 60.0
+
+
 class _Board:
     """The served room plus its change counter: every mutation runs under the lock, bumps
-    the version and wakes the long-polls."""
+    the version and wakes the long-polls.  Long-polls wait on asyncio events set from
+    whichever thread bumped the version, so an open page holds no worker thread.  The names
+    the open pages poll with are the presence list (the reference's HELLO / ROSTER names,
+    app.mjs:59-67), expiring PRESENCE_TTL_S after a page's last poll."""
 
     queued = False    # (mutations apply at once)
 
@@ -228,6 +337,11 @@ class _Board:
         self.room = room
         self.version = 0
         self.cond = threading.Condition()
+        self._init_waiters()
+
+    def _init_waiters(self):
+        self._waiters: set = set()          # (loop, asyncio.Event) of the open long-polls
+        self._seen: dict[str, float] = {}   # presence: name -> monotonic time of its last poll
 
     def read(self, fn):
         with self.cond:
@@ -236,14 +350,57 @@ class _Board:
     def mutate(self, fn):
         with self.cond:
             out = fn(self.room)
-            self.version += 1
-            self.cond.notify_all()
+            self._bump()
             return out
+
+    def _bump(self):
+        """(under the lock) a new version: wake every long-poll."""
+        self.version += 1
+        self.cond.notify_all()
+        for loop, ev in list(self._waiters):
+            try:
+                loop.call_soon_threadsafe(ev.set)
+            except RuntimeError:   # (its loop has closed)
+                self._waiters.discard((loop, ev))
 
     def wait_past(self, since: int, timeout: float) -> int:
         with self.cond:
             self.cond.wait_for(lambda: self.version != since, timeout=max(0.0, timeout))
             return self.version
+
+    async def wait_past_async(self, since: int, timeout: float) -> int:
+        ev = asyncio.Event()
+        w = (asyncio.get_running_loop(), ev)
+        with self.cond:
+            if self.version != since:
+                return self.version
+            self._waiters.add(w)
+        try:
+            await asyncio.wait_for(ev.wait(), max(0.0, timeout))
+        except asyncio.TimeoutError:
+            pass
+        finally:
+            with self.cond:
+                self._waiters.discard(w)
+        with self.cond:
+            return self.version
+
+    def seen(self, name: str):
+        """A page polled as ``name``: a new name (or one back after expiring) is a change."""
+        name = name.strip()[:64]
+        if not name:
+            return
+        now = time.monotonic()
+        with self.cond:
+            fresh = name not in self._seen or now - self._seen[name] > PRESENCE_TTL_S
+            self._seen[name] = now
+            if fresh:
+                self._bump()
+
+    def presence_names(self) -> list[str]:
+        now = time.monotonic()
+        with self.cond:
+            return sorted(n for n, t in self._seen.items() if now - t <= PRESENCE_TTL_S)
 
 
 class _QueuedRoom:
@@ -284,6 +441,7 @@ class _ReplicaBoard(_Board):
         self.replica = replica
         self.version = 0
         self.cond = threading.Condition()
+        self._init_waiters()
         self.interval = float(interval)
         self.error = None
         self._stop = threading.Event()
@@ -303,17 +461,29 @@ class _ReplicaBoard(_Board):
             return fn(_QueuedRoom(self.replica))
 
     def _rounds(self):
+        """The session's rounds.  Only the round's local steps hold the board's lock -- taking
+        the queued ops, then applying the gathered ones; the collectives (the all-gather, and an
+        epoch change's group formation and full-state broadcast) run without it, so a slow or
+        dead peer stalls this thread, not the handlers."""
+        rep = self.replica
         roster = None
-        while not self._stop.is_set() and not self.replica.left:
+        while not self._stop.is_set() and not rep.left:
             try:
-                with self.cond:      # (a round applies ops to the room the handlers read)
-                    applied = self.replica.sync()
-                    if applied or self.replica.roster != roster:
-                        roster = list(self.replica.roster)
-                        self.version += 1
-                        self.cond.notify_all()
+                with self.cond:
+                    msg = rep.round_begin()
+                parts = rep.round_exchange(msg)
+                with self.cond:      # (the ops change the room the handlers read)
+                    applied, change = rep.round_apply(parts)
+                    if applied or rep.roster != roster or change is not None:
+                        roster = list(rep.roster)
+                        self._bump()
+                if change is not None and rep.round_transition(change):
+                    with self.cond:
+                        self._bump()
             except Exception as e:  # noqa: BLE001 -- a dead session: keep serving the last state
                 self.error = f"{type(e).__name__}: {e}"
+                with self.cond:
+                    self._bump()
                 return
             self._stop.wait(self.interval)
 
@@ -327,6 +497,57 @@ class _ReplicaBoard(_Board):
             deadline -= 1
         self._stop.set()
         self._thread.join(timeout=5)
+
+
+class _BodyCap:
+    """ASGI middleware: 413 for a request whose body passes ``limit`` bytes, by its declared
+    Content-Length or -- chunked transfers declare none -- by the bytes actually received
+    (the handler's body read raises the 413 HTTPException once the count passes the cap)."""
+
+    def __init__(self, app, limit: int):
+        self.app, self.limit = app, int(limit)
+
+    async def __call__(self, scope, receive, send):
+        if scope["type"] != "http":
+            return await self.app(scope, receive, send)
+        limit = self.limit
+        for k, v in scope.get("headers", []):
+            if k == b"content-length":
+                try:
+                    declared = int(v)
+                except ValueError:
+                    declared = 0
+                if declared > limit:
+                    resp = JSONResponse({"detail": f"request body over {limit} bytes"}, status_code=413,
+                                        headers=SECURITY_HEADERS)
+                    return await resp(scope, receive, send)
+        got, over, replaced = 0, False, False
+
+        async def capped():
+            # past the cap the body ends here (the handler then fails on what it got) and the
+            # answer is replaced by the 413 below
+            nonlocal got, over
+            if over:
+                return {"type": "http.request", "body": b"", "more_body": False}
+            msg = await receive()
+            if msg["type"] == "http.request":
+                got += len(msg.get("body", b""))
+                if got > limit:
+                    over = True
+                    return {"type": "http.request", "body": b"", "more_body": False}
+            return msg
+
+        async def send_checked(msg):
+            nonlocal replaced
+            if over and not replaced and msg["type"] == "http.response.start":
+                replaced = True
+                resp = JSONResponse({"detail": f"request body over {limit} bytes"}, status_code=413,
+                                    headers=SECURITY_HEADERS)
+                return await resp(scope, capped, send)
+            if replaced:
+                return None       # (the handler's own answer to the truncated body)
+            return await send(msg)
+        return await self.app(scope, capped, send_checked)
 
 
 def create_app(room: Room | None = None, model=None, *, device=None, max_body_bytes: int = MAX_BODY_BYTES,
@@ -346,22 +567,16 @@ def create_app(room: Room | None = None, model=None, *, device=None, max_body_by
 
     @app.middleware("http")
     async def _headers(request, call_next):
-        n = request.headers.get("content-length")
-        try:
-            too_big = n is not None and int(n) > max_body_bytes
-        except ValueError:
-            too_big = False
-        if too_big:
-            resp = JSONResponse({"detail": f"request body over {max_body_bytes} bytes"}, status_code=413)
-        else:
-            resp = await call_next(request)
-            # session mode: a room edit is queued for the next round, not applied yet
-            if (board.queued and resp.status_code == 200 and request.method in ("POST", "DELETE")
-                    and request.url.path.startswith("/api/") and request.url.path not in _READ_POSTS):
-                resp.status_code = 202
+        resp = await call_next(request)
+        # session mode: a room edit is queued for the next round, not applied yet
+        if (board.queued and resp.status_code == 200 and request.method in ("POST", "DELETE")
+                and request.url.path.startswith("/api/") and request.url.path not in _READ_POSTS):
+            resp.status_code = 202
         for k, v in SECURITY_HEADERS.items():
             resp.headers[k] = v
         return resp
+
+    app.add_middleware(_BodyCap, limit=max_body_bytes)
 
     @app.get("/", response_class=HTMLResponse)
     def page():
@@ -381,20 +596,28 @@ def create_app(room: Room | None = None, model=None, *, device=None, max_body_by
     @app.get("/api/state")
     def room_state():
         def snap(r):
+            pos = {k[4:]: v for k, v in r.meta.to_dict().items() if k.startswith("pos:")}
             out = {"room": r.room, "version": board.version, "cards": r.cards, "centroids": r.centroids,
                    "meta": {"mode": r.meta.get("mode"), "iteration": r.meta.get("iteration")},
-                   "dashboard": r.dashboard()}
+                   "positions": pos, "dashboard": r.dashboard()}
+            names = board.presence_names()
             if board.queued:    # the session's presence (the reference's roster, app.mjs:66-67, :94-95)
                 rep = board.replica
                 out["session"] = {"round": rep.round, "epoch": rep.epoch, "peers": rep.peers,
                                   "roster": rep.roster, "error": board.error}
+                out["presence"] = {"peers": rep.peers, "names": sorted(set(names) | set(rep.roster)),
+                                   "link": f"round {rep.round}" if board.error is None else "session lost"}
+            else:   # (the browsers on this board: the pages polling it, by their names)
+                out["presence"] = {"peers": max(0, len(names) - 1), "names": names, "link": "local"}
             return _jsonable(out)
         return board.read(snap)
 
     @app.get("/api/changes")
-    def changes(since: int = -1, wait: float = 0.0):
-        """Long-poll: the current version as soon as it differs from ``since``."""
-        v = board.wait_past(int(since), min(float(wait), LONG_POLL_S))
+    async def changes(since: int = -1, wait: float = 0.0, user: str = ""):
+        """Long-poll: the current version as soon as it differs from ``since`` (an async wait:
+        open pages hold no worker thread).  ``user``: the polling page's name (presence)."""
+        board.seen(user)
+        v = await board.wait_past_async(int(since), min(float(wait), LONG_POLL_S))
         return {"version": v, "changed": v != since}
 
     @app.post("/api/room/import")
@@ -443,6 +666,31 @@ def create_app(room: Room | None = None, model=None, *, device=None, max_body_by
         ok = board.mutate(lambda r: r.update_card_assign(body.get("card"), body.get("centroid") or None))
         if not ok:
             raise HTTPException(409, "not assigned (unknown card or locked centroid)")
+        return {"ok": True}
+
+    @app.post("/api/drop")
+    def drop(body: dict = Body(...)):
+        """Drag-and-drop: a card dropped on a centroid zone at the normalised position (x, y)
+        (clamped, refused on a locked centroid, the assignment and ``pos:<id>`` in one
+        transaction, app.mjs:356-372), or on Unassigned (``centroid`` null: unassigned and its
+        ``pos:`` deleted, app.mjs:421-433)."""
+        import math
+
+        card, cid = body.get("card"), body.get("centroid") or None
+        if not isinstance(card, str):
+            raise HTTPException(400, "card: a card id")
+        if cid is None:
+            ok = board.mutate(lambda r: r.update_card_assign(card, None))
+        else:
+            try:
+                x, y = float(body.get("x", 0.05)), float(body.get("y", 0.18))
+            except (TypeError, ValueError):
+                raise HTTPException(400, "x, y: numbers") from None
+            if not (math.isfinite(x) and math.isfinite(y)):
+                raise HTTPException(400, "x, y: finite numbers")
+            ok = board.mutate(lambda r: r.drop_card(card, str(cid), x, y))
+        if not ok:
+            raise HTTPException(409, "not dropped (unknown card or centroid, or a locked centroid)")
         return {"ok": True}
 
     @app.post("/api/populate")

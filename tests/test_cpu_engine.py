@@ -210,6 +210,7 @@ def test_algorithm_option_cpu():
     a = mikmeans.KMeans(6, device="cpu", seed=1).fit(X)
     b = mikmeans.KMeans(6, device="cpu", seed=1, algorithm="elkan").fit(X)
     assert b.algorithm == "hamerly" and b.get_config().algorithm == "hamerly"
+    assert a.algorithm == "auto" and a.algorithm_ == "lloyd"      # (the CPU path assigns every row)
     assert torch.equal(a.cluster_centers_, b.cluster_centers_) and a.inertia_ == b.inertia_
     assert mikmeans.KMeans.from_config(b.get_config()).algorithm == "hamerly"
     with pytest.raises(ValueError):
@@ -326,3 +327,30 @@ def test_kmeans_parallel_too_few_candidates_keeps_caller_options(monkeypatch):
     assert seen == {"trials": 4, "sampling": "two-stage"}
     assert C.shape == (3, 4)
     assert bool((C[:, None, :] == X[None]).all(-1).any(1).all())
+
+
+def test_auto_algorithm_votes():
+    """algorithm='auto' (the default) votes for the bounded E-step only for the option set it
+    reproduces bit for bit and problems big enough for the bounds to pay; the memory plan with
+    the bounds is what decides on a GPU (tests/test_gpu_bounded.py: the fits equal 'lloyd')."""
+    from mikmeans.parallel import memplan
+
+    km = mikmeans.KMeans(1024)
+    n = 1 << 20
+    assert km._auto_bounded_ok(n, weighted=False)
+    assert not km._auto_bounded_ok(n, weighted=True)
+    assert not km._auto_bounded_ok(1000, weighted=False)
+    assert not mikmeans.KMeans(8)._auto_bounded_ok(n, weighted=False)
+    assert not mikmeans.KMeans(1024, metric="cosine")._auto_bounded_ok(n, weighted=False)
+    assert not mikmeans.KMeans(1024, empty_cluster="farthest")._auto_bounded_ok(n, weighted=False)
+    assert not mikmeans.KMeans(1024, chunk_rows=1 << 16)._auto_bounded_ok(n, weighted=False)
+    # the headline shape: the bounds (~21 B/row) fit beside a resident 1e8 x 128 bf16 shard
+    b = memplan.plan_fit(100_000_000, 128, 1024, "bfloat16", budget=280 << 30, x_on_device=True, bounded=True)
+    p = memplan.plan_fit(100_000_000, 128, 1024, "bfloat16", budget=280 << 30, x_on_device=True)
+    assert b.mode == "resident" and b.fits
+    assert 15 * 100_000_000 <= b.peak - p.peak <= 30 * 100_000_000
+    # a budget the plain shard fits and the bounds do not: auto falls back to lloyd
+    tight = (p.peak + b.peak) // 2
+    with pytest.raises(memplan.HBMCapacityError):
+        memplan.plan_fit(100_000_000, 128, 1024, "bfloat16", budget=tight, x_on_device=True, bounded=True)
+    assert memplan.plan_fit(100_000_000, 128, 1024, "bfloat16", budget=tight, x_on_device=True).fits

@@ -411,3 +411,26 @@ def test_bounded_graph_farthest_matches_eager(native):
         assert torch.equal(ea.centers, eb.centers), it
         assert torch.equal(ea.labels, eb.labels), it
         assert ea.last_stats().inertia == eb.last_stats().inertia, it
+
+
+@pytest.mark.parametrize("dtype,d,k,init", [(torch.bfloat16, 128, 256, "random"), (torch.bfloat16, 64, 96, "k-means||"),
+                                            (torch.float32, 128, 64, "random"), (torch.float32, 64, 128, "k-means||")])
+def test_auto_algorithm_is_bounded_and_equals_lloyd(native, dtype, d, k, init):
+    """KMeans' default algorithm='auto' takes the bounded E-step where the bounds fit resident
+    and gives 'lloyd's centres, labels and n_iter_ bit for bit; history_ carries the inertia."""
+    X = B.make_blobs(300_000, d, k, seed=d + k, dtype=dtype, device=DEV)
+    kw = dict(init=init, max_iter=40, tol=1e-6, seed=5, dtype=dtype)
+    a = KMeans(k, **kw).fit(X)
+    f = KMeans(k, algorithm="lloyd", **kw).fit(X)
+    assert a.algorithm == "auto" and a.algorithm_ == "hamerly" and f.algorithm_ == "lloyd"
+    assert a.n_iter_ == f.n_iter_
+    assert torch.equal(a.cluster_centers_, f.cluster_centers_)
+    assert torch.equal(a.labels_, f.labels_)
+    assert a.inertia_ == f.inertia_
+    assert len(a.history_) == a.n_iter_ and all(h["inertia"] > 0 for h in a.history_)
+    for ha, hf in zip(a.history_, f.history_):
+        assert ha["n_changed"] == hf["n_changed"]
+        assert ha["inertia"] == pytest.approx(hf["inertia"], rel=1e-5)
+    # small problems stay on the full E-step
+    s = KMeans(k, **kw).fit(X[:20_000])
+    assert s.algorithm_ == "lloyd"

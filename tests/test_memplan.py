@@ -32,6 +32,9 @@ def test_plan_h_mirror_matches_native():
     for kp in (16, 256, 1024, 4352):
         assert M.assign_cn_len(kp) == C.assign_cn_len(kp)
     assert (M.NSLOT, M.SLOT_STRIDE) == (C.NSLOT, C.SLOT_STRIDE)
+    for dt, n, dp in itertools.product((0, 1), (1, 17, 1000, 40_000, 1 << 20, 100_000_000), (16, 64, 128, 256, 1024)):
+        es = 2 if dt == 1 else 4
+        assert M.colstat_rows(es, n, dp) == C.colstat_rows(dt, n, dp), (dt, n, dp)
     assert M.WDOT_SCRATCH == C.WDOT_SCRATCH
 
 
