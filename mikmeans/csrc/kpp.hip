@@ -594,85 +594,102 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 // NORMS: the squared row norms of the stored values are fused in (xn != nullptr).
+//
+// A grid-stride loop over 64-row wave tiles (a few workgroups per CU instead of one short
+// workgroup per 8 rows: the per-wave start-up and the dispatch of ~3M workgroups per 1e8 rows
+// dominated the D=128 pass).  Each lane draws the blob id of ONE row of its wave's tile (one
+// Philox per 64 rows instead of one per TPR-lane row group, and a coalesced label store); the
+// tile's rows are then filled TPR lanes per row in 64/TPR sub-steps, the id shuffled from its
+// owner lane.  Every value, label and fused norm is bitwise the one-row-per-lane-group form's.
 template <typename T, int TPR, bool NORMS>
 __global__ __launch_bounds__(256) void blobs_kernel(T* X, int64_t i0, int64_t n, int D, int64_t ldx,
                                                     const float* __restrict__ centers,
                                                     int n_centers, float stddev, uint32_t k0,
                                                     uint32_t k1, int32_t* y, float* xn, int vec) {
   constexpr int EL = sizeof(T) == 2 ? 8 : 4;  // values per Philox call (= 16-byte store)
+  constexpr int RPS = 64 / TPR;               // rows per sub-step of a wave
   const int G = (D + EL - 1) / EL;
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t il = e / TPR;
-  const int t = (int)(e % TPR);
-  const bool row_ok = il < n;
-  const uint64_t gi = (uint64_t)(i0 + (row_ok ? il : 0));
-  int cid = 0;
-  if (t == 0) {
-    const U4 rc = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), TAG_CID, 0u}, k0, k1);
-    cid = (int)__umulhi(rc.x, (uint32_t)n_centers);
-  }
-  cid = __shfl(cid, (int)(threadIdx.x & 63) & ~(TPR - 1), 64);
-  float sq = 0.f;
-  if (row_ok) {
-    if (y && t == 0) y[il] = cid;
-    const float* mu = centers + (int64_t)cid * D;
-    T* out = X + il * ldx;
-    if (vec) {
-      // Branch-free path (D % EL == 0, 16-byte aligned centres and rows): the group's
-      // means are dwordx4 loads issued before the Philox rounds, so their L2 latency
-      // hides under them (the general path waits on dependent dword loads).  Same bits.
-      for (int g = t; g < G; g += TPR) {
-        f32x4 m[EL / 4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int t = lane % TPR, rs = lane / TPR;
+  const int64_t tstride = (int64_t)gridDim.x * 256;
+  for (int64_t w0 = (int64_t)blockIdx.x * 256 + wid * 64; w0 < n; w0 += tstride) {
+    // this lane's row of the tile: its blob id (one Philox per lane)
+    int cid_l = 0;
+    {
+      const int64_t ir = w0 + lane;
+      const uint64_t gr = (uint64_t)(i0 + (ir < n ? ir : 0));
+      const U4 rc = philox(U4{(uint32_t)gr, (uint32_t)(gr >> 32), TAG_CID, 0u}, k0, k1);
+      cid_l = (int)__umulhi(rc.x, (uint32_t)n_centers);
+      if (y && ir < n) y[ir] = cid_l;
+    }
+#pragma unroll 1
+    for (int sub = 0; sub < TPR; ++sub) {
+      const int64_t il = w0 + sub * RPS + rs;
+      const bool row_ok = il < n;
+      const uint64_t gi = (uint64_t)(i0 + (row_ok ? il : 0));
+      const int cid = __shfl(cid_l, sub * RPS + rs, 64);
+      float sq = 0.f;
+      if (row_ok) {
+        const float* mu = centers + (int64_t)cid * D;
+        T* out = X + il * ldx;
+        if (vec) {
+          // Branch-free path (D % EL == 0, 16-byte aligned centres and rows): the group's
+          // means are dwordx4 loads issued before the Philox rounds, so their L2 latency
+          // hides under them (the general path waits on dependent dword loads).  Same bits.
+          for (int g = t; g < G; g += TPR) {
+            f32x4 m[EL / 4];
 #pragma unroll
-        for (int q = 0; q < EL / 4; ++q) m[q] = *(const f32x4*)(mu + EL * g + 4 * q);
-        const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
-        float z[EL], f[EL];
-        box_muller<T>(r, z);
+            for (int q = 0; q < EL / 4; ++q) m[q] = *(const f32x4*)(mu + EL * g + 4 * q);
+            const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
+            float z[EL], f[EL];
+            box_muller<T>(r, z);
 #pragma unroll
-        for (int j = 0; j < EL; ++j) f[j] = __builtin_fmaf(stddev, z[j], m[j / 4][j % 4]);
-        if constexpr (sizeof(T) == 2) {
-          // RNE to bf16 two values per v_cvt_pk_bf16_f32 (gfx950; values are finite by
-          // construction, so the bits equal the integer rounding of the NumPy mirror)
-          u32x4 w;
+            for (int j = 0; j < EL; ++j) f[j] = __builtin_fmaf(stddev, z[j], m[j / 4][j % 4]);
+            if constexpr (sizeof(T) == 2) {
+              // RNE to bf16 two values per v_cvt_pk_bf16_f32 (gfx950; values are finite by
+              // construction, so the bits equal the integer rounding of the NumPy mirror)
+              u32x4 w;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            w[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{f[2 * j], f[2 * j + 1]}, bf16x2));
-            if constexpr (NORMS) {   // both squares of the stored pair in one v_dot2c_f32_bf16
-              const bf16x2 h = __builtin_bit_cast(bf16x2, w[j]);
-              sq = __builtin_amdgcn_fdot2_f32_bf16(h, h, sq, false);
+              for (int j = 0; j < 4; ++j) {
+                w[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{f[2 * j], f[2 * j + 1]}, bf16x2));
+                if constexpr (NORMS) {   // both squares of the stored pair in one v_dot2c_f32_bf16
+                  const bf16x2 h = __builtin_bit_cast(bf16x2, w[j]);
+                  sq = __builtin_amdgcn_fdot2_f32_bf16(h, h, sq, false);
+                }
+              }
+              *(u32x4*)(out + EL * g) = w;
+            } else {
+              if constexpr (NORMS) {
+#pragma unroll
+                for (int j = 0; j < EL; ++j) sq = __builtin_fmaf(f[j], f[j], sq);
+              }
+              *(f32x4*)(out + EL * g) = f32x4{f[0], f[1], f[2], f[3]};
             }
           }
-          *(u32x4*)(out + EL * g) = w;
         } else {
-          if constexpr (NORMS) {
+          for (int g = t; g < G; g += TPR) {
+            const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
+            float z[EL];
+            box_muller<T>(r, z);
 #pragma unroll
-            for (int j = 0; j < EL; ++j) sq = __builtin_fmaf(f[j], f[j], sq);
+            for (int j = 0; j < EL; ++j) {
+              const int d = EL * g + j;
+              if (d < D) {
+                const T v = Elem<T>::from_f32(__builtin_fmaf(stddev, z[j], mu[d]));
+                const float f = Elem<T>::to_f32(v);
+                sq = __builtin_fmaf(f, f, sq);
+                out[d] = v;
+              }
+            }
           }
-          *(f32x4*)(out + EL * g) = f32x4{f[0], f[1], f[2], f[3]};
         }
       }
-    } else {
-      for (int g = t; g < G; g += TPR) {
-        const U4 r = philox(U4{(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)g, TAG_NRM}, k0, k1);
-        float z[EL];
-        box_muller<T>(r, z);
+      if constexpr (NORMS) {
 #pragma unroll
-        for (int j = 0; j < EL; ++j) {
-          const int d = EL * g + j;
-          if (d < D) {
-            const T v = Elem<T>::from_f32(__builtin_fmaf(stddev, z[j], mu[d]));
-            const float f = Elem<T>::to_f32(v);
-            sq = __builtin_fmaf(f, f, sq);
-            out[d] = v;
-          }
-        }
+        for (int o = 1; o < TPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
+        if (row_ok && t == 0) xn[il] = sq;
       }
     }
-  }
-  if constexpr (NORMS) {
-#pragma unroll
-    for (int o = 1; o < TPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
-    if (row_ok && t == 0) xn[il] = sq;
   }
 }
 
@@ -694,8 +711,10 @@ hipError_t launch_blobs(int dtype, void* X, int64_t i0, int64_t n, int D, int64_
   const int tv = variant(V_BLOBS_TPR);
   const int tpr_cap = tv < 0 ? 8 : (tv >= 1 && tv <= 16 ? tv : 16);
   while (tpr < G && tpr * 2 <= tpr_cap) tpr *= 2;
-  const int64_t tot = n * tpr;
-  const unsigned nb = (unsigned)((tot + 255) / 256);
+  // 256 rows per workgroup step; at most 16 workgroups per CU's worth of grid (then strided)
+  int64_t nb64 = (n + 255) / 256;
+  if (nb64 > 4096) nb64 = 4096;
+  const unsigned nb = (unsigned)nb64;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #define MK_BLOBS(TT, TP)                                                                           \
   do {                                                                                             \

@@ -1081,6 +1081,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(const long long* __restrict
     }
     packed[e] = acc;
   }
+  // (the slots' own workgroup, one past the message's: it runs beside the others)
   if (blockIdx.x == gridDim.x - 1) slots_collect(slots, packed + total);
 }
 
@@ -1089,7 +1090,7 @@ hipError_t launch_reduce(const long long* slab, const long long* cnt_slab, int n
                          hipStream_t s, long long* tot, const int* dcount, int dcap) {
   if (tot && !dcount) return hipErrorInvalidValue;
   const int64_t total = (int64_t)K * D + K;
-  const unsigned nb = (unsigned)((total + 255) / 256);
+  const unsigned nb = (unsigned)((total + 255) / 256) + 1;
   hipLaunchKernelGGL(reduce_kernel, dim3(nb), dim3(256), 0, s, slab, cnt_slab, n_chunks, K, D,
                      col_exp, ldexp(1.0, -cnt_exp), slots, packed, tot, dcount, dcap);
   return hipGetLastError();

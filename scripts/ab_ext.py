@@ -122,7 +122,25 @@ def cmd_run(a) -> int:
             t["cnt"] = torch.empty(t["nch"] * a.k, dtype=torch.int64, device=dev)
         m.update(eng.X, eng.labels, a.k, t["slab"], t["cnt"], t["nch"], None, eng.col_exp, eng.cnt_exp, False)
 
-    fn = run_update if a.what == "update" else run_assign
+    def run_blobs(t):    # the on-device generator (+ fused row norms) into each module's own buffer
+        if "bx" not in t:
+            t["bx"] = torch.empty_like(eng.X)
+            t["bn"] = torch.empty(a.n, dtype=torch.float32, device=dev)
+            t["bc"] = blob_centers(a.k, a.d, 10.0, 0, device=dev)
+        t["m"].blobs(t["bx"], 0, t["bc"], 1.0, 7, None, t["bn"])
+
+    def run_colstats(t):  # the setup pass: column statistics + fused row norms
+        m = t["m"]
+        t.setdefault("cs", (torch.zeros(eng.Dp, dtype=torch.int32, device=dev),
+                            torch.zeros(3 * eng.Dp, dtype=torch.float64, device=dev),
+                            torch.zeros(eng.Dp, dtype=torch.int64, device=dev),
+                            torch.zeros(eng.Dp, dtype=torch.int32, device=dev),
+                            torch.empty(a.n, dtype=torch.float32, device=dev)))
+        out, fst, nnz, lowbit, xn = t["cs"]
+        out.zero_(); nnz.zero_(); lowbit.fill_(1 << 30)
+        m.col_absmax(eng.X, out, fst, nnz, lowbit, xn)
+
+    fn = {"update": run_update, "blobs": run_blobs, "colstats": run_colstats}.get(a.what, run_assign)
     for t in per.values():          # warm-up (kernel attributes, code objects)
         fn(t)
     torch.cuda.synchronize()
@@ -130,6 +148,15 @@ def cmd_run(a) -> int:
         for t in per.values():
             t["ts"] += _timed(lambda t=t: fn(t), a.reps)
     base = per["head"]
+    if a.what == "blobs":           # the same rows and norms from every module
+        for tag, t in per.items():
+            t["same"] = bool(torch.equal(t["bx"], per["head"]["bx"]) and torch.equal(t["bn"], per["head"]["bn"]))
+    if a.what == "colstats":        # the same max / counts / norms; the f64 sums to ~1e-12
+        h = per["head"]["cs"]
+        for tag, t in per.items():
+            c = t["cs"]
+            t["same"] = bool(torch.equal(c[0], h[0]) and torch.equal(c[2], h[2]) and torch.equal(c[3], h[3])
+                             and torch.equal(c[4], h[4]) and torch.allclose(c[1], h[1], rtol=1e-12, atol=0))
     if a.what == "update":          # the same integer sums from every module
         red = {tag: (t["slab"].view(t["nch"], -1).sum(0), t["cnt"].view(t["nch"], -1).sum(0)) for tag, t in per.items()}
         for tag, t in per.items():
@@ -142,7 +169,7 @@ def cmd_run(a) -> int:
             "tflops": round(2.0 * a.n * a.k * a.d / (med * 1e-3) / 1e12, 1),
             "x_TBps": round(a.n * a.d * (2 if a.dtype == "bf16" else 4) / (med * 1e-3) / 1e12, 2),
             "label_mismatch_vs_head": int((t["lab"] != base["lab"]).sum()) if a.what == "assign" else None,
-            "sums_equal_head": t.get("same"),
+            "outputs_equal_head": t.get("same"),
             "vs_head": round(statistics.median(base["ts"]) / med, 4),
         }
     print(json.dumps(out), flush=True)
@@ -162,7 +189,7 @@ def main(argv=None) -> int:
     r.add_argument("--dtype", default="bf16")
     r.add_argument("--rounds", type=int, default=5)
     r.add_argument("--reps", type=int, default=5)
-    r.add_argument("--what", default="assign", choices=["assign", "update"])
+    r.add_argument("--what", default="assign", choices=["assign", "update", "blobs", "colstats"])
     a = ap.parse_args(argv)
     if a.cmd == "build":
         cmd_build(a.ref)

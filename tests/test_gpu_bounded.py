@@ -430,7 +430,9 @@ def test_auto_algorithm_is_bounded_and_equals_lloyd(native, dtype, d, k, init):
     assert len(a.history_) == a.n_iter_ and all(h["inertia"] > 0 for h in a.history_)
     for ha, hf in zip(a.history_, f.history_):
         assert ha["n_changed"] == hf["n_changed"]
-        assert ha["inertia"] == pytest.approx(hf["inertia"], rel=1e-5)
+        # (the bounded step's inertia comes from the sums, sxx + sum_k (n_k |c_k|^2 - 2 c_k.S_k), the
+        # full step's from the per-row f32 scores: two roundings of the same quantity)
+        assert ha["inertia"] == pytest.approx(hf["inertia"], rel=1e-4)
     # small problems stay on the full E-step
     s = KMeans(k, **kw).fit(X[:20_000])
     assert s.algorithm_ == "lloyd"
