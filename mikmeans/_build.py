@@ -129,7 +129,9 @@ def build(force: bool = False, verbose: bool = True, jobs: int | None = None, *,
             o.unlink()
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        sources = [s for s in HIP_SOURCES if (csrc / s).exists()]
+        # (another checkout -- scripts/ab_ext.py -- compiles every HIP TU it has, its own list)
+        sources = ([s for s in HIP_SOURCES if (csrc / s).exists()] if csrc == CSRC
+                   else sorted(p.name for p in csrc.glob("*.hip")))
         futs = [ex.submit(_compile, csrc / s, source_flags(s, csrc), verbose, build_dir) for s in sources]
         futs.append(ex.submit(_compile, csrc / BINDING, binding_flags, verbose, build_dir))
         objs = [f.result() for f in futs]

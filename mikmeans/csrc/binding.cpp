@@ -616,7 +616,7 @@ static const char* const kVariantEnv[V_COUNT] = {"MIKMEANS_ASSIGN_VARG", "MIKMEA
                                                  "MIKMEANS_ASSIGN_GEOM", "MIKMEANS_UPDATE_KS",
                                                  "MIKMEANS_UPDATE_KS_GM", "MIKMEANS_BLOBS_TPR",
                                                  "MIKMEANS_ASSIGN_TOP2_GEOM", "MIKMEANS_ASSIGN_EPI",
-                                                 "MIKMEANS_ASSIGN_EARLY"};
+                                                 "MIKMEANS_ASSIGN_EARLY", "MIKMEANS_COLSTAT_BLOCKS"};
 static int* variant_table() {
   static int t[V_COUNT] = {};
   static const bool init = [] {

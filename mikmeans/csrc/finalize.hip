@@ -161,7 +161,7 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
 // bf16) never needs it, and otherwise the max is compared with the mean of the NONZERO |x|
 // (sparse columns stay single-pass).  NORMS (the launch covers whole rows, <= 64 pieces): also
 // every row's |x|^2 in row_sqnorm_kernel's canonical order -- the fit's setup reads X once.
-constexpr int COLSTAT_BLOCKS = 2048;
+constexpr int COLSTAT_BLOCKS = 8192;   // the partials' row cap (colstat_cap sizes a launch)
 
 // Branch-free (it runs once per element of the pass; the branchy form cost ~20 VALU + SALU
 // exec-mask instructions per element and made the statistics pass VALU-bound): with y = |f|'s
@@ -324,6 +324,17 @@ __global__ __launch_bounds__(256) void colstat_reduce_kernel(const double* __res
 
 int colstat_blocks() { return COLSTAT_BLOCKS; }
 
+// The launch's block cap for D columns: as many blocks as keep the f64 partials within 32 MiB,
+// between 2048 and COLSTAT_BLOCKS (8192 at D <= 128) -- more, shorter-lived blocks run the
+// pass faster: 7.24 / 6.99 / 6.89 ms at 2048 / 4096 / 8192 blocks, N=1e8 D=128
+// (profiles/r6_05_setup_blocks_d128.log); or the A/B switch V_COLSTAT_BLOCKS (1..8192).
+static int colstat_cap(int D) {
+  const int v = variant(V_COLSTAT_BLOCKS);
+  if (v > 0 && v <= COLSTAT_BLOCKS) return v;
+  const int64_t fit = (int64_t)(32 << 20) / ((int64_t)24 * (D > 0 ? D : 1));
+  return (int)(fit < 2048 ? 2048 : fit > COLSTAT_BLOCKS ? COLSTAT_BLOCKS : fit);
+}
+
 // Blocks of the widest launch launch_col_absmax makes for N rows of D columns: the rows of
 // fpart it writes (the caller's allocation; ADVICE r5: sized to N, not to COLSTAT_BLOCKS).
 int colstat_rows(int dtype, int64_t N, int D) {
@@ -335,7 +346,7 @@ int colstat_rows(int dtype, int64_t N, int D) {
     int L = 1;
     while (L < NP) L *= 2;
     int64_t nb = (N + 256 / L - 1) / (256 / L);
-    if (nb > COLSTAT_BLOCKS) nb = COLSTAT_BLOCKS;
+    if (nb > colstat_cap(D)) nb = colstat_cap(D);
     rows = nb > rows ? nb : rows;
   }
   return (int)rows;
@@ -359,7 +370,10 @@ hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t
     while (L < NP) L *= 2;
     const int R = 256 / L;
     int64_t nb = (N + R - 1) / R;
-    if (nb > COLSTAT_BLOCKS) nb = COLSTAT_BLOCKS;  // 8 per CU; each streams its rows with 4 loads in flight per lane
+    // each block streams its rows with 4 loads in flight per lane (colstat_cap: one resident
+    // round of longer-lived blocks, 768, measured 7.6 % slower than 2048,
+    // profiles/r6_04_ab_colstats_d128.log)
+    if (nb > colstat_cap(D)) nb = colstat_cap(D);
     const dim3 g((unsigned)nb), b(256);
     double* fp = fpart ? fpart + c0 : nullptr;
     unsigned long long* nz = nnz ? nnz + c0 : nullptr;

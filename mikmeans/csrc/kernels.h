@@ -35,7 +35,7 @@ constexpr int SLOT_STRIDE = 8;
 // (Round 6 removed the measured losers: the persistent grid, the centre-stationary kernel, the
 // first-wave stagger and the prologue priority; their results stay in profiles/.)
 enum Variant { V_ASSIGN_VARG = 0, V_ASSIGN_PMAJ, V_ASSIGN_GEOM, V_UPDATE_KS, V_UPDATE_KS_GM, V_BLOBS_TPR,
-               V_ASSIGN_TOP2_GEOM, V_ASSIGN_EPI, V_ASSIGN_EARLY, V_COUNT };
+               V_ASSIGN_TOP2_GEOM, V_ASSIGN_EPI, V_ASSIGN_EARLY, V_COLSTAT_BLOCKS, V_COUNT };
 int variant(Variant v);
 void set_variant(Variant v, int value);
 

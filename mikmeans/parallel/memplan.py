@@ -269,7 +269,12 @@ class MemoryPlan:
         return s
 
 
-COLSTAT_BLOCKS = 2048     # csrc/finalize.hip
+COLSTAT_BLOCKS = 8192     # csrc/finalize.hip
+
+
+def colstat_cap(Dp: int) -> int:
+    """csrc/finalize.hip ``colstat_cap``: blocks keeping the f64 partials within 32 MiB, 2048..8192."""
+    return max(2048, min(COLSTAT_BLOCKS, (32 << 20) // (24 * max(Dp, 1))))
 
 
 def colstat_rows(es: int, n: int, Dp: int) -> int:
@@ -281,7 +286,7 @@ def colstat_rows(es: int, n: int, Dp: int) -> int:
         L = 1
         while L < min(64, npt - p0):
             L *= 2
-        rows = max(rows, min(COLSTAT_BLOCKS, -(-n // (256 // L))))
+        rows = max(rows, min(colstat_cap(Dp), -(-n // (256 // L))))
     return rows
 
 

@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--blocks", default="", help="comma list of statistics-grid block caps to A/B")
+    ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     dev = torch.device("cuda")
     X = make_blobs(a.n, a.d, a.k, seed=0, dtype=torch.bfloat16, device=dev,
@@ -57,6 +59,16 @@ def main():
     torch.cuda.synchronize()
     res["engine_init_s"] = round(time.perf_counter() - t0, 4)
     res["fused_norms_equal_row_sqnorm"] = bool(torch.equal(eng.xn, ops.row_sqnorm(X)))
+    if a.blocks:   # A/B of the statistics grid's block cap (switch colstat_blocks), interleaved
+        from mikmeans.ops import native
+
+        arms = [int(b) for b in a.blocks.split(",")]
+        ts = {b: [] for b in arms}
+        for _ in range(a.rounds):
+            for b in arms:
+                with native.variant("colstat_blocks", b):
+                    ts[b].append(timed(lambda: ops.col_stats(X, xn=xn), a.reps)["median_ms"])
+        res["blocks_ab"] = {str(b): round(statistics.median(v), 3) for b, v in ts.items()}
     print(json.dumps(res), flush=True)
 
 

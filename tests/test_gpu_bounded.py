@@ -164,7 +164,7 @@ def test_bounded_trajectory_bitwise(native, dtype, d, k, init, spread):
 
 def test_kmeans_hamerly_fit(native):
     X = B.make_blobs(400_000, 64, 50, seed=2, dtype=torch.float32, device=DEV)
-    ka = KMeans(50, init="random", seed=4, max_iter=40, tol=1e-6, device=DEV).fit(X)
+    ka = KMeans(50, init="random", seed=4, max_iter=40, tol=1e-6, device=DEV, algorithm="lloyd").fit(X)
     kb = KMeans(50, init="random", seed=4, max_iter=40, tol=1e-6, device=DEV, algorithm="hamerly").fit(X)
     assert kb._engine.bounded and not ka._engine.bounded
     assert kb.inertia_ == pytest.approx(ka.inertia_, rel=1e-5)

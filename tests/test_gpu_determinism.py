@@ -16,15 +16,18 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_identical_fits_log_bitwise_equal_inertia(native, dtype):
+@pytest.mark.parametrize("dtype,algorithm", [(torch.bfloat16, "lloyd"), (torch.float32, "lloyd"),
+                                             (torch.bfloat16, "auto")])
+def test_identical_fits_log_bitwise_equal_inertia(native, dtype, algorithm):
     """Five identical 10-step fits: centres, labels and every history_ record (inertia,
-    changed count, shift) equal bit for bit."""
+    changed count, shift) equal bit for bit -- the full E-step's inertia from the order-free
+    slots, the bounded one's (algorithm='auto' here) from the M-step's integer sums."""
     X = B.make_blobs(600_000, 128, 96, seed=3, dtype=dtype, device=DEV)
     runs = []
     for _ in range(5):
-        km = KMeans(256, init="random", max_iter=10, tol=0.0, seed=11, dtype=dtype).fit(X)
+        km = KMeans(256, init="random", max_iter=10, tol=0.0, seed=11, dtype=dtype, algorithm=algorithm).fit(X)
         runs.append(km)
+    assert runs[0].algorithm_ == ("hamerly" if algorithm == "auto" else "lloyd")
     h0 = runs[0].history_
     assert len(h0) == 10 and all("inertia" in h for h in h0)
     for km in runs[1:]:
