@@ -24,7 +24,7 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 BUILD = PKG.parent / "build" / "native"
 ARCH = os.environ.get("MIKMEANS_ARCH", "gfx950")
-HIP_SOURCES = ["assign16.hip", "assign_ring.hip", "update.hip", "finalize.hip", "kpp.hip", "rows.hip", "transform.hip"]
+HIP_SOURCES = ["assign16.hip", "update.hip", "finalize.hip", "kpp.hip", "rows.hip", "transform.hip"]
 BINDING = "binding.cpp"
 
 DEVICE_FLAGS = [
@@ -43,7 +43,7 @@ DEVICE_FLAGS = [
 # Per-source extras.  The assign kernel: no SLP vectorizer, so the MFMA seed adds stay
 # scalar v_add_f32 (packed v_pk_add_f32 seeds intermittently corrupted a point block's
 # scores on gfx950; see seed_add in common.h).
-SOURCE_FLAGS = {"assign16.hip": ["-fno-slp-vectorize"], "assign_ring.hip": ["-fno-slp-vectorize"]}
+SOURCE_FLAGS = {"assign16.hip": ["-fno-slp-vectorize"]}
 
 
 def source_flags(name: str, csrc: Path = CSRC) -> list[str]:

@@ -896,10 +896,6 @@ void set_assign_timeline(unsigned long long* buf, int64_t capacity) {
   g_timeline = buf;
   g_timeline_cap = buf ? capacity : 0;
 }
-unsigned long long* assign_timeline_buffer(int64_t* capacity) {
-  *capacity = g_timeline_cap;
-  return g_timeline;
-}
 
 template <typename T, int DPAD, int P, int CT_, int NBUF_, int OCC, int NW_, bool VARG>
 static void launch16_k(const AssignArgs& b, const dim3& grid, size_t lds, hipStream_t s) {
@@ -1076,7 +1072,6 @@ int assign16_block_rows(int dtype, int dpad, int kpad) {
 }
 
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s) {
-  if (variant(V_ASSIGN_RING) > 0 && assign_ring_takes(dtype, dpad, a)) return launch_assign_ring(dpad, a, s);
   if (dtype == DT_BF16) {
     switch (dpad) {
       case 32: return launch16_d<uint16_t, 32>(a, s);

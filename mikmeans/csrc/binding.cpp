@@ -616,8 +616,7 @@ static const char* const kVariantEnv[V_COUNT] = {"MIKMEANS_ASSIGN_VARG", "MIKMEA
                                                  "MIKMEANS_ASSIGN_GEOM", "MIKMEANS_UPDATE_KS",
                                                  "MIKMEANS_UPDATE_KS_GM", "MIKMEANS_BLOBS_TPR",
                                                  "MIKMEANS_ASSIGN_TOP2_GEOM", "MIKMEANS_ASSIGN_EPI",
-                                                 "MIKMEANS_ASSIGN_EARLY", "MIKMEANS_COLSTAT_BLOCKS",
-                                                 "MIKMEANS_ASSIGN_RING"};
+                                                 "MIKMEANS_ASSIGN_EARLY", "MIKMEANS_COLSTAT_BLOCKS"};
 static int* variant_table() {
   static int t[V_COUNT] = {};
   static const bool init = [] {
@@ -873,7 +872,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("capture_teardown", &capture_teardown, "end a stream capture an error left open (status found)");
   m.def("js_format", &js_format, "ECMAScript Number::toString of a double");
   m.def("js_array", &js_array, "JSON array of a CPU float tensor with JS number formatting");
-  m.def("assign_ring_fault", &mk::assign_ring_fault, "nonzero: a ring-assign spin gave up (A/B kernel)");
   m.def("colstat_rows", &mk::colstat_rows, "f64 partial rows one column-statistics pass of N rows writes");
   m.attr("NSLOT") = mk::NSLOT;
   m.attr("SLOT_STRIDE") = mk::SLOT_STRIDE;

@@ -35,7 +35,7 @@ constexpr int SLOT_STRIDE = 8;
 // (Round 6 removed the measured losers: the persistent grid, the centre-stationary kernel, the
 // first-wave stagger and the prologue priority; their results stay in profiles/.)
 enum Variant { V_ASSIGN_VARG = 0, V_ASSIGN_PMAJ, V_ASSIGN_GEOM, V_UPDATE_KS, V_UPDATE_KS_GM, V_BLOBS_TPR,
-               V_ASSIGN_TOP2_GEOM, V_ASSIGN_EPI, V_ASSIGN_EARLY, V_COLSTAT_BLOCKS, V_ASSIGN_RING, V_COUNT };
+               V_ASSIGN_TOP2_GEOM, V_ASSIGN_EPI, V_ASSIGN_EARLY, V_COLSTAT_BLOCKS, V_COUNT };
 int variant(Variant v);
 void set_variant(Variant v, int value);
 
@@ -86,17 +86,10 @@ struct AssignArgs {
 // Profiling hook: every assign16 launch writes its workgroups' timelines to buf (nullptr: off;
 // the caller sizes it for the grid, 8 u64 per workgroup, capacity in workgroups)
 void set_assign_timeline(unsigned long long* buf, int64_t capacity);
-unsigned long long* assign_timeline_buffer(int64_t* capacity);   // (the armed buffer, or null)
 hipError_t launch_assign16(int dtype, int dpad, const AssignArgs& a, hipStream_t s);
 // Rows per workgroup of the full (ungathered, unbounded) assign for this shape: the block its
 // bf16 seed offset is taken over (mirrors launch16_d / launch16_w)
 int assign16_block_rows(int dtype, int dpad, int kpad);
-// The one-ring-per-CU bf16 assign (assign_ring.hip; A/B switch V_ASSIGN_RING = 1): whether it
-// takes a call (plain full passes with row norms), its launcher, and its fault word (a bounded
-// spin that gave up: nonzero)
-bool assign_ring_takes(int dtype, int dpad, const AssignArgs& a);
-hipError_t launch_assign_ring(int dpad, const AssignArgs& a, hipStream_t s);
-int assign_ring_fault();
 // oseed[i] = the full pass's seed offset of row i (block_rows from assign16_block_rows; bf16)
 hipError_t launch_seed_offsets(const float* xn, int64_t n, int block_rows, float* oseed, hipStream_t s);
 
