@@ -161,6 +161,54 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
 // bf16) never needs it, and otherwise the max is compared with the mean of the NONZERO |x|
 // (sparse columns stay single-pass).  NORMS (the launch covers whole rows, <= 64 pieces): also
 // every row's |x|^2 in row_sqnorm_kernel's canonical order -- the fit's setup reads X once.
+// Packed 16-bit helpers, written out (left to itself the compiler turns min(y, 1) per half into
+// a compare + select per half, six instructions for one).
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_pk_max_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_pk_add_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk_sub_sat_u16(uint32_t a, uint32_t b) {   // max(a - b, 0)
+  uint32_t d;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t b, uint32_t c) {   // a * b + c
+  uint32_t d;
+  asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk_shr_u16(uint32_t a, uint32_t s) {   // a >> s per half
+  uint32_t d;
+  asm("v_pk_lshrrev_b16 %0, %1, %2" : "=v"(d) : "v"(s), "v"(a));
+  return d;
+}
+
+// The lowest-bit keys of two bf16 values at once (y = both values' |bits|, 15 bits a half):
+// key = max(E, 1) + min(ctz(m), 7) per half, the high half offset by 16, and 0x4000 added to
+// a half that is zero, inf or NaN -- lowbit_exp(x) = key - 134 for the others (E the biased
+// exponent, m the 7 mantissa bits; a subnormal's E is 0 and its exponent that of E = 1).
+__device__ __forceinline__ uint32_t lowbit_keys_bf16x2(uint32_t y) {
+  const uint32_t e2 = pk_max_u16(pk_shr_u16(y, 0x00070007u), 0x00010001u);
+  const uint32_t g2 = (y & 0x007f007fu) | 0x00800080u;   // bit 7 stands in for the hidden bit
+  const uint32_t clo = __builtin_ctz(g2);                // min(ctz(m_lo), 7)
+  const uint32_t chi = __builtin_ctz(g2 & 0xffff0000u);  // 16 + min(ctz(m_hi), 7)
+  const uint32_t k2 = e2 + clo + (chi << 16);
+  // invalid halves: y - 1 >= 0x7f7f (y = 0 wraps to 0xffff)
+  const uint32_t inv = pk_min_u16(pk_sub_sat_u16(pk_add_u16(y, 0xffffffffu), 0x7f7e7f7eu), 0x00010001u);
+  return pk_mad_u16(inv, 0x40004000u, k2);
+}
 constexpr int COLSTAT_BLOCKS = 8192;   // the partials' row cap (colstat_cap sizes a launch)
 
 // Branch-free (it runs once per element of the pass; the branchy form cost ~20 VALU + SALU
@@ -176,13 +224,16 @@ __device__ __forceinline__ int lowbit_exp(float f) {
 
 // One launch covers up to 64 16-B pieces of a row (a column block: X, out, fpart, nnz and
 // lowbit point at its first column; fpart rows are fstride columns apart).
-template <typename T, bool STATS, bool NORMS>
+// LT: the lanes per row when fixed at compile time (16: a 128-column bf16 row, whose fused row
+// norms then run without the runtime lane-count branches), 0 = runtime L.
+template <typename T, bool STATS, bool NORMS, int LT = 0>
 __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X, int64_t N, int NP,
-                                                         int L, int64_t ldx, uint32_t* __restrict__ out,
+                                                         int L_, int64_t ldx, uint32_t* __restrict__ out,
                                                          double* __restrict__ fpart, int64_t fstride,
                                                          unsigned long long* __restrict__ nnz,
                                                          int* __restrict__ lowbit, float* __restrict__ xn) {
   constexpr int V = Elem<T>::V;
+  const int L = LT ? LT : L_;
   const int p = threadIdx.x & (L - 1);
   const int R = 256 / L;
   const int64_t step = (int64_t)gridDim.x * R;
@@ -226,6 +277,69 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
       if (p == 0) xn[row] = acc;
     }
   };
+  // bf16 statistics, VALU-lean (the per-element form above made the pass VALU-bound: 6.9 ms
+  // against 4.6 ms for the max alone at N=1e8 D=128, profiles/r6_10_hbm_ceiling.log).  Same
+  // results bit for bit: the max, the nonzero count and the lowest-bit exponent run on packed
+  // 16-bit halves, two values per instruction (|x|'s bf16 bits order like its f32 bits;
+  // lowbit_keys_bf16x2); the f64 sums and the row norms keep their per-row order.
+  [[maybe_unused]] uint32_t mp[4], nzp[4], kp[4];
+  [[maybe_unused]] int pend = 0;
+  [[maybe_unused]] auto flush_nz = [&]() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      nz[2 * j] += nzp[j] & 0xffffu;
+      nz[2 * j + 1] += nzp[j] >> 16;
+      nzp[j] = 0u;
+    }
+    pend = 0;
+  };
+  constexpr bool LEAN = STATS && sizeof(T) == 2;
+  if constexpr (LEAN) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { mp[j] = 0u; nzp[j] = 0u; kp[j] = 0xffffffffu; }
+  }
+  // cnt rows' pieces (rows row0, row0 + step, ...)
+  [[maybe_unused]] auto take_lean = [&](const u32x4* w, auto cnt_c, int64_t row0) {
+    constexpr int cnt = decltype(cnt_c)::value;
+#pragma unroll
+    for (int u = 0; u < cnt; ++u) {
+      float f[V];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t x = w[u][j];
+        const uint32_t y = x & 0x7fff7fffu;
+        mp[j] = pk_max_u16(mp[j], y);
+        nzp[j] = pk_add_u16(nzp[j], pk_min_u16(y, 0x00010001u));
+        kp[j] = pk_min_u16(kp[j], lowbit_keys_bf16x2(y));
+        f[2 * j] = __uint_as_float(x << 16);
+        f[2 * j + 1] = __uint_as_float(x & 0xffff0000u);
+      }
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const double d = (double)f[e];
+        q[e] += fabs(d);
+        sx[e] += d;
+        sxx[e] = __builtin_fma(d, d, sxx[e]);
+      }
+      if constexpr (NORMS) {
+        float acc = 0.f;
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc = __builtin_fmaf(f[e], f[e], acc);
+        for (int g = 16; g < L; g += 16) {
+          const int src = (lane & ~(L - 1)) + ((p + g) & (L - 1));
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            const float o = __shfl(f[e], src, 64);
+            if (p + g < NP) acc = __builtin_fmaf(o, o, acc);
+          }
+        }
+        acc = sum16_xor(acc, L);
+        if (p == 0) xn[row0 + u * step] = acc;
+      }
+    }
+    pend += cnt;
+    if (pend > 65535 - 4) flush_nz();   // (16-bit counts)
+  };
   // (NORMS: a row group's lanes all run the loop -- lanes past the row's pieces take zeros --
   // so the shuffles above see every lane of the group)
   if (NORMS || p < NP) {
@@ -238,10 +352,29 @@ __global__ __launch_bounds__(256) void col_absmax_kernel(const T* __restrict__ X
       u32x4 w[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) w[u] = load(i + u * step);
+      if constexpr (LEAN) {
+        take_lean(w, std::integral_constant<int, 4>{}, i);
+      } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) take(w[u], i + u * step);
+        for (int u = 0; u < 4; ++u) take(w[u], i + u * step);
+      }
     }
-    for (; i < N; i += step) take(load(i), i);
+    for (; i < N; i += step) {
+      const u32x4 w1 = load(i);
+      if constexpr (LEAN) take_lean(&w1, std::integral_constant<int, 1>{}, i);
+      else take(w1, i);
+    }
+  }
+  if constexpr (LEAN) {
+    flush_nz();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      m[2 * j] = mp[j] << 16;
+      m[2 * j + 1] = mp[j] & 0xffff0000u;
+      const int klo = (int)(kp[j] & 0xffffu), khi = (int)(kp[j] >> 16);
+      lb[2 * j] = klo >= 0x4000 ? 1 << 30 : klo - 134;
+      lb[2 * j + 1] = khi >= 0x4000 ? 1 << 30 : khi - 16 - 134;
+    }
   }
   for (int o = L; o < 64; o <<= 1)
 #pragma unroll
@@ -378,15 +511,20 @@ hipError_t launch_col_absmax(int dtype, const void* X, int64_t N, int D, int64_t
     double* fp = fpart ? fpart + c0 : nullptr;
     unsigned long long* nz = nnz ? nnz + c0 : nullptr;
     int* lb = lowbit ? lowbit + c0 : nullptr;
-#define MK_COLSTAT(TT, ST, NR)                                                                              \
-  hipLaunchKernelGGL((col_absmax_kernel<TT, ST, NR>), g, b, 0, s, (const TT*)X + c0, N, NP, L, ldx, out + c0, \
+#define MK_COLSTAT(TT, ST, NR, LT)                                                                              \
+  hipLaunchKernelGGL((col_absmax_kernel<TT, ST, NR, LT>), g, b, 0, s, (const TT*)X + c0, N, NP, L, ldx, out + c0, \
                      fp, (int64_t)D, nz, lb, xn)
     if (dtype == DT_BF16) {
-      if (fstats) { if (xn) MK_COLSTAT(uint16_t, true, true); else MK_COLSTAT(uint16_t, true, false); }
-      else { if (xn) MK_COLSTAT(uint16_t, false, true); else MK_COLSTAT(uint16_t, false, false); }
+      if (fstats) {
+        if (xn && L == 16) MK_COLSTAT(uint16_t, true, true, 16);
+        else if (xn) MK_COLSTAT(uint16_t, true, true, 0);
+        else MK_COLSTAT(uint16_t, true, false, 0);
+      } else {
+        if (xn) MK_COLSTAT(uint16_t, false, true, 0); else MK_COLSTAT(uint16_t, false, false, 0);
+      }
     } else {
-      if (fstats) { if (xn) MK_COLSTAT(float, true, true); else MK_COLSTAT(float, true, false); }
-      else { if (xn) MK_COLSTAT(float, false, true); else MK_COLSTAT(float, false, false); }
+      if (fstats) { if (xn) MK_COLSTAT(float, true, true, 0); else MK_COLSTAT(float, true, false, 0); }
+      else { if (xn) MK_COLSTAT(float, false, true, 0); else MK_COLSTAT(float, false, false, 0); }
     }
 #undef MK_COLSTAT
   }

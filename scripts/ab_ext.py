@@ -157,6 +157,7 @@ def cmd_run(a) -> int:
             c = t["cs"]
             t["same"] = bool(torch.equal(c[0], h[0]) and torch.equal(c[2], h[2]) and torch.equal(c[3], h[3])
                              and torch.equal(c[4], h[4]) and torch.allclose(c[1], h[1], rtol=1e-12, atol=0))
+            t["fsums_bitwise"] = bool(torch.equal(c[1], h[1]))
     if a.what == "update":          # the same integer sums from every module
         red = {tag: (t["slab"].view(t["nch"], -1).sum(0), t["cnt"].view(t["nch"], -1).sum(0)) for tag, t in per.items()}
         for tag, t in per.items():
@@ -170,6 +171,7 @@ def cmd_run(a) -> int:
             "x_TBps": round(a.n * a.d * (2 if a.dtype == "bf16" else 4) / (med * 1e-3) / 1e12, 2),
             "label_mismatch_vs_head": int((t["lab"] != base["lab"]).sum()) if a.what == "assign" else None,
             "outputs_equal_head": t.get("same"),
+            **({"fsums_bitwise": t["fsums_bitwise"]} if "fsums_bitwise" in t else {}),
             "vs_head": round(statistics.median(base["ts"]) / med, 4),
         }
     print(json.dumps(out), flush=True)

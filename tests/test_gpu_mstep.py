@@ -229,6 +229,49 @@ def test_col_stats_native_matches_torch(native, dtype):
     assert int(st.lowbit[6]) == 0
 
 
+@pytest.mark.parametrize("d", [8, 48, 128, 512])
+def test_col_stats_bf16_edge_values(native, d):
+    """The bf16 statistics pass (packed max / nonzero count, lowest-bit exponent recomputed only
+    for row groups that could lower it) against the torch reference on values that stress the
+    screen: magnitudes falling row by row down through the bf16 subnormals to zero (the exact
+    path runs on most groups), +-inf, NaN, -0, an all-zero column, one huge value, a sparse
+    column; row counts with ragged tails.  Max / counts / lowest bits exact, f64 sums to
+    rounding, fused row norms bitwise row_sqnorm's."""
+    from mikmeans.ops import pad_columns
+
+    n = 70_001 + d
+    g = torch.Generator().manual_seed(d)
+    X = torch.randn(n, d, generator=g) * torch.logspace(-3, 3, d)
+    i = torch.arange(n, dtype=torch.float64)
+    X[:, 0] = (2.0 ** (-(i % 20_000) / 100.0)).float()        # falls to 2^-200: subnormals, then 0
+    X[:, 1 % d] = -X[:, 0]
+    if d > 2:
+        X[:, 2] = 0.0
+        X[7, 2] = -0.0
+    if d > 4:
+        X[:, 3] = torch.where(torch.rand(n, generator=g) < 0.003, torch.randn(n, generator=g), torch.zeros(n))
+        X[11, 4] = float("inf")
+        X[12, 4] = float("-inf")
+        X[13, 4] = float("nan")
+    if d > 5:
+        X[n - 1, 5] = 3.0e38
+    Xb = X.to(torch.bfloat16)
+    Xg = pad_columns(Xb.to(DEV))
+    xn = torch.full((n,), -1.0, device=DEV)
+    st = ops.col_stats(Xg, xn=xn) if ops.fused_norms_ok(Xg) else ops.col_stats(Xg)
+    ref = ops.col_stats(Xb)
+    torch.testing.assert_close(st.absmax.cpu()[:d], ref.absmax, rtol=0, atol=0, equal_nan=True)
+    assert torch.equal(st.nnz.cpu()[:d], ref.nnz)
+    assert torch.equal(st.lowbit.cpu()[:d], ref.lowbit)
+    for k in ("sumabs", "sum", "sumsq"):
+        a, b = getattr(st, k).cpu()[:d], getattr(ref, k)
+        fin = torch.isfinite(b)
+        assert torch.equal(torch.isnan(a), torch.isnan(b)) and torch.equal(a[torch.isinf(b)], b[torch.isinf(b)]), k
+        torch.testing.assert_close(a[fin], b[fin], rtol=1e-12, atol=0, msg=k)
+    if ops.fused_norms_ok(Xg):   # (row 13 holds the NaN)
+        torch.testing.assert_close(xn, ops.row_sqnorm(Xg), rtol=0, atol=0, equal_nan=True)
+
+
 def test_sparse_and_grid_exact_columns_stay_single_pass(native):
     """One-hot columns, sparse continuous columns and small-integer columns with a huge
     value are exact on the hi grid or have a nonzero mean near their max: no residual
