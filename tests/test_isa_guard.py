@@ -80,3 +80,17 @@ def test_assign_kernels_register_budget(tmp_path):
     head = [r for r, t in a16 if t[:7] == ["unsigned short", "128", "4", "4", "2", "4", "4"]
             and t[8:] == ["false", "1", "false", "false"]]
     assert head and max(r.vgpr_spills for r in head) <= 2, [(r.name[-60:], r.vgpr_spills) for r in head]
+
+
+def test_colstats_bf16_register_budget(tmp_path):
+    """The packed bf16 column-statistics kernels (csrc/finalize.hip) stay at 4 waves/SIMD
+    without spills: the per-element f64 form held 148 VGPRs (3 waves/SIMD) and a first packed
+    form with a rare-path branch reached 177 and spilled under a 3-wave cap -- 27 % slower
+    than the kernel it replaced (profiles/r6_11_ab_colstats_d128.log)."""
+    src = _build.CSRC / "finalize.hip"
+    obj = _build._compile(src, _build.source_flags(src.name), verbose=False)
+    res = [r for r in isa.kernel_resources(isa.device_elf(obj, tmp_path / "dev.o"))
+           if "col_absmax_kernel<unsigned short, true" in r.name]
+    assert len(res) >= 3, [r.name for r in res]
+    bad = [(r.name, r.vgprs, r.vgpr_spills) for r in res if r.vgprs > 128 or r.vgpr_spills]
+    assert not bad, bad
