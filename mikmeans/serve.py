@@ -501,8 +501,9 @@ class _ReplicaBoard(_Board):
 
 class _BodyCap:
     """ASGI middleware: 413 for a request whose body passes ``limit`` bytes, by its declared
-    Content-Length or -- chunked transfers declare none -- by the bytes actually received
-    (the handler's body read raises the 413 HTTPException once the count passes the cap)."""
+    Content-Length or -- chunked transfers declare none -- by the bytes actually received:
+    past the cap the body the handler reads ends there, and whatever the handler answers to
+    that truncated body is replaced by the 413."""
 
     def __init__(self, app, limit: int):
         self.app, self.limit = app, int(limit)
