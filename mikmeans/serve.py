@@ -322,6 +322,7 @@ def _jsonable(obj):
 
 
 PRESENCE_TTL_S = 60.0
+PRESENCE_MAX = 1024      # names tracked at once (a client cannot grow the list without bound)
 
 
 class _Board:
@@ -393,6 +394,10 @@ class _Board:
         now = time.monotonic()
         with self.cond:
             fresh = name not in self._seen or now - self._seen[name] > PRESENCE_TTL_S
+            if fresh and len(self._seen) >= PRESENCE_MAX:   # (expired names go first; then refuse)
+                self._seen = {n: t for n, t in self._seen.items() if now - t <= PRESENCE_TTL_S}
+                if len(self._seen) >= PRESENCE_MAX:
+                    return
             self._seen[name] = now
             if fresh:
                 self._bump()

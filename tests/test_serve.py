@@ -395,3 +395,15 @@ def test_chunked_body_over_the_cap_is_413():
     assert declared.status_code == 413
     for k, v in SECURITY_HEADERS.items():
         assert big.headers[k] == v and declared.headers[k] == v
+
+
+def test_presence_list_is_bounded():
+    """(round 6) Names seen by the long-poll expire and the list is capped: a client cycling
+    through names cannot grow it without bound."""
+    from mikmeans import serve
+
+    b = serve._Board(serve.Room(seed=0))
+    for i in range(serve.PRESENCE_MAX + 50):
+        b.seen(f"user{i}")
+    assert len(b._seen) == serve.PRESENCE_MAX
+    assert len(b.presence_names()) == serve.PRESENCE_MAX
