@@ -140,7 +140,12 @@ def cmd_run(a) -> int:
         out.zero_(); nnz.zero_(); lowbit.fill_(1 << 30)
         m.col_absmax(eng.X, out, fst, nnz, lowbit, xn)
 
-    fn = {"update": run_update, "blobs": run_blobs, "colstats": run_colstats}.get(a.what, run_assign)
+    def run_rownorms(t):  # the plain row-norm pass
+        t.setdefault("rn", torch.empty(a.n, dtype=torch.float32, device=dev))
+        t["m"].row_sqnorm(eng.X, t["rn"])
+
+    fn = {"update": run_update, "blobs": run_blobs, "colstats": run_colstats,
+          "rownorms": run_rownorms}.get(a.what, run_assign)
     for t in per.values():          # warm-up (kernel attributes, code objects)
         fn(t)
     torch.cuda.synchronize()
@@ -158,6 +163,9 @@ def cmd_run(a) -> int:
             t["same"] = bool(torch.equal(c[0], h[0]) and torch.equal(c[2], h[2]) and torch.equal(c[3], h[3])
                              and torch.equal(c[4], h[4]) and torch.allclose(c[1], h[1], rtol=1e-12, atol=0))
             t["fsums_bitwise"] = bool(torch.equal(c[1], h[1]))
+    if a.what == "rownorms":        # the same bits from every module
+        for tag, t in per.items():
+            t["same"] = bool(torch.equal(t["rn"], per["head"]["rn"]))
     if a.what == "update":          # the same integer sums from every module
         red = {tag: (t["slab"].view(t["nch"], -1).sum(0), t["cnt"].view(t["nch"], -1).sum(0)) for tag, t in per.items()}
         for tag, t in per.items():
@@ -191,7 +199,7 @@ def main(argv=None) -> int:
     r.add_argument("--dtype", default="bf16")
     r.add_argument("--rounds", type=int, default=5)
     r.add_argument("--reps", type=int, default=5)
-    r.add_argument("--what", default="assign", choices=["assign", "update", "blobs", "colstats"])
+    r.add_argument("--what", default="assign", choices=["assign", "update", "blobs", "colstats", "rownorms"])
     a = ap.parse_args(argv)
     if a.cmd == "build":
         cmd_build(a.ref)
