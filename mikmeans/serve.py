@@ -556,6 +556,24 @@ class _BodyCap:
         return await self.app(scope, capped, send_checked)
 
 
+def _npy_view(buf: memoryview) -> np.ndarray:
+    """A ``.npy`` payload as an array viewing ``buf`` (no copy): the header parsed by numpy's
+    own reader, object dtypes refused (nothing is unpickled)."""
+    import io
+
+    f = io.BytesIO(bytes(buf[:65536]))   # (the header: at most a few KiB)
+    major, _ = np.lib.format.read_magic(f)
+    if major == 1:
+        shape, fortran, dtype = np.lib.format.read_array_header_1_0(f)
+    else:
+        shape, fortran, dtype = np.lib.format.read_array_header_2_0(f)
+    if dtype.hasobject:
+        raise ValueError("object arrays are not accepted")
+    count = int(np.prod(shape)) if shape else 1
+    arr = np.frombuffer(buf, dtype=dtype, count=count, offset=f.tell())
+    return arr.reshape(shape[::-1]).T if fortran else arr.reshape(shape)
+
+
 def create_app(room: Room | None = None, model=None, *, device=None, max_body_bytes: int = MAX_BODY_BYTES,
                max_rows: int = MAX_ROWS, max_transform_values: int = MAX_TRANSFORM_VALUES, replica=None,
                session_interval: float = 0.2):
@@ -864,14 +882,30 @@ def create_app(room: Room | None = None, model=None, *, device=None, max_body_by
         import io
 
         m = _model()
-        chunks, size = [], 0
-        async for part in request.stream():
-            size += len(part)
-            if size > max_body_bytes:
-                raise HTTPException(413, f"request body over {max_body_bytes} bytes")
-            chunks.append(part)
         try:
-            arr = np.load(io.BytesIO(b"".join(chunks)), allow_pickle=False)
+            declared = int(request.headers.get("content-length", "-1"))
+        except ValueError:
+            declared = -1
+        if 0 <= declared <= max_body_bytes:
+            # one buffer of the declared size, filled in place (joining ~2000 64-KiB chunks of
+            # a 134 MB batch cost ~90 ms, np.load's copy ~50 ms more)
+            body, size = bytearray(declared), 0
+            async for part in request.stream():
+                if size + len(part) > declared:
+                    raise HTTPException(400, "request body longer than its Content-Length")
+                body[size:size + len(part)] = part
+                size += len(part)
+            body = memoryview(body)[:size]
+        else:
+            chunks, size = [], 0
+            async for part in request.stream():
+                size += len(part)
+                if size > max_body_bytes:
+                    raise HTTPException(413, f"request body over {max_body_bytes} bytes")
+                chunks.append(part)
+            body = memoryview(bytearray(b"".join(chunks)))   # (writable: the rows become a tensor)
+        try:
+            arr = _npy_view(body)
         except Exception as e:  # noqa: BLE001 -- any malformed payload is the client's error
             raise HTTPException(400, f"body must be a .npy array: {e}") from None
         if arr.ndim != 2 or arr.shape[1] != m.cluster_centers_.shape[1]:

@@ -89,6 +89,20 @@ def test_model_serving_matches_predict():
     lab = np.load(io.BytesIO(rb.content), allow_pickle=False)
     assert lab.dtype == np.int32 and lab.tolist() == km.predict(X[:200]).tolist()
     assert c.post("/api/predict.npy", content=b"not npy").status_code == 400
+    # Fortran order, float64 and a version-2 header parse to the same rows (the body is viewed in
+    # place, not unpickled); an object array is refused
+    for arr, kw in ((np.asfortranarray(X[:200].numpy()), {}), (X[:200].numpy().astype(np.float64), {}),
+                    (X[:200].numpy(), {"version": (2, 0)})):
+        buf = io.BytesIO()
+        if kw:
+            np.lib.format.write_array(buf, arr, **kw)
+        else:
+            np.save(buf, arr)
+        rb = c.post("/api/predict.npy", content=buf.getvalue())
+        assert rb.status_code == 200 and np.load(io.BytesIO(rb.content)).tolist() == lab.tolist()
+    buf = io.BytesIO()
+    np.save(buf, np.array([[1, "a"]] * 3, dtype=object), allow_pickle=True)
+    assert c.post("/api/predict.npy", content=buf.getvalue()).status_code == 400
     assert _client(Room(seed=0)).post("/api/predict", json={"points": [[0.0] * 5]}).status_code == 404
 
 
