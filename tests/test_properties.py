@@ -145,3 +145,71 @@ def test_cpu_assign_picks_a_nearest_centre(n, d, k, seed):
     slack = 1e-5 * (X.double().pow(2).sum(1) + C.double().pow(2).sum(1).max() + 1.0)
     assert bool((chosen <= best + slack).all())
     assert bool(((mind.double() - chosen).abs() <= slack + 1e-4 * chosen).all())
+
+
+# -------------------------------------------------------------- the room model
+_ops = st.lists(st.one_of(
+    st.tuples(st.just("add_centroid"), st.sampled_from(["Sweet", "Fresh", "  Bold  ", ""])),
+    st.tuples(st.just("add_card"), st.sampled_from(["Mango", "Lime", "Chili"]),
+              st.lists(st.sampled_from(["sweet", "sour", "hot", "crisp"]), max_size=3)),
+    st.tuples(st.just("assign"), st.integers(0, 9), st.integers(-1, 3)),
+    st.tuples(st.just("drop"), st.integers(0, 9), st.integers(0, 3),
+              st.floats(-2, 3, allow_nan=False), st.floats(-2, 3, allow_nan=False)),
+    st.tuples(st.just("lock"), st.integers(0, 3)),
+    st.tuples(st.just("rename"), st.integers(0, 3), st.sampled_from(["Tart", " ", "Zing"])),
+    st.tuples(st.just("remove_centroid"), st.integers(0, 3)),
+    st.tuples(st.just("delete_card"), st.integers(0, 9)),
+    st.tuples(st.just("shuffle"),),
+    st.tuples(st.just("restart"),),
+), max_size=40)
+
+
+@settings(max_examples=150, deadline=None)
+@given(_ops)
+def test_room_invariants_and_export_round_trip(ops_seq):
+    """Any sequence of board operations keeps the room consistent -- at most max_centroids,
+    every assignment names a live centroid, a position only for an assigned card and inside
+    the drop clamps -- and its export re-imports to the same export, byte for byte."""
+    from mikmeans.models.room import Room
+
+    room = Room("PROP1", seed=3)
+
+    def card(i):
+        return room.cards[i % len(room.cards)]["id"] if room.cards else "none"
+
+    def cent(i):
+        return room.centroids[i % len(room.centroids)]["id"] if room.centroids else "none"
+
+    for op in ops_seq:
+        kind = op[0]
+        if kind == "add_centroid":
+            room.add_centroid(op[1] or None)
+        elif kind == "add_card":
+            room.add_card(op[1], op[2])
+        elif kind == "assign":
+            room.update_card_assign(card(op[1]), None if op[2] < 0 else cent(op[2]))
+        elif kind == "drop":
+            room.drop_card(card(op[1]), cent(op[2]), op[3], op[4])
+        elif kind == "lock":
+            room.toggle_lock(cent(op[1]))
+        elif kind == "rename":
+            room.rename_centroid(cent(op[1]), op[2])
+        elif kind == "remove_centroid":
+            room.remove_centroid(cent(op[1]))
+        elif kind == "delete_card":
+            room.delete_card(card(op[1]))
+        elif kind == "shuffle":
+            room.shuffle_unassigned()
+        else:
+            room.restart_all()
+    assert len(room.centroids) <= room.max_centroids
+    live = {c["id"] for c in room.centroids}
+    assigned = {c["id"] for c in room.cards if c.get("assignedTo")}
+    assert all(c.get("assignedTo") in live for c in room.cards if c.get("assignedTo"))
+    for k, v in room.meta.items():
+        if str(k).startswith("pos:"):
+            assert k[4:] in assigned
+            assert 0.02 <= v["x"] <= 0.92 and 0.10 <= v["y"] <= 0.92
+    exp = room.export_json()
+    assert Room.from_json(exp, "PROP1", seed=3).export_json() == exp
+    room.dashboard()    # (computable on any reachable board)
