@@ -17,7 +17,7 @@ from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-_SET = dict(max_examples=40, deadline=None, derandomize=True, suppress_health_check=list(HealthCheck))
+_SET = dict(max_examples=150, deadline=None, derandomize=True, suppress_health_check=list(HealthCheck))
 
 
 @settings(**_SET)
@@ -51,3 +51,24 @@ def test_cluster_sums_random_shapes(native, n, d, k, bf16, unassigned, seed):
     colmax = X.double().abs().amax(0).clamp_min(1e-30)   # (over every row: the scale's own basis)
     bound = ec.double()[:, None] * colmax[None, :] * 2.0**-19 + 1e-12
     assert bool(((sums.cpu().double() - es.double()).abs() <= bound).all())
+
+
+@settings(**{**_SET, "max_examples": 30})
+@given(n=st.integers(70_000, 200_000), d=st.sampled_from([16, 40, 64, 128, 200, 256]),
+       k=st.integers(32, 600), bf16=st.booleans(), init=st.sampled_from(["random", "k-means++"]),
+       seed=st.integers(0, 2**16))
+def test_bounded_estep_equals_lloyd_random_problems(native, n, d, k, bf16, init, seed):
+    """The exact bounded (Hamerly) E-step -- the default algorithm='auto' takes it here -- gives
+    the full E-step's labels, centres and iteration count bit for bit on random blob problems."""
+    from mikmeans import KMeans
+    from mikmeans.data import blobs as B
+
+    dtype = torch.bfloat16 if bf16 else torch.float32
+    X = B.make_blobs(n, d, max(2, k // 2), seed=seed, dtype=dtype, device=DEV)
+    kw = dict(init=init, max_iter=12, tol=1e-6, seed=seed, dtype=dtype)
+    a = KMeans(k, **kw).fit(X)
+    f = KMeans(k, algorithm="lloyd", **kw).fit(X)
+    assert a.algorithm_ == "hamerly" and f.algorithm_ == "lloyd"
+    assert a.n_iter_ == f.n_iter_
+    assert torch.equal(a.cluster_centers_, f.cluster_centers_)
+    assert torch.equal(a.labels_, f.labels_)
