@@ -72,3 +72,65 @@ def test_bounded_estep_equals_lloyd_random_problems(native, n, d, k, bf16, init,
     assert a.n_iter_ == f.n_iter_
     assert torch.equal(a.cluster_centers_, f.cluster_centers_)
     assert torch.equal(a.labels_, f.labels_)
+
+
+@settings(**{**_SET, "max_examples": 80})
+@given(n=st.integers(1, 3000), d=st.integers(1, 600), k=st.integers(1, 700), bf16=st.booleans(),
+       seed=st.integers(0, 2**20))
+def test_transform_random_shapes(native, n, d, k, bf16, seed):
+    """The MFMA transform kernel's [n, K] distances against torch.cdist on the quantised
+    centres, and its argmin is a nearest centre."""
+    dtype = torch.bfloat16 if bf16 else torch.float32
+    g = torch.Generator().manual_seed(seed)
+    X = (torch.randn(n, d, generator=g) * 2).to(dtype)
+    C = torch.randn(k, d, generator=g) * 2
+    got = ops.transform(X.to(DEV), C.to(DEV)).cpu()
+    exp = torch.cdist(X.float(), ref.quantize_centers(C, dtype))
+    scale = float((X.float() ** 2).sum(1).max() + (C ** 2).sum(1).max()) ** 0.5
+    assert got.shape == (n, k)
+    torch.testing.assert_close(got, exp, rtol=2e-3, atol=2e-3 * scale)
+
+
+@settings(**{**_SET, "max_examples": 60})
+@given(n=st.integers(1, 40_000), d=st.integers(1, 1100), bf16=st.booleans(), sparse=st.booleans(),
+       seed=st.integers(0, 2**20))
+def test_col_stats_random_shapes(native, n, d, bf16, sparse, seed):
+    """Column statistics (max |x|, nonzero counts, lowest-bit exponents exact; f64 sums to
+    rounding) against torch for any shape -- rows wider than one launch's 64 pieces too."""
+    dtype = torch.bfloat16 if bf16 else torch.float32
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(n, d, generator=g) * torch.logspace(-2, 2, d)
+    if sparse:
+        X[torch.rand(n, d, generator=g) < 0.7] = 0.0
+    X = X.to(dtype)
+    st_ = ops.col_stats(ops.pad_columns(X.to(DEV)))
+    rf = ops.col_stats(X)
+    assert torch.equal(st_.absmax.cpu()[:d], rf.absmax)
+    assert torch.equal(st_.nnz.cpu()[:d], rf.nnz)
+    assert torch.equal(st_.lowbit.cpu()[:d], rf.lowbit)
+    for key in ("sumabs", "sum", "sumsq"):
+        a, b = getattr(st_, key).cpu()[:d], getattr(rf, key)
+        tol = 1e-12 * rf.sumabs.abs() if key == "sum" else 1e-12 * b.abs()
+        assert bool(((a - b).abs() <= tol + 1e-300).all()), key
+
+
+@settings(**{**_SET, "max_examples": 40})
+@given(n=st.integers(1, 3000), d=st.integers(1, 300), centres=st.integers(1, 64), bf16=st.booleans(),
+       i0=st.integers(0, 2**40), seed=st.integers(0, 2**32 - 1))
+def test_blobs_match_mirror_random(native, n, d, centres, bf16, i0, seed):
+    """The on-device blob generator against its NumPy mirror for any (row offset, shape, seed):
+    identical cluster ids, values within the hardware transcendentals' few ulp (bf16: one
+    rounding step)."""
+    import numpy as np
+
+    from mikmeans.data import blobs as B
+
+    dtype = torch.bfloat16 if bf16 else torch.float32
+    Cg = B.blob_centers(centres, d, 10.0, seed=seed, device=DEV)
+    Cn = B.blob_centers_np(centres, d, 10.0, seed=seed)
+    Xg, yg = B.make_blobs(n, d, centres, seed=seed, i0=i0, dtype=dtype, device=DEV, return_labels=True,
+                          centers=Cg)
+    Xn, yn = B.blobs_np(i0, n, Cn, 1.0, seed, True, bits16=bf16)
+    assert np.array_equal(yg.cpu().numpy(), yn)
+    tol = 1e-4 if not bf16 else 8e-2
+    np.testing.assert_allclose(Xg.float().cpu().numpy(), Xn, rtol=0, atol=tol)
