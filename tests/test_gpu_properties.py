@@ -134,3 +134,23 @@ def test_blobs_match_mirror_random(native, n, d, centres, bf16, i0, seed):
     assert np.array_equal(yg.cpu().numpy(), yn)
     tol = 1e-4 if not bf16 else 8e-2
     np.testing.assert_allclose(Xg.float().cpu().numpy(), Xn, rtol=0, atol=tol)
+
+
+@settings(**{**_SET, "max_examples": 20})
+@given(n=st.integers(20_000, 120_000), d=st.sampled_from([8, 30, 64, 128, 256, 300]),
+       k=st.integers(2, 300), bf16=st.booleans(), chunk_units=st.integers(2, 12), seed=st.integers(0, 2**16))
+def test_streamed_fit_equals_resident_random(native, n, d, k, bf16, chunk_units, seed):
+    """An out-of-core (streamed) fit from host rows is the resident fit bit for bit, for any
+    chunk size on the 1536-row grid (every chunk resolves near-ties as the resident pass does)."""
+    import mikmeans
+    from mikmeans.data import blobs as B
+
+    X = B.make_blobs(n, d, max(2, k), seed=seed, dtype=torch.float32, device="cpu")
+    Xh = X.to(torch.bfloat16) if bf16 else X
+    kw = dict(init=X[:k].clone(), dtype="bfloat16" if bf16 else "float32", max_iter=4, tol=0, device=DEV,
+              algorithm="lloyd")
+    res = mikmeans.KMeans(k, **kw).fit(Xh.to(DEV))
+    strm = mikmeans.KMeans(k, chunk_rows=1536 * chunk_units, **kw).fit(Xh)
+    assert strm.memory_plan_["mode"] == "streaming"
+    assert torch.equal(strm.cluster_centers_, res.cluster_centers_)
+    assert torch.equal(strm.labels_, res.labels_)
