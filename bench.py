@@ -56,7 +56,9 @@ def main(argv=None):
     ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=False,
                     help="cfg5: generate the next batch on a side stream, started between the "
                          "current batch's assign and its M-step (mikmeans/data/blobs.py kick); measured "
-                         "no faster: the M-step's workgroups hold the CUs (profiles/r5_27_cfg5_*.log)")
+                         "no faster: the M-step's workgroups hold the CUs (profiles/r5_27_cfg5_*.log), and "
+                         "kernel traces show no overlap even where the side stream has a hardware queue "
+                         "of its own (profiles/r6_26_cfg5pf_overlap.json, r6_27_stream_probe.log)")
     ap.add_argument("--gen-norms", action=argparse.BooleanOptionalAction, default=False,
                     help="cfg5 streamed: the generator also writes the rows' |x|^2 (fused) and the "
                          "assign takes them (early prologue) instead of summing its fragments; "
