@@ -16,9 +16,11 @@ from collections import defaultdict
 
 def short(name: str) -> str:
     n = name.split("(")[0]
-    for key in ("assign16_kernel", "update_ks_kernel", "update_kernel", "blobs_kernel", "reduce_kernel",
-                "finalize_kernel", "sample_index_kernel", "col_absmax_kernel", "row_sqnorm_kernel"):
-        if key in n:
+    base = n.split("<")[0].split("::")[-1].split()[-1] if n else n
+    for key in ("assign16_kernel", "update_ks_kernel", "update_kernel", "bounds_update_kernel", "blobs_kernel",
+                "reduce_kernel", "finalize_kernel", "sample_index_kernel", "col_absmax_kernel",
+                "row_sqnorm_kernel", "label_delta_rows_kernel", "label_delta_kernel"):
+        if base == key:
             return key
     return n.split("::")[-1][:40]
 
