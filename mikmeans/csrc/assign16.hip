@@ -405,14 +405,16 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     uint32_t vb[C::P], tb[C::P];   // VARG: running minimum (bits of a positive float), its tile
     // TOP2 (bounded E-step): this lane's second-smallest score (keys: index bits included,
     // <= 2^-17 relative -- the bounds' slack covers it), merged over lanes later; the smallest
-    // is the epilogue's own running minimum (min(best, seg_best)), so TOP2 adds one register
-    // per point block
-    float m2[C::P];
+    // is the epilogue's own running minimum (min(best, seg_best)).  Keys: the segment's own
+    // second-smallest m2s rides along seg_best (one v_med3 + one v_min per key, no per-tile
+    // merge with the global pair) and joins m2 at the segment's end -- 12 VALU per tile and
+    // block instead of 16 (the gathered bounded assign is VALU-bound).
+    float m2[C::P], m2s[C::P];
 #pragma unroll
     for (int p = 0; p < C::P; ++p) {
       best[p] = 3.0e38f; seg_best[p] = 3.0e38f; bg[p] = 0;
       vb[p] = 0x7f7fffffu; tb[p] = 0u;
-      m2[p] = 3.0e38f;
+      m2[p] = 3.0e38f; m2s[p] = 3.0e38f;
     }
     const int ngrp = nch * C::CT;   // one past the last tile (global tile numbering)
     const unsigned kmask = key6_mask();
@@ -513,15 +515,16 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
               const float k0 = pack_key6(sv[0], kmask, t0), k1 = pack_key6(sv[1], kmask, t1);
               const float k2 = pack_key6(sv[2], kmask, t2), k3 = pack_key6(sv[3], kmask, t3);
               if constexpr (TOP2) {
-                // the two smallest of the tile's four keys, merged with the running pair
-                // (min(best, seg_best), m2): second = min(max(old min, new min), m2, new second)
-                const float lo01 = fminf(k0, k1), hi01 = fmaxf(k0, k1);
-                const float lo23 = fminf(k2, k3), hi23 = fmaxf(k2, k3);
-                const float kmin = fminf(lo01, lo23);
-                const float ksec = fminf(fmaxf(lo01, lo23), fminf(hi01, hi23));
-                const float omin = fminf(best[p], seg_best[p]);
-                m2[p] = min3f(fmaxf(omin, kmin), m2[p], ksec);
-                seg_best[p] = fminf(seg_best[p], kmin);
+                // the segment's sorted pair (seg_best, m2s): med3 of (smallest, second, new) is
+                // the new second
+                m2s[p] = __builtin_amdgcn_fmed3f(seg_best[p], m2s[p], k0);
+                seg_best[p] = fminf(seg_best[p], k0);
+                m2s[p] = __builtin_amdgcn_fmed3f(seg_best[p], m2s[p], k1);
+                seg_best[p] = fminf(seg_best[p], k1);
+                m2s[p] = __builtin_amdgcn_fmed3f(seg_best[p], m2s[p], k2);
+                seg_best[p] = fminf(seg_best[p], k2);
+                m2s[p] = __builtin_amdgcn_fmed3f(seg_best[p], m2s[p], k3);
+                seg_best[p] = fminf(seg_best[p], k3);
               } else {
                 seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
               }
@@ -585,6 +588,10 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
             if ((tile & 15) == 15 || tile == ngrp - 1) {
     #pragma unroll
               for (int p = 0; p < C::P; ++p) {
+                if constexpr (TOP2) {   // the two sorted pairs -> the overall second-smallest key
+                  m2[p] = min3f(m2[p], m2s[p], fmaxf(best[p], seg_best[p]));
+                  m2s[p] = 3.0e38f;
+                }
                 // compare values only: on equal (truncated) values the earlier segment keeps
                 // the lower centroid index (all keys are >= 0, see the header)
                 const float sv = __uint_as_float(__float_as_uint(seg_best[p]) & ~63u);
