@@ -163,7 +163,6 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
 // every row's |x|^2 in row_sqnorm_kernel's canonical order -- the fit's setup reads X once.
 // Packed 16-bit helpers, written out (left to itself the compiler turns min(y, 1) per half into
 // a compare + select per half, six instructions for one).
-typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
   uint32_t d;
   asm("v_pk_min_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
