@@ -145,22 +145,6 @@ hipError_t launch_row_sqnorm(int dtype, const void* X, int64_t N, int D, int64_t
   return hipGetLastError();
 }
 
-// Per-column max |x| (the fixed-point M-step's column scales, csrc/update.hip).  L lanes
-// per row (power of two >= the row's 16-byte pieces, <= 64), 256/L rows per pass, four
-// independent row loads in flight per lane; |x| compared as bit patterns (non-negative
-// floats order like unsigned integers, and a NaN's pattern exceeds +inf's, so NaN
-// propagates like torch.aminmax).  One global atomicMax per (block, column).  STATS: also,
-// per column, the sums of |x|, x and x^2 (f64 per lane; every block writes its partial sums
-// to its own row of fpart [COLSTAT_BLOCKS][3][D], which colstat_reduce_kernel then sums in a
-// fixed order -- no f64 atomics, so the statistics are bitwise the same on every launch:
-// fstats = [sum |x| | sum x | sum x^2], the last two give the tol scale's variance without
-// an f32 copy of X), the count of nonzero values and the exponent of the lowest set bit over
-// all nonzero finite values (x is an integer multiple of 2^lowbit; integer atomics, order-free).
-// From these the engine flags wide-range columns for the residual M-step pass: a column whose
-// values all sit on the hi pass's grid (lowbit >= -col_exp: one-hot, small integers, coarse
-// bf16) never needs it, and otherwise the max is compared with the mean of the NONZERO |x|
-// (sparse columns stay single-pass).  NORMS (the launch covers whole rows, <= 64 pieces): also
-// every row's |x|^2 in row_sqnorm_kernel's canonical order -- the fit's setup reads X once.
 // Packed 16-bit helpers, written out (left to itself the compiler turns min(y, 1) per half into
 // a compare + select per half, six instructions for one).
 __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
@@ -208,6 +192,22 @@ __device__ __forceinline__ uint32_t lowbit_keys_bf16x2(uint32_t y) {
   const uint32_t inv = pk_min_u16(pk_sub_sat_u16(pk_add_u16(y, 0xffffffffu), 0x7f7e7f7eu), 0x00010001u);
   return pk_mad_u16(inv, 0x40004000u, k2);
 }
+// Per-column max |x| (the fixed-point M-step's column scales, csrc/update.hip).  L lanes
+// per row (power of two >= the row's 16-byte pieces, <= 64), 256/L rows per pass, four
+// independent row loads in flight per lane; |x| compared as bit patterns (non-negative
+// floats order like unsigned integers, and a NaN's pattern exceeds +inf's, so NaN
+// propagates like torch.aminmax).  One global atomicMax per (block, column).  STATS: also,
+// per column, the sums of |x|, x and x^2 (f64 per lane; every block writes its partial sums
+// to its own row of fpart [COLSTAT_BLOCKS][3][D], which colstat_reduce_kernel then sums in a
+// fixed order -- no f64 atomics, so the statistics are bitwise the same on every launch:
+// fstats = [sum |x| | sum x | sum x^2], the last two give the tol scale's variance without
+// an f32 copy of X), the count of nonzero values and the exponent of the lowest set bit over
+// all nonzero finite values (x is an integer multiple of 2^lowbit; integer atomics, order-free).
+// From these the engine flags wide-range columns for the residual M-step pass: a column whose
+// values all sit on the hi pass's grid (lowbit >= -col_exp: one-hot, small integers, coarse
+// bf16) never needs it, and otherwise the max is compared with the mean of the NONZERO |x|
+// (sparse columns stay single-pass).  NORMS (the launch covers whole rows, <= 64 pieces): also
+// every row's |x|^2 in row_sqnorm_kernel's canonical order -- the fit's setup reads X once.
 constexpr int COLSTAT_BLOCKS = 8192;   // the partials' row cap (colstat_cap sizes a launch)
 
 // Branch-free (it runs once per element of the pass; the branchy form cost ~20 VALU + SALU
