@@ -517,14 +517,15 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
               if constexpr (TOP2) {
                 // the segment's sorted pair (seg_best, m2s): med3 of (smallest, second, new) is
                 // the new second
-                m2s[p] = __builtin_amdgcn_fmed3f(seg_best[p], m2s[p], k0);
-                seg_best[p] = fminf(seg_best[p], k0);
-                m2s[p] = __builtin_amdgcn_fmed3f(seg_best[p], m2s[p], k1);
-                seg_best[p] = fminf(seg_best[p], k1);
-                m2s[p] = __builtin_amdgcn_fmed3f(seg_best[p], m2s[p], k2);
-                seg_best[p] = fminf(seg_best[p], k2);
-                m2s[p] = __builtin_amdgcn_fmed3f(seg_best[p], m2s[p], k3);
-                seg_best[p] = fminf(seg_best[p], k3);
+                // (asm forms: no per-key canonicalisation, see common.h med3f)
+                m2s[p] = med3f(seg_best[p], m2s[p], k0);
+                seg_best[p] = min2f(seg_best[p], k0);
+                m2s[p] = med3f(seg_best[p], m2s[p], k1);
+                seg_best[p] = min2f(seg_best[p], k1);
+                m2s[p] = med3f(seg_best[p], m2s[p], k2);
+                seg_best[p] = min2f(seg_best[p], k2);
+                m2s[p] = med3f(seg_best[p], m2s[p], k3);
+                seg_best[p] = min2f(seg_best[p], k3);
               } else {
                 seg_best[p] = min3f(min3f(k0, k1, k2), k3, seg_best[p]);
               }

@@ -126,6 +126,19 @@ __device__ __forceinline__ float min3f(float a, float b, float c) {
   return d;
 }
 
+// v_med3_f32 / v_min_f32 the same way (the TOP2 epilogue's per-key pair update: with fminf /
+// the builtin med3 hipcc canonicalised every key first, one v_max_f32 per key).
+__device__ __forceinline__ float med3f(float a, float b, float c) {
+  float d;
+  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ float min2f(float a, float b) {
+  float d;
+  asm("v_min_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+
 // (score, centre) as one u64 whose unsigned order is (score, then lower index): the
 // float's bits mapped to an order-preserving u32 in the high word.
 __device__ __forceinline__ unsigned long long split_key(float v, int k) {
