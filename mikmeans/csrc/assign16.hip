@@ -590,7 +590,7 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
     #pragma unroll
               for (int p = 0; p < C::P; ++p) {
                 if constexpr (TOP2) {   // the two sorted pairs -> the overall second-smallest key
-                  m2[p] = min3f(m2[p], m2s[p], fmaxf(best[p], seg_best[p]));
+                  m2[p] = min3f(m2[p], m2s[p], max2f(best[p], seg_best[p]));
                   m2s[p] = 3.0e38f;
                 }
                 // compare values only: on equal (truncated) values the earlier segment keeps

@@ -138,6 +138,11 @@ __device__ __forceinline__ float min2f(float a, float b) {
   asm("v_min_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
   return d;
 }
+__device__ __forceinline__ float max2f(float a, float b) {
+  float d;
+  asm("v_max_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
 
 // (score, centre) as one u64 whose unsigned order is (score, then lower index): the
 // float's bits mapped to an order-preserving u32 in the high word.
