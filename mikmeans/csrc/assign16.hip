@@ -540,13 +540,25 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
           };
           if constexpr (WIDE) {
             // wide rows (DPAD > 256): one A fragment at a time, each against the P blocks --
-            // all NQ of a tile would not fit in registers beside the rows
+            // all NQ of a tile would not fit in registers beside the rows.  The reads run WPF
+            // fragments ahead of the MFMAs that use them, pinned in that order: left to the
+            // scheduler, each read sat right before its P MFMAs behind an lgkmcnt(0), so one
+            // wave per SIMD waited out every LDS round trip (bf16 D=512: 870 TF/s against
+            // 1410 at D=256, profiles/r6_43_assign_sweep.log)
             const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
+            // (2 ahead where the rows leave room for 2 waves per SIMD under 256 VGPRs: bf16 D=384
+            // at 4 ahead took 265 and ran 15 % slower at one wave, r6_44_ab_wide_d384_bf16.log)
+            constexpr int WPF = C::NQ < 4 ? C::NQ : (C::P * C::NQ * 4 <= 192 ? 2 : 4);
+            u32x4 aq[C::NQ];
+#pragma unroll
+            for (int q = 0; q < WPF; ++q) aq[q] = *(const u32x4*)(tl + q * 1024);
 #pragma unroll
             for (int q = 0; q < C::NQ; ++q) {
-              const u32x4 aq = *(const u32x4*)(tl + q * 1024);
+              if (q + WPF < C::NQ) aq[q + WPF] = *(const u32x4*)(tl + (q + WPF) * 1024);
+              __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-              for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aq, xr[p][q], acc[p]);
+              for (int p = 0; p < C::P; ++p) acc[p] = Mfma16<T>::run(aq[q], xr[p][q], acc[p]);
+              __builtin_amdgcn_sched_barrier(0);
             }
           } else if constexpr (PMAJ) {
             // point-block-major issue, pinned in this order
