@@ -973,7 +973,7 @@ constexpr int p_narrow() {
 }
 template <typename T, int DPAD>
 constexpr int p_wide() {
-  return sizeof(T) == 2 ? (DPAD <= 512 ? 4 : 2) : (DPAD <= 512 ? 2 : 1);
+  return sizeof(T) == 2 ? (DPAD == 512 ? 3 : DPAD <= 512 ? 4 : 2) : (DPAD <= 512 ? 2 : 1);
 }
 
 // The workgroup's point count (NW*P*16) must divide parallel/shard.py ROW_ALIGN (1536).
@@ -1034,8 +1034,11 @@ int assign_kpad(int dtype, int dpad, int K) { return plan::assign_kpad(dtype == 
 int assign_cn_len(int kpad) { return plan::assign_cn_len(kpad); }
 
 // Wide rows (DPAD 384..1024, e.g. sentence-embedding widths): one centre tile per chunk
-// (12-32 KiB), one wave per SIMD, and as many point blocks as ~256 registers of rows hold --
-// bf16 4 blocks up to 512 features and 2 beyond, f32 2 and 1.  The fragment layout, the
+// (12-32 KiB), and as many point blocks as ~256 registers of rows hold -- bf16 4 blocks at
+// 384 features, 2 beyond 512, f32 2 and 1 -- at one wave per SIMD, or two where the kernel
+// stays under 256 VGPRs (D=384, D=768).  bf16 D=512 takes 3 blocks (192 registers of rows,
+// 2 waves/SIMD): +18 % at K=1024 and 4096, +26 % at K=256 against 4 blocks at one wave
+// (profiles/r6_45_ab_d512_*.log).  The fragment layout, the
 // seed offsets and the argmin epilogue are the narrow kernels'; only the MFMA issue reads
 // the A fragments one at a time (WIDE in assign16_kernel).
 template <typename T, int DPAD>
