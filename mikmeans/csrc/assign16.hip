@@ -547,8 +547,9 @@ __global__ __launch_bounds__(NW_ * 64, OCC) void assign16_kernel(AssignArgs a) {
             // 1410 at D=256, profiles/r6_43_assign_sweep.log)
             const char* tl = buf + tl_i * C::TILE_BYTES + lane * 16;
             // (2 ahead where the rows leave room for 2 waves per SIMD under 256 VGPRs: bf16 D=384
-            // at 4 ahead took 265 and ran 15 % slower at one wave, r6_44_ab_wide_d384_bf16.log)
-            constexpr int WPF = C::NQ < 4 ? C::NQ : (C::P * C::NQ * 4 <= 192 ? 2 : 4);
+            // at 4 ahead took 265 and ran 15 % slower at one wave, r6_44_ab_wide_d384_bf16.log;
+            // 1 ahead for its bounded E-step, whose second-best keys spilled at 2)
+            constexpr int WPF = C::NQ < 4 ? C::NQ : (C::P * C::NQ * 4 <= 192 ? (TOP2 && C::P == 4 ? 1 : 2) : 4);
             u32x4 aq[C::NQ];
 #pragma unroll
             for (int q = 0; q < WPF; ++q) aq[q] = *(const u32x4*)(tl + q * 1024);
@@ -1042,12 +1043,19 @@ int assign_cn_len(int kpad) { return plan::assign_cn_len(kpad); }
 // seed offsets and the argmin epilogue are the narrow kernels'; only the MFMA issue reads
 // the A fragments one at a time (WIDE in assign16_kernel).
 template <typename T, int DPAD>
+constexpr int C_wide_rows() {   // registers of rows per lane: P blocks x NQ 16-B pieces x 4
+  return p_wide<T, DPAD>() * (DPAD / 4 / Elem<T>::V) * 4;
+}
+template <typename T, int DPAD>
 static hipError_t launch16_w(const AssignArgs& a, hipStream_t s) {
   constexpr int CT = chunk_tiles16(sizeof(T), DPAD);
   static_assert(CT == 1, "wide rows: one tile per chunk");
   constexpr int P = p_wide<T, DPAD>();
   static_assert(1536 % (4 * P * 16) == 0, "workgroup points must tile the shard grid");
-  return launch16_t<T, DPAD, P, CT, 2, 1>(a, s);
+  // rows in <= 192 registers: hold the kernel to 2 waves/SIMD (the bounded E-step's D=384
+  // build took 257 VGPRs without the bound)
+  constexpr int OCC = C_wide_rows<T, DPAD>() <= 192 ? 2 : 1;
+  return launch16_t<T, DPAD, P, CT, 2, OCC>(a, s);
 }
 
 // NW * P * 16 of the geometry launch16_d / launch16_w pick for a call without bounds (the A/B

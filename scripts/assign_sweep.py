@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--d", default="32,64,128,256,512")
     ap.add_argument("--k", default="64,256,1024,4096")
     ap.add_argument("--dtypes", default="bf16,f32")
+    ap.add_argument("--what", default="both", choices=["both", "assign", "mstep"],
+                    help="time one kernel only (a counter run over one of them)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     comm = Comm.local(dev)
@@ -56,14 +58,17 @@ def main():
                     init_random(X, d, k, n, 0, comm, 0))
                 for _ in range(2):
                     eng.step()
-                ta = timed(lambda: eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True))
-                tm = timed(lambda: eng._C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks,
-                                                 eng.weights, eng.col_exp, eng.cnt_exp, False))
+                ta = tm = float("nan")
+                if a.what != "mstep":
+                    ta = timed(lambda: eng.pk.assign(eng.X, eng.xn, eng.labels, eng.mind, eng.slots, True))
+                if a.what != "assign":
+                    tm = timed(lambda: eng._C.update(eng.X, eng.labels, eng.K, eng.slab, eng.cnt_slab, eng.n_chunks,
+                                                     eng.weights, eng.col_exp, eng.cnt_exp, False))
                 xb = X.numel() * X.element_size()
                 r = {"dtype": dts, "n": n, "d": d, "k": k, "assign_ms": round(ta, 4),
                      "assign_tflops": round(2.0 * n * k * d / (ta * 1e-3) / 1e12, 1),
                      "mstep_ms": round(tm, 4), "mstep_TBps": round(xb / (tm * 1e-3) / 1e12, 2),
-                     "it_per_s_estimate": round(1e3 / (ta + tm), 1)}
+                     "it_per_s_estimate": round(1e3 / (ta + tm), 1) if a.what == "both" else None}
                 rows.append(r)
                 print(json.dumps(r), flush=True)
                 del eng

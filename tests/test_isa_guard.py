@@ -94,3 +94,20 @@ def test_colstats_bf16_register_budget(tmp_path):
     assert len(res) >= 3, [r.name for r in res]
     bad = [(r.name, r.vgprs, r.vgpr_spills) for r in res if r.vgprs > 128 or r.vgpr_spills]
     assert not bad, bad
+
+
+def test_wide_assign_two_wave_budget(tmp_path):
+    """The wide-row bf16 assign kernels sized for 2 waves/SIMD (D = 384 with 4 point blocks,
+    512 with 3, 768 with 2) stay at or under 256 VGPRs and spill nothing: crossing 256 drops
+    them to one wave per SIMD (D=384 with its A reads 4 ahead took 265 VGPRs and ran 15 %
+    slower, profiles/r6_44_ab_wide_d384_bf16.log; 3 blocks at D=512 gained 18-26 % over 4 at
+    one wave, profiles/r6_45_ab_d512_*.log)."""
+    obj = _build._compile(SRC, _build.source_flags(SRC.name), verbose=False)
+    res = isa.kernel_resources(isa.device_elf(obj, tmp_path / "dev.o"))
+    want = {"384": "4", "512": "3", "768": "2"}
+    wide = [(r, t) for r, t in ((r, isa.assign16_template_args(r.name)) for r in res)
+            if t and t[0] == "unsigned short" and t[1] in want]
+    assert {t[1] for _, t in wide} == set(want), [t[:3] for _, t in wide]
+    assert all(t[2] == want[t[1]] for _, t in wide), [t[:3] for _, t in wide]
+    bad = [(t[:3], r.vgprs, r.vgpr_spills) for r, t in wide if r.vgprs > 256 or r.vgpr_spills]
+    assert not bad, bad
