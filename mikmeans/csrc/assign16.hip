@@ -974,7 +974,7 @@ constexpr int p_narrow() {
 }
 template <typename T, int DPAD>
 constexpr int p_wide() {
-  return sizeof(T) == 2 ? (DPAD == 512 ? 3 : DPAD <= 512 ? 4 : 2) : (DPAD <= 512 ? 2 : 1);
+  return sizeof(T) == 2 ? (DPAD == 512 || DPAD == 1024 ? 3 : DPAD <= 512 ? 4 : 2) : (DPAD <= 512 ? 2 : 1);
 }
 
 // The workgroup's point count (NW*P*16) must divide parallel/shard.py ROW_ALIGN (1536).
@@ -1036,10 +1036,11 @@ int assign_cn_len(int kpad) { return plan::assign_cn_len(kpad); }
 
 // Wide rows (DPAD 384..1024, e.g. sentence-embedding widths): one centre tile per chunk
 // (12-32 KiB), and as many point blocks as ~256 registers of rows hold -- bf16 4 blocks at
-// 384 features, 2 beyond 512, f32 2 and 1 -- at one wave per SIMD, or two where the kernel
+// 384 features, 2 at 768, f32 2 and 1 -- at one wave per SIMD, or two where the kernel
 // stays under 256 VGPRs (D=384, D=768).  bf16 D=512 takes 3 blocks (192 registers of rows,
 // 2 waves/SIMD): +18 % at K=1024 and 4096, +26 % at K=256 against 4 blocks at one wave
-// (profiles/r6_45_ab_d512_*.log).  The fragment layout, the
+// (profiles/r6_45_ab_d512_*.log); bf16 D=1024 takes 3 blocks at one wave (~450 VGPRs): +1.3 %
+// at K=1024, +1.9 % at 4096 against 2 (profiles/r6_53_ab_*.log).  The fragment layout, the
 // seed offsets and the argmin epilogue are the narrow kernels'; only the MFMA issue reads
 // the A fragments one at a time (WIDE in assign16_kernel).
 template <typename T, int DPAD>
