@@ -115,9 +115,9 @@ inline bool choose_ks(int esize, int K, int D, KsPlan* p) {
       // profiles/r2_05_update_study.md)
       const double m = 64.0 / ks;
       const int g = (int)ceil((m + 2.5 * sqrt(m)) / (64.0 / lpr));
-      // (whole 1-KiB rows, m = 1: 3 groups beat 6 at K=4096 D=384 / 512, 1.57 vs 1.80 ms at
-      // N=5e6, profiles/r6_55_mstep_gm*.log)
-      p->gm = g <= 2 ? 2 : (g <= 3 || (g == 4 && lpr == 64)) ? 3 : 6;
+      // (g = 4 takes 3 groups: 3 beat 6 at D=64 K=2048 by 11 %, D=128 K=2048 by 4 % and
+      // D=384 / 512 K=4096 by 13 %; 6 stays ahead from g = 5, profiles/r6_55_*, r6_56_*, r6_57_*)
+      p->gm = g <= 2 ? 2 : g <= 4 ? 3 : 6;
       return true;
     }
     if (ks >= 64) return false;
